@@ -1,0 +1,85 @@
+"""Read the initializer table (name, dims, external offset/length) of a Genie graph.
+
+The character directory's relinked graphs carry the tensor layout of the
+fp16/fp32 weight bins as ONNX external-data entries (`g/ModelManager.py:80-103`).
+Only the fields that table needs are decoded from the protobuf wire format
+(ModelProto.graph=7; GraphProto.initializer=5; TensorProto dims=1, name=8,
+external_data=13{key=1,value=2}, data_location=14).  The `onnx` package is
+not a dependency of this engine.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+
+def _varint(b: bytes, p: int) -> Tuple[int, int]:
+    r = s = 0
+    while True:
+        c = b[p]
+        p += 1
+        r |= (c & 0x7F) << s
+        if c < 0x80:
+            return r, p
+        s += 7
+
+
+def _walk(b: bytes):
+    p, n = 0, len(b)
+    while p < n:
+        k, p = _varint(b, p)
+        f, wt = k >> 3, k & 7
+        if wt == 0:
+            v, p = _varint(b, p)
+        elif wt == 2:
+            ln, p = _varint(b, p)
+            v = b[p:p + ln]
+            p += ln
+        elif wt == 1:
+            v, p = b[p:p + 8], p + 8
+        elif wt == 5:
+            v, p = b[p:p + 4], p + 4
+        else:
+            raise ValueError(f"bad wire type {wt}")
+        yield f, wt, v
+
+
+def _tensor_entry(b: bytes):
+    name = ""
+    dims: List[int] = []
+    ext: Dict[str, str] = {}
+    for f, wt, v in _walk(b):
+        if f == 1:
+            if wt == 0:
+                dims.append(v)
+            else:
+                q = 0
+                while q < len(v):
+                    d, q = _varint(v, q)
+                    dims.append(d)
+        elif f == 8:
+            name = bytes(v).decode()
+        elif f == 13:
+            key = val = ""
+            for f2, _, v2 in _walk(v):
+                if f2 == 1:
+                    key = bytes(v2).decode()
+                elif f2 == 2:
+                    val = bytes(v2).decode()
+            ext[key] = val
+    off: Optional[int] = int(ext["offset"]) if "offset" in ext else None
+    ln: Optional[int] = int(ext["length"]) if "length" in ext else None
+    return name, dims, off, ln
+
+
+def read_initializer_table(path: str) -> Dict[str, Tuple[List[int], Optional[int], Optional[int]]]:
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    table = {}
+    for f, _, v in _walk(buf):
+        if f != 7:
+            continue
+        for f2, _, v2 in _walk(v):
+            if f2 == 5:
+                name, dims, off, ln = _tensor_entry(v2)
+                table[name] = (dims, off, ln)
+    return table
