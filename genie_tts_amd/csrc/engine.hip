@@ -1,0 +1,632 @@
+// Host side of the MI355X GPT-SoVITS engine: weight staging/upload, device
+// state, and the C ABI declared in include/genie_engine.h.
+//
+// T2S orchestration restates GENIE.t2s_cpu (src/genie_tts/Core/Inference.py:63-109):
+// encoder -> first-stage decoder -> <=500 stage-decoder steps -> trim; the step
+// loop runs on the device as a replayed hipGraph (state lives in HBM, the host
+// only polls the per-sequence done flags between graph chunks).
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/genie_engine.h"
+#include "engine_internal.h"
+#include "kernels.h"
+
+using namespace gsv;
+
+static thread_local std::string g_err;
+
+const char* gsv_last_error(void) { return g_err.c_str(); }
+const char* gsv_version(void) { return "genie-mi355x 0.1 (gfx950)"; }
+
+namespace gsv {
+int set_error(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace gsv
+
+// ------------------------------------------------------------ allocation
+void* gsv_engine::dalloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
+    allocs.push_back(p);
+    return p;
+}
+
+void gsv_engine::release_all() {
+    for (auto& kv : graphs) hipGraphExecDestroy(kv.second);
+    graphs.clear();
+    for (void* p : allocs) hipFree(p);
+    allocs.clear();
+}
+
+gsv_engine::~gsv_engine() {
+    release_all();
+    if (own_stream && stream) hipStreamDestroy(stream);
+    for (auto& e : ev) if (e) hipEventDestroy(e);
+}
+
+// ------------------------------------------------------------ weights
+const Staged* gsv_engine::find(const std::string& n) const {
+    auto it = staged.find(n);
+    return it == staged.end() ? nullptr : &it->second;
+}
+
+float* gsv_engine::up_f32(const std::string& n, int* err) {
+    const Staged* s = find(n);
+    if (!s) { *err = set_error(GSV_E_WEIGHT, "missing weight " + n); return nullptr; }
+    float* d = (float*)dalloc(s->data.size() * 4);
+    if (!d) { *err = set_error(GSV_E_HIP, "hipMalloc failed for " + n); return nullptr; }
+    hipMemcpy(d, s->data.data(), s->data.size() * 4, hipMemcpyHostToDevice);
+    return d;
+}
+
+__half* gsv_engine::up_f16(const std::string& n, int* err) {
+    const Staged* s = find(n);
+    if (!s) { *err = set_error(GSV_E_WEIGHT, "missing weight " + n); return nullptr; }
+    std::vector<__half> h(s->data.size());
+    for (size_t i = 0; i < h.size(); ++i) h[i] = __float2half(s->data[i]);
+    __half* d = (__half*)dalloc(h.size() * 2);
+    if (!d) { *err = set_error(GSV_E_HIP, "hipMalloc failed for " + n); return nullptr; }
+    hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    return d;
+}
+
+static std::vector<float> default_div_term() {
+    // exp(-2i ln(1e4)/512) in fp32; a character directory may override it with
+    // the exact constant of its own graph ("pe.div_term").
+    std::vector<float> d(256);
+    const float c = (float)(-(std::log(10000.0) / 512.0));
+    for (int i = 0; i < 256; ++i) d[i] = std::exp((float)(2 * i) * c);
+    return d;
+}
+
+int gsv_engine::finalize_t2s() {
+    int err = 0;
+    // PE table rows 0..pe_max-1 at 1-based positions (row p = position p).
+    std::vector<float> div = default_div_term();
+    if (const Staged* s = find("pe.div_term"))
+        if (s->data.size() == 256) div = s->data;
+    pe_max = 4096;
+    std::vector<float> pe((size_t)pe_max * 512);
+    for (int p = 0; p < pe_max; ++p)
+        for (int i = 0; i < 256; ++i) {
+            const float ang = (float)p * div[i];
+            pe[(size_t)p * 512 + 2 * i] = std::sin(ang);
+            pe[(size_t)p * 512 + 2 * i + 1] = std::cos(ang);
+        }
+    pe_tab = (float*)dalloc(pe.size() * 4);
+    hipMemcpy(pe_tab, pe.data(), pe.size() * 4, hipMemcpyHostToDevice);
+
+    // ar_audio_position alpha etc.
+    emb_audio = up_f16("ar_audio_embedding.word_embeddings.weight", &err);
+    alpha_audio = up_f32("ar_audio_position.alpha", &err);
+    w_pred = up_f16("ar_predict_layer.weight", &err);
+    for (int l = 0; l < 24 && !err; ++l) {
+        const std::string p = "transformer_encoder.layers." + std::to_string(l) + ".";
+        T2SLayerW& L = layers[l];
+        L.w_in = up_f16(p + "self_attn.in_proj_weight", &err);
+        L.b_in = up_f32(p + "self_attn.in_proj_bias", &err);
+        L.w_out = up_f16(p + "self_attn.out_proj.weight", &err);
+        L.b_out = up_f32(p + "self_attn.out_proj.bias", &err);
+        L.w1 = up_f16(p + "linear1.weight", &err);
+        L.b1 = up_f32(p + "linear1.bias", &err);
+        L.w2 = up_f16(p + "linear2.weight", &err);
+        L.b2 = up_f32(p + "linear2.bias", &err);
+        L.n1w = up_f32(p + "norm1.weight", &err);
+        L.n1b = up_f32(p + "norm1.bias", &err);
+        L.n2w = up_f32(p + "norm2.weight", &err);
+        L.n2b = up_f32(p + "norm2.bias", &err);
+    }
+    if (err) return err;
+    text_emb = up_f32("encoder.ar_text_embedding.word_embeddings.weight", &err);
+    bert_w = up_f32("encoder.bert_proj.weight", &err);
+    bert_b = up_f32("encoder.bert_proj.bias", &err);
+    alpha_text = up_f32("encoder.ar_text_position.alpha", &err);
+    ssl_w = up_f32("vits.ssl_proj.weight", &err);
+    ssl_b = up_f32("vits.ssl_proj.bias", &err);
+    codebook = up_f32("vits.quantizer.vq.layers.0._codebook.embed", &err);
+    if (err) return err;
+    cb_sumsq = (float*)dalloc(1024 * 4);
+    sumsq_rows(codebook, 768, 1024, 768, cb_sumsq, nullptr);
+    // qk scale exactly as the graph: Sqrt(Div(1, Sqrt(Cast(32))))  (stage#84-90)
+    qk_scale = std::sqrt(1.0f / std::sqrt(32.0f));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : set_error(GSV_E_HIP, "finalize_t2s sync");
+}
+
+// ------------------------------------------------------------ capacity
+int gsv_engine::reserve(int batch, int tokens) {
+    if (batch <= max_batch && tokens <= tmax) return 0;
+    if (batch > 64) return set_error(GSV_E_CAPACITY, "batch > 64 not supported");
+    if (tokens > pe_max - 1) return set_error(GSV_E_CAPACITY, "tokens exceed PE table");
+    // graphs capture buffer addresses: drop them before reallocating
+    for (auto& kv : graphs) hipGraphExecDestroy(kv.second);
+    graphs.clear();
+    const int nb = std::max(batch, max_batch), nt = std::max(tokens, tmax);
+    for (void* p : state_allocs) hipFree(p);
+    state_allocs.clear();
+    auto A = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
+        state_allocs.push_back(p);
+        return p;
+    };
+    const size_t kv_layer = (size_t)nb * 16 * nt * 32;
+    for (int l = 0; l < 24; ++l) {
+        kcache[l] = (float*)A(kv_layer * 4);
+        vcache[l] = (float*)A(kv_layer * 4);
+        if (!kcache[l] || !vcache[l]) return set_error(GSV_E_HIP, "KV cache allocation failed");
+    }
+    y = (int64_t*)A((size_t)nb * nt * 8);
+    ny = (int*)A(nb * 4);
+    kvlen = (int*)A(nb * 4);
+    steps = (int*)A(nb * 4);
+    done = (uint8_t*)A(nb);
+    stopf = (uint8_t*)A(nb);
+    seen = (uint32_t*)A((size_t)nb * 33 * 4);
+    h = (float*)A((size_t)nb * 512 * 4);
+    h1 = (float*)A((size_t)nb * 512 * 4);
+    s1 = (float*)A((size_t)nb * 512 * 4);
+    s2 = (float*)A((size_t)nb * 512 * 4);
+    q = (float*)A((size_t)nb * 512 * 4);
+    o = (float*)A((size_t)nb * 512 * 4);
+    f = (float*)A((size_t)nb * 2048 * 4);
+    logits = (float*)A((size_t)nb * 1025 * 4);
+    ident = (int*)A(nb * 4);
+    pH = (float*)A((size_t)nt * 512 * 4);
+    pQ = (float*)A((size_t)nt * 512 * 4);
+    pO = (float*)A((size_t)nt * 512 * 4);
+    pS = (float*)A((size_t)nt * 512 * 4);
+    pH1 = (float*)A((size_t)nt * 512 * 4);
+    pF = (float*)A((size_t)nt * 2048 * 4);
+    prow_len = (int*)A((size_t)nt * 4);
+    prompts_buf = (int64_t*)A((size_t)nt * 8);
+    if (!pF || !prompts_buf) return set_error(GSV_E_HIP, "state allocation failed");
+    std::vector<int> id(nb);
+    for (int i = 0; i < nb; ++i) id[i] = i;
+    hipMemcpy(ident, id.data(), nb * 4, hipMemcpyHostToDevice);
+    hipMemset(done, 1, nb);
+    max_batch = nb;
+    tmax = nt;
+    return 0;
+}
+
+// ------------------------------------------------------------ encoder
+static __global__ void k_fill_row_len(int* rl, int L, int N0) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < N0) rl[r] = r < L ? L : r + 1;
+}
+
+int gsv_engine::ensure_enc_ws(int P, int L) {
+    if (P <= enc_cap_p && L <= enc_cap_l) return 0;
+    const int cp = std::max(P, enc_cap_p), cl = std::max(L, enc_cap_l);
+    e_im2col = (float*)dalloc((size_t)cp * 1536 * 4);
+    e_h = (float*)dalloc((size_t)cp * 768 * 4);
+    e_hh = (float*)dalloc((size_t)cp * 4);
+    e_dist = (float*)dalloc((size_t)cp * 1024 * 4);
+    e_bproj = (float*)dalloc((size_t)cl * 512 * 4);
+    e_bert = (float*)dalloc((size_t)cl * 1024 * 4);
+    if (!e_bert) return set_error(GSV_E_HIP, "encoder workspace");
+    enc_cap_p = cp;
+    enc_cap_l = cl;
+    return 0;
+}
+
+int gsv_engine::encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st) {
+    const int L = u->n_ref + u->n_text, P = u->n_ssl / 2;
+    if (L <= 0 || P <= 0) return set_error(GSV_E_ARG, "empty utterance");
+    if (int e = ensure_enc_ws(P, L)) return e;
+    // K2: ssl_proj Conv1d(768,768,k2,s2) as GEMM over im2col, then VQ argmin (#2-48)
+    ssl_im2col(u->ssl, u->n_ssl, e_im2col, st);
+    GemmArgs g{};
+    g.M = P; g.N = 768; g.K = 1536;
+    g.A = e_im2col; g.lda = 1536;
+    g.W = ssl_w; g.ldw = 1536; g.w_f16 = 0;
+    g.bias = ssl_b; g.C = e_h; g.ldc = 768; g.mode = EPI_STORE;
+    gemm_nt(g, st);
+    sumsq_rows(e_h, 768, P, 768, e_hh, st);
+    GemmArgs d{};
+    d.M = P; d.N = 1024; d.K = 768;
+    d.A = e_h; d.lda = 768; d.W = codebook; d.ldw = 768; d.w_f16 = 0;
+    d.C = e_dist; d.ldc = 1024; d.mode = EPI_VQDIST; d.rowsq = e_hh; d.colsq = cb_sumsq;
+    gemm_nt(d, st);
+    argmin_dist_rows(e_dist, P, 1024, prompts, st);
+    // K1: text embedding + bert projection + PE (#49-83)
+    const float* bproj = nullptr;
+    if (u->ref_bert || u->text_bert) {
+        if (u->ref_bert)
+            hipMemcpyAsync(e_bert, u->ref_bert, (size_t)u->n_ref * 1024 * 4, hipMemcpyDeviceToDevice, st);
+        else
+            hipMemsetAsync(e_bert, 0, (size_t)u->n_ref * 1024 * 4, st);
+        if (u->text_bert)
+            hipMemcpyAsync(e_bert + (size_t)u->n_ref * 1024, u->text_bert, (size_t)u->n_text * 1024 * 4,
+                           hipMemcpyDeviceToDevice, st);
+        else
+            hipMemsetAsync(e_bert + (size_t)u->n_ref * 1024, 0, (size_t)u->n_text * 1024 * 4, st);
+        GemmArgs b{};
+        b.M = L; b.N = 512; b.K = 1024;
+        b.A = e_bert; b.lda = 1024; b.W = bert_w; b.ldw = 1024; b.w_f16 = 0;
+        b.C = e_bproj; b.ldc = 512; b.mode = EPI_STORE;
+        gemm_nt(b, st);
+        bproj = e_bproj;
+    }
+    text_embed(u->ref_seq, u->n_ref, u->text_seq, u->n_text, text_emb, bproj, bert_b, alpha_text,
+               pe_tab, x, st);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "encode launch");
+}
+
+// ------------------------------------------------------------ prefill
+int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, int P,
+                             const gsv_sampler* sp, float* logits_out, hipStream_t st) {
+    const int N0 = L + P;
+    if (N0 + 1 > tmax) return set_error(GSV_E_CAPACITY, "prefill exceeds reserved tokens");
+    if (x != pH) hipMemcpyAsync(pH, x, (size_t)L * 512 * 4, hipMemcpyDeviceToDevice, st);
+    seq_state_init(b, pr, P, L, y, tmax, ny, kvlen, steps, done, seen, st);
+    audio_embed_prompts(pr, P, emb_audio, alpha_audio, pe_tab, pH + (size_t)L * 512, st);
+    hipLaunchKernelGGL(k_fill_row_len, dim3((N0 + 255) / 256), dim3(256), 0, st, prow_len, L, N0);
+    const long sstride = (long)16 * tmax * 32;
+    for (int l = 0; l < 24; ++l) {
+        const T2SLayerW& W = layers[l];
+        GemmArgs g{};
+        g.M = N0; g.N = 1536; g.K = 512; g.A = pH; g.lda = 512;
+        g.W = W.w_in; g.ldw = 512; g.w_f16 = 1; g.bias = W.b_in;
+        g.C = pQ; g.ldc = 512; g.mode = EPI_QKV;
+        g.kv.k = kcache[l] + b * sstride; g.kv.v = vcache[l] + b * sstride;
+        g.kv.tmax = tmax; g.kv.pos0 = 0; g.kv.seq_stride = sstride;
+        gemm_nt(g, st);
+        AttnArgs at{};
+        at.q = pQ; at.ldq = 512; at.k = kcache[l] + b * sstride; at.v = vcache[l] + b * sstride;
+        at.seq_stride = sstride; at.tmax = tmax; at.row_len = prow_len; at.out = pO; at.ldo = 512;
+        at.rows = N0; at.scale = qk_scale;
+        attn_rows(at, st);
+        GemmArgs go{};
+        go.M = N0; go.N = 512; go.K = 512; go.A = pO; go.lda = 512;
+        go.W = W.w_out; go.ldw = 512; go.w_f16 = 1; go.bias = W.b_out;
+        go.C = pS; go.ldc = 512; go.mode = EPI_RESID; go.res = pH; go.ldr = 512;
+        gemm_nt(go, st);
+        layernorm_rows(pS, pH1, N0, W.n1w, W.n1b, st);
+        GemmArgs g1{};
+        g1.M = N0; g1.N = 2048; g1.K = 512; g1.A = pH1; g1.lda = 512;
+        g1.W = W.w1; g1.ldw = 512; g1.w_f16 = 1; g1.bias = W.b1;
+        g1.C = pF; g1.ldc = 2048; g1.mode = EPI_RELU;
+        gemm_nt(g1, st);
+        GemmArgs g2{};
+        g2.M = N0; g2.N = 512; g2.K = 2048; g2.A = pF; g2.lda = 2048;
+        g2.W = W.w2; g2.ldw = 2048; g2.w_f16 = 1; g2.bias = W.b2;
+        g2.C = pS; g2.ldc = 512; g2.mode = EPI_RESID; g2.res = pH1; g2.ldr = 512;
+        gemm_nt(g2, st);
+        layernorm_rows(pS, pH, N0, W.n2w, W.n2b, st);
+    }
+    // logits of the last row (#1785-1788), first-stage sampler on prompts (#1789-1815)
+    GemvArgs lg{};
+    lg.B = 1; lg.N = 1025; lg.K = 512; lg.src = pH + (size_t)(N0 - 1) * 512; lg.lds = 512;
+    lg.W = w_pred; lg.C = logits + (size_t)b * 1025; lg.ldc = 1025; lg.mode = EPI_STORE;
+    gemv_f16(lg, st);
+    SampleArgs sa = sampler_args(sp, 1);
+    sa.logits = logits + (size_t)b * 1025;
+    sa.y = y + (size_t)b * tmax; sa.ny = ny + b; sa.seen = seen + (size_t)b * 33;
+    sa.done = done + b; sa.stop_out = nullptr; sa.steps = steps + b; sa.kvlen = kvlen + b;
+    sa.prefill = 1; sa.logits_out = logits_out; sa.ldlo = 1025;
+    sample_tokens(sa, st);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "prefill launch");
+}
+
+SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
+    SampleArgs sa{};
+    sa.B = B;
+    sa.logits = logits; sa.ldl = 1025;
+    sa.y = y; sa.ldy = tmax; sa.ny = ny; sa.seen = seen;
+    sa.done = done; sa.stop_out = stopf; sa.steps = steps; sa.kvlen = kvlen;
+    sa.top_k = sp ? sp->top_k : 15;
+    sa.temperature = sp ? sp->temperature : 1.0f;
+    sa.rep_penalty = sp ? sp->repetition_penalty : 1.35f;
+    sa.greedy = sp ? sp->greedy : 1;
+    sa.seed = sp ? sp->seed : 0;
+    sa.max_steps = sp ? sp->max_steps : 500;
+    sa.force_steps = sp ? sp->force_steps : 0;
+    sa.prefill = 0;
+    return sa;
+}
+
+// ------------------------------------------------------------ decode step
+void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st) {
+    const long sstride = (long)16 * tmax * 32;
+    decode_embed(B, y, tmax, ny, emb_audio, alpha_audio, pe_tab, h, done, st);
+    for (int l = 0; l < 24; ++l) {
+        const T2SLayerW& W = layers[l];
+        GemvArgs a{};
+        a.B = B; a.N = 1536; a.K = 512;
+        if (l == 0) { a.src = h; a.lds = 512; }
+        else { a.src = s2; a.lds = 512; a.ln_g = layers[l - 1].n2w; a.ln_b = layers[l - 1].n2b; a.ln_out = h; }
+        a.W = W.w_in; a.bias = W.b_in; a.C = q; a.ldc = 512; a.mode = EPI_QKV;
+        a.kv.k = kcache[l]; a.kv.v = vcache[l]; a.kv.tmax = tmax; a.kv.row_pos = kvlen;
+        a.kv.seq_stride = sstride; a.kv.row_skip = done;
+        gemv_f16(a, st);
+        AttnArgs at{};
+        at.q = q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l]; at.seq_stride = sstride;
+        at.tmax = tmax; at.row_len = kvlen; at.row_seq = ident; at.out = o; at.ldo = 512;
+        at.rows = B; at.scale = qk_scale; at.row_skip = done;
+        attn_rows_plus(at, 1, st);
+        GemvArgs c{};
+        c.B = B; c.N = 512; c.K = 512; c.src = o; c.lds = 512;
+        c.W = W.w_out; c.bias = W.b_out; c.C = s1; c.ldc = 512; c.mode = EPI_RESID;
+        c.res = h; c.ldr = 512;
+        gemv_f16(c, st);
+        GemvArgs f1{};
+        f1.B = B; f1.N = 2048; f1.K = 512; f1.src = s1; f1.lds = 512;
+        f1.ln_g = W.n1w; f1.ln_b = W.n1b; f1.ln_out = h1;
+        f1.W = W.w1; f1.bias = W.b1; f1.C = f; f1.ldc = 2048; f1.mode = EPI_RELU;
+        gemv_f16(f1, st);
+        GemvArgs f2{};
+        f2.B = B; f2.N = 512; f2.K = 2048; f2.src = f; f2.lds = 2048;
+        f2.W = W.w2; f2.bias = W.b2; f2.C = s2; f2.ldc = 512; f2.mode = EPI_RESID;
+        f2.res = h1; f2.ldr = 512;
+        gemv_f16(f2, st);
+    }
+    GemvArgs lg{};
+    lg.B = B; lg.N = 1025; lg.K = 512; lg.src = s2; lg.lds = 512;
+    lg.ln_g = layers[23].n2w; lg.ln_b = layers[23].n2b;
+    lg.W = w_pred; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
+    gemv_f16(lg, st);
+    SampleArgs sa = sampler_args(sp, B);
+    sa.logits_out = logits_out; sa.ldlo = 1025;
+    sample_tokens(sa, st);
+}
+
+hipGraphExec_t gsv_engine::step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st) {
+    const std::string key = std::to_string(B) + ":" + std::to_string(chunk) + ":" +
+                            std::to_string(sp->top_k) + ":" + std::to_string(sp->greedy) + ":" +
+                            std::to_string(sp->seed) + ":" + std::to_string(sp->max_steps) + ":" +
+                            std::to_string(sp->force_steps) + ":" +
+                            std::to_string(sp->temperature) + ":" +
+                            std::to_string(sp->repetition_penalty);
+    auto it = graphs.find(key);
+    if (it != graphs.end()) return it->second;
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return nullptr;
+    for (int i = 0; i < chunk; ++i) decode_step(B, sp, nullptr, st);
+    if (hipStreamEndCapture(st, &g) != hipSuccess) return nullptr;
+    hipGraphExec_t ex = nullptr;
+    if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) ex = nullptr;
+    hipGraphDestroy(g);
+    if (ex) graphs[key] = ex;
+    return ex;
+}
+
+int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
+    const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
+    const int chunk = 8;
+    hipGraphExec_t ex = step_graph(B, sp, chunk, st);
+    if (!ex) return set_error(GSV_E_HIP, "decode graph capture failed");
+    std::vector<uint8_t> hd(B);
+    int launched = 0;
+    while (launched < limit) {
+        if (hipGraphLaunch(ex, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
+        launched += chunk;
+        hipMemcpyAsync(hd.data(), done, B, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "decode sync");
+        bool all = true;
+        for (int b = 0; b < B; ++b) all = all && hd[b];
+        if (all) break;
+    }
+    return 0;
+}
+
+// ============================================================ C ABI
+#define ENG_CHECK(e) \
+    if (!(e)) return set_error(GSV_E_ARG, "null engine")
+
+extern "C" int gsv_engine_create(int device, int version, gsv_engine** out) {
+    if (!out) return set_error(GSV_E_ARG, "out is null");
+    if (hipSetDevice(device) != hipSuccess) return set_error(GSV_E_HIP, "hipSetDevice failed");
+    auto* e = new gsv_engine();
+    e->device = device;
+    e->version = version;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return set_error(GSV_E_HIP, "stream create failed");
+    }
+    e->own_stream = true;
+    for (auto& x : e->ev) hipEventCreate(&x);
+    *out = e;
+    return 0;
+}
+
+extern "C" int gsv_engine_destroy(gsv_engine* eng) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    hipDeviceSynchronize();
+    delete eng;
+    return 0;
+}
+
+extern "C" int gsv_set_weight(gsv_engine* eng, const char* name, const void* host, int dtype,
+                              const int64_t* dims, int ndim) {
+    ENG_CHECK(eng);
+    if (!name || !host || ndim < 0 || (ndim > 0 && !dims)) return set_error(GSV_E_ARG, "bad weight args");
+    Staged s;
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) { s.dims.push_back(dims[i]); n *= (size_t)dims[i]; }
+    s.data.resize(n);
+    if (dtype == GSV_F32) {
+        std::memcpy(s.data.data(), host, n * 4);
+    } else if (dtype == GSV_F16) {
+        const __half* hp = (const __half*)host;
+        for (size_t i = 0; i < n; ++i) s.data[i] = __half2float(hp[i]);
+    } else {
+        return set_error(GSV_E_ARG, "unknown dtype");
+    }
+    eng->staged[name] = std::move(s);
+    return 0;
+}
+
+extern "C" int gsv_finalize_weights(gsv_engine* eng) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (eng->finalized) return set_error(GSV_E_STATE, "already finalized");
+    if (int e = eng->finalize_t2s()) return e;
+    if (eng->find("vq_model.dec.conv_pre.weight")) {
+        if (int e = eng->finalize_vits()) return e;
+    }
+    if (eng->find("sv_emb.weight")) {
+        if (int e = eng->finalize_prompt_encoder()) return e;
+    }
+    eng->staged.clear();
+    eng->finalized = true;
+    return 0;
+}
+
+extern "C" int gsv_reserve(gsv_engine* eng, int max_batch, int max_tokens) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    return eng->reserve(max_batch, max_tokens);
+}
+
+static hipStream_t pick(gsv_engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
+
+extern "C" int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64_t* prompts,
+                              void* stream) {
+    ENG_CHECK(eng);
+    if (!u || !x || !prompts) return set_error(GSV_E_ARG, "null arg");
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    hipSetDevice(eng->device);
+    return eng->encode(u, x, prompts, pick(eng, stream));
+}
+
+extern "C" int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t n_x,
+                               const int64_t* prompts, int32_t n_prompts, const gsv_sampler* s,
+                               int64_t* yout, float* logits_out, void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    if (seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_CAPACITY, "slot out of range");
+    hipStream_t st = pick(eng, stream);
+    if (int e = eng->prefill_slot(seq, x, n_x, prompts, n_prompts, s, logits_out, st)) return e;
+    if (yout)
+        hipMemcpyAsync(yout, eng->y + (size_t)seq * eng->tmax, (size_t)(n_prompts + 1) * 8,
+                       hipMemcpyDeviceToDevice, st);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "prefill");
+}
+
+// Steps on slot `seq` only: temporarily view the batch as that single slot.
+extern "C" int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int nsteps, const gsv_sampler* s,
+                                    int64_t* yout, uint8_t* stop, float* logits_out, void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (seq != 0) return set_error(GSV_E_ARG, "decode_steps supports slot 0");
+    hipStream_t st = pick(eng, stream);
+    gsv_sampler sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
+    sp.force_steps = 1 << 30;   // session semantics: the caller owns the stop decision
+    hipMemsetAsync(eng->done, 0, 1, st);
+    for (int i = 0; i < nsteps; ++i) {
+        eng->decode_step(1, &sp, logits_out ? logits_out + (size_t)i * 1025 : nullptr, st);
+        if (stop) hipMemcpyAsync(stop + i, eng->stopf, 1, hipMemcpyDeviceToDevice, st);
+    }
+    if (yout) {
+        int n = 0;
+        hipMemcpyAsync(&n, eng->ny, 4, hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        hipMemcpyAsync(yout, eng->y, (size_t)n * 8, hipMemcpyDeviceToDevice, st);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "decode_steps");
+}
+
+extern "C" int gsv_t2s_read_kv(gsv_engine* eng, int seq, int layer, float* k, float* v, int32_t* n,
+                               void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (layer < 0 || layer >= 24 || seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_ARG, "range");
+    hipStream_t st = pick(eng, stream);
+    int len = 0;
+    hipMemcpyAsync(&len, eng->kvlen + seq, 4, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    if (n) *n = len;
+    const long sstride = (long)16 * eng->tmax * 32;
+    for (int hh = 0; hh < 16; ++hh) {
+        const float* ks = eng->kcache[layer] + seq * sstride + (long)hh * eng->tmax * 32;
+        const float* vs = eng->vcache[layer] + seq * sstride + (long)hh * eng->tmax * 32;
+        hipMemcpy2DAsync(k + hh * 32, 512 * 4, ks, 32 * 4, 32 * 4, len, hipMemcpyDeviceToDevice, st);
+        hipMemcpy2DAsync(v + hh * 32, 512 * 4, vs, 32 * 4, 32 * 4, len, hipMemcpyDeviceToDevice, st);
+    }
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : set_error(GSV_E_HIP, "read_kv");
+}
+
+extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
+                                const gsv_sampler* s, int64_t* out_tokens, int32_t out_stride,
+                                int32_t* out_len, void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    if (batch <= 0 || !utts || !out_tokens || !out_len) return set_error(GSV_E_ARG, "bad args");
+    gsv_sampler sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
+    if (sp.max_steps <= 0) sp.max_steps = 500;
+    const int steps_cap = sp.force_steps > 0 ? sp.force_steps : sp.max_steps;
+    int need = 0;
+    for (int b = 0; b < batch; ++b) {
+        const int n0 = utts[b].n_ref + utts[b].n_text + utts[b].n_ssl / 2;
+        need = std::max(need, n0 + steps_cap + 16);
+    }
+    if (int e = eng->reserve(batch, need)) return e;
+    hipStream_t st = pick(eng, stream);
+    if (eng->timing) hipEventRecord(eng->ev[0], st);
+    hipMemsetAsync(eng->done, 1, eng->max_batch, st);
+    for (int b = 0; b < batch; ++b) {
+        const gsv_utt& u = utts[b];
+        const int L = u.n_ref + u.n_text, P = u.n_ssl / 2;
+        if (int e = eng->encode(&u, eng->pH, eng->prompts_buf, st)) return e;
+        if (eng->timing && b == 0) hipEventRecord(eng->ev[1], st);
+        if (int e = eng->prefill_slot(b, eng->pH, L, eng->prompts_buf, P, &sp, nullptr, st)) return e;
+    }
+    if (eng->timing) hipEventRecord(eng->ev[2], st);
+    if (int e = eng->decode_loop(batch, &sp, st)) return e;
+    if (eng->timing) hipEventRecord(eng->ev[3], st);
+    // trim on host (Inference.py:108-109, then :41-44)
+    std::vector<int> hny(batch), hsteps(batch);
+    hipMemcpyAsync(hny.data(), eng->ny, batch * 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(hsteps.data(), eng->steps, batch * 4, hipMemcpyDeviceToHost, st);
+    std::vector<int64_t> hy((size_t)batch * eng->tmax);
+    hipMemcpyAsync(hy.data(), eng->y, hy.size() * 8, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "generate sync");
+    if (eng->timing) {
+        hipEventElapsedTime(&eng->ms[0], eng->ev[0], eng->ev[1]);
+        hipEventElapsedTime(&eng->ms[1], eng->ev[1], eng->ev[2]);
+        hipEventElapsedTime(&eng->ms[2], eng->ev[2], eng->ev[3]);
+    }
+    for (int b = 0; b < batch; ++b) {
+        const int n = hny[b];
+        int64_t* yy = hy.data() + (size_t)b * eng->tmax;
+        yy[n - 1] = 0;
+        const int idx = hsteps[b] - 1;
+        int start = idx > 0 ? n - idx : 0;      // y[:, -idx:] ; idx == 0 -> whole y
+        int cnt = n - start;
+        for (int i = 0; i < cnt; ++i)
+            if (yy[start + i] >= 1024) { cnt = i; break; }
+        if (cnt > out_stride) return set_error(GSV_E_CAPACITY, "out_stride too small");
+        std::memcpy(out_tokens + (size_t)b * out_stride, yy + start, (size_t)cnt * 8);
+        out_len[b] = cnt;
+    }
+    return 0;
+}
+
+extern "C" int gsv_set_timing(gsv_engine* eng, int enabled) {
+    ENG_CHECK(eng);
+    eng->timing = enabled != 0;
+    return 0;
+}
+
+extern "C" int gsv_get_timing(gsv_engine* eng, float* ms4) {
+    ENG_CHECK(eng);
+    for (int i = 0; i < 4; ++i) ms4[i] = eng->ms[i];
+    return 0;
+}

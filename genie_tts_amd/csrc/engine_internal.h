@@ -1,0 +1,100 @@
+// Internal engine state (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/genie_engine.h"
+#include "kernels.h"
+#include "vits.h"
+
+namespace gsv {
+int set_error(int code, const std::string& msg);
+
+struct Staged {
+    std::vector<int64_t> dims;
+    std::vector<float> data;   // host fp32 copy (fp16 inputs upcast exactly)
+};
+
+struct T2SLayerW {
+    __half *w_in = nullptr, *w_out = nullptr, *w1 = nullptr, *w2 = nullptr;
+    float *b_in = nullptr, *b_out = nullptr, *b1 = nullptr, *b2 = nullptr;
+    float *n1w = nullptr, *n1b = nullptr, *n2w = nullptr, *n2b = nullptr;
+};
+}  // namespace gsv
+
+struct gsv_engine {
+    int device = 0, version = GSV_V2;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool finalized = false;
+    std::map<std::string, gsv::Staged> staged;
+    std::vector<void*> allocs;        // weights + workspaces (engine lifetime)
+    std::vector<void*> state_allocs;  // decode capacity (re-sized by reserve)
+
+    // ---- T2S weights
+    __half* emb_audio = nullptr;
+    float* alpha_audio = nullptr;
+    __half* w_pred = nullptr;
+    gsv::T2SLayerW layers[24];
+    float *text_emb = nullptr, *bert_w = nullptr, *bert_b = nullptr, *alpha_text = nullptr;
+    float *ssl_w = nullptr, *ssl_b = nullptr, *codebook = nullptr, *cb_sumsq = nullptr;
+    float* pe_tab = nullptr;
+    int pe_max = 0;
+    float qk_scale = 0.f;
+
+    // ---- decode capacity / state
+    int max_batch = 0, tmax = 0;
+    float *kcache[24] = {}, *vcache[24] = {};
+    int64_t* y = nullptr;
+    int *ny = nullptr, *kvlen = nullptr, *steps = nullptr, *ident = nullptr;
+    uint8_t *done = nullptr, *stopf = nullptr;
+    uint32_t* seen = nullptr;
+    float *h = nullptr, *h1 = nullptr, *s1 = nullptr, *s2 = nullptr, *q = nullptr, *o = nullptr;
+    float *f = nullptr, *logits = nullptr;
+    float *pH = nullptr, *pQ = nullptr, *pO = nullptr, *pS = nullptr, *pH1 = nullptr, *pF = nullptr;
+    int* prow_len = nullptr;
+    int64_t* prompts_buf = nullptr;
+
+    // ---- encoder workspace
+    int enc_cap_p = 0, enc_cap_l = 0;
+    float *e_im2col = nullptr, *e_h = nullptr, *e_hh = nullptr, *e_dist = nullptr;
+    float *e_bproj = nullptr, *e_bert = nullptr;
+
+    // ---- VITS
+    gsv::VitsWeights vits;
+    gsv::VitsWorkspace vws;
+    gsv::PromptEncWeights penc;
+
+    std::map<std::string, hipGraphExec_t> graphs;
+    bool timing = false;
+    float ms[4] = {0, 0, 0, 0};
+    hipEvent_t ev[6] = {};
+
+    ~gsv_engine();
+    void* dalloc(size_t bytes);
+    void release_all();
+    const gsv::Staged* find(const std::string& n) const;
+    float* up_f32(const std::string& n, int* err);
+    __half* up_f16(const std::string& n, int* err);
+    int finalize_t2s();
+    int finalize_vits();
+    int finalize_prompt_encoder();
+    int reserve(int batch, int tokens);
+    int ensure_enc_ws(int P, int L);
+    int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st);
+    int prefill_slot(int b, const float* x, int L, const int64_t* pr, int P, const gsv_sampler* sp,
+                     float* logits_out, hipStream_t st);
+    gsv::SampleArgs sampler_args(const gsv_sampler* sp, int B);
+    void decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st);
+    hipGraphExec_t step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st);
+    int decode_loop(int B, const gsv_sampler* sp, hipStream_t st);
+    int vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
+                    const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
+                    const float* eps, float noise_scale, float* audio, hipStream_t st);
+    int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
+                      float* ge_adv, hipStream_t st);
+};

@@ -1,0 +1,123 @@
+// Host-side launchers of the engine's HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsv {
+
+// ------------------------------------------------------------ GEMM (MFMA)
+// C(m,n) = epi( sum_k A(m,k) * W(n,k) + bias[n] )   -- fp32 in, fp32 accumulate
+//   A(m,k) = A[m*lda + k]            (row-major, fp32)
+//   W(n,k) = W[n*ldw + k]            (row-major, fp16 or fp32)
+enum EpiMode {
+    EPI_STORE = 0,       // C[m*ldc+n] = v
+    EPI_RELU = 1,        // C = max(v, 0)
+    EPI_RESID = 2,       // C = res[m*ldr+n] + v          (post-norm residual)
+    EPI_QKV = 3,         // n<512 -> q[m*512+n]; n<1024 -> K cache; else V cache
+    EPI_VQDIST = 4,      // C = (rowsq[m] - v) + colsq[n]   (VQ distance, encoder #30-34)
+};
+
+struct KVScatter {
+    float* k;            // [heads][tmax][32] for the sequence
+    float* v;
+    int tmax;
+    int pos0;            // cache position of row 0
+    const int* row_pos;  // optional per-row positions (batched decode), else pos0 + m
+    long seq_stride;     // elements between sequences' caches (batched decode)
+    const int* row_seq;  // optional per-row sequence index
+    const uint8_t* row_skip; // optional: per-row "done" flags (no cache write)
+};
+
+struct GemmArgs {
+    int M, N, K;
+    const float* A; long lda;
+    const void* W; long ldw; int w_f16;
+    const float* bias;
+    float* C; long ldc;
+    int mode;
+    const float* res; long ldr;
+    const float* rowsq; const float* colsq;
+    KVScatter kv;
+};
+void gemm_nt(const GemmArgs& a, hipStream_t s);
+
+// --------------------------------------------------------- row kernels
+void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,
+                    hipStream_t s);   // D = 512, eps 1e-5
+void sumsq_rows(const float* in, long ld, int rows, int cols, float* out, hipStream_t s);
+void argmin_dist_rows(const float* dist, int rows, int cols, int64_t* out, hipStream_t s);
+
+// ------------------------------------------------------------- T2S misc
+// x[l] = E_text[seq[l]] + (bias + bproj[l]) + alpha*pe[l+1]   (encoder #57-83)
+void text_embed(const int64_t* ref_seq, int n_ref, const int64_t* text_seq, int n_text,
+                const float* emb, const float* bproj /*[L,512] or null*/, const float* bias,
+                const float* alpha, const float* pe, float* x, hipStream_t s);
+// rows [0,P): out[p] = E_audio[tok[p]] + alpha*pe[p+1]; also writes y_emb raw if non-null
+void audio_embed_prompts(const int64_t* tok, int P, const __half* emb, const float* alpha,
+                         const float* pe, float* out, hipStream_t s);
+// im2col for Conv1d(768->768, k2, s2): A[t][ci*2+j] = ssl[ci][2t+j]
+void ssl_im2col(const float* ssl, int n_ssl, float* A, hipStream_t s);
+
+// Attention over a cached prefix, one (head, row) per block.
+//   q: [rows][512] (unscaled), K/V cache [heads][tmax][32] per sequence
+//   len(row) = row < n_full ? n_full : (first_causal + row - n_full + 1) ... given as array
+struct AttnArgs {
+    const float* q; long ldq;
+    const float* k; const float* v;   // cache base of sequence 0
+    long seq_stride;                   // elements between sequences
+    int tmax;
+    const int* row_len;                // keys visible to row r: [0, row_len[r])
+    const int* row_seq;                // sequence of row r (or null: 0)
+    float* out; long ldo;
+    int rows;
+    float scale;                       // sqrt(1/sqrt(32)) applied to q and k separately
+    const uint8_t* row_skip;
+};
+void attn_rows(const AttnArgs& a, hipStream_t s);
+// same, with len(row) = row_len[r] + len_add (decode: kvlen + 1)
+void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s);
+
+// ---------------------------------------------------------- decode GEMV
+// Batched (B <= 8) fp16-weight GEMV with optional LayerNorm prologue:
+//   xin[b] = ln ? LN(src[b]) : src[b];  if ln_out && block 0: ln_out[b] = xin[b]
+//   v = W[n] . xin[b] + bias[n]; epilogue per mode (EPI_STORE/RELU/RESID/QKV)
+struct GemvArgs {
+    int B, N, K;
+    const float* src; long lds;
+    const float* ln_g; const float* ln_b; float* ln_out;
+    const __half* W;
+    const float* bias;
+    float* C; long ldc;
+    int mode;
+    const float* res; long ldr;
+    KVScatter kv;
+};
+void gemv_f16(const GemvArgs& a, hipStream_t s);
+
+// Decode embedding: for active b: tok = y[b][ny[b]-1]; h[b] = E[tok] + alpha*pe[ny[b]]
+void decode_embed(int B, const int64_t* y, long ldy, const int* ny, const __half* emb,
+                  const float* alpha, const float* pe, float* h, const uint8_t* done,
+                  hipStream_t s);
+
+struct SampleArgs {
+    int B;
+    const float* logits; long ldl;     // [B][1025]
+    int64_t* y; long ldy; int* ny;     // history, appended on success
+    uint32_t* seen;                    // [B][33] presence bitmap (y tokens)
+    uint8_t* done; uint8_t* stop_out;  // stop flags out (per b) ; done updated
+    int* steps;                        // per-b executed loop steps
+    int* kvlen;                        // per-b KV length, +1 per executed step
+    int top_k; float temperature; float rep_penalty;
+    int greedy; uint64_t seed;
+    int max_steps; int force_steps;
+    int prefill;                       // 1: first-stage sampler (no stop, no step count)
+    float* logits_out; long ldlo;      // optional copy of raw logits
+};
+void sample_tokens(const SampleArgs& a, hipStream_t s);
+
+// Decode-state init of slot b after the encoder: y[0..P) = prompts, ny = P,
+// kvlen = L + P, steps = 0, done = 0, seen = bits(prompts).
+void seq_state_init(int b, const int64_t* prompts, int P, int L, int64_t* y, long ldy, int* ny,
+                    int* kvlen, int* steps, uint8_t* done, uint32_t* seen, hipStream_t s);
+
+}  // namespace gsv

@@ -1,0 +1,636 @@
+// T2S kernels for gfx950: f32-MFMA GEMM (prefill / encoder), batched fp16-weight
+// GEMV with fused LayerNorm prologue (decode), prefix attention, sampler.
+//
+// Numerics follow the reference graphs (fp32 activations, fp16-valued weights
+// upcast exactly as g/ModelManager.py:75-76): t2s_first_stage_decoder_fp32.onnx
+// and t2s_stage_decoder_fp32.onnx (node indices cited per kernel).
+#include "common.h"
+#include "kernels.h"
+
+namespace gsv {
+
+// =====================================================================
+// GEMM NT:  C(m,n) = sum_k A(m,k) W(n,k)  via v_mfma_f32_32x32x2_f32
+// (exact f32 FMA chain, 157 TF/s peak).  Block tile 64x64, 4 waves of 32x32,
+// K-step 32 staged through padded LDS (stride 33 -> conflict-free b32 reads).
+// =====================================================================
+template <bool F16W>
+__global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs a) {
+    __shared__ float As[64][33];
+    __shared__ float Ws[64][33];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const int sr = tid >> 2, sc = (tid & 3) * 8;
+    const int gm = m0 + sr, gn = n0 + sr;
+    for (int k0 = 0; k0 < a.K; k0 += 32) {
+        float av[8], wv[8];
+        if (gm < a.M) {
+            const float4* p = reinterpret_cast<const float4*>(a.A + (long)gm * a.lda + k0 + sc);
+            float4 x0 = p[0], x1 = p[1];
+            av[0] = x0.x; av[1] = x0.y; av[2] = x0.z; av[3] = x0.w;
+            av[4] = x1.x; av[5] = x1.y; av[6] = x1.z; av[7] = x1.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) av[i] = 0.f;
+        }
+        if (gn < a.N) {
+            if (F16W) {
+                const __half* wp = reinterpret_cast<const __half*>(a.W) + (long)gn * a.ldw + k0 + sc;
+                h8_to_f8(*reinterpret_cast<const uint4*>(wp), wv);
+            } else {
+                const float4* p = reinterpret_cast<const float4*>(
+                    reinterpret_cast<const float*>(a.W) + (long)gn * a.ldw + k0 + sc);
+                float4 x0 = p[0], x1 = p[1];
+                wv[0] = x0.x; wv[1] = x0.y; wv[2] = x0.z; wv[3] = x0.w;
+                wv[4] = x1.x; wv[5] = x1.y; wv[6] = x1.z; wv[7] = x1.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wv[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            As[sr][sc + i] = av[i];
+            Ws[sr][sc + i] = wv[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const float x = As[wm * 32 + (lane & 31)][2 * kk + (lane >> 5)];
+            const float y = Ws[wn * 32 + (lane & 31)][2 * kk + (lane >> 5)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    const int col = n0 + wn * 32 + (lane & 31);
+    if (col >= a.N) return;
+    const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= a.M) continue;
+        const float v = a.bias ? bv + acc[r] : acc[r];   // Add(bias, MatMul)
+        switch (a.mode) {
+            case EPI_STORE: a.C[(long)row * a.ldc + col] = v; break;
+            case EPI_RELU: a.C[(long)row * a.ldc + col] = fmaxf(v, 0.f); break;
+            case EPI_RESID: a.C[(long)row * a.ldc + col] = a.res[(long)row * a.ldr + col] + v; break;
+            case EPI_VQDIST:   // (sum h^2) - (2h).c + (sum c^2); x2 is exact so (2h).c == 2(h.c)
+                a.C[(long)row * a.ldc + col] = (a.rowsq[row] - 2.0f * acc[r]) + a.colsq[col];
+                break;
+            case EPI_QKV: {
+                if (col < 512) {
+                    a.C[(long)row * a.ldc + col] = v;
+                } else {
+                    if (a.kv.row_skip && a.kv.row_skip[a.kv.row_seq ? a.kv.row_seq[row] : 0]) break;
+                    const int seq = a.kv.row_seq ? a.kv.row_seq[row] : 0;
+                    const int pos = a.kv.row_pos ? a.kv.row_pos[row] : a.kv.pos0 + row;
+                    const int c = (col - 512) & 511;
+                    float* dst = (col < 1024 ? a.kv.k : a.kv.v) + (long)seq * a.kv.seq_stride;
+                    dst[((long)(c >> 5) * a.kv.tmax + pos) * 32 + (c & 31)] = v;
+                }
+            } break;
+        }
+    }
+}
+
+void gemm_nt(const GemmArgs& a, hipStream_t s) {
+    dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
+    if (a.w_f16)
+        hipLaunchKernelGGL(k_gemm_nt<true>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_gemm_nt<false>, grid, dim3(256), 0, s, a);
+}
+
+// =====================================================================
+// Row kernels
+// =====================================================================
+// LayerNormalization(axis -1, eps 1e-5) over D=512 (stage#105,#114), one row per block.
+__global__ __launch_bounds__(256) void k_layernorm512(const float* in, float* out, const float* g,
+                                                      const float* b) {
+    __shared__ float red[16];
+    const long r = blockIdx.x;
+    const int t = threadIdx.x;
+    const float v0 = in[r * 512 + t], v1 = in[r * 512 + t + 256];
+    const float mean = block_sum(v0 + v1, red) * (1.0f / 512.0f);
+    const float d0 = v0 - mean, d1 = v1 - mean;
+    const float var = block_sum(d0 * d0 + d1 * d1, red) * (1.0f / 512.0f);
+    const float den = sqrtf(var + 1e-5f);
+    out[r * 512 + t] = d0 / den * g[t] + b[t];
+    out[r * 512 + t + 256] = d1 / den * g[t + 256] + b[t + 256];
+}
+
+void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,
+                    hipStream_t s) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_layernorm512, dim3(rows), dim3(256), 0, s, in, out, g, b);
+}
+
+// out[r] = sum_c in[r*ld+c]^2  (encoder #25-26 / #32-33)
+__global__ __launch_bounds__(256) void k_sumsq(const float* in, long ld, int cols, float* out) {
+    __shared__ float red[16];
+    const long r = blockIdx.x;
+    float acc = 0.f;
+    for (int c = threadIdx.x; c < cols; c += 256) {
+        const float v = in[r * ld + c];
+        acc += v * v;
+    }
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) out[r] = acc;
+}
+
+void sumsq_rows(const float* in, long ld, int rows, int cols, float* out, hipStream_t s) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_sumsq, dim3(rows), dim3(256), 0, s, in, ld, cols, out);
+}
+
+// prompts[r] = argmax_c(-dist[r][c]) with first-index ties (encoder #35-36)
+__global__ __launch_bounds__(256) void k_argmin_rows(const float* dist, int cols, int64_t* out) {
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    const long r = blockIdx.x;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = threadIdx.x; c < cols; c += 256) {
+        const float v = -dist[r * cols + c];
+        if (v > best || (v == best && c < bi)) { best = v; bi = c; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sv[w] = best; si[w] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 4; ++i)
+            if (sv[i] > best || (sv[i] == best && si[i] < bi)) { best = sv[i]; bi = si[i]; }
+        out[r] = bi;
+    }
+}
+
+void argmin_dist_rows(const float* dist, int rows, int cols, int64_t* out, hipStream_t s) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_argmin_rows, dim3(rows), dim3(256), 0, s, dist, cols, out);
+}
+
+// =====================================================================
+// Embeddings + sinusoidal PE
+// =====================================================================
+__global__ __launch_bounds__(256) void k_text_embed(const int64_t* ref_seq, int n_ref,
+                                                    const int64_t* text_seq, const float* emb,
+                                                    const float* bproj, const float* bias,
+                                                    const float* alpha, const float* pe,
+                                                    float* x) {
+    const int l = blockIdx.x;
+    const int64_t tok = l < n_ref ? ref_seq[l] : text_seq[l - n_ref];
+    const float al = alpha[0];
+    for (int d = threadIdx.x; d < 512; d += 256) {
+        const float bp = bproj ? bias[d] + bproj[(long)l * 512 + d] : bias[d];
+        const float e = emb[tok * 512 + d] + bp;
+        x[(long)l * 512 + d] = e * 1.0f + al * pe[(long)(l + 1) * 512 + d];
+    }
+}
+
+void text_embed(const int64_t* ref_seq, int n_ref, const int64_t* text_seq, int n_text,
+                const float* emb, const float* bproj, const float* bias, const float* alpha,
+                const float* pe, float* x, hipStream_t s) {
+    const int L = n_ref + n_text;
+    if (L <= 0) return;
+    hipLaunchKernelGGL(k_text_embed, dim3(L), dim3(256), 0, s, ref_seq, n_ref, text_seq, emb,
+                       bproj, bias, alpha, pe, x);
+}
+
+__global__ __launch_bounds__(256) void k_audio_embed(const int64_t* tok, const __half* emb,
+                                                     const float* alpha, const float* pe,
+                                                     float* out) {
+    const int p = blockIdx.x;
+    const int64_t t = tok[p];
+    const float al = alpha[0];
+    for (int d = threadIdx.x; d < 512; d += 256)
+        out[(long)p * 512 + d] = __half2float(emb[t * 512 + d]) + al * pe[(long)(p + 1) * 512 + d];
+}
+
+void audio_embed_prompts(const int64_t* tok, int P, const __half* emb, const float* alpha,
+                         const float* pe, float* out, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_audio_embed, dim3(P), dim3(256), 0, s, tok, emb, alpha, pe, out);
+}
+
+__global__ __launch_bounds__(256) void k_ssl_im2col(const float* ssl, int n_ssl, float* A) {
+    const int t = blockIdx.x;
+    for (int i = threadIdx.x; i < 1536; i += 256) {
+        const int ci = i >> 1, j = i & 1;
+        A[(long)t * 1536 + i] = ssl[(long)ci * n_ssl + 2 * t + j];
+    }
+}
+
+void ssl_im2col(const float* ssl, int n_ssl, float* A, hipStream_t s) {
+    const int P = n_ssl / 2;
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_ssl_im2col, dim3(P), dim3(256), 0, s, ssl, n_ssl, A);
+}
+
+__global__ __launch_bounds__(256) void k_decode_embed(const int64_t* y, long ldy, const int* ny,
+                                                      const __half* emb, const float* alpha,
+                                                      const float* pe, float* h,
+                                                      const uint8_t* done) {
+    const int b = blockIdx.x;
+    if (done && done[b]) return;
+    const int n = ny[b];
+    const int64_t tok = y[(long)b * ldy + n - 1];
+    const float al = alpha[0];
+    for (int d = threadIdx.x; d < 512; d += 256)
+        h[(long)b * 512 + d] = __half2float(emb[tok * 512 + d]) + al * pe[(long)n * 512 + d];
+}
+
+void decode_embed(int B, const int64_t* y, long ldy, const int* ny, const __half* emb,
+                  const float* alpha, const float* pe, float* h, const uint8_t* done,
+                  hipStream_t s) {
+    hipLaunchKernelGGL(k_decode_embed, dim3(B), dim3(256), 0, s, y, ldy, ny, emb, alpha, pe, h,
+                       done);
+}
+
+// =====================================================================
+// Prefix attention: one block per (head, row); keys [0, len).
+// Scores (q*s)(k*s) as stage#91-94; softmax #95; P @ V #96.
+// =====================================================================
+#define ATTN_MAXT 4096
+__global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a, int len_add) {
+    __shared__ float p[ATTN_MAXT];
+    __shared__ float qs[32];
+    __shared__ float red[16];
+    __shared__ float part[8][33];
+    const int h = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+    const int seq = a.row_seq ? a.row_seq[r] : 0;
+    if (a.row_skip && a.row_skip[seq]) return;
+    const int len = a.row_len[r] + len_add;
+    const float* K = a.k + (long)seq * a.seq_stride + (long)h * a.tmax * 32;
+    const float* V = a.v + (long)seq * a.seq_stride + (long)h * a.tmax * 32;
+    const float sc = a.scale;
+    if (tid < 32) qs[tid] = a.q[(long)r * a.ldq + h * 32 + tid] * sc;
+    __syncthreads();
+    float lmax = -INFINITY;
+    for (int t = tid; t < len; t += 256) {
+        const float4* kr = reinterpret_cast<const float4*>(K + (long)t * 32);
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 kv = kr[i];
+            s += qs[4 * i] * (kv.x * sc);
+            s += qs[4 * i + 1] * (kv.y * sc);
+            s += qs[4 * i + 2] * (kv.z * sc);
+            s += qs[4 * i + 3] * (kv.w * sc);
+        }
+        p[t] = s;
+        lmax = fmaxf(lmax, s);
+    }
+    const float m = block_max(lmax, red);
+    float lsum = 0.f;
+    for (int t = tid; t < len; t += 256) {
+        const float e = expf(p[t] - m);
+        p[t] = e;
+        lsum += e;
+    }
+    const float sum = block_sum(lsum, red);
+    for (int t = tid; t < len; t += 256) p[t] = p[t] / sum;
+    __syncthreads();
+    const int g = tid >> 5, d = tid & 31;
+    float acc = 0.f;
+    for (int t = g; t < len; t += 8) acc += p[t] * V[(long)t * 32 + d];
+    part[g][d] = acc;
+    __syncthreads();
+    if (tid < 32) {
+        float o = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o += part[i][tid];
+        a.out[(long)r * a.ldo + h * 32 + tid] = o;
+    }
+}
+
+void attn_rows(const AttnArgs& a, hipStream_t s) {
+    if (a.rows <= 0) return;
+    hipLaunchKernelGGL(k_attn_rows, dim3(16, a.rows), dim3(256), 0, s, a, 0);
+}
+
+void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s) {
+    if (a.rows <= 0) return;
+    hipLaunchKernelGGL(k_attn_rows, dim3(16, a.rows), dim3(256), 0, s, a, len_add);
+}
+
+// =====================================================================
+// Decode GEMV: fp16 weights streamed straight to VGPRs (16 B / lane), fp32
+// activations from LDS, optional LayerNorm prologue (LN fused into consumer).
+// Each wave owns ROWS output rows for all B sequences.
+// =====================================================================
+template <int K, int ROWS, int NB>
+__global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+    extern __shared__ float xs[];   // [NB][K]
+    __shared__ float red[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int B = a.B;
+    if (a.ln_g) {
+        for (int b = 0; b < B; ++b) {
+            const float* src = a.src + (long)b * a.lds;
+            const float v0 = src[tid], v1 = src[tid + 256];
+            const float mean = block_sum(v0 + v1, red) * (1.0f / 512.0f);
+            const float d0 = v0 - mean, d1 = v1 - mean;
+            const float var = block_sum(d0 * d0 + d1 * d1, red) * (1.0f / 512.0f);
+            const float den = sqrtf(var + 1e-5f);
+            const float o0 = d0 / den * a.ln_g[tid] + a.ln_b[tid];
+            const float o1 = d1 / den * a.ln_g[tid + 256] + a.ln_b[tid + 256];
+            xs[b * K + tid] = o0;
+            xs[b * K + tid + 256] = o1;
+            if (a.ln_out && blockIdx.x == 0) {
+                a.ln_out[(long)b * 512 + tid] = o0;
+                a.ln_out[(long)b * 512 + tid + 256] = o1;
+            }
+        }
+    } else {
+        for (int b = 0; b < B; ++b)
+            for (int i = tid * 4; i < K; i += 1024)
+                *reinterpret_cast<float4*>(&xs[b * K + i]) =
+                    *reinterpret_cast<const float4*>(a.src + (long)b * a.lds + i);
+    }
+    __syncthreads();
+    const int nbase = (blockIdx.x * 4 + w) * ROWS;
+    constexpr int KI = K / 512;
+    uint4 wr[ROWS][KI];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        const int n = min(nbase + r, a.N - 1);
+        const __half* wp = a.W + (long)n * K + lane * 8;
+#pragma unroll
+        for (int i = 0; i < KI; ++i) wr[r][i] = *reinterpret_cast<const uint4*>(wp + i * 512);
+    }
+    float acc[ROWS][NB];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[r][b] = 0.f;
+#pragma unroll
+    for (int i = 0; i < KI; ++i) {
+        float wf[ROWS][8];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) h8_to_f8(wr[r][i], wf[r]);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b < B) {
+                const float4 x0 = *reinterpret_cast<const float4*>(&xs[b * K + i * 512 + lane * 8]);
+                const float4 x1 = *reinterpret_cast<const float4*>(&xs[b * K + i * 512 + lane * 8 + 4]);
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) {
+                    float s = acc[r][b];
+                    s += wf[r][0] * x0.x; s += wf[r][1] * x0.y; s += wf[r][2] * x0.z; s += wf[r][3] * x0.w;
+                    s += wf[r][4] * x1.x; s += wf[r][5] * x1.y; s += wf[r][6] * x1.z; s += wf[r][7] * x1.w;
+                    acc[r][b] = s;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        const int n = nbase + r;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b >= B) continue;
+            const float sum = wave_sum(acc[r][b]);
+            if (lane != 0 || n >= a.N) continue;
+            const float v = a.bias ? a.bias[n] + sum : sum;
+            switch (a.mode) {
+                case EPI_STORE: a.C[(long)b * a.ldc + n] = v; break;
+                case EPI_RELU: a.C[(long)b * a.ldc + n] = fmaxf(v, 0.f); break;
+                case EPI_RESID: a.C[(long)b * a.ldc + n] = a.res[(long)b * a.ldr + n] + v; break;
+                case EPI_QKV:
+                    if (n < 512) {
+                        a.C[(long)b * a.ldc + n] = v;
+                    } else {
+                        if (a.kv.row_skip && a.kv.row_skip[b]) break;
+                        const int pos = a.kv.row_pos ? a.kv.row_pos[b] : a.kv.pos0;
+                        const int c = (n - 512) & 511;
+                        float* dst = (n < 1024 ? a.kv.k : a.kv.v) + (long)b * a.kv.seq_stride;
+                        dst[((long)(c >> 5) * a.kv.tmax + pos) * 32 + (c & 31)] = v;
+                    }
+                    break;
+                default: break;
+            }
+        }
+    }
+}
+
+template <int K, int ROWS>
+static void launch_gemv_k(const GemvArgs& a, hipStream_t s) {
+    const int rows_per_block = 4 * ROWS;
+    dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
+    int nb = a.B <= 1 ? 1 : a.B <= 2 ? 2 : a.B <= 4 ? 4 : 8;
+    const size_t shm = (size_t)nb * K * sizeof(float);
+    switch (nb) {
+        case 1: hipLaunchKernelGGL((k_gemv<K, ROWS, 1>), grid, dim3(256), shm, s, a); break;
+        case 2: hipLaunchKernelGGL((k_gemv<K, ROWS, 2>), grid, dim3(256), shm, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gemv<K, ROWS, 4>), grid, dim3(256), shm, s, a); break;
+        default: hipLaunchKernelGGL((k_gemv<K, ROWS, 8>), grid, dim3(256), shm, s, a); break;
+    }
+}
+
+void gemv_f16(const GemvArgs& a, hipStream_t s) {
+    if (a.K == 512) {
+        if (a.N >= 1536) launch_gemv_k<512, 2>(a, s);
+        else launch_gemv_k<512, 1>(a, s);
+    } else {
+        launch_gemv_k<2048, 1>(a, s);
+    }
+}
+
+// =====================================================================
+// Sampler (t2s_stage_decoder_fp32.onnx#1775-1821, first-stage #1789-1820):
+// repetition penalty over the history set, /temperature, top-k threshold
+// (k-th largest by radix select), softmax, argmax(p / q) with q = 1 (greedy)
+// or q ~ N(0,1) (Philox + Box-Muller), stop = argmax(raw)==EOS || tok==EOS.
+// One 1024-thread block per sequence.
+// =====================================================================
+__device__ __forceinline__ uint32_t f2key(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+    const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    return __uint_as_float(u);
+}
+
+__device__ __forceinline__ void argmax_merge(float& v, int& i, float ov, int oi) {
+    if (ov > v || (ov == v && oi < i) || (v != v && ov == ov)) { v = ov; i = oi; }
+}
+
+__device__ void block_argmax(float& v, int& i, float* sv, int* si) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(i, o, 64);
+        argmax_merge(v, i, ov, oi);
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { sv[w] = v; si[w] = i; }
+    __syncthreads();
+    v = sv[0];
+    i = si[0];
+    const int nw = blockDim.x >> 6;
+    for (int k = 1; k < nw; ++k) argmax_merge(v, i, sv[k], si[k]);
+}
+
+#define VOCAB 1025
+__global__ __launch_bounds__(1024) void k_sample(SampleArgs a) {
+    __shared__ float vals[VOCAB];
+    __shared__ uint32_t hist[256];
+    __shared__ float sv[16];
+    __shared__ int si[16];
+    __shared__ uint32_t sel_prefix, sel_remain;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (!a.prefill && a.done[b]) {
+        if (tid == 0 && a.stop_out) a.stop_out[b] = 0;
+        return;
+    }
+    const float* lg = a.logits + (long)b * a.ldl;
+    const uint32_t* seen = a.seen + (long)b * 33;
+    float rv = -INFINITY;
+    int ri = 0x7fffffff;
+    for (int i = tid; i < VOCAB; i += 1024) {
+        const float l = lg[i];
+        if (a.logits_out) a.logits_out[(long)b * a.ldlo + i] = l;
+        argmax_merge(rv, ri, l, i);
+        float pen = l;
+        if ((seen[i >> 5] >> (i & 31)) & 1u) pen = l < 0.f ? l * a.rep_penalty : l / a.rep_penalty;
+        vals[i] = pen / a.temperature;
+    }
+    block_argmax(rv, ri, sv, si);
+    const int raw_arg = ri;
+    // ---- k-th largest (with multiplicity) by MSB-first radix select
+    if (tid == 0) { sel_prefix = 0; sel_remain = (uint32_t)a.top_k; }
+    uint32_t mask = 0;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        const uint32_t prefix = sel_prefix;
+        for (int i = tid; i < VOCAB; i += 1024) {
+            const uint32_t k = f2key(vals[i]);
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // lane l owns bins 255-4l .. 252-4l (descending)
+            uint32_t c[4], s = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { c[j] = hist[255 - 4 * tid - j]; s += c[j]; }
+            uint32_t incl = s;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o, 64);
+                if (tid >= o) incl += t;
+            }
+            const uint32_t excl = incl - s;
+            const uint32_t rem = sel_remain;
+            const bool mine = excl < rem && incl >= rem;
+            if (mine) {
+                uint32_t cum = excl;
+                for (int j = 0; j < 4; ++j) {
+                    if (cum + c[j] >= rem) {
+                        sel_prefix = prefix | ((uint32_t)(255 - 4 * tid - j) << shift);
+                        sel_remain = rem - cum;
+                        break;
+                    }
+                    cum += c[j];
+                }
+            }
+        }
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    const float thr = key2f(sel_prefix);
+    // ---- softmax over kept entries, then argmax(p / q)
+    float lmax = -INFINITY;
+    for (int i = tid; i < VOCAB; i += 1024) {
+        const float v = vals[i] < thr ? -INFINITY : vals[i];
+        vals[i] = v;
+        lmax = fmaxf(lmax, v);
+    }
+    const float m = block_max(lmax, sv);
+    float lsum = 0.f;
+    for (int i = tid; i < VOCAB; i += 1024) {
+        const float e = expf(vals[i] - m);
+        vals[i] = e;
+        lsum += e;
+    }
+    const float sum = block_sum(lsum, sv);
+    const int step = a.prefill ? 0 : a.steps[b] + 1;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < VOCAB; i += 1024) {
+        const float p = vals[i] / sum;
+        float q = 1.0f;
+        if (!a.greedy) {
+            const uint4 r = philox4x32(make_uint4((uint32_t)i, (uint32_t)step, (uint32_t)b, 0x51u),
+                                       make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
+            const float u1 = u01_open(r.x), u2 = u01_open(r.y);
+            q = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+        }
+        argmax_merge(bv, bi, p / q, i);
+    }
+    block_argmax(bv, bi, sv, si);
+    if (tid == 0) {
+        const int tok = bi;
+        const int n = a.ny[b];
+        a.y[(long)b * a.ldy + n] = tok;
+        a.ny[b] = n + 1;
+        a.seen[(long)b * 33 + (tok >> 5)] |= 1u << (tok & 31);
+        if (!a.prefill) {
+            const bool stop = raw_arg == 1024 || tok == 1024;
+            if (a.stop_out) a.stop_out[b] = stop ? 1 : 0;
+            const int st = a.steps[b] + 1;
+            a.steps[b] = st;
+            a.kvlen[b] += 1;
+            bool fin;
+            if (a.force_steps > 0) fin = st >= a.force_steps;
+            else fin = stop || st >= a.max_steps;
+            if (fin) a.done[b] = 1;
+        }
+    }
+}
+
+void sample_tokens(const SampleArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_sample, dim3(a.B), dim3(1024), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void k_seq_init(int b, const int64_t* prompts, int P, int L,
+                                                  int64_t* y, long ldy, int* ny, int* kvlen,
+                                                  int* steps, uint8_t* done, uint32_t* seen) {
+    __shared__ uint32_t bits[33];
+    if (threadIdx.x < 33) bits[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += 256) {
+        const int64_t t = prompts[i];
+        y[(long)b * ldy + i] = t;
+        atomicOr(&bits[t >> 5], 1u << (t & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < 33) seen[(long)b * 33 + threadIdx.x] = bits[threadIdx.x];
+    if (threadIdx.x == 0) {
+        ny[b] = P;
+        kvlen[b] = L + P;
+        steps[b] = 0;
+        done[b] = 0;
+    }
+}
+
+void seq_state_init(int b, const int64_t* prompts, int P, int L, int64_t* y, long ldy, int* ny,
+                    int* kvlen, int* steps, uint8_t* done, uint32_t* seen, hipStream_t s) {
+    hipLaunchKernelGGL(k_seq_init, dim3(1), dim3(256), 0, s, b, prompts, P, L, y, ldy, ny, kvlen,
+                       steps, done, seen);
+}
+
+}  // namespace gsv

@@ -1,0 +1,281 @@
+"""ctypes binding of libgenie_engine.so (C ABI: include/genie_engine.h).
+
+PyTorch is plumbing here: device buffers are torch tensors whose data_ptr()
+is handed to the engine, and calls run on torch's current HIP stream.  There
+is no CPU fallback: if the library is missing or fails to load, every entry
+point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import weights as W
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libgenie_engine.so")
+_lib = None
+
+GSV_F32, GSV_F16 = 0, 1
+GSV_V2, GSV_V2PP = 0, 1
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class Utt(ctypes.Structure):
+    _fields_ = [
+        ("ref_seq", ctypes.c_void_p), ("n_ref", ctypes.c_int32),
+        ("text_seq", ctypes.c_void_p), ("n_text", ctypes.c_int32),
+        ("ref_bert", ctypes.c_void_p), ("text_bert", ctypes.c_void_p),
+        ("ssl", ctypes.c_void_p), ("n_ssl", ctypes.c_int32),
+    ]
+
+
+class Sampler(ctypes.Structure):
+    _fields_ = [
+        ("top_k", ctypes.c_int32), ("temperature", ctypes.c_float),
+        ("repetition_penalty", ctypes.c_float), ("greedy", ctypes.c_int32),
+        ("seed", ctypes.c_uint64), ("max_steps", ctypes.c_int32),
+        ("force_steps", ctypes.c_int32),
+    ]
+
+
+def make_sampler(top_k: int = 15, temperature: float = 1.0, repetition_penalty: float = 1.35,
+                 greedy: bool = True, seed: int = 1234, max_steps: int = 500,
+                 force_steps: int = 0) -> Sampler:
+    """Defaults are the constants baked into the reference graphs
+    (t2s_stage_decoder_fp32.onnx#1780-1790, Inference.py:95)."""
+    return Sampler(top_k, temperature, repetition_penalty, int(greedy), seed, max_steps, force_steps)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise EngineError(f"{_LIB_PATH} missing: build it with `python -m genie_tts_amd.build`")
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i32, i64p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)
+        L.gsv_last_error.restype = ctypes.c_char_p
+        L.gsv_version.restype = ctypes.c_char_p
+        L.gsv_engine_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.gsv_engine_destroy.argtypes = [vp]
+        L.gsv_set_weight.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int, i64p, ctypes.c_int]
+        L.gsv_finalize_weights.argtypes = [vp]
+        L.gsv_reserve.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.gsv_t2s_encode.argtypes = [vp, ctypes.POINTER(Utt), vp, vp, vp]
+        L.gsv_t2s_generate.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Utt), ctypes.POINTER(Sampler),
+                                       vp, i32, vp, vp]
+        L.gsv_t2s_prefill.argtypes = [vp, ctypes.c_int, vp, i32, vp, i32, ctypes.POINTER(Sampler),
+                                      vp, vp, vp]
+        L.gsv_t2s_decode_steps.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Sampler),
+                                           vp, vp, vp, vp]
+        L.gsv_t2s_read_kv.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp,
+                                      ctypes.POINTER(ctypes.c_int32), vp]
+        L.gsv_vits_decode.argtypes = [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, ctypes.c_float, vp, vp]
+        L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.gsv_set_timing.argtypes = [vp, ctypes.c_int]
+        L.gsv_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+        _lib = L
+    return _lib
+
+
+EXPORTED = (
+    "gsv_last_error", "gsv_version", "gsv_engine_create", "gsv_engine_destroy", "gsv_set_weight",
+    "gsv_finalize_weights", "gsv_reserve", "gsv_t2s_encode", "gsv_t2s_generate", "gsv_t2s_prefill",
+    "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
+    "gsv_set_timing", "gsv_get_timing",
+)
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().gsv_last_error().decode(errors="replace")
+        raise EngineError(f"{what} failed ({rc}): {msg}")
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise EngineError("no HIP device visible: the MI355X engine has no CPU fallback")
+    return torch
+
+
+def _stream():
+    return ctypes.c_void_p(_torch().cuda.current_stream().cuda_stream)
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+class Engine:
+    """One engine per GPU process, holding one character's weights."""
+
+    def __init__(self, weights: Dict[str, Dict[str, np.ndarray]], version: str = "v2",
+                 device: int = 0, pe_div_term: Optional[np.ndarray] = None):
+        torch = _torch()
+        self.torch = torch
+        self.device = device
+        self.version = version
+        torch.cuda.set_device(device)
+        h = ctypes.c_void_p()
+        _check(lib().gsv_engine_create(device, GSV_V2 if version == "v2" else GSV_V2PP,
+                                       ctypes.byref(h)), "gsv_engine_create")
+        self.h = h
+        for group in weights.values():
+            for name, arr in group.items():
+                self._set(name, arr)
+        if pe_div_term is not None:
+            self._set("pe.div_term", np.asarray(pe_div_term, np.float32))
+        _check(lib().gsv_finalize_weights(self.h), "gsv_finalize_weights")
+        self.dev = torch.device("cuda", device)
+
+    def _set(self, name: str, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        if a.dtype == np.float16:
+            dt = GSV_F16
+        else:
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            dt = GSV_F32
+        dims = (ctypes.c_int64 * max(1, a.ndim))(*a.shape)
+        _check(lib().gsv_set_weight(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), dt,
+                                    dims, a.ndim), f"gsv_set_weight({name})")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gsv_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- helpers
+    def _dev(self, x, dtype):
+        t = self.torch
+        if x is None:
+            return None
+        if isinstance(x, t.Tensor):
+            return x.to(device=self.dev, dtype=dtype).contiguous()
+        return t.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=self.dev).contiguous()
+
+    def make_utt(self, ref_seq, text_seq, ref_bert, text_bert, ssl):
+        t = self.torch
+        keep = [self._dev(np.asarray(ref_seq).reshape(-1), t.int64),
+                self._dev(np.asarray(text_seq).reshape(-1), t.int64),
+                None if ref_bert is None else self._dev(ref_bert, t.float32),
+                None if text_bert is None else self._dev(text_bert, t.float32),
+                self._dev(np.asarray(ssl).reshape(768, -1), t.float32)]
+        u = Utt(keep[0].data_ptr(), keep[0].numel(), keep[1].data_ptr(), keep[1].numel(),
+                0 if keep[2] is None else keep[2].data_ptr(),
+                0 if keep[3] is None else keep[3].data_ptr(),
+                keep[4].data_ptr(), keep[4].shape[1])
+        return u, keep
+
+    def reserve(self, batch: int, tokens: int):
+        _check(lib().gsv_reserve(self.h, batch, tokens), "gsv_reserve")
+
+    # -------------------------------------------------------------- T2S
+    def t2s_encode(self, ref_seq, text_seq, ref_bert, text_bert, ssl):
+        t = self.torch
+        u, keep = self.make_utt(ref_seq, text_seq, ref_bert, text_bert, ssl)
+        L = u.n_ref + u.n_text
+        x = t.empty((L, 512), dtype=t.float32, device=self.dev)
+        prompts = t.empty((u.n_ssl // 2,), dtype=t.int64, device=self.dev)
+        _check(lib().gsv_t2s_encode(self.h, ctypes.byref(u), _ptr(x), _ptr(prompts), _stream()),
+               "gsv_t2s_encode")
+        return x, prompts
+
+    def t2s_generate(self, utts: Sequence[Tuple], sampler: Optional[Sampler] = None,
+                     out_stride: int = 1024) -> List[np.ndarray]:
+        """utts: sequence of (ref_seq, text_seq, ref_bert, text_bert, ssl)."""
+        arr = (Utt * len(utts))()
+        keep = []
+        for i, u in enumerate(utts):
+            arr[i], k = self.make_utt(*u)
+            keep.append(k)
+        sp = sampler or make_sampler()
+        out = np.zeros((len(utts), out_stride), dtype=np.int64)
+        lens = np.zeros(len(utts), dtype=np.int32)
+        _check(lib().gsv_t2s_generate(self.h, len(utts), arr, ctypes.byref(sp),
+                                      out.ctypes.data_as(ctypes.c_void_p), out_stride,
+                                      lens.ctypes.data_as(ctypes.c_void_p), _stream()),
+               "gsv_t2s_generate")
+        return [out[i, :lens[i]].copy() for i in range(len(utts))]
+
+    def t2s_prefill(self, x, prompts, sampler: Optional[Sampler] = None, seq: int = 0):
+        t = self.torch
+        x = self._dev(x, t.float32).reshape(-1, 512)
+        prompts = self._dev(np.asarray(prompts).reshape(-1) if not isinstance(prompts, t.Tensor)
+                            else prompts.reshape(-1), t.int64)
+        L, P = x.shape[0], prompts.numel()
+        self.reserve(max(1, seq + 1), L + P + 520)
+        y = t.empty((P + 1,), dtype=t.int64, device=self.dev)
+        logits = t.empty((1025,), dtype=t.float32, device=self.dev)
+        sp = sampler or make_sampler()
+        _check(lib().gsv_t2s_prefill(self.h, seq, _ptr(x), L, _ptr(prompts), P, ctypes.byref(sp),
+                                     _ptr(y), _ptr(logits), _stream()), "gsv_t2s_prefill")
+        return y, logits
+
+    def t2s_decode_steps(self, steps: int, sampler: Optional[Sampler] = None, y_cap: int = 4096):
+        t = self.torch
+        y = t.empty((y_cap,), dtype=t.int64, device=self.dev)
+        stop = t.empty((steps,), dtype=t.uint8, device=self.dev)
+        logits = t.empty((steps, 1025), dtype=t.float32, device=self.dev)
+        sp = sampler or make_sampler()
+        _check(lib().gsv_t2s_decode_steps(self.h, 0, steps, ctypes.byref(sp), _ptr(y), _ptr(stop),
+                                          _ptr(logits), _stream()), "gsv_t2s_decode_steps")
+        return y, stop, logits
+
+    def t2s_read_kv(self, layer: int, seq: int = 0, cap: int = 4096):
+        t = self.torch
+        k = t.empty((cap, 512), dtype=t.float32, device=self.dev)
+        v = t.empty((cap, 512), dtype=t.float32, device=self.dev)
+        n = ctypes.c_int32()
+        _check(lib().gsv_t2s_read_kv(self.h, seq, layer, _ptr(k), _ptr(v), ctypes.byref(n),
+                                     _stream()), "gsv_t2s_read_kv")
+        return k[:n.value], v[:n.value]
+
+    # -------------------------------------------------------------- VITS
+    def vits_decode(self, text_seq, pred_semantic, ref_audio=None, ge=None, ge_advanced=None,
+                    eps=None, noise_scale: float = 0.5):
+        t = self.torch
+        ts = self._dev(np.asarray(text_seq).reshape(-1) if not isinstance(text_seq, t.Tensor)
+                       else text_seq.reshape(-1), t.int64)
+        sem = self._dev(np.asarray(pred_semantic).reshape(-1) if not isinstance(pred_semantic, t.Tensor)
+                        else pred_semantic.reshape(-1), t.int64)
+        G = sem.numel()
+        ra = None if ref_audio is None else self._dev(ref_audio, t.float32).reshape(-1)
+        g = None if ge is None else self._dev(ge, t.float32).reshape(-1)
+        ga = None if ge_advanced is None else self._dev(ge_advanced, t.float32).reshape(-1)
+        e = None if eps is None else self._dev(eps, t.float32).reshape(192, 2 * G)
+        audio = t.empty((1280 * G,), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_vits_decode(self.h, _ptr(ts), ts.numel(), _ptr(sem), G, _ptr(ra),
+                                     0 if ra is None else ra.numel(), _ptr(g), _ptr(ga), _ptr(e),
+                                     ctypes.c_float(noise_scale), _ptr(audio), _stream()),
+               "gsv_vits_decode")
+        return audio
+
+    def prompt_encode(self, ref_audio, sv_emb):
+        t = self.torch
+        ra = self._dev(ref_audio, t.float32).reshape(-1)
+        sv = self._dev(sv_emb, t.float32).reshape(-1)
+        ge = t.empty((1024,), dtype=t.float32, device=self.dev)
+        ga = t.empty((512,), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_prompt_encode(self.h, _ptr(ra), ra.numel(), _ptr(sv), _ptr(ge), _ptr(ga),
+                                       _stream()), "gsv_prompt_encode")
+        return ge, ga
+
+    def set_timing(self, on: bool = True):
+        _check(lib().gsv_set_timing(self.h, int(on)), "gsv_set_timing")
+
+    def timing(self) -> List[float]:
+        a = (ctypes.c_float * 4)()
+        _check(lib().gsv_get_timing(self.h, a), "gsv_get_timing")
+        return list(a)

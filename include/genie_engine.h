@@ -1,0 +1,149 @@
+/*
+ * genie_engine.h -- C ABI of the MI355X GPT-SoVITS engine (libgenie_engine.so).
+ *
+ * Drop-in replacement for the onnxruntime InferenceSession objects that Genie
+ * holds per character in `GSVModel` (reference: src/genie_tts/ModelManager.py:48-56)
+ * and calls from `GENIE.tts` / `GENIE.t2s_cpu` (src/genie_tts/Core/Inference.py:16-109).
+ *
+ *   reference call                                   replaced by
+ *   ------------------------------------------------ ------------------------------------
+ *   load_session_with_fp16_conversion (ModelManager.py:59-114)
+ *                                                    gsv_engine_create + gsv_set_weight
+ *                                                    + gsv_finalize_weights
+ *   encoder.run            (Inference.py:76-85)      gsv_t2s_encode
+ *   first_stage_decoder.run(Inference.py:88-90)      gsv_t2s_prefill
+ *   stage_decoder.run      (Inference.py:102)        gsv_t2s_decode_steps (k steps)
+ *   the 500-step loop + trim (Inference.py:95-109)   gsv_t2s_generate (on device, hipGraph)
+ *   vocoder.run            (Inference.py:47-60)      gsv_vits_decode
+ *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
+ *
+ * Conventions
+ *   - All functions return 0 on success, a negative GSV_E* code on failure;
+ *     gsv_last_error() returns a thread-local message for the last failure.
+ *   - Weights are engine-owned device memory.  Every other pointer argument
+ *     marked (device) is a caller-owned device buffer (e.g. a torch tensor's
+ *     data_ptr()); (host) arguments are read before the call returns.
+ *   - `stream` is a hipStream_t passed as void* (NULL = engine's stream).
+ *     Calls on one engine are serialised by the caller (one engine per GPU
+ *     process, as the reference serialises on its single TTS worker thread,
+ *     Core/TTSPlayer.py:55).
+ *   - Integer ids are int64 (the graphs' dtype); audio/features fp32.
+ */
+#ifndef GENIE_ENGINE_H
+#define GENIE_ENGINE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSV_OK 0
+#define GSV_E_ARG -1
+#define GSV_E_HIP -2
+#define GSV_E_STATE -3
+#define GSV_E_WEIGHT -4
+#define GSV_E_CAPACITY -5
+
+typedef struct gsv_engine gsv_engine;
+
+/* dtype codes for gsv_set_weight */
+#define GSV_F32 0
+#define GSV_F16 1
+
+/* Model families (ModelManager.py:287-293: prompt encoder present => V2ProPlus). */
+#define GSV_V2 0
+#define GSV_V2PP 1
+
+const char* gsv_last_error(void);
+const char* gsv_version(void);
+
+/* Create an engine on HIP device `device` for model family `version`. */
+int gsv_engine_create(int device, int version, gsv_engine** out);
+int gsv_engine_destroy(gsv_engine* eng);
+
+/* Stage one weight tensor (host memory, any of GSV_F32/GSV_F16) by its graph
+ * initializer name (e.g. "transformer_encoder.layers.0.linear1.weight",
+ * "vq_model.dec.ups.0.weight_v").  Copied before return. */
+int gsv_set_weight(gsv_engine* eng, const char* name, const void* host, int dtype,
+                   const int64_t* dims, int ndim);
+
+/* Fold weight norm (w = v/||v|| * g), convert, upload; must follow the last
+ * gsv_set_weight.  Missing tensors are an error (GSV_E_WEIGHT). */
+int gsv_finalize_weights(gsv_engine* eng);
+
+/* Reserve decode capacity: up to `max_batch` sequences of up to `max_tokens`
+ * positions (x + prompts + generated) each.  Allocates the KV cache. */
+int gsv_reserve(gsv_engine* eng, int max_batch, int max_tokens);
+
+/* ---------------------------------------------------------------- T2S ---- */
+/* One utterance of a batch.  All pointers (device). */
+typedef struct {
+    const int64_t* ref_seq;   int32_t n_ref;    /* phonemes of the reference text  */
+    const int64_t* text_seq;  int32_t n_text;   /* phonemes of the target text     */
+    const float*   ref_bert;                    /* [n_ref, 1024]  or NULL = zeros  */
+    const float*   text_bert;                   /* [n_text, 1024] or NULL = zeros  */
+    const float*   ssl;       int32_t n_ssl;    /* ssl_content [768, n_ssl]        */
+} gsv_utt;
+
+/* Sampler (reference constants: t2s_stage_decoder_fp32.onnx#1780-1801). */
+typedef struct {
+    int32_t top_k;               /* 15 */
+    float   temperature;         /* 1.0 */
+    float   repetition_penalty;  /* 1.35 */
+    int32_t greedy;              /* 1: RandomNormalLike := 1 (argmax of penalised logits) */
+    uint64_t seed;               /* Philox key for N(0,1) when !greedy */
+    int32_t max_steps;           /* 500 (Inference.py:95) */
+    int32_t force_steps;         /* >0: ignore EOS and run exactly this many loop steps */
+} gsv_sampler;
+
+/* Encoder (t2s_encoder_fp32.onnx) for one utterance:
+ * x (device, [n_ref+n_text, 512] f32), prompts (device, [n_ssl/2] i64). */
+int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64_t* prompts, void* stream);
+
+/* Full T2S of a batch: encoder, prefill, decode loop on device, and the
+ * reference's token trim + EOS filter (Inference.py:41-44,108-109).
+ * out_tokens (host) [batch][out_stride] i64, out_len (host) [batch].
+ * Returns the trimmed semantic tokens per utterance. */
+int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts, const gsv_sampler* s,
+                     int64_t* out_tokens, int32_t out_stride, int32_t* out_len, void* stream);
+
+/* Parity/session entry points mirroring the reference graphs one call at a time.
+ * prefill: x (device [L,512]), prompts (device [P]) -> writes slot `seq` of the
+ *   engine KV cache, y (device i64 [P+1]), logits (device f32 [1025], may be NULL).
+ * decode_steps: runs `steps` stage-decoder steps on slot `seq`, appending to y
+ *   (device i64, capacity >= P+1+steps); stop (device u8 [steps]);
+ *   logits (device [steps][1025] or NULL). */
+int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t n_x, const int64_t* prompts,
+                    int32_t n_prompts, const gsv_sampler* s, int64_t* y, float* logits, void* stream);
+int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int steps, const gsv_sampler* s, int64_t* y,
+                         uint8_t* stop, float* logits, void* stream);
+/* Copy the KV cache of slot `seq`, layer `layer` as [n,512] k and v (device). */
+int gsv_t2s_read_kv(gsv_engine* eng, int seq, int layer, float* k, float* v, int32_t* n, void* stream);
+
+/* --------------------------------------------------------------- VITS ---- */
+/* vits_fp32.onnx.  text_seq (device i64 [n_text]), sem (device i64 [n_sem]).
+ * V2: ref_audio (device f32 [n_audio] at 32 kHz), ge/ge_adv NULL.
+ * V2ProPlus: ge (device [1024]), ge_adv (device [512]), ref_audio NULL.
+ * eps: (device [192, 2*n_sem]) noise for z_p, or NULL => zeros.
+ * audio (device f32 [640*2*n_sem]). */
+int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
+                    const int64_t* sem, int32_t n_sem, const float* ref_audio, int32_t n_audio,
+                    const float* ge, const float* ge_adv, const float* eps, float noise_scale,
+                    float* audio, void* stream);
+
+/* prompt_encoder_fp32.onnx (V2ProPlus): ref_audio (device [n_audio]),
+ * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */
+int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
+                      const float* sv_emb, float* ge, float* ge_adv, void* stream);
+
+/* Per-phase device time of the last gsv_t2s_generate / gsv_vits_decode (ms):
+ * [0]=encode [1]=prefill [2]=decode [3]=vits.  Filled when timing is enabled. */
+int gsv_set_timing(gsv_engine* eng, int enabled);
+int gsv_get_timing(gsv_engine* eng, float* ms4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GENIE_ENGINE_H */
