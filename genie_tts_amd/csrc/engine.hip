@@ -54,6 +54,8 @@ gsv_engine::~gsv_engine() {
     release_all();
     if (own_stream && stream) hipStreamDestroy(stream);
     for (auto& e : ev) if (e) hipEventDestroy(e);
+    if (ev_in) hipEventDestroy(ev_in);
+    if (ev_out) hipEventDestroy(ev_out);
 }
 
 // ------------------------------------------------------------ weights
@@ -438,6 +440,8 @@ extern "C" int gsv_engine_create(int device, int version, gsv_engine** out) {
     }
     e->own_stream = true;
     for (auto& x : e->ev) hipEventCreate(&x);
+    hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming);
+    hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming);
     *out = e;
     return 0;
 }
@@ -493,7 +497,6 @@ extern "C" int gsv_reserve(gsv_engine* eng, int max_batch, int max_tokens) {
     return eng->reserve(max_batch, max_tokens);
 }
 
-static hipStream_t pick(gsv_engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
 
 extern "C" int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64_t* prompts,
                               void* stream) {
@@ -501,7 +504,8 @@ extern "C" int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64
     if (!u || !x || !prompts) return set_error(GSV_E_ARG, "null arg");
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     hipSetDevice(eng->device);
-    return eng->encode(u, x, prompts, pick(eng, stream));
+    StreamScope sc(eng, stream);
+    return eng->encode(u, x, prompts, sc.st());
 }
 
 extern "C" int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t n_x,
@@ -511,7 +515,8 @@ extern "C" int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_CAPACITY, "slot out of range");
-    hipStream_t st = pick(eng, stream);
+    StreamScope sc(eng, stream);
+    hipStream_t st = sc.st();
     if (int e = eng->prefill_slot(seq, x, n_x, prompts, n_prompts, s, logits_out, st)) return e;
     if (yout)
         hipMemcpyAsync(yout, eng->y + (size_t)seq * eng->tmax, (size_t)(n_prompts + 1) * 8,
@@ -525,7 +530,8 @@ extern "C" int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int nsteps, const 
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
     if (seq != 0) return set_error(GSV_E_ARG, "decode_steps supports slot 0");
-    hipStream_t st = pick(eng, stream);
+    StreamScope sc(eng, stream);
+    hipStream_t st = sc.st();
     gsv_sampler sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
     sp.force_steps = 1 << 30;   // session semantics: the caller owns the stop decision
     hipMemsetAsync(eng->done, 0, 1, st);
@@ -547,7 +553,8 @@ extern "C" int gsv_t2s_read_kv(gsv_engine* eng, int seq, int layer, float* k, fl
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
     if (layer < 0 || layer >= 24 || seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_ARG, "range");
-    hipStream_t st = pick(eng, stream);
+    StreamScope sc(eng, stream);
+    hipStream_t st = sc.st();
     int len = 0;
     hipMemcpyAsync(&len, eng->kvlen + seq, 4, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
@@ -578,7 +585,8 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
         need = std::max(need, n0 + steps_cap + 16);
     }
     if (int e = eng->reserve(batch, need)) return e;
-    hipStream_t st = pick(eng, stream);
+    StreamScope sc(eng, stream);
+    hipStream_t st = sc.st();
     if (eng->timing) hipEventRecord(eng->ev[0], st);
     hipMemsetAsync(eng->done, 1, eng->max_batch, st);
     for (int b = 0; b < batch; ++b) {

@@ -13,6 +13,7 @@
 
 namespace gsv {
 int set_error(int code, const std::string& msg);
+struct StreamScope;
 
 struct Staged {
     std::vector<int64_t> dims;
@@ -73,6 +74,7 @@ struct gsv_engine {
     bool timing = false;
     float ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
 
     ~gsv_engine();
     void* dalloc(size_t bytes);
@@ -98,3 +100,22 @@ struct gsv_engine {
     int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                       float* ge_adv, hipStream_t st);
 };
+
+namespace gsv {
+// Orders engine work (always on the engine's own stream, which can be graph-
+// captured) after the caller's stream, and the caller's stream after it.
+// The caller's stream may be the HIP null stream.
+struct StreamScope {
+    gsv_engine* e;
+    hipStream_t caller;
+    StreamScope(gsv_engine* eng, void* s) : e(eng), caller((hipStream_t)s) {
+        hipEventRecord(e->ev_in, caller);
+        hipStreamWaitEvent(e->stream, e->ev_in, 0);
+    }
+    ~StreamScope() {
+        hipEventRecord(e->ev_out, e->stream);
+        hipStreamWaitEvent(caller, e->ev_out, 0);
+    }
+    hipStream_t st() const { return e->stream; }
+};
+}  // namespace gsv

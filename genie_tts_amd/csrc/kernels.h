@@ -15,6 +15,7 @@ enum EpiMode {
     EPI_RESID = 2,       // C = res[m*ldr+n] + v          (post-norm residual)
     EPI_QKV = 3,         // n<512 -> q[m*512+n]; n<1024 -> K cache; else V cache
     EPI_VQDIST = 4,      // C = (rowsq[m] - v) + colsq[n]   (VQ distance, encoder #30-34)
+    EPI_MISH = 5,        // C = v * tanh(softplus(v))        (MelStyleEncoder spectral)
 };
 
 struct KVScatter {

@@ -78,6 +78,10 @@ __global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs a) {
             case EPI_STORE: a.C[(long)row * a.ldc + col] = v; break;
             case EPI_RELU: a.C[(long)row * a.ldc + col] = fmaxf(v, 0.f); break;
             case EPI_RESID: a.C[(long)row * a.ldc + col] = a.res[(long)row * a.ldr + col] + v; break;
+            case EPI_MISH: {
+                const float sp = v > 0.f ? v + log1pf(expf(-v)) : log1pf(expf(v));
+                a.C[(long)row * a.ldc + col] = v * tanhf(sp);
+            } break;
             case EPI_VQDIST:   // (sum h^2) - (2h).c + (sum c^2); x2 is exact so (2h).c == 2(h.c)
                 a.C[(long)row * a.ldc + col] = (a.rowsq[row] - 2.0f * acc[r]) + a.colsq[col];
                 break;

@@ -1,0 +1,347 @@
+// VITS kernels for gfx950 (SoVITS TextEncoder/MRTE/flow + HiFi-GAN generator +
+// MelStyleEncoder).  Reference graph: src/genie_tts/Data/{v2,v2ProPlus}/Models/vits_fp32.onnx.
+//
+// The generator's dilated residual convs are >95 % of the FLOPs (SURVEY §8a:
+// 130 GFLOP per 3.2 s utterance).  They run as an implicit GEMM on
+// v_mfma_f32_32x32x2_f32 (exact fp32 FMA chain: the reference is fp32 and the
+// parity bar is waveform RMS <= 1e-4): M = Cout, N = time, K = Cin x taps, with
+// the LeakyReLU pre-activation fused into the LDS staging of the input and the
+// residual / MRF-mean / tanh fused into the epilogue.  ConvTranspose1d runs as
+// `stride` polyphase convs of the same kernel (blockIdx.z = phase).
+#include "common.h"
+#include "vits.h"
+
+namespace gsv {
+
+template <int KT> struct ConvCfg {
+    static constexpr int CI = KT == 1 ? 32 : KT == 2 ? 32 : KT <= 4 ? 16 : KT <= 7 ? 8 : 4;
+    static constexpr int KC = CI * KT;            // K-chunk (even)
+};
+
+#define CONV_BN 64
+#define CONV_BM 64
+#define CONV_XW_MAX 128
+
+template <int KT>
+__global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
+    constexpr int CI = ConvCfg<KT>::CI, KC = ConvCfg<KT>::KC;
+    __shared__ float Xs[CI * CONV_XW_MAX];
+    __shared__ float Ws[CONV_BM][KC + 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int t0 = blockIdx.x * CONV_BN, co0 = blockIdx.y * CONV_BM, ph = blockIdx.z;
+    const float* W = a.w + (long)ph * a.w_phase_stride;
+    const int dil = a.dil;
+    const int XW = CONV_BN + (KT - 1) * dil;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const int ncol = wn * 32 + (lane & 31);
+    const int h = lane >> 5;
+    const long wrow = (long)a.Cin * KT;
+    for (int ci0 = 0; ci0 < a.Cin; ci0 += CI) {
+        // stage input chunk (with pre-activation); zero padding outside [0, Tin)
+        for (int e = tid; e < CI * XW; e += 256) {
+            const int ci = e / XW, u = e - ci * XW;
+            const int tin = t0 - a.pad + u;
+            float v = 0.f;
+            if (ci0 + ci < a.Cin && tin >= 0 && tin < a.Tin) {
+                v = a.x[(long)(ci0 + ci) * a.x_cs + (long)tin * a.x_ts];
+                if (a.in_act) v = v >= 0.f ? v : v * a.in_slope;
+            }
+            Xs[ci * XW + u] = v;
+        }
+        // stage weights [co][kc] for kc in this chunk
+        for (int e = tid; e < CONV_BM * KC; e += 256) {
+            const int r = e / KC, kc = e - r * KC;
+            const int co = co0 + r, ci = ci0 + kc / KT;
+            Ws[r][kc] = (co < a.Cout && ci < a.Cin) ? W[(long)co * wrow + (long)ci0 * KT + kc] : 0.f;
+        }
+        __syncthreads();
+        const int arow = wm * 32 + (lane & 31);
+#pragma unroll
+        for (int kp = 0; kp < KC / 2; ++kp) {
+            const int k0 = 2 * kp, k1 = 2 * kp + 1;
+            const int off0 = (k0 / KT) * XW + (k0 % KT) * dil;
+            const int off1 = (k1 / KT) * XW + (k1 % KT) * dil;
+            const float av = Ws[arow][h ? k1 : k0];
+            const float bv = Xs[(h ? off1 : off0) + ncol];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    const int t = t0 + ncol;
+    if (t >= a.n_t) return;
+    const int tp = t * a.o_tstride + a.o_toff + ph;
+    if (tp < 0 || tp >= a.o_len) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= a.Cout) continue;
+        const float v = a.bias ? a.bias[co] + acc[r] : acc[r];
+        const long oi = (long)co * a.o_cs + (long)tp * a.o_ts;
+        switch (a.mode) {
+            case CV_STORE: a.out[oi] = v; break;
+            case CV_RELU: a.out[oi] = fmaxf(v, 0.f); break;
+            case CV_RESID: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
+            case CV_VEC: a.out[oi] = v + a.vec[co]; break;
+            case CV_SUB: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] - v; break;
+            case CV_TANH: a.out[oi] = tanhf(v); break;
+            case CV_ACC_FIRST: a.acc[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
+            case CV_ACC_ADD: a.acc[oi] = a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v); break;
+            case CV_ACC_MEAN:
+                a.out[oi] = (a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v)) / a.div;
+                break;
+            case CV_RESID_VEC:
+                a.out[oi] = (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v) + a.vec[co];
+                break;
+            case CV_SPLIT_RESID:
+                if (co < a.split) {
+                    a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v;
+                } else {
+                    const long o2 = (long)(co - a.split) * a.o_cs + (long)tp * a.o_ts;
+                    a.out2[o2] = a.res2[o2] + v;
+                }
+                break;
+        }
+    }
+}
+
+void conv1d(const ConvArgs& a, hipStream_t s) {
+    dim3 grid((a.n_t + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM,
+              a.phases > 0 ? a.phases : 1);
+    switch (a.K) {
+        case 1: hipLaunchKernelGGL(k_conv1d<1>, grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_conv1d<2>, grid, dim3(256), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_conv1d<3>, grid, dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(k_conv1d<4>, grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(k_conv1d<5>, grid, dim3(256), 0, s, a); break;
+        case 7: hipLaunchKernelGGL(k_conv1d<7>, grid, dim3(256), 0, s, a); break;
+        case 11: hipLaunchKernelGGL(k_conv1d<11>, grid, dim3(256), 0, s, a); break;
+        default: break;   // host validates K
+    }
+}
+
+// ----------------------------------------------------------------- LN over C
+// modules.LayerNorm: transpose -> layer_norm(channels, eps 1e-5) -> transpose
+__global__ __launch_bounds__(64) void k_ln_channels(const float* x, const float* y, float* out,
+                                                    int C, int T, const float* g, const float* b) {
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= T) return;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += y ? x[(long)c * T + t] + y[(long)c * T + t] : x[(long)c * T + t];
+    const float mean = s / (float)C;
+    float v = 0.f;
+    for (int c = 0; c < C; ++c) {
+        const float d = (y ? x[(long)c * T + t] + y[(long)c * T + t] : x[(long)c * T + t]) - mean;
+        v += d * d;
+    }
+    const float den = sqrtf(v / (float)C + 1e-5f);
+    for (int c = 0; c < C; ++c) {
+        const float xv = y ? x[(long)c * T + t] + y[(long)c * T + t] : x[(long)c * T + t];
+        out[(long)c * T + t] = (xv - mean) / den * g[c] + b[c];
+    }
+}
+
+void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
+                 const float* b, hipStream_t s) {
+    hipLaunchKernelGGL(k_ln_channels, dim3((T + 63) / 64), dim3(64), 0, s, x, y, out, C, T, g, b);
+}
+
+// ----------------------------------------------------------------- attention
+// One block per (head, query row).  attentions.MultiHeadAttention (rel-pos,
+// window 4; (v2)#308-...) and MelStyleEncoder's ScaledDotProductAttention.
+#define MHA_MAXK 2048
+#define MHA_MAXD 128
+__global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
+    __shared__ float qs[MHA_MAXD];
+    __shared__ float p[MHA_MAXK];
+    __shared__ float red[16];
+    __shared__ float part[2][MHA_MAXD];
+    const int hd = blockIdx.x, i = blockIdx.y, tid = threadIdx.x;
+    const int dk = a.dk, c0 = hd * dk;
+    for (int d = tid; d < dk; d += 256) {
+        const float qv = a.q[(long)i * a.q_ts + (long)(c0 + d) * a.q_cs];
+        qs[d] = a.postdiv ? qv : qv / a.scale;
+    }
+    __syncthreads();
+    float lmax = -INFINITY;
+    for (int j = tid; j < a.nk; j += 256) {
+        float s = 0.f;
+        for (int d = 0; d < dk; ++d) s += qs[d] * a.k[(long)j * a.k_ts + (long)(c0 + d) * a.k_cs];
+        if (a.postdiv) s = s / a.scale;
+        if (a.ek) {
+            const int r = j - i;
+            if (r >= -a.window && r <= a.window) {
+                const float* e = a.ek + (long)(r + a.window) * dk;
+                float sl = 0.f;
+                for (int d = 0; d < dk; ++d) sl += qs[d] * e[d];
+                s = s + sl;
+            }
+        }
+        p[j] = s;
+        lmax = fmaxf(lmax, s);
+    }
+    const float m = block_max(lmax, red);
+    float lsum = 0.f;
+    for (int j = tid; j < a.nk; j += 256) {
+        const float e = expf(p[j] - m);
+        p[j] = e;
+        lsum += e;
+    }
+    const float sum = block_sum(lsum, red);
+    for (int j = tid; j < a.nk; j += 256) p[j] = p[j] / sum;
+    __syncthreads();
+    // out[d] = sum_j p_j v[j][d]  (+ sum_{|j-i|<=W} p_j ev[j-i+W][d])
+    const int half = tid >> 7, dd = tid & 127;
+    for (int d = dd; d < dk; d += 128) {
+        float o = 0.f;
+        for (int j = half; j < a.nk; j += 2) o += p[j] * a.v[(long)j * a.v_ts + (long)(c0 + d) * a.v_cs];
+        part[half][d] = o;
+    }
+    __syncthreads();
+    for (int d = tid; d < dk; d += 256) {
+        float o = part[0][d] + part[1][d];
+        if (a.ev) {
+            float ol = 0.f;
+            for (int r = -a.window; r <= a.window; ++r) {
+                const int j = i + r;
+                if (j >= 0 && j < a.nk) ol += p[j] * a.ev[(long)(r + a.window) * dk + d];
+            }
+            o = o + ol;
+        }
+        a.out[(long)i * a.o_ts + (long)(c0 + d) * a.o_cs] = o;
+    }
+}
+
+void mha(const MhaArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_mha, dim3(a.heads, a.nq), dim3(256), 0, s, a);
+}
+
+// ----------------------------------------------------------------- elementwise
+// quantizer.decode + x2 nearest (torch.cat([q, q]).permute(1,2,0).view): out[c][2t+r] = cb[sem[t]][c]
+__global__ void k_cb_up2(const int64_t* sem, int G, const float* cb, float* out) {
+    const int c = blockIdx.y, t2 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t2 >= 2 * G) return;
+    out[(long)c * 2 * G + t2] = cb[sem[t2 >> 1] * 768 + c];
+}
+void codebook_upsample2(const int64_t* sem, int G, const float* cb, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_cb_up2, dim3((2 * G + 127) / 128, 768), dim3(128), 0, s, sem, G, cb, out);
+}
+
+__global__ void k_embed_ch(const int64_t* ids, int n, const float* emb, int C, float* out) {
+    const int c = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    out[(long)c * n + t] = emb[ids[t] * C + c];
+}
+void embed_channels(const int64_t* ids, int n, const float* emb, int C, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_embed_ch, dim3((n + 127) / 128, C), dim3(128), 0, s, ids, n, emb, C, out);
+}
+
+// commons.fused_add_tanh_sigmoid_multiply (cond already added by the conv epilogue)
+__global__ void k_wn_gate(const float* xin, float* acts, int H, int T) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)H * T) return;
+    const float a = xin[i], b = xin[i + (long)H * T];
+    acts[i] = tanhf(a) * (1.0f / (1.0f + expf(-b)));
+}
+void wn_gate(const float* xin, float* acts, int H, int T, hipStream_t s) {
+    const long n = (long)H * T;
+    hipLaunchKernelGGL(k_wn_gate, dim3((n + 255) / 256), dim3(256), 0, s, xin, acts, H, T);
+}
+
+// Conv1dGLU: out = x + a * sigmoid(b), h = [a; b] channel-major [2C][T]
+__global__ void k_glu(const float* h, const float* x, float* out, int C, int T, long x_cs, long x_ts) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)C * T) return;
+    const int c = (int)(i / T), t = (int)(i - (long)c * T);
+    const float a = h[i], b = h[i + (long)C * T];
+    const long xi = (long)c * x_cs + (long)t * x_ts;
+    out[xi] = x[xi] + a * (1.0f / (1.0f + expf(-b)));
+}
+void glu_resid(const float* h, const float* x, float* out, int C, int T, long x_cs, long x_ts,
+               hipStream_t s) {
+    const long n = (long)C * T;
+    hipLaunchKernelGGL(k_glu, dim3((n + 255) / 256), dim3(256), 0, s, h, x, out, C, T, x_cs, x_ts);
+}
+
+// z_p = m_p + (eps * exp(logs_p)) * noise_scale   ((v2)#6490-6495)
+__global__ void k_noise(const float* m, const float* logs, const float* eps, float sc, float* z, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float e = eps ? eps[i] : 0.f;
+    z[i] = m[i] + (e * expf(logs[i])) * sc;
+}
+void noise_zp(const float* m, const float* logs, const float* eps, float scale, float* z, int n,
+              hipStream_t s) {
+    hipLaunchKernelGGL(k_noise, dim3((n + 255) / 256), dim3(256), 0, s, m, logs, eps, scale, z, n);
+}
+
+__global__ void k_flip(const float* in, float* out, int C, int T) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)C * T) return;
+    const int c = (int)(i / T), t = (int)(i - (long)c * T);
+    out[i] = in[(long)(C - 1 - c) * T + t];
+}
+void flip_channels(const float* in, float* out, int C, int T, hipStream_t s) {
+    const long n = (long)C * T;
+    hipLaunchKernelGGL(k_flip, dim3((n + 255) / 256), dim3(256), 0, s, in, out, C, T);
+}
+
+__global__ void k_reflect_pad(const float* x, int n, int pad, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = n + 2 * pad;
+    if (i >= m) return;
+    int j = i - pad;
+    if (j < 0) j = -j;
+    if (j >= n) j = 2 * (n - 1) - j;
+    out[i] = x[j];
+}
+void reflect_pad(const float* x, int n, int pad, float* out, hipStream_t s) {
+    const int m = n + 2 * pad;
+    hipLaunchKernelGGL(k_reflect_pad, dim3((m + 255) / 256), dim3(256), 0, s, x, n, pad, out);
+}
+
+// sqrt(re^2 + im^2 + 1e-6)  ((v2)#40-45), reim rows interleaved [re0, im0, re1, im1, ...]
+__global__ void k_stft_mag(const float* reim, int frames, int bins, float* spec) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= frames * bins) return;
+    const int f = i / bins, b = i - f * bins;
+    const float re = reim[(long)f * 2 * bins + 2 * b], im = reim[(long)f * 2 * bins + 2 * b + 1];
+    spec[i] = sqrtf((re * re + im * im) + 1e-6f);
+}
+void stft_mag(const float* reim, int frames, int bins, float* spec, hipStream_t s) {
+    const int n = frames * bins;
+    hipLaunchKernelGGL(k_stft_mag, dim3((n + 255) / 256), dim3(256), 0, s, reim, frames, bins, spec);
+}
+
+// temporal_avg_pool: sum over time / T (the mask is all ones at batch 1)
+__global__ void k_time_mean(const float* x, int T, int C, float* out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += x[(long)t * C + c];
+    out[c] = s / (float)T;
+}
+void time_mean(const float* x, int T, int C, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_time_mean, dim3((C + 63) / 64), dim3(64), 0, s, x, T, C, out);
+}
+
+__global__ void k_prelu(const float* x, const float* a, float* out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = x[i] >= 0.f ? x[i] : x[i] * a[i];
+}
+void prelu_vec(const float* x, const float* a, float* out, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_prelu, dim3((n + 255) / 256), dim3(256), 0, s, x, a, out, n);
+}
+
+__global__ void k_add(const float* a, const float* b, float* out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = a[i] + b[i];
+}
+void add_vec(const float* a, const float* b, float* out, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_add, dim3((n + 255) / 256), dim3(256), 0, s, a, b, out, n);
+}
+
+}  // namespace gsv

@@ -1,29 +1,569 @@
-// VITS orchestration (placeholder until the VITS kernels land).
+// VITS orchestration: restates vits_fp32.onnx (V2 / V2ProPlus) and
+// prompt_encoder_fp32.onnx on the engine's kernels.  Called from
+// gsv_vits_decode / gsv_prompt_encode (reference call sites:
+// src/genie_tts/Core/Inference.py:47-60, src/genie_tts/Audio/ReferenceAudio.py:68-76).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
 #include "engine_internal.h"
+
 using namespace gsv;
 
-int gsv_engine::finalize_vits() { return 0; }
-int gsv_engine::finalize_prompt_encoder() { return 0; }
-int gsv_engine::vits_decode(const int64_t*, int, const int64_t*, int, const float*, int, const float*,
-                            const float*, const float*, float, float*, hipStream_t) {
-    return set_error(GSV_E_STATE, "VITS path not built");
+namespace {
+
+std::vector<float> fold_wn(const Staged* v, const Staged* g) {
+    // w = (v / ||v||_2 over dims 1..) * g  (ReduceL2 -> Div -> Mul in the graph)
+    const long o = v->dims[0];
+    const long per = (long)v->data.size() / o;
+    std::vector<float> w(v->data.size());
+    for (long i = 0; i < o; ++i) {
+        double s = 0;
+        for (long j = 0; j < per; ++j) s += (double)v->data[i * per + j] * v->data[i * per + j];
+        const float nrm = (float)std::sqrt(s);
+        const float gg = g->data[i];
+        for (long j = 0; j < per; ++j) w[i * per + j] = (v->data[i * per + j] / nrm) * gg;
+    }
+    return w;
 }
-int gsv_engine::prompt_encode(const float*, int, const float*, float*, float*, hipStream_t) {
-    return set_error(GSV_E_STATE, "prompt encoder not built");
+
+}  // namespace
+
+// upload helpers ------------------------------------------------------------
+static float* up_vec(gsv_engine* e, const std::vector<float>& v) {
+    float* d = (float*)e->dalloc(v.size() * 4);
+    if (d) hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice);
+    return d;
 }
+
+static int load_conv(gsv_engine* e, const std::string& base, Conv& c, bool wn, bool bias = true) {
+    std::vector<float> w;
+    const Staged* s = nullptr;
+    if (wn) {
+        const Staged* v = e->find(base + ".weight_v");
+        const Staged* g = e->find(base + ".weight_g");
+        if (!v || !g) return set_error(GSV_E_WEIGHT, "missing weight " + base + ".weight_v/g");
+        w = fold_wn(v, g);
+        s = v;
+    } else {
+        s = e->find(base + ".weight");
+        if (!s) return set_error(GSV_E_WEIGHT, "missing weight " + base + ".weight");
+        w = s->data;
+    }
+    c.cout = (int)s->dims[0];
+    c.cin = (int)s->dims[1];
+    c.k = s->dims.size() > 2 ? (int)s->dims[2] : 1;
+    c.w = up_vec(e, w);
+    if (bias) {
+        const Staged* b = e->find(base + ".bias");
+        if (!b) return set_error(GSV_E_WEIGHT, "missing weight " + base + ".bias");
+        c.b = up_vec(e, b->data);
+    }
+    return 0;
+}
+
+// ConvTranspose1d(Cin, Cout, k, stride u, pad (k-u)/2), weight [Cin][Cout][k] (WN over dim 0)
+// -> u polyphase convs of M = ceil(k/u) taps: W_r[co][ci][j] = w[ci][co][r + (M-1-j)*u]
+static int load_convT(gsv_engine* e, const std::string& base, int u, Conv& c) {
+    const Staged* v = e->find(base + ".weight_v");
+    const Staged* g = e->find(base + ".weight_g");
+    const Staged* b = e->find(base + ".bias");
+    if (!v || !g || !b) return set_error(GSV_E_WEIGHT, "missing weight " + base);
+    std::vector<float> w = fold_wn(v, g);
+    const int cin = (int)v->dims[0], cout = (int)v->dims[1], k = (int)v->dims[2];
+    const int M = (k + u - 1) / u;
+    std::vector<float> pw((size_t)u * cout * cin * M, 0.f);
+    for (int r = 0; r < u; ++r)
+        for (int co = 0; co < cout; ++co)
+            for (int ci = 0; ci < cin; ++ci)
+                for (int j = 0; j < M; ++j) {
+                    const int kk = r + (M - 1 - j) * u;
+                    if (kk < k)
+                        pw[(((size_t)r * cout + co) * cin + ci) * M + j] = w[((size_t)ci * cout + co) * k + kk];
+                }
+    c.w = up_vec(e, pw);
+    c.b = up_vec(e, b->data);
+    c.cout = cout;
+    c.cin = cin;
+    c.k = M;
+    c.phases = u;
+    return 0;
+}
+
+static int load_concat(gsv_engine* e, const std::vector<std::string>& bases, Conv& c) {
+    std::vector<float> w, b;
+    int cin = 0, cout = 0;
+    for (const auto& n : bases) {
+        const Staged* s = e->find(n + ".weight");
+        const Staged* sb = e->find(n + ".bias");
+        if (!s || !sb) return set_error(GSV_E_WEIGHT, "missing weight " + n);
+        w.insert(w.end(), s->data.begin(), s->data.end());
+        b.insert(b.end(), sb->data.begin(), sb->data.end());
+        cout += (int)s->dims[0];
+        cin = (int)s->dims[1];
+    }
+    c.w = up_vec(e, w);
+    c.b = up_vec(e, b);
+    c.cout = cout;
+    c.cin = cin;
+    c.k = 1;
+    return 0;
+}
+
+static float* up_named(gsv_engine* e, const std::string& n, int* err) { return e->up_f32(n, err); }
+
+static int load_attn_layers(gsv_engine* e, const std::string& pre, int n, std::vector<AttnLayer>& out) {
+    out.resize(n);
+    int err = 0;
+    for (int i = 0; i < n; ++i) {
+        const std::string a = pre + ".attn_layers." + std::to_string(i) + ".";
+        AttnLayer& L = out[i];
+        if (int r = load_concat(e, {a + "conv_q", a + "conv_k", a + "conv_v"}, L.qkv)) return r;
+        if (int r = load_conv(e, a + "conv_o", L.o, false)) return r;
+        if (int r = load_conv(e, pre + ".ffn_layers." + std::to_string(i) + ".conv_1", L.ffn1, false)) return r;
+        if (int r = load_conv(e, pre + ".ffn_layers." + std::to_string(i) + ".conv_2", L.ffn2, false)) return r;
+        L.ek = up_named(e, a + "emb_rel_k", &err);
+        L.ev = up_named(e, a + "emb_rel_v", &err);
+        L.g1 = up_named(e, pre + ".norm_layers_1." + std::to_string(i) + ".gamma", &err);
+        L.b1 = up_named(e, pre + ".norm_layers_1." + std::to_string(i) + ".beta", &err);
+        L.g2 = up_named(e, pre + ".norm_layers_2." + std::to_string(i) + ".gamma", &err);
+        L.b2 = up_named(e, pre + ".norm_layers_2." + std::to_string(i) + ".beta", &err);
+        if (err) return err;
+    }
+    return 0;
+}
+
+static int load_ref_enc(gsv_engine* e, const std::string& p, RefEnc& r) {
+    int err = 0;
+    r.fc0_w = e->up_f32(p + "spectral.0.fc.weight", &err);
+    r.fc0_b = e->up_f32(p + "spectral.0.fc.bias", &err);
+    r.fc3_w = e->up_f32(p + "spectral.3.fc.weight", &err);
+    r.fc3_b = e->up_f32(p + "spectral.3.fc.bias", &err);
+    if (err) return err;
+    for (int i = 0; i < 2; ++i)
+        if (int x = load_conv(e, p + "temporal." + std::to_string(i) + ".conv1.conv", r.temporal[i], false)) return x;
+    Conv qkv;
+    if (int x = load_concat(e, {p + "slf_attn.w_qs", p + "slf_attn.w_ks", p + "slf_attn.w_vs"}, qkv)) return x;
+    r.wqkv = qkv.w;
+    r.bqkv = qkv.b;
+    r.fcw = e->up_f32(p + "slf_attn.fc.weight", &err);
+    r.fcb = e->up_f32(p + "slf_attn.fc.bias", &err);
+    r.out_w = e->up_f32(p + "fc.fc.weight", &err);
+    r.out_b = e->up_f32(p + "fc.fc.bias", &err);
+    if (err) return err;
+    r.out_dim = (int)e->find(p + "fc.fc.weight")->dims[0];
+    // windowed one-sided DFT basis for STFT(n_fft 2048), bins [0, 704), periodic Hann
+    std::vector<float> basis((size_t)1408 * 2048);
+    for (int b = 0; b < 704; ++b)
+        for (int n = 0; n < 2048; ++n) {
+            const double win = 0.5 - 0.5 * std::cos(2.0 * M_PI * n / 2048.0);
+            const double ang = 2.0 * M_PI * (double)((long)b * n % 2048) / 2048.0;
+            basis[(size_t)(2 * b) * 2048 + n] = (float)(win * std::cos(ang));
+            basis[(size_t)(2 * b + 1) * 2048 + n] = (float)(-win * std::sin(ang));
+        }
+    r.dft = up_vec(e, basis);
+    return r.dft ? 0 : set_error(GSV_E_HIP, "dft alloc");
+}
+
+int gsv_engine::finalize_vits() {
+    VitsWeights& V = vits;
+    const bool pp = version == GSV_V2PP;
+    V.gin = pp ? 1024 : 512;
+    V.upc = pp ? 768 : 512;
+    const int rates[5] = {10, 8, 2, 2, 2};
+    const int ks_v2[5] = {16, 16, 8, 2, 2}, ks_pp[5] = {20, 16, 8, 2, 2};
+    for (int i = 0; i < 5; ++i) { V.up_rate[i] = rates[i]; V.up_k[i] = pp ? ks_pp[i] : ks_v2[i]; }
+    int err = 0;
+    const std::string P = "vq_model.enc_p.";
+    V.codebook = up_f32("vq_model.quantizer.vq.layers.0._codebook.embed", &err);
+    V.text_emb = up_f32(P + "text_embedding.weight", &err);
+    if (err) return err;
+    if (int r = load_conv(this, P + "ssl_proj", V.ssl_proj, false)) return r;
+    if (int r = load_attn_layers(this, P + "encoder_ssl", 3, V.enc_ssl)) return r;
+    if (int r = load_attn_layers(this, P + "encoder_text", 6, V.enc_text)) return r;
+    if (int r = load_attn_layers(this, P + "encoder2", 3, V.enc2)) return r;
+    const std::string M = P + "mrte.";
+    if (int r = load_conv(this, M + "c_pre", V.c_pre, false)) return r;
+    if (int r = load_conv(this, M + "text_pre", V.text_pre, false)) return r;
+    if (int r = load_conv(this, M + "c_post", V.c_post, false)) return r;
+    if (int r = load_conv(this, M + "cross_attention.conv_q", V.mrte_qkv_q, false)) return r;
+    if (int r = load_concat(this, {M + "cross_attention.conv_k", M + "cross_attention.conv_v"}, V.mrte_kv)) return r;
+    if (int r = load_conv(this, M + "cross_attention.conv_o", V.mrte_o, false)) return r;
+    if (int r = load_conv(this, P + "proj", V.proj, false)) return r;
+    for (int f = 0; f < 4; ++f) {
+        const std::string F = "vq_model.flow.flows." + std::to_string(2 * f) + ".";
+        auto& fl = V.flows[f];
+        if (int r = load_conv(this, F + "pre", fl.pre, false)) return r;
+        if (int r = load_conv(this, F + "post", fl.post, false)) return r;
+        if (int r = load_conv(this, F + "enc.cond_layer", fl.cond, true)) return r;
+        for (int l = 0; l < 4; ++l) {
+            if (int r = load_conv(this, F + "enc.in_layers." + std::to_string(l), fl.in_l[l], true)) return r;
+            if (int r = load_conv(this, F + "enc.res_skip_layers." + std::to_string(l), fl.rs[l], true)) return r;
+        }
+    }
+    const std::string D = "vq_model.dec.";
+    if (int r = load_conv(this, D + "conv_pre", V.conv_pre, false)) return r;
+    if (int r = load_conv(this, D + "cond", V.cond, false)) return r;
+    if (int r = load_conv(this, D + "conv_post", V.conv_post, false, false)) return r;
+    for (int i = 0; i < 5; ++i)
+        if (int r = load_convT(this, D + "ups." + std::to_string(i), V.up_rate[i], V.ups[i])) return r;
+    for (int j = 0; j < 15; ++j)
+        for (int c = 0; c < 2; ++c)
+            for (int m = 0; m < 3; ++m) {
+                const std::string n = D + "resblocks." + std::to_string(j) + (c == 0 ? ".convs1." : ".convs2.") +
+                                      std::to_string(m);
+                if (int r = load_conv(this, n, V.rb[j][c][m], true)) return r;
+            }
+    if (!pp)
+        if (int r = load_ref_enc(this, "vq_model.ref_enc.", V.ref)) return r;
+    V.ready = true;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : set_error(GSV_E_HIP, "finalize_vits");
+}
+
+int gsv_engine::finalize_prompt_encoder() {
+    int err = 0;
+    if (int r = load_ref_enc(this, "ref_enc.", penc.ref)) return r;
+    penc.sv_w = up_f16("sv_emb.weight", &err);
+    penc.sv_b = up_f32("sv_emb.bias", &err);
+    penc.to512_w = up_f32("ge_to512.weight", &err);
+    penc.to512_b = up_f32("ge_to512.bias", &err);
+    penc.prelu = up_f32("prelu.weight", &err);
+    if (err) return err;
+    penc.ready = true;
+    return 0;
+}
+
+// ---------------------------------------------------------------- helpers
+static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode = CV_STORE) {
+    ConvArgs a{};
+    a.x = x; a.x_cs = T; a.x_ts = 1; a.Cin = c.cin; a.Tin = T;
+    a.w = c.w; a.Cout = c.cout; a.K = c.k; a.dil = 1; a.pad = (c.k - 1) / 2;
+    a.bias = c.b;
+    a.out = out; a.o_cs = T; a.o_ts = 1; a.n_t = T; a.o_tstride = 1; a.o_toff = 0; a.o_len = T;
+    a.mode = mode; a.r_cs = T; a.r_ts = 1;
+    a.phases = 1;
+    return a;
+}
+
+static void attn_encoder(gsv_engine* e, const std::vector<AttnLayer>& Ls, float* x, int T, float* qkv,
+                         float* att, float* tmp, float* ffn, hipStream_t s) {
+    for (const AttnLayer& L : Ls) {
+        conv1d(cargs(L.qkv, x, T, qkv), s);
+        MhaArgs m{};
+        m.q = qkv; m.q_ts = 1; m.q_cs = T;
+        m.k = qkv + (size_t)192 * T; m.k_ts = 1; m.k_cs = T;
+        m.v = qkv + (size_t)384 * T; m.v_ts = 1; m.v_cs = T;
+        m.out = att; m.o_ts = 1; m.o_cs = T;
+        m.nq = T; m.nk = T; m.heads = 2; m.dk = 96; m.postdiv = 0; m.scale = std::sqrt(96.0f);
+        m.ek = L.ek; m.ev = L.ev; m.window = 4;
+        mha(m, s);
+        conv1d(cargs(L.o, att, T, tmp), s);
+        ln_channels(x, tmp, x, 192, T, L.g1, L.b1, s);
+        conv1d(cargs(L.ffn1, x, T, ffn, CV_RELU), s);
+        conv1d(cargs(L.ffn2, ffn, T, tmp), s);
+        ln_channels(x, tmp, x, 192, T, L.g2, L.b2, s);
+    }
+}
+
+// MelStyleEncoder on an STFT magnitude [F][704] -> ge [out_dim] (vits(v2)#79-271)
+static void run_ref_enc(gsv_engine* e, const RefEnc& R, const float* audio, int n, float* ge,
+                        hipStream_t s) {
+    VitsWorkspace& W = e->vws;
+    const int padded = n + 2 * 704;
+    const int F = (padded - 2048) / 640 + 1;
+    reflect_pad(audio, n, 704, W.pad, s);
+    GemmArgs g{};
+    g.M = F; g.N = 1408; g.K = 2048; g.A = W.pad; g.lda = 640;
+    g.W = R.dft; g.ldw = 2048; g.w_f16 = 0; g.C = W.reim; g.ldc = 1408; g.mode = EPI_STORE;
+    gemm_nt(g, s);
+    stft_mag(W.reim, F, 704, W.spec, s);
+    GemmArgs l0{};
+    l0.M = F; l0.N = 128; l0.K = 704; l0.A = W.spec; l0.lda = 704;
+    l0.W = R.fc0_w; l0.ldw = 704; l0.bias = R.fc0_b; l0.C = W.r0; l0.ldc = 128; l0.mode = EPI_MISH;
+    gemm_nt(l0, s);
+    GemmArgs l1 = l0;
+    l1.K = 128; l1.A = W.r0; l1.lda = 128; l1.W = R.fc3_w; l1.ldw = 128; l1.bias = R.fc3_b; l1.C = W.r1;
+    gemm_nt(l1, s);
+    // temporal Conv1dGLU x2 on the [F][128] rows viewed channel-major via strides
+    float* xin = W.r1;
+    float* xout = W.r2;
+    for (int i = 0; i < 2; ++i) {
+        ConvArgs c = cargs(R.temporal[i], xin, F, W.r3);
+        c.x_cs = 1; c.x_ts = 128;               // x(ci, t) = rows[t][ci]
+        conv1d(c, s);                            // -> [256][F] channel-major
+        glu_resid(W.r3, xin, xout, 128, F, 1, 128, s);
+        float* t = xin; xin = xout; xout = (i == 0 ? W.r1 : t);
+    }
+    // xin: [F][128] rows.  Self-attention (2 heads x 64, temperature sqrt(128)) + residual
+    GemmArgs q{};
+    q.M = F; q.N = 384; q.K = 128; q.A = xin; q.lda = 128; q.W = R.wqkv; q.ldw = 128;
+    q.bias = R.bqkv; q.C = W.rq; q.ldc = 384; q.mode = EPI_STORE;
+    gemm_nt(q, s);
+    MhaArgs m{};
+    m.q = W.rq; m.q_ts = 384; m.q_cs = 1;
+    m.k = W.rq + 128; m.k_ts = 384; m.k_cs = 1;
+    m.v = W.rq + 256; m.v_ts = 384; m.v_cs = 1;
+    m.out = W.ratt; m.o_ts = 128; m.o_cs = 1;
+    m.nq = F; m.nk = F; m.heads = 2; m.dk = 64; m.postdiv = 1; m.scale = std::sqrt(128.0f);
+    mha(m, s);
+    GemmArgs fc{};
+    fc.M = F; fc.N = 128; fc.K = 128; fc.A = W.ratt; fc.lda = 128; fc.W = R.fcw; fc.ldw = 128;
+    fc.bias = R.fcb; fc.C = W.r3; fc.ldc = 128; fc.mode = EPI_RESID; fc.res = xin; fc.ldr = 128;
+    gemm_nt(fc, s);
+    GemmArgs o{};
+    o.M = F; o.N = R.out_dim; o.K = 128; o.A = W.r3; o.lda = 128; o.W = R.out_w; o.ldw = 128;
+    o.bias = R.out_b; o.C = W.r0; o.ldc = R.out_dim; o.mode = EPI_STORE;
+    gemm_nt(o, s);
+    time_mean(W.r0, F, R.out_dim, ge, s);
+}
+
+static int ensure_vits_ws(gsv_engine* e, int T, int S, int n_audio) {
+    VitsWorkspace& W = e->vws;
+    const VitsWeights& V = e->vits;
+    const size_t gen = (size_t)V.upc * T * 20;    // max C*T over generator stages: upc/2^(i+1) * T*prod(u)
+    const int F = n_audio > 0 ? (n_audio + 1408 - 2048) / 640 + 1 : 0;
+    if ((size_t)T <= W.cap_t && S <= W.cap_text && gen <= W.cap_gen && F <= W.cap_spec) return 0;
+    const size_t t = std::max((size_t)T, W.cap_t);
+    const int sT = std::max(S, W.cap_text);
+    const size_t g = std::max(gen, W.cap_gen);
+    const int f = std::max(F, W.cap_spec);
+    auto A = [&](size_t n) { return (float*)e->dalloc(n * 4); };
+    W.q = A(768 * t); W.y = A(192 * t); W.te = A(192 * (size_t)sT);
+    W.qkv = A(576 * t); W.att = A(192 * t); W.a = A(512 * t); W.ffn = A(768 * t);
+    W.tqkv = A(576 * (size_t)sT); W.tatt = A(192 * (size_t)sT); W.ta = A(192 * (size_t)sT);
+    W.tffn = A(768 * (size_t)sT);
+    W.ssl_enc = A(512 * t); W.text_enc = A(512 * (size_t)sT); W.mq = A(512 * t);
+    W.mkv = A(1024 * (size_t)sT); W.mo = A(512 * t);
+    W.stats = A(384 * t); W.z = A(192 * t); W.z2 = A(192 * t); W.fh = A(192 * t);
+    W.fx = A(384 * t); W.fa = A(192 * t); W.fskip = A(192 * t); W.fm = A(96 * t);
+    W.gcond = A(4 * 1536); W.dcond = A(1024); W.ge = A(1024); W.pe_ge = A(1024); W.sv = A(1024);
+    W.g0 = A(g); W.g1 = A(g); W.g2 = A(g); W.g3 = A(g); W.g4 = A(g);
+    if (f > 0) {
+        W.pad = A((size_t)f * 640 + 2048 + 1408);
+        W.reim = A((size_t)f * 1408); W.spec = A((size_t)f * 704);
+        W.r0 = A((size_t)f * 1024); W.r1 = A((size_t)f * 128); W.r2 = A((size_t)f * 128);
+        W.r3 = A((size_t)f * 256); W.rq = A((size_t)f * 384); W.ratt = A((size_t)f * 128);
+    }
+    if (!W.g4) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
+    W.cap_t = t; W.cap_text = sT; W.cap_gen = g; W.cap_spec = f;
+    return 0;
+}
+
+int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int G,
+                            const float* ref_audio, int n_audio, const float* ge_in,
+                            const float* ge_adv_in, const float* eps, float noise_scale, float* audio,
+                            hipStream_t s) {
+    const VitsWeights& V = vits;
+    if (!V.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
+    if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
+    const bool pp = version == GSV_V2PP;
+    if (pp ? (!ge_in || !ge_adv_in) : !ref_audio) return set_error(GSV_E_ARG, "missing conditioning input");
+    const int T = 2 * G, S = n_text;
+    if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
+    if (int r = ensure_vits_ws(this, T, S, pp ? 0 : n_audio)) return r;
+    VitsWorkspace& W = vws;
+    if (timing) hipEventRecord(ev[4], s);
+    // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
+    const float* ge;
+    const float* ge_m;
+    if (!pp) {
+        run_ref_enc(this, V.ref, ref_audio, n_audio, W.ge, s);
+        ge = W.ge;
+        ge_m = W.ge;
+    } else {
+        ge = ge_in;
+        ge_m = ge_adv_in;
+    }
+    // ---- enc_p: codebook decode x2, ssl_proj, encoder_ssl
+    codebook_upsample2(sem, G, V.codebook, W.q, s);
+    conv1d(cargs(V.ssl_proj, W.q, T, W.y), s);
+    attn_encoder(this, V.enc_ssl, W.y, T, W.qkv, W.att, W.a, W.ffn, s);
+    embed_channels(text_seq, S, V.text_emb, 192, W.te, s);
+    attn_encoder(this, V.enc_text, W.te, S, W.tqkv, W.tatt, W.ta, W.tffn, s);
+    // ---- MRTE
+    conv1d(cargs(V.c_pre, W.y, T, W.ssl_enc), s);
+    conv1d(cargs(V.text_pre, W.te, S, W.text_enc), s);
+    conv1d(cargs(V.mrte_qkv_q, W.ssl_enc, T, W.mq), s);
+    conv1d(cargs(V.mrte_kv, W.text_enc, S, W.mkv), s);
+    MhaArgs m{};
+    m.q = W.mq; m.q_ts = 1; m.q_cs = T;
+    m.k = W.mkv; m.k_ts = 1; m.k_cs = S;
+    m.v = W.mkv + (size_t)512 * S; m.v_ts = 1; m.v_cs = S;
+    m.out = W.mo; m.o_ts = 1; m.o_cs = T;
+    m.nq = T; m.nk = S; m.heads = 4; m.dk = 128; m.postdiv = 0; m.scale = std::sqrt(128.0f);
+    mha(m, s);
+    ConvArgs co = cargs(V.mrte_o, W.mo, T, W.a, CV_RESID_VEC);
+    co.res = W.ssl_enc; co.vec = ge_m;
+    conv1d(co, s);
+    conv1d(cargs(V.c_post, W.a, T, W.y), s);
+    attn_encoder(this, V.enc2, W.y, T, W.qkv, W.att, W.a, W.ffn, s);
+    conv1d(cargs(V.proj, W.y, T, W.stats), s);
+    // ---- z_p = m_p + eps*exp(logs_p)*noise_scale
+    noise_zp(W.stats, W.stats + (size_t)192 * T, eps, noise_scale, W.z, 192 * T, s);
+    // ---- reverse flow: for f = 6,4,2,0: flip, coupling (mean-only)
+    for (int fi = 3; fi >= 0; --fi) {
+        const auto& fl = V.flows[fi];
+        flip_channels(W.z, W.z2, 192, T, s);
+        // cond: g = cond_layer(ge) [1536]
+        ConvArgs gc = cargs(fl.cond, ge, 1, W.gcond);
+        conv1d(gc, s);
+        conv1d(cargs(fl.pre, W.z2, T, W.fh), s);                 // h = pre(x0)   (x0 = first 96 ch)
+        hipMemsetAsync(W.fskip, 0, (size_t)192 * T * 4, s);
+        for (int l = 0; l < 4; ++l) {
+            ConvArgs ci = cargs(fl.in_l[l], W.fh, T, W.fx, CV_VEC);
+            ci.vec = W.gcond + l * 384;
+            conv1d(ci, s);
+            wn_gate(W.fx, W.fa, 192, T, s);
+            if (l < 3) {
+                ConvArgs rs = cargs(fl.rs[l], W.fa, T, W.fh, CV_SPLIT_RESID);
+                rs.res = W.fh; rs.split = 192; rs.out2 = W.fskip; rs.res2 = W.fskip;
+                conv1d(rs, s);
+            } else {
+                ConvArgs rs = cargs(fl.rs[l], W.fa, T, W.fskip, CV_RESID);
+                rs.res = W.fskip;
+                conv1d(rs, s);
+            }
+        }
+        // x1 = x1 - post(skip); z = cat(x0, x1)
+        ConvArgs po = cargs(fl.post, W.fskip, T, W.z2 + (size_t)96 * T, CV_SUB);
+        po.res = W.z2 + (size_t)96 * T;
+        conv1d(po, s);
+        float* t = W.z; W.z = W.z2; W.z2 = t;
+    }
+    // ---- generator
+    {
+        float* x = W.g0;
+        // x = conv_pre(z) + cond(ge)   (dec#: Conv -> Add(cond))
+        conv1d(cargs(V.cond, ge, 1, W.dcond), s);
+        ConvArgs c2 = cargs(V.conv_pre, W.z, T, x, CV_VEC);
+        c2.vec = W.dcond;
+        conv1d(c2, s);
+        int C = V.upc, Tc = T;
+        float* bufs[4] = {W.g1, W.g2, W.g3, W.g4};
+        for (int i = 0; i < 5; ++i) {
+            const Conv& up = V.ups[i];
+            const int u = V.up_rate[i], kfull = V.up_k[i], padT = (kfull - u) / 2;
+            const int Tn = (Tc - 1) * u - 2 * padT + kfull;
+            float* yb = bufs[0];
+            ConvArgs ct{};
+            ct.x = x; ct.x_cs = Tc; ct.x_ts = 1; ct.Cin = C; ct.Tin = Tc;
+            ct.w = up.w; ct.Cout = up.cout; ct.K = up.k; ct.dil = 1; ct.pad = up.k - 1;
+            ct.bias = up.b; ct.out = yb; ct.o_cs = Tn; ct.o_ts = 1;
+            ct.n_t = (Tn + padT + u - 1) / u; ct.o_tstride = u; ct.o_toff = -padT; ct.o_len = Tn;
+            ct.in_act = 1; ct.in_slope = 0.1f; ct.mode = CV_STORE;
+            ct.phases = u; ct.w_phase_stride = (long)up.cout * up.cin * up.k;
+            conv1d(ct, s);
+            C = up.cout;
+            Tc = Tn;
+            float* rbuf = bufs[1];
+            float* xt = bufs[2];
+            float* accb = bufs[3];
+            for (int j = 0; j < 3; ++j) {
+                const int kk = V.rb_k[j];
+                const float* rcur = yb;
+                for (int mi = 0; mi < 3; ++mi) {
+                    const int d = V.rb_d[mi];
+                    const Conv& c1 = V.rb[i * 3 + j][0][mi];
+                    const Conv& c2w = V.rb[i * 3 + j][1][mi];
+                    ConvArgs a1 = cargs(c1, rcur, Tc, xt);
+                    a1.dil = d; a1.pad = (kk * d - d) / 2; a1.in_act = 1; a1.in_slope = 0.1f;
+                    conv1d(a1, s);
+                    ConvArgs a2 = cargs(c2w, xt, Tc, rbuf);
+                    a2.in_act = 1; a2.in_slope = 0.1f; a2.res = rcur;
+                    if (mi < 2) {
+                        a2.mode = CV_RESID;
+                    } else if (j == 0) {
+                        a2.mode = CV_ACC_FIRST; a2.acc = accb;
+                    } else if (j == 1) {
+                        a2.mode = CV_ACC_ADD; a2.acc = accb;
+                    } else {
+                        a2.mode = CV_ACC_MEAN; a2.acc = accb; a2.div = 3.0f; a2.out = x;
+                    }
+                    conv1d(a2, s);
+                    rcur = rbuf;
+                }
+            }
+        }
+        ConvArgs cp = cargs(V.conv_post, x, Tc, audio, CV_TANH);
+        cp.in_act = 1; cp.in_slope = 0.01f;
+        conv1d(cp, s);
+    }
+    if (timing) {
+        hipEventRecord(ev[5], s);
+        hipEventSynchronize(ev[5]);
+        hipEventElapsedTime(&ms[3], ev[4], ev[5]);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vits launch");
+}
+
+int gsv_engine::prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
+                              float* ge_adv, hipStream_t s) {
+    if (!penc.ready) return set_error(GSV_E_STATE, "prompt encoder weights not loaded");
+    if (n_audio < 2048) return set_error(GSV_E_ARG, "reference audio too short");
+    if (int r = ensure_vits_ws(this, 2, 2, n_audio)) return r;
+    VitsWorkspace& W = vws;
+    run_ref_enc(this, penc.ref, ref_audio, n_audio, W.pe_ge, s);
+    // ge = PReLU(ref_enc + (sv_emb @ W^T + b)); ge_adv = ge @ W512^T + b  (prompt_encoder#269-280)
+    GemmArgs g{};
+    g.M = 1; g.N = 1024; g.K = 20480; g.A = sv_emb; g.lda = 20480;
+    g.W = penc.sv_w; g.ldw = 20480; g.w_f16 = 1; g.bias = penc.sv_b; g.C = W.sv; g.ldc = 1024;
+    g.mode = EPI_STORE;
+    gemm_nt(g, s);
+    add_vec(W.pe_ge, W.sv, W.pe_ge, 1024, s);
+    prelu_vec(W.pe_ge, penc.prelu, ge, 1024, s);
+    GemmArgs a{};
+    a.M = 1; a.N = 512; a.K = 1024; a.A = ge; a.lda = 1024; a.W = penc.to512_w; a.ldw = 1024;
+    a.bias = penc.to512_b; a.C = ge_adv; a.ldc = 512; a.mode = EPI_STORE;
+    gemm_nt(a, s);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "prompt encoder launch");
+}
+
 extern "C" int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
                                const int64_t* sem, int32_t n_sem, const float* ref_audio,
                                int32_t n_audio, const float* ge, const float* ge_adv,
                                const float* eps, float noise_scale, float* audio, void* stream) {
     if (!eng) return set_error(GSV_E_ARG, "null engine");
     hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    StreamScope sc(eng, stream);
     return eng->vits_decode(text_seq, n_text, sem, n_sem, ref_audio, n_audio, ge, ge_adv, eps,
-                            noise_scale, audio, stream ? (hipStream_t)stream : eng->stream);
+                            noise_scale, audio, sc.st());
 }
+
 extern "C" int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
                                  const float* sv_emb, float* ge, float* ge_adv, void* stream) {
     if (!eng) return set_error(GSV_E_ARG, "null engine");
     hipSetDevice(eng->device);
-    return eng->prompt_encode(ref_audio, n_audio, sv_emb, ge, ge_adv,
-                              stream ? (hipStream_t)stream : eng->stream);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    StreamScope sc(eng, stream);
+    return eng->prompt_encode(ref_audio, n_audio, sv_emb, ge, ge_adv, sc.st());
+}
+
+// ---------------------------------------------------------------- debug hooks
+extern "C" int gsv_debug_copy(gsv_engine* eng, const char* name, float* dst, int64_t n, void* stream) {
+    if (!eng || !name || !dst) return set_error(GSV_E_ARG, "null arg");
+    const VitsWorkspace& W = eng->vws;
+    const std::string nm(name);
+    const float* src = nm == "ge" ? W.ge : nm == "stats" ? W.stats : nm == "z" ? W.z
+                     : nm == "y" ? W.y : nm == "q" ? W.q : nm == "te" ? W.te : nm == "g0" ? W.g0
+                     : nm == "g1" ? W.g1 : nm == "spec" ? W.spec : nm == "a" ? W.a : nullptr;
+    if (!src) return set_error(GSV_E_ARG, "unknown debug buffer " + nm);
+    StreamScope sc(eng, stream);
+    return hipMemcpyAsync(dst, src, (size_t)n * 4, hipMemcpyDeviceToDevice, sc.st()) == hipSuccess
+               ? 0 : set_error(GSV_E_HIP, "debug copy");
+}
+
+extern "C" int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout, int k,
+                                int dil, int pad, const float* bias, float* out, int tout,
+                                int in_act, float slope, void* stream) {
+    ConvArgs a{};
+    a.x = x; a.x_cs = tin; a.x_ts = 1; a.Cin = cin; a.Tin = tin;
+    a.w = w; a.Cout = cout; a.K = k; a.dil = dil; a.pad = pad; a.bias = bias;
+    a.out = out; a.o_cs = tout; a.o_ts = 1; a.n_t = tout; a.o_tstride = 1; a.o_toff = 0; a.o_len = tout;
+    a.in_act = in_act; a.in_slope = slope; a.mode = CV_STORE; a.phases = 1;
+    conv1d(a, (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "debug conv");
 }

@@ -77,6 +77,10 @@ def lib():
                                       ctypes.POINTER(ctypes.c_int32), vp]
         L.gsv_vits_decode.argtypes = [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, ctypes.c_float, vp, vp]
         L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
+        L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_float, vp]
         L.gsv_set_timing.argtypes = [vp, ctypes.c_int]
         L.gsv_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         _lib = L
@@ -87,7 +91,7 @@ EXPORTED = (
     "gsv_last_error", "gsv_version", "gsv_engine_create", "gsv_engine_destroy", "gsv_set_weight",
     "gsv_finalize_weights", "gsv_reserve", "gsv_t2s_encode", "gsv_t2s_generate", "gsv_t2s_prefill",
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
-    "gsv_set_timing", "gsv_get_timing",
+    "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
 )
 
 
@@ -110,6 +114,18 @@ def _stream():
 
 def _ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def debug_conv1d(x, w, bias=None, dil=1, pad=0, in_act=False, slope=0.1):
+    """Run the engine's conv1d kernel once (tests): x [Cin,T], w [Cout,Cin,K] cuda fp32."""
+    torch = _torch()
+    cin, tin = x.shape
+    cout, _, k = w.shape
+    tout = tin + 2 * pad - dil * (k - 1)
+    out = torch.empty((cout, tout), dtype=torch.float32, device=x.device)
+    _check(lib().gsv_debug_conv1d(_ptr(x), cin, tin, _ptr(w), cout, k, dil, pad, _ptr(bias), _ptr(out),
+                                  tout, int(in_act), ctypes.c_float(slope), _stream()), "gsv_debug_conv1d")
+    return out
 
 
 class Engine:
@@ -271,6 +287,12 @@ class Engine:
         _check(lib().gsv_prompt_encode(self.h, _ptr(ra), ra.numel(), _ptr(sv), _ptr(ge), _ptr(ga),
                                        _stream()), "gsv_prompt_encode")
         return ge, ga
+
+    def debug_copy(self, name: str, n: int):
+        t = self.torch
+        out = t.empty((n,), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_debug_copy(self.h, name.encode(), _ptr(out), n, _stream()), "gsv_debug_copy")
+        return out
 
     def set_timing(self, on: bool = True):
         _check(lib().gsv_set_timing(self.h, int(on)), "gsv_set_timing")

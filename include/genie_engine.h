@@ -23,7 +23,10 @@
  *   - Weights are engine-owned device memory.  Every other pointer argument
  *     marked (device) is a caller-owned device buffer (e.g. a torch tensor's
  *     data_ptr()); (host) arguments are read before the call returns.
- *   - `stream` is a hipStream_t passed as void* (NULL = engine's stream).
+ *   - `stream` is the caller's hipStream_t passed as void* (NULL = the HIP null
+ *     stream).  The engine runs on its own stream (so its decode loop can be
+ *     graph-captured), ordered after `stream` on entry and before it on exit
+ *     by events: results are stream-ordered for the caller.
  *     Calls on one engine are serialised by the caller (one engine per GPU
  *     process, as the reference serialises on its single TTS worker thread,
  *     Core/TTSPlayer.py:55).
@@ -137,6 +140,14 @@ int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */
 int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
                       const float* sv_emb, float* ge, float* ge_adv, void* stream);
+
+/* Debug hooks (tests only): copy a named VITS workspace buffer after
+ * gsv_vits_decode ("ge","stats","z","y","q","te","g0","g1","spec","a");
+ * run one conv1d (zero padding) on device buffers. */
+int gsv_debug_copy(gsv_engine* eng, const char* name, float* dst, int64_t n, void* stream);
+int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout, int k, int dil,
+                     int pad, const float* bias, float* out, int tout, int in_act, float slope,
+                     void* stream);
 
 /* Per-phase device time of the last gsv_t2s_generate / gsv_vits_decode (ms):
  * [0]=encode [1]=prefill [2]=decode [3]=vits.  Filled when timing is enabled. */
