@@ -71,3 +71,51 @@ __device__ __forceinline__ uint4 philox4x32(uint4 ctr, uint2 key) {
 __device__ __forceinline__ float u01_open(uint32_t x) {   // (0, 1]
     return (float)((x >> 8) + 1) * (1.0f / 16777216.0f);
 }
+
+// ----------------------------------------------------------------------
+// LayerNorm statistics over 512 values held 2 per thread, single reduction
+// (Chan et al. pairwise merge of (mean, M2)), for up to NB rows at once.
+// ----------------------------------------------------------------------
+template <int NB>
+__device__ __forceinline__ void block_meanvar512(const float (&v0)[NB], const float (&v1)[NB], int B,
+                                                 float (&mean)[NB], float (&rstd_den)[NB],
+                                                 float* red /* >= 4*NB*2 */) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= B) break;
+        float mu = 0.5f * (v0[b] + v1[b]);
+        const float d = v0[b] - v1[b];
+        float m2 = 0.5f * d * d;
+        float n = 2.f;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float mu_o = __shfl_xor(mu, o, 64);
+            const float m2_o = __shfl_xor(m2, o, 64);
+            const float dl = mu_o - mu;
+            m2 = m2 + m2_o + dl * dl * (n * 0.5f);   // equal counts: nA nB / (nA+nB) = n/2
+            mu = mu + dl * 0.5f;
+            n *= 2.f;
+        }
+        if (lane == 0) { red[(w * NB + b) * 2] = mu; red[(w * NB + b) * 2 + 1] = m2; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= B) break;
+        float mu = red[b * 2], m2 = red[b * 2 + 1], n = 128.f;
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) {
+            const float mo = red[(ww * NB + b) * 2], m2o = red[(ww * NB + b) * 2 + 1];
+            const float dl = mo - mu;
+            // merge (n, mu, m2) with (128, mo, m2o)
+            const float nt = n + 128.f;
+            mu = mu + dl * (128.f / nt);
+            m2 = m2 + m2o + dl * dl * (n * 128.f / nt);
+            n = nt;
+        }
+        mean[b] = mu;
+        rstd_den[b] = sqrtf(m2 * (1.0f / 512.0f) + 1e-5f);
+    }
+}
+

@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -53,6 +54,8 @@ void gsv_engine::release_all() {
 gsv_engine::~gsv_engine() {
     release_all();
     if (own_stream && stream) hipStreamDestroy(stream);
+    if (done_host) hipHostFree(done_host);
+    for (auto& e : poll_ev) if (e) hipEventDestroy(e);
     for (auto& e : ev) if (e) hipEventDestroy(e);
     if (ev_in) hipEventDestroy(ev_in);
     if (ev_out) hipEventDestroy(ev_out);
@@ -84,6 +87,19 @@ __half* gsv_engine::up_f16(const std::string& n, int* err) {
     return d;
 }
 
+__half* gsv_engine::up_f16_t(const std::string& n, int* err) {
+    const Staged* s = find(n);
+    if (!s || s->dims.size() != 2) { *err = set_error(GSV_E_WEIGHT, "missing 2-D weight " + n); return nullptr; }
+    const size_t R = s->dims[0], C = s->dims[1];
+    std::vector<__half> h(R * C);
+    for (size_t r = 0; r < R; ++r)
+        for (size_t c = 0; c < C; ++c) h[c * R + r] = __float2half(s->data[r * C + c]);
+    __half* d = (__half*)dalloc(h.size() * 2);
+    if (!d) { *err = set_error(GSV_E_HIP, "hipMalloc failed for " + n); return nullptr; }
+    hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    return d;
+}
+
 static std::vector<float> default_div_term() {
     // exp(-2i ln(1e4)/512) in fp32; a character directory may override it with
     // the exact constant of its own graph ("pe.div_term").
@@ -100,6 +116,8 @@ int gsv_engine::finalize_t2s() {
     if (const Staged* s = find("pe.div_term"))
         if (s->data.size() == 256) div = s->data;
     pe_max = 4096;
+    if (const char* e = std::getenv("GENIE_FFN_SLICES")) ffn_slices = std::atoi(e) == 32 ? 32 : 64;
+    if (const char* e = std::getenv("GENIE_DECODE_FUSE")) fuse_qkv = std::atoi(e) == 2;
     std::vector<float> pe((size_t)pe_max * 512);
     for (int p = 0; p < pe_max; ++p)
         for (int i = 0; i < 256; ++i) {
@@ -124,6 +142,8 @@ int gsv_engine::finalize_t2s() {
         L.w1 = up_f16(p + "linear1.weight", &err);
         L.b1 = up_f32(p + "linear1.bias", &err);
         L.w2 = up_f16(p + "linear2.weight", &err);
+        L.woT = up_f16_t(p + "self_attn.out_proj.weight", &err);
+        L.w2T = up_f16_t(p + "linear2.weight", &err);
         L.b2 = up_f32(p + "linear2.bias", &err);
         L.n1w = up_f32(p + "norm1.weight", &err);
         L.n1b = up_f32(p + "norm1.bias", &err);
@@ -184,6 +204,8 @@ int gsv_engine::reserve(int batch, int tokens) {
     o = (float*)A((size_t)nb * 512 * 4);
     f = (float*)A((size_t)nb * 2048 * 4);
     logits = (float*)A((size_t)nb * 1025 * 4);
+    attn_part = (float*)A((size_t)16 * nb * 512 * 4);
+    ffn_part = (float*)A((size_t)64 * nb * 512 * 4);
     ident = (int*)A(nb * 4);
     pH = (float*)A((size_t)nt * 512 * 4);
     pQ = (float*)A((size_t)nt * 512 * 4);
@@ -344,42 +366,95 @@ SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
 void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st) {
     const long sstride = (long)16 * tmax * 32;
     decode_embed(B, y, tmax, ny, emb_audio, alpha_audio, pe_tab, h, done, st);
-    for (int l = 0; l < 24; ++l) {
-        const T2SLayerW& W = layers[l];
-        GemvArgs a{};
-        a.B = B; a.N = 1536; a.K = 512;
-        if (l == 0) { a.src = h; a.lds = 512; }
-        else { a.src = s2; a.lds = 512; a.ln_g = layers[l - 1].n2w; a.ln_b = layers[l - 1].n2b; a.ln_out = h; }
-        a.W = W.w_in; a.bias = W.b_in; a.C = q; a.ldc = 512; a.mode = EPI_QKV;
-        a.kv.k = kcache[l]; a.kv.v = vcache[l]; a.kv.tmax = tmax; a.kv.row_pos = kvlen;
-        a.kv.seq_stride = sstride; a.kv.row_skip = done;
-        gemv_f16(a, st);
-        AttnArgs at{};
-        at.q = q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l]; at.seq_stride = sstride;
-        at.tmax = tmax; at.row_len = kvlen; at.row_seq = ident; at.out = o; at.ldo = 512;
-        at.rows = B; at.scale = qk_scale; at.row_skip = done;
-        attn_rows_plus(at, 1, st);
-        GemvArgs c{};
-        c.B = B; c.N = 512; c.K = 512; c.src = o; c.lds = 512;
-        c.W = W.w_out; c.bias = W.b_out; c.C = s1; c.ldc = 512; c.mode = EPI_RESID;
-        c.res = h; c.ldr = 512;
-        gemv_f16(c, st);
-        GemvArgs f1{};
-        f1.B = B; f1.N = 2048; f1.K = 512; f1.src = s1; f1.lds = 512;
-        f1.ln_g = W.n1w; f1.ln_b = W.n1b; f1.ln_out = h1;
-        f1.W = W.w1; f1.bias = W.b1; f1.C = f; f1.ldc = 2048; f1.mode = EPI_RELU;
-        gemv_f16(f1, st);
-        GemvArgs f2{};
-        f2.B = B; f2.N = 512; f2.K = 2048; f2.src = f; f2.lds = 2048;
-        f2.W = W.w2; f2.bias = W.b2; f2.C = s2; f2.ldc = 512; f2.mode = EPI_RESID;
-        f2.res = h1; f2.ldr = 512;
-        gemv_f16(f2, st);
+    if (B <= 8 && tmax <= 1024) {
+        // fused path: 2 launches per layer (QKV+attention+out-proj | FFN1+FFN2)
+        for (int l = 0; l < 24; ++l) {
+            const T2SLayerW& W = layers[l];
+            if (fuse_qkv) {
+                QkvAttnArgs qa{};
+                qa.B = B;
+                if (l == 0) {
+                    qa.src = h;
+                } else {
+                    qa.part = ffn_part; qa.n_part = ffn_slices; qa.part_stride = (long)B * 512;
+                    qa.part_bias = layers[l - 1].b2; qa.part_res = h1;
+                    qa.ln_g = layers[l - 1].n2w; qa.ln_b = layers[l - 1].n2b; qa.ln_out = h;
+                }
+                qa.W_in = W.w_in; qa.b_in = W.b_in; qa.k = kcache[l]; qa.v = vcache[l];
+                qa.seq_stride = sstride; qa.tmax = tmax; qa.kvlen = kvlen; qa.done = done;
+                qa.scale = qk_scale; qa.WoT = W.woT; qa.attn_part = attn_part;
+                qkv_attn_outproj(qa, st);
+            } else {
+                GemvArgs a{};
+                a.B = B; a.N = 1536; a.K = 512;
+                if (l == 0) {
+                    a.src = h; a.lds = 512;
+                } else {
+                    a.part = ffn_part; a.n_part = ffn_slices; a.part_stride = (long)B * 512;
+                    a.part_bias = layers[l - 1].b2; a.part_res = h1;
+                    a.ln_g = layers[l - 1].n2w; a.ln_b = layers[l - 1].n2b; a.ln_out = h;
+                }
+                a.W = W.w_in; a.bias = W.b_in; a.C = q; a.ldc = 512; a.mode = EPI_QKV;
+                a.kv.k = kcache[l]; a.kv.v = vcache[l]; a.kv.tmax = tmax; a.kv.row_pos = kvlen;
+                a.kv.seq_stride = sstride; a.kv.row_skip = done;
+                gemv_f16(a, st);
+                AttnOutArgs ao{};
+                ao.B = B; ao.q = q; ao.k = kcache[l]; ao.v = vcache[l]; ao.seq_stride = sstride;
+                ao.tmax = tmax; ao.kvlen = kvlen; ao.done = done; ao.scale = qk_scale;
+                ao.WoT = W.woT; ao.part = attn_part;
+                attn_outproj(ao, st);
+            }
+            FfnArgs fa{};
+            fa.B = B; fa.nslices = ffn_slices; fa.h = h; fa.bo = W.b_out; fa.attn_part = attn_part;
+            fa.ln_g = W.n1w; fa.ln_b = W.n1b; fa.h1 = h1;
+            fa.W1 = W.w1; fa.b1 = W.b1; fa.W2T = W.w2T; fa.part = ffn_part;
+            ffn_fused(fa, st);
+        }
+        GemvArgs lg{};
+        lg.B = B; lg.N = 1025; lg.K = 512;
+        lg.part = ffn_part; lg.n_part = ffn_slices; lg.part_stride = (long)B * 512;
+        lg.part_bias = layers[23].b2; lg.part_res = h1;
+        lg.ln_g = layers[23].n2w; lg.ln_b = layers[23].n2b;
+        lg.W = w_pred; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
+        gemv_f16(lg, st);
+    } else {
+        // batched path: f32-MFMA GEMMs over the B rows + row LayerNorms
+        for (int l = 0; l < 24; ++l) {
+            const T2SLayerW& W = layers[l];
+            if (l > 0) layernorm_rows(s2, h, B, layers[l - 1].n2w, layers[l - 1].n2b, st);
+            GemmArgs g{};
+            g.M = B; g.N = 1536; g.K = 512; g.A = h; g.lda = 512;
+            g.W = W.w_in; g.ldw = 512; g.w_f16 = 1; g.bias = W.b_in; g.C = q; g.ldc = 512;
+            g.mode = EPI_QKV; g.kv.k = kcache[l]; g.kv.v = vcache[l]; g.kv.tmax = tmax;
+            g.kv.row_pos = kvlen; g.kv.row_seq = ident; g.kv.seq_stride = sstride; g.kv.row_skip = done;
+            gemm_nt(g, st);
+            AttnArgs at{};
+            at.q = q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l]; at.seq_stride = sstride;
+            at.tmax = tmax; at.row_len = kvlen; at.row_seq = ident; at.out = o; at.ldo = 512;
+            at.rows = B; at.scale = qk_scale; at.row_skip = done;
+            attn_rows_plus(at, 1, st);
+            GemmArgs go{};
+            go.M = B; go.N = 512; go.K = 512; go.A = o; go.lda = 512; go.W = W.w_out; go.ldw = 512;
+            go.w_f16 = 1; go.bias = W.b_out; go.C = s1; go.ldc = 512; go.mode = EPI_RESID;
+            go.res = h; go.ldr = 512;
+            gemm_nt(go, st);
+            layernorm_rows(s1, h1, B, W.n1w, W.n1b, st);
+            GemmArgs g1{};
+            g1.M = B; g1.N = 2048; g1.K = 512; g1.A = h1; g1.lda = 512; g1.W = W.w1; g1.ldw = 512;
+            g1.w_f16 = 1; g1.bias = W.b1; g1.C = f; g1.ldc = 2048; g1.mode = EPI_RELU;
+            gemm_nt(g1, st);
+            GemmArgs g2{};
+            g2.M = B; g2.N = 512; g2.K = 2048; g2.A = f; g2.lda = 2048; g2.W = W.w2; g2.ldw = 2048;
+            g2.w_f16 = 1; g2.bias = W.b2; g2.C = s2; g2.ldc = 512; g2.mode = EPI_RESID;
+            g2.res = h1; g2.ldr = 512;
+            gemm_nt(g2, st);
+        }
+        layernorm_rows(s2, h, B, layers[23].n2w, layers[23].n2b, st);
+        GemmArgs lg{};
+        lg.M = B; lg.N = 1025; lg.K = 512; lg.A = h; lg.lda = 512; lg.W = w_pred; lg.ldw = 512;
+        lg.w_f16 = 1; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
+        gemm_nt(lg, st);
     }
-    GemvArgs lg{};
-    lg.B = B; lg.N = 1025; lg.K = 512; lg.src = s2; lg.lds = 512;
-    lg.ln_g = layers[23].n2w; lg.ln_b = layers[23].n2b;
-    lg.W = w_pred; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
-    gemv_f16(lg, st);
     SampleArgs sa = sampler_args(sp, B);
     sa.logits_out = logits_out; sa.ldlo = 1025;
     sample_tokens(sa, st);
@@ -406,22 +481,44 @@ hipGraphExec_t gsv_engine::step_graph(int B, const gsv_sampler* sp, int chunk, h
 }
 
 int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
+    // Steps are launched as replayed hipGraphs (chunk of 8 steps, tail by 1-step
+    // graphs so forced lengths run no extra step).  The host polls the done flags
+    // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     const int chunk = 8;
-    hipGraphExec_t ex = step_graph(B, sp, chunk, st);
-    if (!ex) return set_error(GSV_E_HIP, "decode graph capture failed");
-    std::vector<uint8_t> hd(B);
-    int launched = 0;
-    while (launched < limit) {
-        if (hipGraphLaunch(ex, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
-        launched += chunk;
-        hipMemcpyAsync(hd.data(), done, B, hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "decode sync");
-        bool all = true;
-        for (int b = 0; b < B; ++b) all = all && hd[b];
-        if (all) break;
+    hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
+    hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
+    if (!ex8 || !ex1) return set_error(GSV_E_HIP, "decode graph capture failed");
+    if (!done_host) {
+        if (hipHostMalloc((void**)&done_host, 2 * 64, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "pinned alloc");
+        for (auto& e : poll_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     }
-    return 0;
+    int launched = 0, k = 0, checked = 0;
+    bool finished = false;
+    while (launched < limit && !finished) {
+        const int n = std::min(chunk, limit - launched);
+        if (n == chunk) {
+            if (hipGraphLaunch(ex8, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
+        } else {
+            for (int i = 0; i < n; ++i)
+                if (hipGraphLaunch(ex1, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
+        }
+        launched += n;
+        const int slot = k & 1;
+        hipMemcpyAsync(done_host + 64 * slot, done, B, hipMemcpyDeviceToHost, st);
+        hipEventRecord(poll_ev[slot], st);
+        ++k;
+        if (k - checked >= 2) {   // inspect the older chunk while the newer one runs
+            const int cs = checked & 1;
+            if (hipEventSynchronize(poll_ev[cs]) != hipSuccess) return set_error(GSV_E_HIP, "poll");
+            bool all = true;
+            for (int b = 0; b < B; ++b) all = all && done_host[64 * cs + b];
+            ++checked;
+            if (all) finished = true;
+        }
+    }
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : set_error(GSV_E_HIP, "decode sync");
 }
 
 // ============================================================ C ABI

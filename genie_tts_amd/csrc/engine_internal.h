@@ -22,6 +22,7 @@ struct Staged {
 
 struct T2SLayerW {
     __half *w_in = nullptr, *w_out = nullptr, *w1 = nullptr, *w2 = nullptr;
+    __half *woT = nullptr, *w2T = nullptr;   // transposed copies for the fused decode path
     float *b_in = nullptr, *b_out = nullptr, *b1 = nullptr, *b2 = nullptr;
     float *n1w = nullptr, *n1b = nullptr, *n2w = nullptr, *n2b = nullptr;
 };
@@ -56,6 +57,9 @@ struct gsv_engine {
     uint32_t* seen = nullptr;
     float *h = nullptr, *h1 = nullptr, *s1 = nullptr, *s2 = nullptr, *q = nullptr, *o = nullptr;
     float *f = nullptr, *logits = nullptr;
+    float *attn_part = nullptr, *ffn_part = nullptr;
+    int ffn_slices = 64;
+    bool fuse_qkv = false;  // 3 launches/layer measured faster than 2 (GENIE_DECODE_FUSE=2 to A/B)
     float *pH = nullptr, *pQ = nullptr, *pO = nullptr, *pS = nullptr, *pH1 = nullptr, *pF = nullptr;
     int* prow_len = nullptr;
     int64_t* prompts_buf = nullptr;
@@ -75,6 +79,8 @@ struct gsv_engine {
     float ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    uint8_t* done_host = nullptr;       // pinned, 2 slots x 64
+    hipEvent_t poll_ev[2] = {};
 
     ~gsv_engine();
     void* dalloc(size_t bytes);
@@ -82,6 +88,7 @@ struct gsv_engine {
     const gsv::Staged* find(const std::string& n) const;
     float* up_f32(const std::string& n, int* err);
     __half* up_f16(const std::string& n, int* err);
+    __half* up_f16_t(const std::string& n, int* err);   // transposed 2-D upload
     int finalize_t2s();
     int finalize_vits();
     int finalize_prompt_encoder();

@@ -85,6 +85,9 @@ void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s);
 struct GemvArgs {
     int B, N, K;
     const float* src; long lds;
+    // optional split-K partial reduce in the prologue (FFN2 partials of the previous layer):
+    //   src[b][k] := part_res[b][k] + (part_bias[k] + sum_j part[j][b][k])
+    const float* part; int n_part; long part_stride; const float* part_bias; const float* part_res;
     const float* ln_g; const float* ln_b; float* ln_out;
     const __half* W;
     const float* bias;
@@ -94,6 +97,50 @@ struct GemvArgs {
     KVScatter kv;
 };
 void gemv_f16(const GemvArgs& a, hipStream_t s);
+
+// Fused decode attention + out-proj partial, one block per (head, sequence):
+//   o_h = softmax((q_h s)(K_h s)^T) V_h over keys [0, kvlen[b] + 1)
+//   part[h][b][n] = sum_d WoT[h*32+d][n] * o_h[d]            (n < 512)
+struct AttnOutArgs {
+    int B;
+    const float* q;                        // [B][512]
+    const float* k; const float* v; long seq_stride; int tmax;
+    const int* kvlen; const uint8_t* done;
+    float scale;
+    const __half* WoT;                     // [512 in][512 out]
+    float* part;                           // [16][B][512]
+};
+void attn_outproj(const AttnOutArgs& a, hipStream_t s);
+
+// Fused QKV + attention + out-proj partial, one block per (head, sequence):
+//   x = layer input (LN2 of the previous layer's reduced FFN partials, or h0);
+//   q,k,v of head h from W_in rows; new k,v appended to the cache at kvlen[b];
+//   attention over [0, kvlen] ; part[h][b] = WoT[h-slice]^T o_h.
+struct QkvAttnArgs {
+    int B;
+    const float* src;                              // layer 0: h0 [B][512]
+    const float* part; int n_part; long part_stride; const float* part_bias; const float* part_res;
+    const float* ln_g; const float* ln_b; float* ln_out;   // ln_out: x for the residual
+    const __half* W_in; const float* b_in;
+    float* k; float* v; long seq_stride; int tmax;
+    const int* kvlen; const uint8_t* done;
+    float scale;
+    const __half* WoT;
+    float* attn_part;                              // [16][B][512]
+};
+void qkv_attn_outproj(const QkvAttnArgs& a, hipStream_t s);
+
+// Fused FFN, split-K over the 2048 hidden units (one slice per block):
+//   s1[b] = h[b] + (bo + sum_h attn_part[h][b]);  x = LN1(s1); block 0 writes h1 = x
+//   f = relu(W1[slice] x + b1[slice]);  part[j][b][n] = sum_{r in slice} W2T[r][n] f_r
+struct FfnArgs {
+    int B, nslices;
+    const float* h; const float* bo; const float* attn_part;   // [16][B][512]
+    const float* ln_g; const float* ln_b; float* h1;
+    const __half* W1; const float* b1; const __half* W2T;      // W2T [2048][512]
+    float* part;                                               // [nslices][B][512]
+};
+void ffn_fused(const FfnArgs& a, hipStream_t s);
 
 // Decode embedding: for active b: tok = y[b][ny[b]-1]; h[b] = E[tok] + alpha*pe[ny[b]]
 void decode_embed(int B, const int64_t* y, long ldy, const int* ny, const __half* emb,

@@ -280,19 +280,24 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a, int len_add) {
     if (tid < 32) qs[tid] = a.q[(long)r * a.ldq + h * 32 + tid] * sc;
     __syncthreads();
     float lmax = -INFINITY;
-    for (int t = tid; t < len; t += 256) {
-        const float4* kr = reinterpret_cast<const float4*>(K + (long)t * 32);
-        float s = 0.f;
+    for (int t0 = 0; t0 < len; t0 += 512) {
+        // two keys per thread in flight
+        const int ta = t0 + tid, tb = t0 + 256 + tid;
+        float4 ka[8], kb[8];
+        const float4* kra = reinterpret_cast<const float4*>(K + (long)min(ta, len - 1) * 32);
+        const float4* krb = reinterpret_cast<const float4*>(K + (long)min(tb, len - 1) * 32);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { ka[i] = kra[i]; kb[i] = krb[i]; }
+        float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const float4 kv = kr[i];
-            s += qs[4 * i] * (kv.x * sc);
-            s += qs[4 * i + 1] * (kv.y * sc);
-            s += qs[4 * i + 2] * (kv.z * sc);
-            s += qs[4 * i + 3] * (kv.w * sc);
+            sa += qs[4 * i] * (ka[i].x * sc); sa += qs[4 * i + 1] * (ka[i].y * sc);
+            sa += qs[4 * i + 2] * (ka[i].z * sc); sa += qs[4 * i + 3] * (ka[i].w * sc);
+            sb += qs[4 * i] * (kb[i].x * sc); sb += qs[4 * i + 1] * (kb[i].y * sc);
+            sb += qs[4 * i + 2] * (kb[i].z * sc); sb += qs[4 * i + 3] * (kb[i].w * sc);
         }
-        p[t] = s;
-        lmax = fmaxf(lmax, s);
+        if (ta < len) { p[ta] = sa; lmax = fmaxf(lmax, sa); }
+        if (tb < len) { p[tb] = sb; lmax = fmaxf(lmax, sb); }
     }
     const float m = block_max(lmax, red);
     float lsum = 0.f;
@@ -306,7 +311,15 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a, int len_add) {
     __syncthreads();
     const int g = tid >> 5, d = tid & 31;
     float acc = 0.f;
-    for (int t = g; t < len; t += 8) acc += p[t] * V[(long)t * 32 + d];
+    int t = g;
+    for (; t + 56 < len; t += 64) {
+        float vv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vv[i] = V[(long)(t + 8 * i) * 32 + d];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += p[t + 8 * i] * vv[i];
+    }
+    for (; t < len; t += 8) acc += p[t] * V[(long)t * 32 + d];
     part[g][d] = acc;
     __syncthreads();
     if (tid < 32) {
@@ -335,19 +348,54 @@ void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s) {
 template <int K, int ROWS, int NB>
 __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     extern __shared__ float xs[];   // [NB][K]
-    __shared__ float red[16];
+    __shared__ float red[64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int B = a.B;
+    // weights first: their HBM latency overlaps the activation load + LN prologue
+    const int nbase = (blockIdx.x * 4 + w) * ROWS;
+    constexpr int KI = K / 512;
+    uint4 wr[ROWS][KI];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        const int n = min(nbase + r, a.N - 1);
+        const __half* wp = a.W + (long)n * K + lane * 8;
+#pragma unroll
+        for (int i = 0; i < KI; ++i) wr[r][i] = *reinterpret_cast<const uint4*>(wp + i * 512);
+    }
     if (a.ln_g) {
-        for (int b = 0; b < B; ++b) {
-            const float* src = a.src + (long)b * a.lds;
-            const float v0 = src[tid], v1 = src[tid + 256];
-            const float mean = block_sum(v0 + v1, red) * (1.0f / 512.0f);
-            const float d0 = v0 - mean, d1 = v1 - mean;
-            const float var = block_sum(d0 * d0 + d1 * d1, red) * (1.0f / 512.0f);
-            const float den = sqrtf(var + 1e-5f);
-            const float o0 = d0 / den * a.ln_g[tid] + a.ln_b[tid];
-            const float o1 = d1 / den * a.ln_g[tid + 256] + a.ln_b[tid + 256];
+        float v0[NB], v1[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b < B) {
+                if (a.part) {
+                    // split-K partial reduce: res + (bias + sum_j part_j), fixed order
+                    float p0 = a.part_bias[tid], p1 = a.part_bias[tid + 256];
+                    for (int j0 = 0; j0 < a.n_part; j0 += 16) {
+                        float q0[16], q1[16];
+#pragma unroll
+                        for (int jj = 0; jj < 16; ++jj) {
+                            const float* pp = a.part + (long)(j0 + jj) * a.part_stride + (long)b * 512;
+                            q0[jj] = pp[tid];
+                            q1[jj] = pp[tid + 256];
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < 16; ++jj) { p0 += q0[jj]; p1 += q1[jj]; }
+                    }
+                    v0[b] = a.part_res[(long)b * 512 + tid] + p0;
+                    v1[b] = a.part_res[(long)b * 512 + tid + 256] + p1;
+                } else {
+                    v0[b] = a.src[(long)b * a.lds + tid];
+                    v1[b] = a.src[(long)b * a.lds + tid + 256];
+                }
+            }
+        }
+        float mean[NB], den[NB];
+        block_meanvar512<NB>(v0, v1, B, mean, den, red);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b >= B) break;
+            const float o0 = (v0[b] - mean[b]) / den[b] * a.ln_g[tid] + a.ln_b[tid];
+            const float o1 = (v1[b] - mean[b]) / den[b] * a.ln_g[tid + 256] + a.ln_b[tid + 256];
             xs[b * K + tid] = o0;
             xs[b * K + tid + 256] = o1;
             if (a.ln_out && blockIdx.x == 0) {
@@ -362,16 +410,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                     *reinterpret_cast<const float4*>(a.src + (long)b * a.lds + i);
     }
     __syncthreads();
-    const int nbase = (blockIdx.x * 4 + w) * ROWS;
-    constexpr int KI = K / 512;
-    uint4 wr[ROWS][KI];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-        const int n = min(nbase + r, a.N - 1);
-        const __half* wp = a.W + (long)n * K + lane * 8;
-#pragma unroll
-        for (int i = 0; i < KI; ++i) wr[r][i] = *reinterpret_cast<const uint4*>(wp + i * 512);
-    }
     float acc[ROWS][NB];
 #pragma unroll
     for (int r = 0; r < ROWS; ++r)

@@ -1,0 +1,428 @@
+// Fused decode-step kernels (B small, latency-bound): one T2S layer of the
+// stage decoder (t2s_stage_decoder_fp32.onnx#43-114 per layer) runs as three
+// launches instead of five:
+//   1. QKV GEMV            prologue: reduce the previous layer's FFN2 split-K
+//                          partials + residual, LayerNorm2 (k_gemv, t2s.hip)
+//   2. attention + out-proj split over heads (this file)
+//   3. FFN1 + FFN2 split over the hidden units; prologue reduces the
+//      out-proj partials + residual, LayerNorm1 (this file)
+// Partial sums are reduced in a fixed order (deterministic).
+#include "common.h"
+#include "kernels.h"
+
+namespace gsv {
+
+// ---------------------------------------------------------------------------
+// Attention (one head, one sequence) + out-projection partial for that head.
+// ---------------------------------------------------------------------------
+#define DEC_KP 4          // keys per thread held in registers (len <= 1024)
+// Reduce-scatter of a 32-vector over the 64 lanes of a wave: afterwards lane l
+// holds sum over all lanes of a[l & 31].
+__device__ __forceinline__ float wave_reduce_scatter32(float (&a)[32]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 16; s >= 1; s >>= 1) {
+        const bool up = (lane & s) != 0;
+#pragma unroll
+        for (int j = 0; j < s; ++j) {
+            const float send = up ? a[j] : a[j + s];
+            const float keep = up ? a[j + s] : a[j];
+            a[j] = keep + __shfl_xor(send, s, 64);
+        }
+    }
+    return a[0] + __shfl_xor(a[0], 32, 64);
+}
+
+// Lane layout: 8 lanes per key row (lane & 7 = 16-byte chunk c of the 128-byte
+// K/V head row), 8 keys per wave instruction, 32 keys per block pass: every
+// load instruction reads 1 KB contiguous.  Each lane keeps an online softmax
+// state (m, l) and the 4 output dims of its chunk.
+__global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
+    __shared__ float os[32];
+    __shared__ float redm[4];
+    __shared__ float redl[4][8];
+    __shared__ float reda[4][32];
+    __shared__ float ored[4][512];
+    const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (a.done && a.done[b]) return;
+    uint4 wo[8];
+    {
+        const __half* base = a.WoT + (long)(h * 32) * 512 + 8 * lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wo[i] = *reinterpret_cast<const uint4*>(base + (long)(w + 4 * i) * 512);
+    }
+    const int len = a.kvlen[b] + 1;
+    const float* K = a.k + (long)b * a.seq_stride + (long)h * a.tmax * 32;
+    const float* V = a.v + (long)b * a.seq_stride + (long)h * a.tmax * 32;
+    const float sc = a.scale;
+    const int c = lane & 7, g = (w << 3) | (lane >> 3);     // chunk, key group (0..31)
+    const float4 qv = *reinterpret_cast<const float4*>(a.q + (long)b * 512 + h * 32 + 4 * c);
+    const float q0 = qv.x * sc, q1 = qv.y * sc, q2 = qv.z * sc, q3 = qv.w * sc;
+    float mt = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+    constexpr int U = 4;
+    for (int base = 0; base < len; base += 32 * U) {
+        float4 kk[U], vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = min(base + u * 32 + g, len - 1);
+            kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
+            vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float sv = q0 * (kk[u].x * sc);
+            sv += q1 * (kk[u].y * sc);
+            sv += q2 * (kk[u].z * sc);
+            sv += q3 * (kk[u].w * sc);
+            sv += __shfl_xor(sv, 1, 64);
+            sv += __shfl_xor(sv, 2, 64);
+            sv += __shfl_xor(sv, 4, 64);
+            if (base + u * 32 + g < len) {          // uniform within the 8-lane group
+                const float mn = fmaxf(mt, sv);
+                const float f = expf(mt - mn);
+                const float p = expf(sv - mn);
+                l = l * f + p;
+                o0 = o0 * f + p * vv[u].x;
+                o1 = o1 * f + p * vv[u].y;
+                o2 = o2 * f + p * vv[u].z;
+                o3 = o3 * f + p * vv[u].w;
+                mt = mn;
+            }
+        }
+    }
+    // block max of the per-group maxima
+    const float bm = wave_max(mt);
+    if (lane == 0) redm[w] = bm;
+    __syncthreads();
+    const float m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    const float fs = mt == -INFINITY ? 0.f : expf(mt - m);
+    l *= fs; o0 *= fs; o1 *= fs; o2 *= fs; o3 *= fs;
+    // sum over the 8 key groups of this wave (lanes with equal chunk c)
+#pragma unroll
+    for (int x = 8; x < 64; x <<= 1) {
+        l += __shfl_xor(l, x, 64);
+        o0 += __shfl_xor(o0, x, 64);
+        o1 += __shfl_xor(o1, x, 64);
+        o2 += __shfl_xor(o2, x, 64);
+        o3 += __shfl_xor(o3, x, 64);
+    }
+    if (lane < 8) {
+        reda[w][4 * lane] = o0; reda[w][4 * lane + 1] = o1;
+        reda[w][4 * lane + 2] = o2; reda[w][4 * lane + 3] = o3;
+        redl[w][lane] = l;
+    }
+    __syncthreads();
+    if (tid < 32) {
+        const float L = (redl[0][0] + redl[1][0]) + (redl[2][0] + redl[3][0]);
+        os[tid] = ((reda[0][tid] + reda[1][tid]) + (reda[2][tid] + reda[3][tid])) / L;
+    }
+    __syncthreads();
+    float r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float wf[8];
+        h8_to_f8(wo[i], wf);
+        const float ov = os[w + 4 * i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += wf[k] * ov;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ored[w][8 * lane + k] = r[k];
+    __syncthreads();
+    float* dst = a.part + ((long)h * a.B + b) * 512;
+    dst[tid] = (ored[0][tid] + ored[1][tid]) + (ored[2][tid] + ored[3][tid]);
+    dst[tid + 256] = (ored[0][tid + 256] + ored[1][tid + 256]) + (ored[2][tid + 256] + ored[3][tid + 256]);
+}
+
+void attn_outproj(const AttnOutArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_attn_out, dim3(16, a.B), dim3(256), 0, s, a);
+}
+
+// ---------------------------------------------------------------------------
+// FFN1 + FFN2 (split-K over hidden units); RPB hidden rows per block.
+// ---------------------------------------------------------------------------
+template <int RPB, int NB>
+__global__ __launch_bounds__(256) void k_ffn(FfnArgs a) {
+    __shared__ float xs[NB][512];
+    __shared__ float fs[NB][RPB];
+    __shared__ float red[4 * NB * 2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int j = blockIdx.x, B = a.B;
+    constexpr int RW = RPB / 4;            // FFN1 rows per wave
+    // prefetch FFN1 rows (one 16 B chunk per lane per row) and the W2T slice
+    uint4 w1r[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+        w1r[r] = *reinterpret_cast<const uint4*>(a.W1 + (long)(j * RPB + w * RW + r) * 512 + lane * 8);
+    // W2T slice rows j*RPB + w + 4*i (i < RPB/4), columns [8*lane, +8)
+    uint4 w2r[RPB / 4];
+#pragma unroll
+    for (int i = 0; i < RPB / 4; ++i)
+        w2r[i] = *reinterpret_cast<const uint4*>(a.W2T + (long)(j * RPB + w + 4 * i) * 512 + 8 * lane);
+    // prologue: s1 = h + (bo + sum_h attn_part[h]); LN1
+    float v0[NB], v1[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= B) break;
+        float p0 = a.bo[tid], p1 = a.bo[tid + 256];
+#pragma unroll
+        for (int hh = 0; hh < 16; ++hh) {
+            const float* pp = a.attn_part + ((long)hh * B + b) * 512;
+            p0 += pp[tid];
+            p1 += pp[tid + 256];
+        }
+        v0[b] = a.h[(long)b * 512 + tid] + p0;
+        v1[b] = a.h[(long)b * 512 + tid + 256] + p1;
+    }
+    float mean[NB], den[NB];
+    block_meanvar512<NB>(v0, v1, B, mean, den, red);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b >= B) break;
+        const float o0 = (v0[b] - mean[b]) / den[b] * a.ln_g[tid] + a.ln_b[tid];
+        const float o1 = (v1[b] - mean[b]) / den[b] * a.ln_g[tid + 256] + a.ln_b[tid + 256];
+        xs[b][tid] = o0;
+        xs[b][tid + 256] = o1;
+        if (j == 0) {
+            a.h1[(long)b * 512 + tid] = o0;
+            a.h1[(long)b * 512 + tid + 256] = o1;
+        }
+    }
+    __syncthreads();
+    // FFN1 rows of this slice
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        float wf[8];
+        h8_to_f8(w1r[r], wf);
+        const int row = j * RPB + w * RW + r;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (b >= B) break;
+            const float4 x0 = *reinterpret_cast<const float4*>(&xs[b][lane * 8]);
+            const float4 x1 = *reinterpret_cast<const float4*>(&xs[b][lane * 8 + 4]);
+            float s = 0.f;
+            s += wf[0] * x0.x; s += wf[1] * x0.y; s += wf[2] * x0.z; s += wf[3] * x0.w;
+            s += wf[4] * x1.x; s += wf[5] * x1.y; s += wf[6] * x1.z; s += wf[7] * x1.w;
+            s = wave_sum(s);
+            if (lane == 0) fs[b][w * RW + r] = fmaxf(a.b1[row] + s, 0.f);
+        }
+    }
+    __syncthreads();
+    // FFN2 partial: each wave sums its rows for 8 columns per lane, then LDS reduce
+    __shared__ float fred[4][512];
+    for (int b = 0; b < B; ++b) {
+        float r8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r8[k] = 0.f;
+#pragma unroll
+        for (int i = 0; i < RPB / 4; ++i) {
+            float wf[8];
+            h8_to_f8(w2r[i], wf);
+            const float fv = fs[b][w + 4 * i];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r8[k] += wf[k] * fv;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) fred[w][8 * lane + k] = r8[k];
+        __syncthreads();
+        float* dst = a.part + ((long)j * B + b) * 512;
+        dst[tid] = (fred[0][tid] + fred[1][tid]) + (fred[2][tid] + fred[3][tid]);
+        dst[tid + 256] = (fred[0][tid + 256] + fred[1][tid + 256]) + (fred[2][tid + 256] + fred[3][tid + 256]);
+        __syncthreads();
+    }
+}
+
+template <int RPB>
+static void launch_ffn(const FfnArgs& a, hipStream_t s) {
+    const int nb = a.B <= 1 ? 1 : a.B <= 2 ? 2 : a.B <= 4 ? 4 : 8;
+    switch (nb) {
+        case 1: hipLaunchKernelGGL((k_ffn<RPB, 1>), dim3(a.nslices), dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_ffn<RPB, 2>), dim3(a.nslices), dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_ffn<RPB, 4>), dim3(a.nslices), dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_ffn<RPB, 8>), dim3(a.nslices), dim3(256), 0, s, a); break;
+    }
+}
+
+void ffn_fused(const FfnArgs& a, hipStream_t s) {
+    if (a.nslices == 64) launch_ffn<32>(a, s);
+    else launch_ffn<64>(a, s);   // nslices == 32
+}
+
+// ---------------------------------------------------------------------------
+// QKV (head slice) + attention + out-proj partial in one launch.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_qkv_attn(QkvAttnArgs a) {
+    __shared__ float xs[512];
+    __shared__ float qkv[3][32];
+    __shared__ float os[32];
+    __shared__ float red[16];
+    __shared__ float redm[4];
+    __shared__ float redl[4][8];
+    __shared__ float reda[4][32];
+    __shared__ float ored[4][512];
+    const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (a.done && a.done[b]) return;
+    // 1. weight prefetch: W_in rows {q,k,v} x (h*32 + w*8 + r), 16 B per lane; WoT slice
+    uint4 wq[3][8];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            wq[m][r] = *reinterpret_cast<const uint4*>(a.W_in + (long)(m * 512 + h * 32 + w * 8 + r) * 512 + lane * 8);
+    uint4 wo[8];
+    {
+        const __half* base = a.WoT + (long)(h * 32) * 512 + 8 * lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wo[i] = *reinterpret_cast<const uint4*>(base + (long)(w + 4 * i) * 512);
+    }
+    // 2. layer input
+    if (a.part) {
+        float p0 = a.part_bias[tid], p1 = a.part_bias[tid + 256];
+        for (int j0 = 0; j0 < a.n_part; j0 += 16) {
+            float q0[16], q1[16];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const float* pp = a.part + (long)(j0 + jj) * a.part_stride + (long)b * 512;
+                q0[jj] = pp[tid];
+                q1[jj] = pp[tid + 256];
+            }
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) { p0 += q0[jj]; p1 += q1[jj]; }
+        }
+        float v0[1] = {a.part_res[(long)b * 512 + tid] + p0};
+        float v1[1] = {a.part_res[(long)b * 512 + tid + 256] + p1};
+        float mean[1], den[1];
+        block_meanvar512<1>(v0, v1, 1, mean, den, red);
+        const float o0 = (v0[0] - mean[0]) / den[0] * a.ln_g[tid] + a.ln_b[tid];
+        const float o1 = (v1[0] - mean[0]) / den[0] * a.ln_g[tid + 256] + a.ln_b[tid + 256];
+        xs[tid] = o0;
+        xs[tid + 256] = o1;
+        if (h == 0) {
+            a.ln_out[(long)b * 512 + tid] = o0;
+            a.ln_out[(long)b * 512 + tid + 256] = o1;
+        }
+    } else {
+        xs[tid] = a.src[(long)b * 512 + tid];
+        xs[tid + 256] = a.src[(long)b * 512 + tid + 256];
+    }
+    __syncthreads();
+    // 3. q, k, v of this head (24 rows per wave)
+    {
+        const float4 x0 = *reinterpret_cast<const float4*>(&xs[lane * 8]);
+        const float4 x1 = *reinterpret_cast<const float4*>(&xs[lane * 8 + 4]);
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                float wf[8];
+                h8_to_f8(wq[m][r], wf);
+                float sacc = 0.f;
+                sacc += wf[0] * x0.x; sacc += wf[1] * x0.y; sacc += wf[2] * x0.z; sacc += wf[3] * x0.w;
+                sacc += wf[4] * x1.x; sacc += wf[5] * x1.y; sacc += wf[6] * x1.z; sacc += wf[7] * x1.w;
+                sacc = wave_sum(sacc);
+                if (lane == 0) {
+                    const int row = m * 512 + h * 32 + w * 8 + r;
+                    qkv[m][w * 8 + r] = a.b_in[row] + sacc;
+                }
+            }
+    }
+    __syncthreads();
+    const int kvl = a.kvlen[b];
+    float* Kc = a.k + (long)b * a.seq_stride + (long)h * a.tmax * 32;
+    float* Vc = a.v + (long)b * a.seq_stride + (long)h * a.tmax * 32;
+    if (tid < 32) Kc[(long)kvl * 32 + tid] = qkv[1][tid];
+    else if (tid < 64) Vc[(long)kvl * 32 + tid - 32] = qkv[2][tid - 32];
+    // 4. attention over [0, kvl] (key kvl taken from LDS)
+    const float sc = a.scale;
+    const int c = lane & 7, g = (w << 3) | (lane >> 3);
+    const float q0 = qkv[0][4 * c] * sc, q1 = qkv[0][4 * c + 1] * sc;
+    const float q2 = qkv[0][4 * c + 2] * sc, q3 = qkv[0][4 * c + 3] * sc;
+    const float4 knew = make_float4(qkv[1][4 * c], qkv[1][4 * c + 1], qkv[1][4 * c + 2], qkv[1][4 * c + 3]);
+    const float4 vnew = make_float4(qkv[2][4 * c], qkv[2][4 * c + 1], qkv[2][4 * c + 2], qkv[2][4 * c + 3]);
+    const int len = kvl + 1;
+    float mt = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+    constexpr int U = 4;
+    for (int base = 0; base < len; base += 32 * U) {
+        float4 kk[U], vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = min(base + u * 32 + g, kvl - 1);
+            kk[u] = *reinterpret_cast<const float4*>(Kc + (long)t * 32 + 4 * c);
+            vv[u] = *reinterpret_cast<const float4*>(Vc + (long)t * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = base + u * 32 + g;
+            if (t == kvl) { kk[u] = knew; vv[u] = vnew; }
+            float sv = q0 * (kk[u].x * sc);
+            sv += q1 * (kk[u].y * sc);
+            sv += q2 * (kk[u].z * sc);
+            sv += q3 * (kk[u].w * sc);
+            sv += __shfl_xor(sv, 1, 64);
+            sv += __shfl_xor(sv, 2, 64);
+            sv += __shfl_xor(sv, 4, 64);
+            if (t < len) {
+                const float mn = fmaxf(mt, sv);
+                const float f = expf(mt - mn);
+                const float p = expf(sv - mn);
+                l = l * f + p;
+                o0 = o0 * f + p * vv[u].x;
+                o1 = o1 * f + p * vv[u].y;
+                o2 = o2 * f + p * vv[u].z;
+                o3 = o3 * f + p * vv[u].w;
+                mt = mn;
+            }
+        }
+    }
+    const float bm = wave_max(mt);
+    if (lane == 0) redm[w] = bm;
+    __syncthreads();
+    const float m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    const float fsc = mt == -INFINITY ? 0.f : expf(mt - m);
+    l *= fsc; o0 *= fsc; o1 *= fsc; o2 *= fsc; o3 *= fsc;
+#pragma unroll
+    for (int x = 8; x < 64; x <<= 1) {
+        l += __shfl_xor(l, x, 64);
+        o0 += __shfl_xor(o0, x, 64);
+        o1 += __shfl_xor(o1, x, 64);
+        o2 += __shfl_xor(o2, x, 64);
+        o3 += __shfl_xor(o3, x, 64);
+    }
+    if (lane < 8) {
+        reda[w][4 * lane] = o0; reda[w][4 * lane + 1] = o1;
+        reda[w][4 * lane + 2] = o2; reda[w][4 * lane + 3] = o3;
+        redl[w][lane] = l;
+    }
+    __syncthreads();
+    if (tid < 32) {
+        const float L = (redl[0][0] + redl[1][0]) + (redl[2][0] + redl[3][0]);
+        os[tid] = ((reda[0][tid] + reda[1][tid]) + (reda[2][tid] + reda[3][tid])) / L;
+    }
+    __syncthreads();
+    // 5. out-proj partial
+    float r8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r8[k] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float wf[8];
+        h8_to_f8(wo[i], wf);
+        const float ov = os[w + 4 * i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r8[k] += wf[k] * ov;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ored[w][8 * lane + k] = r8[k];
+    __syncthreads();
+    float* dst = a.attn_part + ((long)h * a.B + b) * 512;
+    dst[tid] = (ored[0][tid] + ored[1][tid]) + (ored[2][tid] + ored[3][tid]);
+    dst[tid + 256] = (ored[0][tid + 256] + ored[1][tid + 256]) + (ored[2][tid + 256] + ored[3][tid + 256]);
+}
+
+void qkv_attn_outproj(const QkvAttnArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_qkv_attn, dim3(16, a.B), dim3(256), 0, s, a);
+}
+
+}  // namespace gsv

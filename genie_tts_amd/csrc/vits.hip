@@ -15,59 +15,114 @@ namespace gsv {
 
 template <int KT> struct ConvCfg {
     static constexpr int CI = KT == 1 ? 32 : KT == 2 ? 32 : KT <= 4 ? 16 : KT <= 7 ? 8 : 4;
-    static constexpr int KC = CI * KT;            // K-chunk (even)
+    static constexpr int KC = CI * KT;            // K-chunk per pipeline stage (multiple of 4)
 };
 
 #define CONV_BN 64
 #define CONV_BM 64
 #define CONV_XW_MAX 128
 
-template <int KT>
+// Software pipeline: the next K-chunk (input halo tile + weight tile) is loaded
+// into registers while the MFMAs consume the current chunk from LDS; LDS is
+// double-buffered so each chunk costs one barrier.
+template <int KT, bool V4>
 __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
     constexpr int CI = ConvCfg<KT>::CI, KC = ConvCfg<KT>::KC;
-    __shared__ float Xs[CI * CONV_XW_MAX];
-    __shared__ float Ws[CONV_BM][KC + 1];
+    constexpr int NX = (CI * CONV_XW_MAX + 255) / 256;     // input elements per thread (max)
+    constexpr int NW = (CONV_BM * KC / 4 + 255) / 256;     // weight float4 per thread
+    __shared__ float Xs[2][CI * CONV_XW_MAX];
+    __shared__ float Ws[2][CONV_BM][KC + 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w >> 1, wn = w & 1;
     const int t0 = blockIdx.x * CONV_BN, co0 = blockIdx.y * CONV_BM, ph = blockIdx.z;
     const float* W = a.w + (long)ph * a.w_phase_stride;
     const int dil = a.dil;
     const int XW = CONV_BN + (KT - 1) * dil;
+    const long wrow = (long)a.Cin * KT;
+    const int nch = (a.Cin + CI - 1) / CI;
+    float xr[NX];
+    float4 wr[NW];
+
+    auto load = [&](int ci0) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const int e = tid + i * 256;
+            float v = 0.f;
+            if (e < CI * XW) {
+                const int ci = e / XW, u = e - ci * XW;
+                const int tin = t0 - a.pad + u;
+                if (ci0 + ci < a.Cin && tin >= 0 && tin < a.Tin) {
+                    v = a.x[(long)(ci0 + ci) * a.x_cs + (long)tin * a.x_ts];
+                    if (a.in_act) v = v >= 0.f ? v : v * a.in_slope;
+                }
+            }
+            xr[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int e = tid + i * 256;          // float4 index in the 64 x KC tile
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < CONV_BM * KC / 4) {
+                const int r = e / (KC / 4), kc = (e - r * (KC / 4)) * 4;
+                const int co = co0 + r;
+                const long kabs = (long)ci0 * KT + kc;
+                if (co < a.Cout) {
+                    if (V4) {
+                        if (kabs < wrow) v = *reinterpret_cast<const float4*>(W + co * wrow + kabs);
+                    } else {
+                        const float* src = W + co * wrow + kabs;
+                        if (kabs < wrow) v.x = src[0];
+                        if (kabs + 1 < wrow) v.y = src[1];
+                        if (kabs + 2 < wrow) v.z = src[2];
+                        if (kabs + 3 < wrow) v.w = src[3];
+                    }
+                }
+            }
+            wr[i] = v;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const int e = tid + i * 256;
+            if (e < CI * XW) Xs[buf][e] = xr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int e = tid + i * 256;
+            if (e < CONV_BM * KC / 4) {
+                const int r = e / (KC / 4), kc = (e - r * (KC / 4)) * 4;
+                Ws[buf][r][kc] = wr[i].x;
+                Ws[buf][r][kc + 1] = wr[i].y;
+                Ws[buf][r][kc + 2] = wr[i].z;
+                Ws[buf][r][kc + 3] = wr[i].w;
+            }
+        }
+    };
+
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     const int ncol = wn * 32 + (lane & 31);
     const int h = lane >> 5;
-    const long wrow = (long)a.Cin * KT;
-    for (int ci0 = 0; ci0 < a.Cin; ci0 += CI) {
-        // stage input chunk (with pre-activation); zero padding outside [0, Tin)
-        for (int e = tid; e < CI * XW; e += 256) {
-            const int ci = e / XW, u = e - ci * XW;
-            const int tin = t0 - a.pad + u;
-            float v = 0.f;
-            if (ci0 + ci < a.Cin && tin >= 0 && tin < a.Tin) {
-                v = a.x[(long)(ci0 + ci) * a.x_cs + (long)tin * a.x_ts];
-                if (a.in_act) v = v >= 0.f ? v : v * a.in_slope;
-            }
-            Xs[ci * XW + u] = v;
-        }
-        // stage weights [co][kc] for kc in this chunk
-        for (int e = tid; e < CONV_BM * KC; e += 256) {
-            const int r = e / KC, kc = e - r * KC;
-            const int co = co0 + r, ci = ci0 + kc / KT;
-            Ws[r][kc] = (co < a.Cout && ci < a.Cin) ? W[(long)co * wrow + (long)ci0 * KT + kc] : 0.f;
-        }
-        __syncthreads();
-        const int arow = wm * 32 + (lane & 31);
+    const int arow = wm * 32 + (lane & 31);
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) load((c + 1) * CI);
+        const float* xs = Xs[buf];
 #pragma unroll
         for (int kp = 0; kp < KC / 2; ++kp) {
             const int k0 = 2 * kp, k1 = 2 * kp + 1;
             const int off0 = (k0 / KT) * XW + (k0 % KT) * dil;
             const int off1 = (k1 / KT) * XW + (k1 % KT) * dil;
-            const float av = Ws[arow][h ? k1 : k0];
-            const float bv = Xs[(h ? off1 : off0) + ncol];
+            const float av = Ws[buf][arow][h ? k1 : k0];
+            const float bv = xs[(h ? off1 : off0) + ncol];
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
         }
+        if (c + 1 < nch) store(buf ^ 1);
         __syncthreads();
     }
     const int t = t0 + ncol;
@@ -107,45 +162,80 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
     }
 }
 
+template <int KT>
+static void launch_conv(const ConvArgs& a, dim3 grid, hipStream_t s) {
+    const bool v4 = ((a.Cin * KT) % 4 == 0) && ((reinterpret_cast<uintptr_t>(a.w) & 15) == 0) &&
+                    ((a.w_phase_stride % 4) == 0);
+    if (v4) hipLaunchKernelGGL((k_conv1d<KT, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv1d<KT, false>), grid, dim3(256), 0, s, a);
+}
+
 void conv1d(const ConvArgs& a, hipStream_t s) {
     dim3 grid((a.n_t + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM,
               a.phases > 0 ? a.phases : 1);
     switch (a.K) {
-        case 1: hipLaunchKernelGGL(k_conv1d<1>, grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_conv1d<2>, grid, dim3(256), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_conv1d<3>, grid, dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_conv1d<4>, grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(k_conv1d<5>, grid, dim3(256), 0, s, a); break;
-        case 7: hipLaunchKernelGGL(k_conv1d<7>, grid, dim3(256), 0, s, a); break;
-        case 11: hipLaunchKernelGGL(k_conv1d<11>, grid, dim3(256), 0, s, a); break;
+        case 1: launch_conv<1>(a, grid, s); break;
+        case 2: launch_conv<2>(a, grid, s); break;
+        case 3: launch_conv<3>(a, grid, s); break;
+        case 4: launch_conv<4>(a, grid, s); break;
+        case 5: launch_conv<5>(a, grid, s); break;
+        case 7: launch_conv<7>(a, grid, s); break;
+        case 11: launch_conv<11>(a, grid, s); break;
         default: break;   // host validates K
     }
 }
 
 // ----------------------------------------------------------------- LN over C
-// modules.LayerNorm: transpose -> layer_norm(channels, eps 1e-5) -> transpose
-__global__ __launch_bounds__(64) void k_ln_channels(const float* x, const float* y, float* out,
-                                                    int C, int T, const float* g, const float* b) {
-    const int t = blockIdx.x * 64 + threadIdx.x;
-    if (t >= T) return;
+// modules.LayerNorm: transpose -> layer_norm(channels, eps 1e-5) -> transpose.
+// Block = 64 time columns x 4 channel groups; each thread keeps its channel
+// slice in registers (C <= 4*LNC_MAX), coalesced along t.
+#define LNC_MAX 64
+__global__ __launch_bounds__(256) void k_ln_channels(const float* x, const float* y, float* out,
+                                                     int C, int T, const float* g, const float* b) {
+    __shared__ float red[4][64];
+    const int tl = threadIdx.x & 63, cg = threadIdx.x >> 6;
+    const int t = blockIdx.x * 64 + tl;
+    const bool ok = t < T;
+    float v[LNC_MAX];
     float s = 0.f;
-    for (int c = 0; c < C; ++c) s += y ? x[(long)c * T + t] + y[(long)c * T + t] : x[(long)c * T + t];
-    const float mean = s / (float)C;
-    float v = 0.f;
-    for (int c = 0; c < C; ++c) {
-        const float d = (y ? x[(long)c * T + t] + y[(long)c * T + t] : x[(long)c * T + t]) - mean;
-        v += d * d;
+#pragma unroll
+    for (int i = 0; i < LNC_MAX; ++i) {
+        const int c = cg + 4 * i;
+        float xv = 0.f;
+        if (c < C && ok) {
+            xv = x[(long)c * T + t];
+            if (y) xv = xv + y[(long)c * T + t];
+        }
+        v[i] = xv;
+        s += xv;
     }
-    const float den = sqrtf(v / (float)C + 1e-5f);
-    for (int c = 0; c < C; ++c) {
-        const float xv = y ? x[(long)c * T + t] + y[(long)c * T + t] : x[(long)c * T + t];
-        out[(long)c * T + t] = (xv - mean) / den * g[c] + b[c];
+    red[cg][tl] = s;
+    __syncthreads();
+    const float mean = (red[0][tl] + red[1][tl] + red[2][tl] + red[3][tl]) / (float)C;
+    __syncthreads();
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < LNC_MAX; ++i) {
+        const int c = cg + 4 * i;
+        if (c < C) {
+            const float d = v[i] - mean;
+            q += d * d;
+        }
+    }
+    red[cg][tl] = q;
+    __syncthreads();
+    const float den = sqrtf((red[0][tl] + red[1][tl] + red[2][tl] + red[3][tl]) / (float)C + 1e-5f);
+    if (!ok) return;
+#pragma unroll
+    for (int i = 0; i < LNC_MAX; ++i) {
+        const int c = cg + 4 * i;
+        if (c < C) out[(long)c * T + t] = (v[i] - mean) / den * g[c] + b[c];
     }
 }
 
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
                  const float* b, hipStream_t s) {
-    hipLaunchKernelGGL(k_ln_channels, dim3((T + 63) / 64), dim3(64), 0, s, x, y, out, C, T, g, b);
+    hipLaunchKernelGGL(k_ln_channels, dim3((T + 63) / 64), dim3(256), 0, s, x, y, out, C, T, g, b);
 }
 
 // ----------------------------------------------------------------- attention

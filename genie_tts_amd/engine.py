@@ -81,6 +81,8 @@ def lib():
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_float, vp]
+        L.gsv_probe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_float), vp]
         L.gsv_set_timing.argtypes = [vp, ctypes.c_int]
         L.gsv_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         _lib = L
@@ -92,6 +94,7 @@ EXPORTED = (
     "gsv_finalize_weights", "gsv_reserve", "gsv_t2s_encode", "gsv_t2s_generate", "gsv_t2s_prefill",
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
+    "gsv_probe",
 )
 
 
@@ -183,11 +186,12 @@ class Engine:
 
     def make_utt(self, ref_seq, text_seq, ref_bert, text_bert, ssl):
         t = self.torch
-        keep = [self._dev(np.asarray(ref_seq).reshape(-1), t.int64),
-                self._dev(np.asarray(text_seq).reshape(-1), t.int64),
+        flat = lambda a: a.reshape(-1) if isinstance(a, t.Tensor) else np.asarray(a).reshape(-1)
+        keep = [self._dev(flat(ref_seq), t.int64),
+                self._dev(flat(text_seq), t.int64),
                 None if ref_bert is None else self._dev(ref_bert, t.float32),
                 None if text_bert is None else self._dev(text_bert, t.float32),
-                self._dev(np.asarray(ssl).reshape(768, -1), t.float32)]
+                self._dev(ssl, t.float32).reshape(768, -1)]
         u = Utt(keep[0].data_ptr(), keep[0].numel(), keep[1].data_ptr(), keep[1].numel(),
                 0 if keep[2] is None else keep[2].data_ptr(),
                 0 if keep[3] is None else keep[3].data_ptr(),
@@ -293,6 +297,12 @@ class Engine:
         out = t.empty((n,), dtype=t.float32, device=self.dev)
         _check(lib().gsv_debug_copy(self.h, name.encode(), _ptr(out), n, _stream()), "gsv_debug_copy")
         return out
+
+    def probe(self, which: int, batch: int = 1, iters: int = 200) -> float:
+        """Average microseconds per launch of one kernel configuration (see gsv_probe)."""
+        us = ctypes.c_float()
+        _check(lib().gsv_probe(self.h, which, batch, iters, ctypes.byref(us), _stream()), "gsv_probe")
+        return us.value
 
     def set_timing(self, on: bool = True):
         _check(lib().gsv_set_timing(self.h, int(on)), "gsv_set_timing")

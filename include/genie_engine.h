@@ -149,6 +149,13 @@ int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout,
                      int pad, const float* bias, float* out, int tout, int in_act, float slope,
                      void* stream);
 
+/* Probe: replay one kernel configuration `iters` times (hipGraph) between HIP
+ * events on the engine stream; *us = average microseconds per launch.
+ * which: 0/1 empty kernel (1/256 blocks), 2 QKV GEMV (+LN prologue), 3 QKV GEMV,
+ * 4 FFN1 GEMV (+LN), 5 FFN2 GEMV, 6 out-proj GEMV, 7 decode attention,
+ * 8 one full decode step (graph) for batch B.  Requires gsv_reserve(B, ...). */
+int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us, void* stream);
+
 /* Per-phase device time of the last gsv_t2s_generate / gsv_vits_decode (ms):
  * [0]=encode [1]=prefill [2]=decode [3]=vits.  Filled when timing is enabled. */
 int gsv_set_timing(gsv_engine* eng, int enabled);
