@@ -274,8 +274,9 @@ def load_fp16_bin(onnx_path: str, bin_path: str, spec: Spec) -> Dict[str, np.nda
 
     Mirrors `load_session_with_fp16_conversion` (`g/ModelManager.py:59-114`):
     the relinked graph's EXTERNAL (offset, length) pairs address the fp32
-    upcast of the bin, so the fp16 slice is [offset/2, (offset+length)/2).
+    upcast of the bin, so the fp16 slice is elements [offset/4, (offset+length)/4).
     Values are returned as fp16 (lossless; the reference's upcast adds nothing).
+    The fp16 element index of a tensor is offset/4 (fp32 byte offset / 4 B).
     """
     from .onnx_table import read_initializer_table
     table = read_initializer_table(onnx_path)
@@ -289,7 +290,7 @@ def load_fp16_bin(onnx_path: str, bin_path: str, spec: Spec) -> Dict[str, np.nda
             raise ValueError(f"{name}: shape {dims} in graph, expected {shape}")
         if offset is None:
             raise ValueError(f"{name}: not an external initializer")
-        lo, n = offset // 2, length // 4
+        lo, n = offset // 4, length // 4
         if lo + n > raw.size:
             raise ValueError(f"{name}: range exceeds {bin_path}")
         out[name] = raw[lo: lo + n].reshape(shape)

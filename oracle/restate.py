@@ -34,9 +34,19 @@ def pe_div_term(d: int = 512) -> T:
     return torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
 
 
+_DIV_OVERRIDE = None
+
+
+def set_div_term(div) -> None:
+    """Use the exact div_term constant of a graph (e.g. tests/golden/pe_div_term.npy)."""
+    global _DIV_OVERRIDE
+    _DIV_OVERRIDE = None if div is None else torch.as_tensor(np.asarray(div, np.float32))
+
+
 def sine_pe(positions: T, d: int = 512) -> T:
     """Interleaved sin/cos at 1-based positions (`stage#15-30`): pe[2i]=sin, pe[2i+1]=cos."""
-    ang = positions.to(torch.float32).reshape(-1, 1) * pe_div_term(d).reshape(1, -1)
+    div = _DIV_OVERRIDE if _DIV_OVERRIDE is not None else pe_div_term(d)
+    ang = positions.to(torch.float32).reshape(-1, 1) * div.reshape(1, -1)
     return torch.stack([torch.sin(ang), torch.cos(ang)], dim=-1).reshape(-1, d)
 
 

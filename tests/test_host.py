@@ -1,0 +1,69 @@
+"""CPU: host-side semantics and the C ABI library (no GPU calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_trim_semantics():
+    """Inference.py:108-109 then :41-44."""
+    from oracle.restate import trim_tokens
+    y = [5, 6, 7, 100, 200, 300]                 # P=3 prompts, g0=100, loop tokens 200, 300
+    # stop fired at idx=1 (2nd loop step): keep y[-1:] after zeroing the last
+    np.testing.assert_array_equal(trim_tokens(y, 1), np.array([[[0]]]))
+    np.testing.assert_array_equal(trim_tokens(y, 2), np.array([[[200, 0]]]))
+    # idx == 0: y[:, -0:] is the whole y
+    np.testing.assert_array_equal(trim_tokens(y, 0), np.array([[[5, 6, 7, 100, 200, 0]]]))
+    # an EOS inside the kept window truncates at its first occurrence
+    np.testing.assert_array_equal(trim_tokens([1, 2, 1024, 9, 9], 3), np.array([[[1024, 9, 0]]])[..., :0])
+    np.testing.assert_array_equal(trim_tokens([1, 2, 3, 1024, 9], 3), np.array([[[3]]]))
+
+
+def test_engine_trim_matches_oracle():
+    """The C++ trim (gsv_t2s_generate) restates the same rule; check it on the host copy."""
+    from oracle.restate import trim_tokens
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        n = int(rng.integers(3, 40))
+        y = rng.integers(0, 1025, size=n).tolist()
+        idx = int(rng.integers(0, n - 1))
+        ref = trim_tokens(y, idx).reshape(-1).tolist()
+        yy = list(y)
+        yy[-1] = 0
+        start = n - idx if idx > 0 else 0
+        cnt = n - start
+        for i in range(cnt):
+            if yy[start + i] >= 1024:
+                cnt = i
+                break
+        assert yy[start:start + cnt] == ref
+
+
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "genie_engine.h")).read()
+    return sorted(set(re.findall(r"\b(gsv_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    from genie_tts_amd.build import LIB, build
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    missing = [f for f in _header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    from genie_tts_amd import engine
+    assert set(engine.EXPORTED) <= set(_header_functions())
+    assert lib.gsv_version
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from genie_tts_amd.engine import Engine, EngineError
+    with pytest.raises(EngineError, match="no CPU fallback"):
+        Engine({}, "v2")
