@@ -55,6 +55,7 @@ gsv_engine::~gsv_engine() {
     release_all();
     if (own_stream && stream) hipStreamDestroy(stream);
     if (done_host) hipHostFree(done_host);
+    for (auto& e : kev) if (e) hipEventDestroy(e);
     for (auto& e : poll_ev) if (e) hipEventDestroy(e);
     for (auto& e : ev) if (e) hipEventDestroy(e);
     if (ev_in) hipEventDestroy(ev_in);
@@ -408,7 +409,8 @@ void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hi
             fa.B = B; fa.nslices = ffn_slices; fa.h = h; fa.bo = W.b_out; fa.attn_part = attn_part;
             fa.ln_g = W.n1w; fa.ln_b = W.n1b; fa.h1 = h1;
             fa.W1 = W.w1; fa.b1 = W.b1; fa.W2T = W.w2T; fa.part = ffn_part;
-            ffn_fused(fa, st);
+            if (probe_now && l == probe_layer) ffn_fused(fa, st, kev[0], kev[1]);
+            else ffn_fused(fa, st);
         }
         GemvArgs lg{};
         lg.B = B; lg.N = 1025; lg.K = 512;
@@ -495,10 +497,22 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
         for (auto& e : poll_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     }
     int launched = 0, k = 0, checked = 0;
-    bool finished = false;
+    bool finished = false, probed = false;
+    // Live kernel timing: the step after the first chunk runs eagerly (same kernels as the
+    // graph) so the probed FFN launch can carry start/stop events -- graph event nodes are
+    // not timing events on HIP.  The host is ahead of the GPU then, so the eager launches
+    // queue behind the running chunk and execute back to back, as inside the graph.
+    bool probe_pending = timing && kev[0] != nullptr;
     while (launched < limit && !finished) {
-        const int n = std::min(chunk, limit - launched);
-        if (n == chunk) {
+        int n = std::min(chunk, limit - launched);
+        if (probe_pending && launched == chunk) {
+            n = 1;
+            probe_now = true;
+            decode_step(B, sp, nullptr, st);
+            probe_now = false;
+            probe_pending = false;
+            probed = true;
+        } else if (n == chunk) {
             if (hipGraphLaunch(ex8, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
         } else {
             for (int i = 0; i < n; ++i)
@@ -518,7 +532,20 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
             if (all) finished = true;
         }
     }
-    return hipStreamSynchronize(st) == hipSuccess ? 0 : set_error(GSV_E_HIP, "decode sync");
+    if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "decode sync");
+    if (probed) {
+        // one sample per decode loop: the probed step's layer-`probe_layer` FFN launch
+        float ms = 0.f;
+        const hipError_t e = hipEventElapsedTime(&ms, kev[0], kev[1]);
+        if (e == hipSuccess && ms > 0.f) {
+            kern_us_sum += ms * 1000.0;
+            ++kern_n;
+        } else {
+            kern_err = e == hipSuccess ? -1 : (int)e;
+            (void)hipGetLastError();
+        }
+    }
+    return 0;
 }
 
 // ============================================================ C ABI
@@ -727,6 +754,19 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
 extern "C" int gsv_set_timing(gsv_engine* eng, int enabled) {
     ENG_CHECK(eng);
     eng->timing = enabled != 0;
+    if (eng->timing && !eng->kev[0]) {
+        hipEventCreate(&eng->kev[0]);
+        hipEventCreate(&eng->kev[1]);
+    }
+    eng->kern_us_sum = 0.0;
+    eng->kern_n = 0;
+    return 0;
+}
+
+extern "C" int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples) {
+    ENG_CHECK(eng);
+    if (avg_us) *avg_us = eng->kern_n ? (float)(eng->kern_us_sum / eng->kern_n) : 0.f;
+    if (samples) *samples = eng->kern_n ? eng->kern_n : -eng->kern_err;
     return 0;
 }
 

@@ -80,6 +80,13 @@ struct gsv_engine {
     hipEvent_t ev[6] = {};
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     uint8_t* done_host = nullptr;       // pinned, 2 slots x 64
+    // live kernel timing: event pair captured around layer `probe_layer`'s FFN launch
+    hipEvent_t kev[2] = {};
+    int probe_layer = 12;
+    double kern_us_sum = 0.0;
+    int kern_n = 0;
+    int kern_err = 0;        // last hipEventElapsedTime failure (reported as -samples)
+    bool probe_now = false;  // eager step in flight: time the probed FFN launch
     hipEvent_t poll_ev[2] = {};
 
     ~gsv_engine();

@@ -140,7 +140,7 @@ struct FfnArgs {
     const __half* W1; const float* b1; const __half* W2T;      // W2T [2048][512]
     float* part;                                               // [nslices][B][512]
 };
-void ffn_fused(const FfnArgs& a, hipStream_t s);
+void ffn_fused(const FfnArgs& a, hipStream_t s, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 // Decode embedding: for active b: tok = y[b][ny[b]-1]; h[b] = E[tok] + alpha*pe[ny[b]]
 void decode_embed(int B, const int64_t* y, long ldy, const int* ny, const __half* emb,

@@ -9,6 +9,7 @@
 // Partial sums are reduced in a fixed order (deterministic).
 #include "common.h"
 #include "kernels.h"
+#include <hip/hip_ext.h>
 
 namespace gsv {
 
@@ -234,20 +235,23 @@ __global__ __launch_bounds__(256) void k_ffn(FfnArgs a) {
     }
 }
 
+// start/stop (optional): hipExtLaunchKernelGGL stamps them from the dispatch packet's
+// own begin/end timestamps -- the bench's live per-launch duration of this kernel.
 template <int RPB>
-static void launch_ffn(const FfnArgs& a, hipStream_t s) {
+static void launch_ffn(const FfnArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     const int nb = a.B <= 1 ? 1 : a.B <= 2 ? 2 : a.B <= 4 ? 4 : 8;
+    const dim3 g(a.nslices), blk(256);
     switch (nb) {
-        case 1: hipLaunchKernelGGL((k_ffn<RPB, 1>), dim3(a.nslices), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_ffn<RPB, 2>), dim3(a.nslices), dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_ffn<RPB, 4>), dim3(a.nslices), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_ffn<RPB, 8>), dim3(a.nslices), dim3(256), 0, s, a); break;
+        case 1: hipExtLaunchKernelGGL((k_ffn<RPB, 1>), g, blk, 0, s, start, stop, 0, a); break;
+        case 2: hipExtLaunchKernelGGL((k_ffn<RPB, 2>), g, blk, 0, s, start, stop, 0, a); break;
+        case 4: hipExtLaunchKernelGGL((k_ffn<RPB, 4>), g, blk, 0, s, start, stop, 0, a); break;
+        default: hipExtLaunchKernelGGL((k_ffn<RPB, 8>), g, blk, 0, s, start, stop, 0, a); break;
     }
 }
 
-void ffn_fused(const FfnArgs& a, hipStream_t s) {
-    if (a.nslices == 64) launch_ffn<32>(a, s);
-    else launch_ffn<64>(a, s);   // nslices == 32
+void ffn_fused(const FfnArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    if (a.nslices == 64) launch_ffn<32>(a, s, start, stop);
+    else launch_ffn<64>(a, s, start, stop);   // nslices == 32
 }
 
 // ---------------------------------------------------------------------------

@@ -365,6 +365,7 @@ int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* 
     if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, T, S, pp ? 0 : n_audio)) return r;
     VitsWorkspace& W = vws;
+    (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timing) hipEventRecord(ev[4], s);
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
     const float* ge;
@@ -505,6 +506,7 @@ int gsv_engine::prompt_encode(const float* ref_audio, int n_audio, const float* 
     if (n_audio < 2048) return set_error(GSV_E_ARG, "reference audio too short");
     if (int r = ensure_vits_ws(this, 2, 2, n_audio)) return r;
     VitsWorkspace& W = vws;
+    (void)hipGetLastError();
     run_ref_enc(this, penc.ref, ref_audio, n_audio, W.pe_ge, s);
     // ge = PReLU(ref_enc + (sv_emb @ W^T + b)); ge_adv = ge @ W512^T + b  (prompt_encoder#269-280)
     GemmArgs g{};

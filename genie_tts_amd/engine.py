@@ -85,6 +85,7 @@ def lib():
                                 ctypes.POINTER(ctypes.c_float), vp]
         L.gsv_set_timing.argtypes = [vp, ctypes.c_int]
         L.gsv_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+        L.gsv_get_kernel_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32)]
         _lib = L
     return _lib
 
@@ -94,7 +95,7 @@ EXPORTED = (
     "gsv_finalize_weights", "gsv_reserve", "gsv_t2s_encode", "gsv_t2s_generate", "gsv_t2s_prefill",
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
-    "gsv_probe",
+    "gsv_probe", "gsv_get_kernel_timing",
 )
 
 
@@ -306,6 +307,12 @@ class Engine:
 
     def set_timing(self, on: bool = True):
         _check(lib().gsv_set_timing(self.h, int(on)), "gsv_set_timing")
+
+    def kernel_timing(self):
+        """(average microseconds, samples) of the live-sampled dominant decode kernel."""
+        us, n = ctypes.c_float(), ctypes.c_int32()
+        _check(lib().gsv_get_kernel_timing(self.h, ctypes.byref(us), ctypes.byref(n)), "gsv_get_kernel_timing")
+        return us.value, n.value
 
     def timing(self) -> List[float]:
         a = (ctypes.c_float * 4)()

@@ -1,0 +1,44 @@
+"""Roofline of the dominant kernel, from the engine's live in-loop timing.
+
+Dominant kernel (rocprofv3, profiles/): the fused decode FFN (`k_ffn`, one
+launch per layer per step) -- HBM-bound weight streaming.  Its algorithmic
+bytes per launch at batch B (the unique bytes the math needs, each once):
+  W1 fp16 2048x512 + W2^T fp16 2048x512          4,194,304
+  b1 f32 2048 + bo/ln1 gamma/beta f32 3x512       14,336
+  per sequence: attention partials 16x512 f32 read (32,768), residual h 512
+  f32 read (2,048), FFN2 partials 64x512 f32 written (131,072), h1 written (2,048)
+The duration is the average, over the timed region, of start/stop HIP events
+that hipExtLaunchKernelGGL stamps from the dispatch packet of that launch: one
+launch per utterance (layer 12 of the 9th decode step, run eagerly because graph
+event nodes are not timing events on HIP; see engine.hip decode_loop).
+"""
+from __future__ import annotations
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def ffn_algorithmic_bytes(B: int = 1, slices: int = 64) -> int:
+    weights = 2 * 2048 * 512 * 2
+    params = 2048 * 4 + 3 * 512 * 4
+    per_seq = 16 * 512 * 4 + 512 * 4 + slices * 512 * 4 + 512 * 4
+    return weights + params + B * per_seq
+
+
+def dominant_kernel_roofline(eng, B: int = 1):
+    us, n = eng.kernel_timing()
+    if n <= 0 or us <= 0:
+        return {"error": f"no live kernel samples (hipEventElapsedTime error {-n})"}
+    bytes_ = ffn_algorithmic_bytes(B)
+    achieved = bytes_ / (us * 1e-6) / 1e9
+    return {
+        "kernel": "k_ffn (fused FFN1+FFN2 split-K, decode, layer 12, B=%d)" % B,
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": None,
+        "algorithmic_bytes_per_launch": bytes_,
+        "avg_launch_us": us,
+        "samples": n,
+    }
