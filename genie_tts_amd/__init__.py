@@ -1,0 +1,13 @@
+"""MI355X-native GPT-SoVITS inference engine (the Genie-TTS synthesis hot path).
+
+The product is libgenie_engine.so (C ABI, include/genie_engine.h) built from
+genie_tts_amd/csrc; this package is its host side: ctypes bindings (engine),
+onnxruntime-session-shaped objects (sessions), the character cache
+(model_manager), the reference's inference driver (inference) and the
+`genie_tts` entry points (api).  There is no CPU fallback.
+"""
+from .api import (clear_reference_audio_cache, load_character, load_weights, set_g2p,  # noqa: F401
+                  set_reference_audio, stop, tts, unload_character)
+
+__all__ = ["load_character", "load_weights", "unload_character", "set_reference_audio", "set_g2p", "tts", "stop",
+           "clear_reference_audio_cache"]

@@ -1,0 +1,154 @@
+"""GENIE inference driver (hot path), mirroring src/genie_tts/Core/Inference.py.
+
+`GENIE.tts` has the reference's signature (Inference.py:16-61): it takes the
+reference-audio features and the five sessions of a `GSVModel`, runs T2S, the
+EOS filter and the vocoder, and returns `audio f32 [1280*G]`.  When the
+sessions are this package's engine-backed ones (always, through
+`model_manager`), T2S is one `gsv_t2s_generate` call: encoder, prefill, the
+decode loop on the device as replayed hipGraphs, and the reference's trim +
+EOS filter (Inference.py:41-44,108-109) -- no per-step host round trip.
+`GENIE.t2s_cpu` is the reference's own session-by-session loop
+(Inference.py:63-109) over the same sessions, kept for parity tests.
+
+G2P (`get_phones_and_bert`, src/genie_tts/GetPhonesAndBert.py) is outside this
+path: `tts` accepts phoneme ids (+ BERT features) directly, or text together
+with a caller-supplied `g2p(text, language) -> (text_seq [1,S] i64, text_bert
+[S,1024] f32)` -- e.g. the reference's own function.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Union
+
+import numpy as np
+
+from .engine import Sampler
+from .sessions import (EncoderSession, FirstStageDecoderSession, StageDecoderSession, VitsSession,
+                       PromptEncoderSession)
+
+EOS = 1024
+MAX_STEPS = 500          # Inference.py:95
+
+
+@dataclass
+class ReferenceAudio:
+    """Reference-audio features (the fields GENIE.tts reads from the reference's
+    ReferenceAudio, src/genie_tts/Audio/ReferenceAudio.py:28-76).  Extraction from a
+    wav (soxr resampling, CN-HuBERT, SV model) is SURVEY §8(f) and not part of
+    this path: supply the features."""
+    phonemes_seq: np.ndarray             # i64 [1, R]
+    text_bert: np.ndarray                # f32 [R, 1024]
+    audio_32k: np.ndarray                # f32 [1, N32]
+    ssl_content: np.ndarray              # f32 [1, 768, H]
+    sv_emb: Optional[np.ndarray] = None  # f32 [1, 20480] (V2ProPlus)
+    global_emb: Optional[np.ndarray] = None
+    global_emb_advanced: Optional[np.ndarray] = None
+    text: str = ""
+
+    def update_global_emb(self, prompt_encoder) -> None:
+        """ReferenceAudio.py:68-76 (cached after the first call)."""
+        if self.global_emb is not None:
+            return
+        if self.sv_emb is None:
+            raise ValueError("V2ProPlus needs the speaker-verification embedding (sv_emb) of the reference")
+        self.global_emb, self.global_emb_advanced = prompt_encoder.run(None, {
+            "ref_audio": self.audio_32k, "sv_emb": self.sv_emb})
+
+
+def eos_filter(semantic_tokens: np.ndarray) -> np.ndarray:
+    """Inference.py:41-44: cut at the first id >= 1024."""
+    idx = np.where(semantic_tokens >= EOS)
+    if len(idx[0]) > 0:
+        semantic_tokens = semantic_tokens[..., :idx[-1][0]]
+    return semantic_tokens
+
+
+def _engine_of(*sessions):
+    engines = {id(getattr(s, "engine", None)) for s in sessions}
+    if len(engines) == 1 and all(isinstance(s, (EncoderSession, FirstStageDecoderSession, StageDecoderSession,
+                                                VitsSession)) for s in sessions):
+        return sessions[0].engine
+    return None
+
+
+class GENIE:
+    def __init__(self):
+        self.stop_event = threading.Event()
+
+    def tts(self, text: Union[str, np.ndarray], prompt_audio: ReferenceAudio, encoder, first_stage_decoder,
+            stage_decoder, vocoder, prompt_encoder=None, language: str = "japanese",
+            text_bert: Optional[np.ndarray] = None, g2p: Optional[Callable] = None,
+            sampler: Optional[Sampler] = None) -> Optional[np.ndarray]:
+        if isinstance(text, str):
+            if g2p is None:
+                raise ValueError("text input needs a g2p(text, language) callable (G2P is outside this engine)")
+            text_seq, text_bert = g2p("。" + text, language)          # Inference.py:27-28
+        else:
+            text_seq = np.asarray(text, np.int64).reshape(1, -1)
+            if text_bert is None:
+                text_bert = np.zeros((text_seq.shape[1], 1024), np.float32)
+        eng = _engine_of(encoder, first_stage_decoder, stage_decoder, vocoder)
+        if eng is not None:
+            sem = self.t2s(prompt_audio.phonemes_seq, prompt_audio.text_bert, text_seq, text_bert,
+                           prompt_audio.ssl_content, eng, sampler or first_stage_decoder.sampler)
+        else:
+            sem = self.t2s_cpu(prompt_audio.phonemes_seq, prompt_audio.text_bert, text_seq, text_bert,
+                               prompt_audio.ssl_content, encoder, first_stage_decoder, stage_decoder)
+            if sem is None:
+                return None
+            sem = eos_filter(sem)
+        if prompt_encoder is None:
+            return vocoder.run(None, {"text_seq": text_seq, "pred_semantic": sem,
+                                      "ref_audio": prompt_audio.audio_32k})[0]
+        prompt_audio.update_global_emb(prompt_encoder)
+        return vocoder.run(None, {"text_seq": text_seq, "pred_semantic": sem, "ge": prompt_audio.global_emb,
+                                  "ge_advanced": prompt_audio.global_emb_advanced})[0]
+
+    def t2s(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, engine, sampler: Sampler) -> np.ndarray:
+        """Whole T2S on the device; returns the trimmed, EOS-filtered [1,1,G] tokens."""
+        tok = engine.t2s_generate([(ref_seq, text_seq, ref_bert, text_bert,
+                                    np.asarray(ssl_content, np.float32).reshape(768, -1))], sampler)[0]
+        return tok.reshape(1, 1, -1)
+
+    def t2s_cpu(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, encoder, first_stage_decoder,
+                stage_decoder) -> Optional[np.ndarray]:
+        """The reference's loop (Inference.py:63-109) over session objects."""
+        x, prompts = encoder.run(None, {"ref_seq": ref_seq, "text_seq": text_seq, "ref_bert": ref_bert,
+                                        "text_bert": text_bert, "ssl_content": ssl_content})
+        y, y_emb, *present = first_stage_decoder.run(None, {"x": x, "prompts": prompts})
+        names: List[str] = [i.name for i in stage_decoder.get_inputs()]
+        idx = 0
+        for idx in range(0, MAX_STEPS):
+            if self.stop_event.is_set():
+                return None
+            outs = stage_decoder.run(None, dict(zip(names, [y, y_emb, *present])))
+            y, y_emb, stop, *present = outs
+            if stop:
+                break
+        y[0, -1] = 0
+        return np.expand_dims(y[:, -idx:], axis=0)
+
+    def tts_batch(self, items: Sequence[tuple], prompt_audio: ReferenceAudio, model, sampler: Sampler) -> List[np.ndarray]:
+        """Batched synthesis for one character and reference: items are
+        (text_seq, text_bert|None).  All sequences decode together (one batched
+        hipGraph step per token); the vocoder runs per utterance."""
+        eng = model.ENGINE
+        ssl = np.asarray(prompt_audio.ssl_content, np.float32).reshape(768, -1)
+        utts = [(prompt_audio.phonemes_seq, ts, prompt_audio.text_bert, tb, ssl) for ts, tb in items]
+        toks = eng.t2s_generate(utts, sampler)
+        out = []
+        for (ts, _), tok in zip(items, toks):
+            if model.PROMPT_ENCODER is None:
+                a = model.VITS.run(None, {"text_seq": ts, "pred_semantic": tok.reshape(1, 1, -1),
+                                          "ref_audio": prompt_audio.audio_32k})[0]
+            else:
+                prompt_audio.update_global_emb(model.PROMPT_ENCODER)
+                a = model.VITS.run(None, {"text_seq": ts, "pred_semantic": tok.reshape(1, 1, -1),
+                                          "ge": prompt_audio.global_emb,
+                                          "ge_advanced": prompt_audio.global_emb_advanced})[0]
+            out.append(a)
+        return out
+
+
+tts_client = GENIE()

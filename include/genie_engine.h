@@ -160,9 +160,11 @@ int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us, void* str
  * [0]=encode [1]=prefill [2]=decode [3]=vits.  Filled when timing is enabled. */
 int gsv_set_timing(gsv_engine* eng, int enabled);
 int gsv_get_timing(gsv_engine* eng, float* ms4);
-/* Live duration of the dominant decode kernel (fused FFN of layer 12), sampled
- * by an event pair captured in the step graph once per polled chunk while
- * timing is enabled: average microseconds and number of samples. */
+/* Live duration of the dominant decode kernel (fused FFN of layer 12): while
+ * timing is enabled, the 9th step of each decode loop runs eagerly and that
+ * launch carries start/stop events stamped from its dispatch packet
+ * (hipExtLaunchKernelGGL).  Average microseconds and number of samples; a
+ * negative count is -(hipError_t) of a failed hipEventElapsedTime. */
 int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples);
 
 #ifdef __cplusplus

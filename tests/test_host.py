@@ -67,3 +67,35 @@ def test_no_cpu_fallback_without_gpu():
     from genie_tts_amd.engine import Engine, EngineError
     with pytest.raises(EngineError, match="no CPU fallback"):
         Engine({}, "v2")
+
+
+def test_eos_filter_semantics():
+    """inference.eos_filter restates Inference.py:41-44."""
+    from genie_tts_amd.inference import eos_filter
+    a = np.array([[[3, 5, 1024, 7, 1024]]])
+    np.testing.assert_array_equal(eos_filter(a), np.array([[[3, 5]]]))
+    b = np.array([[[3, 5, 7]]])
+    np.testing.assert_array_equal(eos_filter(b), b)
+    np.testing.assert_array_equal(eos_filter(np.array([[[1024, 1]]])).shape, (1, 1, 0))
+
+
+def test_session_interfaces_match_templates():
+    """Input/output names and order of the session shims = SURVEY Appendix A."""
+    from genie_tts_amd import sessions as S
+    st = [i.name for i in S.StageDecoderSession.INPUTS]
+    assert st[:2] == ["iy", "iy_emb"] and len(st) == 50
+    assert st[2:6] == ["past_k_layer_0", "past_v_layer_0", "past_k_layer_1", "past_v_layer_1"]
+    so = [o.name for o in S.StageDecoderSession.OUTPUTS]
+    assert so[:3] == ["y", "y_emb", "stop_condition_tensor"] and so[3] == "present_k_layer_0"
+    assert [i.name for i in S.EncoderSession.INPUTS] == ["ref_seq", "text_seq", "ref_bert", "text_bert",
+                                                         "ssl_content"]
+    assert [o.name for o in S.FirstStageDecoderSession.OUTPUTS][:2] == ["y", "y_emb"]
+    assert [i.name for i in S.PromptEncoderSession.INPUTS] == ["ref_audio", "sv_emb"]
+
+
+def test_api_requires_reference_and_gpu():
+    import genie_tts_amd as G
+    with pytest.raises(ValueError):
+        G.tts("nobody", [3, 4, 5])
+    with pytest.raises(ValueError):
+        G.load_character("x", "/nonexistent", "klingon")
