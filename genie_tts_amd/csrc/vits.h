@@ -45,6 +45,10 @@ struct ConvArgs {
     float* acc; float div;
     int split; float* out2; const float* res2;
     int phases; long w_phase_stride;
+    // split-K workspace (floats); when set, conv1d splits the Cin reduction of
+    // under-filled grids over grid.z into partial slabs [split][Cout][n_t] and a
+    // second kernel sums them in fixed order and applies the epilogue.
+    float* part; long part_cap;
 };
 void conv1d(const ConvArgs& a, hipStream_t s);
 
@@ -138,6 +142,8 @@ struct VitsWorkspace {
     float *g0 = nullptr, *g1 = nullptr, *g2 = nullptr, *g3 = nullptr, *g4 = nullptr;
     float *ge = nullptr, *pad = nullptr, *reim = nullptr, *spec = nullptr, *r0 = nullptr, *r1 = nullptr;
     float *r2 = nullptr, *r3 = nullptr, *rq = nullptr, *ratt = nullptr;
+    float* splitk = nullptr;   // conv split-K partial slabs
+    long splitk_cap = 0;
     float *sv = nullptr, *pe_ge = nullptr;
     int cap_text = 0;
 };

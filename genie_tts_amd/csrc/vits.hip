@@ -10,6 +10,7 @@
 // `stride` polyphase convs of the same kernel (blockIdx.z = phase).
 #include "common.h"
 #include "vits.h"
+#include <algorithm>
 
 namespace gsv {
 
@@ -21,6 +22,39 @@ template <int KT> struct ConvCfg {
 #define CONV_BN 64
 #define CONV_BM 64
 #define CONV_XW_MAX 128
+
+// Output epilogue shared by the direct and the split-K paths: output column t of
+// phase ph -> time tp; bias; the ConvMode fusion.
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int co, int t, int ph, float acc) {
+    const int tp = t * a.o_tstride + a.o_toff + ph;
+    if (tp < 0 || tp >= a.o_len) return;
+    const float v = a.bias ? a.bias[co] + acc : acc;
+    const long oi = (long)co * a.o_cs + (long)tp * a.o_ts;
+    switch (a.mode) {
+        case CV_STORE: a.out[oi] = v; break;
+        case CV_RELU: a.out[oi] = fmaxf(v, 0.f); break;
+        case CV_RESID: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
+        case CV_VEC: a.out[oi] = v + a.vec[co]; break;
+        case CV_SUB: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] - v; break;
+        case CV_TANH: a.out[oi] = tanhf(v); break;
+        case CV_ACC_FIRST: a.acc[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
+        case CV_ACC_ADD: a.acc[oi] = a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v); break;
+        case CV_ACC_MEAN:
+            a.out[oi] = (a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v)) / a.div;
+            break;
+        case CV_RESID_VEC:
+            a.out[oi] = (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v) + a.vec[co];
+            break;
+        case CV_SPLIT_RESID:
+            if (co < a.split) {
+                a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v;
+            } else {
+                const long o2 = (long)(co - a.split) * a.o_cs + (long)tp * a.o_ts;
+                a.out2[o2] = a.res2[o2] + v;
+            }
+            break;
+    }
+}
 
 // Software pipeline: the next K-chunk (input halo tile + weight tile) is loaded
 // into registers while the MFMAs consume the current chunk from LDS; LDS is
@@ -34,12 +68,18 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
     __shared__ float Ws[2][CONV_BM][KC + 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w >> 1, wn = w & 1;
-    const int t0 = blockIdx.x * CONV_BN, co0 = blockIdx.y * CONV_BM, ph = blockIdx.z;
+    const int t0 = blockIdx.x * CONV_BN, co0 = blockIdx.y * CONV_BM;
+    const bool split = a.phases <= 1 && gridDim.z > 1;
+    const int ph = split ? 0 : blockIdx.z;
     const float* W = a.w + (long)ph * a.w_phase_stride;
     const int dil = a.dil;
     const int XW = CONV_BN + (KT - 1) * dil;
     const long wrow = (long)a.Cin * KT;
-    const int nch = (a.Cin + CI - 1) / CI;
+    const int nch_all = (a.Cin + CI - 1) / CI;
+    // split-K: this block reduces Cin chunks [c_lo, c_hi)
+    const int c_lo = split ? (int)((long)blockIdx.z * nch_all / gridDim.z) : 0;
+    const int c_hi = split ? (int)((long)(blockIdx.z + 1) * nch_all / gridDim.z) : nch_all;
+    const int nch = c_hi - c_lo;
     float xr[NX];
     float4 wr[NW];
 
@@ -106,12 +146,12 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
     const int ncol = wn * 32 + (lane & 31);
     const int h = lane >> 5;
     const int arow = wm * 32 + (lane & 31);
-    load(0);
+    load(c_lo * CI);
     store(0);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
         const int buf = c & 1;
-        if (c + 1 < nch) load((c + 1) * CI);
+        if (c + 1 < nch) load((c_lo + c + 1) * CI);
         const float* xs = Xs[buf];
 #pragma unroll
         for (int kp = 0; kp < KC / 2; ++kp) {
@@ -127,39 +167,39 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
     }
     const int t = t0 + ncol;
     if (t >= a.n_t) return;
-    const int tp = t * a.o_tstride + a.o_toff + ph;
-    if (tp < 0 || tp >= a.o_len) return;
+    if (split) {
+        float* P = a.part + (long)blockIdx.z * a.Cout * a.n_t;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (co < a.Cout) P[(long)co * a.n_t + t] = acc[r];
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co >= a.Cout) continue;
-        const float v = a.bias ? a.bias[co] + acc[r] : acc[r];
-        const long oi = (long)co * a.o_cs + (long)tp * a.o_ts;
-        switch (a.mode) {
-            case CV_STORE: a.out[oi] = v; break;
-            case CV_RELU: a.out[oi] = fmaxf(v, 0.f); break;
-            case CV_RESID: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
-            case CV_VEC: a.out[oi] = v + a.vec[co]; break;
-            case CV_SUB: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] - v; break;
-            case CV_TANH: a.out[oi] = tanhf(v); break;
-            case CV_ACC_FIRST: a.acc[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
-            case CV_ACC_ADD: a.acc[oi] = a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v); break;
-            case CV_ACC_MEAN:
-                a.out[oi] = (a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v)) / a.div;
-                break;
-            case CV_RESID_VEC:
-                a.out[oi] = (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v) + a.vec[co];
-                break;
-            case CV_SPLIT_RESID:
-                if (co < a.split) {
-                    a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v;
-                } else {
-                    const long o2 = (long)(co - a.split) * a.o_cs + (long)tp * a.o_ts;
-                    a.out2[o2] = a.res2[o2] + v;
-                }
-                break;
-        }
+        if (co < a.Cout) conv_epilogue(a, co, t, ph, acc[r]);
     }
+}
+
+// Fixed-order sum of the split-K slabs + the conv epilogue (one thread per output).
+__global__ __launch_bounds__(256) void k_conv_reduce(ConvArgs a, int nsplit) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    const long n = (long)a.Cout * a.n_t;
+    if (i >= n) return;
+    const int co = (int)(i / a.n_t), t = (int)(i - (long)co * a.n_t);
+    // slabs loaded 8 at a time (independent loads in flight), summed in slab order
+    float v = 0.f;
+    for (int s0 = 0; s0 < nsplit; s0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = s0 + j < nsplit ? a.part[(long)(s0 + j) * n + i] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (s0 + j < nsplit) v = (s0 + j == 0) ? p[j] : v + p[j];
+    }
+    conv_epilogue(a, co, t, 0, v);
 }
 
 template <int KT>
@@ -170,9 +210,31 @@ static void launch_conv(const ConvArgs& a, dim3 grid, hipStream_t s) {
     else hipLaunchKernelGGL((k_conv1d<KT, false>), grid, dim3(256), 0, s, a);
 }
 
+static int conv_ci(int K) {
+    switch (K) {
+        case 1: return ConvCfg<1>::CI;
+        case 2: return ConvCfg<2>::CI;
+        case 3: return ConvCfg<3>::CI;
+        case 4: return ConvCfg<4>::CI;
+        case 5: return ConvCfg<5>::CI;
+        case 7: return ConvCfg<7>::CI;
+        default: return ConvCfg<11>::CI;
+    }
+}
+
 void conv1d(const ConvArgs& a, hipStream_t s) {
     dim3 grid((a.n_t + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM,
               a.phases > 0 ? a.phases : 1);
+    // Under-filled grids (the T=2G / S-frame encoder, MRTE and flow convs) split
+    // the Cin reduction so the launch covers the chip.
+    int nsplit = 1;
+    const int blocks = (int)(grid.x * grid.y);
+    if (a.part && a.phases <= 1 && blocks < 128) {
+        const int nch = (a.Cin + conv_ci(a.K) - 1) / conv_ci(a.K);
+        nsplit = std::min(nch, (256 + blocks - 1) / blocks);
+        while (nsplit > 1 && (long)nsplit * a.Cout * a.n_t > a.part_cap) --nsplit;
+    }
+    if (nsplit > 1) grid.z = nsplit;
     switch (a.K) {
         case 1: launch_conv<1>(a, grid, s); break;
         case 2: launch_conv<2>(a, grid, s); break;
@@ -181,7 +243,11 @@ void conv1d(const ConvArgs& a, hipStream_t s) {
         case 5: launch_conv<5>(a, grid, s); break;
         case 7: launch_conv<7>(a, grid, s); break;
         case 11: launch_conv<11>(a, grid, s); break;
-        default: break;   // host validates K
+        default: return;   // host validates K
+    }
+    if (nsplit > 1) {
+        const long n = (long)a.Cout * a.n_t;
+        hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, nsplit);
     }
 }
 
@@ -233,9 +299,56 @@ __global__ __launch_bounds__(256) void k_ln_channels(const float* x, const float
     }
 }
 
+// Narrow form for C <= 256, C % 16 == 0 (the 192-channel encoders): one wave per
+// 4 time columns, lane = (t & 3) + 4 * channel group; reductions by shuffles over
+// the 16 groups, so short sequences still spread over T/4 waves.
+__global__ __launch_bounds__(64) void k_ln_channels_w(const float* x, const float* y, float* out,
+                                                     int C, int T, const float* g, const float* b) {
+    const int lane = threadIdx.x, tl = lane & 3, cg = lane >> 2;
+    const int t = blockIdx.x * 4 + tl;
+    const bool ok = t < T;
+    const int nc = C >> 4;
+    float v[16];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        float xv = 0.f;
+        if (i < nc && ok) {
+            const long o = (long)(cg + 16 * i) * T + t;
+            xv = x[o];
+            if (y) xv = xv + y[o];
+        }
+        v[i] = xv;
+        s += xv;
+    }
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i < nc) {
+            const float d = v[i] - mean;
+            q += d * d;
+        }
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
+    const float den = sqrtf(q / (float)C + 1e-5f);
+    if (!ok) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i < nc) {
+            const int c = cg + 16 * i;
+            out[(long)c * T + t] = (v[i] - mean) / den * g[c] + b[c];
+        }
+}
+
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
                  const float* b, hipStream_t s) {
-    hipLaunchKernelGGL(k_ln_channels, dim3((T + 63) / 64), dim3(256), 0, s, x, y, out, C, T, g, b);
+    if (C % 16 == 0 && C <= 256)
+        hipLaunchKernelGGL(k_ln_channels_w, dim3((T + 3) / 4), dim3(64), 0, s, x, y, out, C, T, g, b);
+    else
+        hipLaunchKernelGGL(k_ln_channels, dim3((T + 63) / 64), dim3(256), 0, s, x, y, out, C, T, g, b);
 }
 
 // ----------------------------------------------------------------- attention

@@ -237,8 +237,18 @@ int gsv_engine::finalize_prompt_encoder() {
 }
 
 // ---------------------------------------------------------------- helpers
+// Split-K workspace of the engine whose VITS/prompt-encoder call is running on
+// this thread (set by SplitkScope; conv1d splits only when it is set).
+static thread_local float* tls_splitk = nullptr;
+static thread_local long tls_splitk_cap = 0;
+struct SplitkScope {
+    SplitkScope(float* p, long cap) { tls_splitk = p; tls_splitk_cap = cap; }
+    ~SplitkScope() { tls_splitk = nullptr; tls_splitk_cap = 0; }
+};
+
 static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode = CV_STORE) {
     ConvArgs a{};
+    a.part = tls_splitk; a.part_cap = tls_splitk_cap;
     a.x = x; a.x_cs = T; a.x_ts = 1; a.Cin = c.cin; a.Tin = T;
     a.w = c.w; a.Cout = c.cout; a.K = c.k; a.dil = 1; a.pad = (c.k - 1) / 2;
     a.bias = c.b;
@@ -347,7 +357,11 @@ static int ensure_vits_ws(gsv_engine* e, int T, int S, int n_audio) {
         W.r0 = A((size_t)f * 1024); W.r1 = A((size_t)f * 128); W.r2 = A((size_t)f * 128);
         W.r3 = A((size_t)f * 256); W.rq = A((size_t)f * 384); W.ratt = A((size_t)f * 128);
     }
-    if (!W.g4) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
+    if (!W.splitk) {
+        W.splitk_cap = 2L << 20;   // 8 MB: >= 384 tiles of 64 x 64
+        W.splitk = A((size_t)W.splitk_cap);
+    }
+    if (!W.g4 || !W.splitk) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
     W.cap_t = t; W.cap_text = sT; W.cap_gen = g; W.cap_spec = f;
     return 0;
 }
@@ -365,6 +379,7 @@ int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* 
     if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, T, S, pp ? 0 : n_audio)) return r;
     VitsWorkspace& W = vws;
+    SplitkScope sk(W.splitk, W.splitk_cap);
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timing) hipEventRecord(ev[4], s);
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
@@ -506,6 +521,7 @@ int gsv_engine::prompt_encode(const float* ref_audio, int n_audio, const float* 
     if (n_audio < 2048) return set_error(GSV_E_ARG, "reference audio too short");
     if (int r = ensure_vits_ws(this, 2, 2, n_audio)) return r;
     VitsWorkspace& W = vws;
+    SplitkScope sk(W.splitk, W.splitk_cap);
     (void)hipGetLastError();
     run_ref_enc(this, penc.ref, ref_audio, n_audio, W.pe_ge, s);
     // ge = PReLU(ref_enc + (sv_emb @ W^T + b)); ge_adv = ge @ W512^T + b  (prompt_encoder#269-280)
