@@ -21,6 +21,67 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// DPP wave reductions (VALU latency, no LDS crossbar): quad swaps, half-row and
+// row mirrors, then row_bcast15 / row_bcast31; lane 63 holds the result, read
+// back as a wave-uniform value.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROW_MASK,
+                                                      0xF, false));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_reduce_dpp(float v, Op op) {
+    v = op(v, dpp_f<0xB1, 0xF>(v));    // quad_perm [1,0,3,2]
+    v = op(v, dpp_f<0x4E, 0xF>(v));    // quad_perm [2,3,0,1]
+    v = op(v, dpp_f<0x141, 0xF>(v));   // row_half_mirror
+    v = op(v, dpp_f<0x140, 0xF>(v));   // row_mirror
+    v = op(v, dpp_f<0x142, 0xA>(v));   // row_bcast:15 -> rows 1, 3
+    v = op(v, dpp_f<0x143, 0xC>(v));   // row_bcast:31 -> rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+    return wave_reduce_dpp(v, [](float a, float b) { return fmaxf(a, b); });
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    return wave_reduce_dpp(v, [](float a, float b) { return a + b; });
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ int wave_min_dpp(int v) {
+    v = min(v, dpp_i<0xB1, 0xF>(v));
+    v = min(v, dpp_i<0x4E, 0xF>(v));
+    v = min(v, dpp_i<0x141, 0xF>(v));
+    v = min(v, dpp_i<0x140, 0xF>(v));
+    v = min(v, dpp_i<0x142, 0xA>(v));
+    v = min(v, dpp_i<0x143, 0xC>(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Block (<= 16 waves) reductions on the DPP wave forms: one LDS exchange.
+__device__ __forceinline__ float block_max_dpp(float v, float* red) {
+    const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_max_dpp(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < nw; ++i) r = fmaxf(r, red[i]);
+    return r;
+}
+__device__ __forceinline__ float block_sum_dpp(float v, float* red) {
+    const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_sum_dpp(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < nw; ++i) r += red[i];
+    return r;
+}
+
 // Block-wide sum for blockDim.x <= 1024; `red` needs >= 16 floats of LDS.
 __device__ __forceinline__ float block_sum(float v, float* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;

@@ -639,6 +639,7 @@ extern "C" int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_CAPACITY, "slot out of range");
+    if (s && (s->top_k < 1 || s->top_k > 64)) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
     if (int e = eng->prefill_slot(seq, x, n_x, prompts, n_prompts, s, logits_out, st)) return e;
@@ -657,6 +658,7 @@ extern "C" int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int nsteps, const 
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
     gsv_sampler sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
+    if (sp.top_k < 1 || sp.top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
     sp.force_steps = 1 << 30;   // session semantics: the caller owns the stop decision
     hipMemsetAsync(eng->done, 0, 1, st);
     for (int i = 0; i < nsteps; ++i) {
@@ -701,6 +703,7 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (batch <= 0 || !utts || !out_tokens || !out_len) return set_error(GSV_E_ARG, "bad args");
     gsv_sampler sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
+    if (sp.top_k < 1 || sp.top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
     if (sp.max_steps <= 0) sp.max_steps = 500;
     const int steps_cap = sp.force_steps > 0 ? sp.force_steps : sp.max_steps;
     int need = 0;
@@ -774,4 +777,35 @@ extern "C" int gsv_get_timing(gsv_engine* eng, float* ms4) {
     ENG_CHECK(eng);
     for (int i = 0; i < 4; ++i) ms4[i] = eng->ms[i];
     return 0;
+}
+
+extern "C" int gsv_debug_sample(const float* logits, const uint32_t* seen, int B, const gsv_sampler* s,
+                                int step, int64_t* tokens, uint8_t* stop, void* stream) {
+    if (!logits || !seen || !s || !tokens || B <= 0 || step < 1) return set_error(GSV_E_ARG, "bad args");
+    if (s->top_k < 1 || s->top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
+    hipStream_t st = (hipStream_t)stream;
+    // scratch decode state: y[b] (ldy 1), ny = 0, steps = step - 1, done = 0
+    char* buf = nullptr;
+    const size_t need = (size_t)B * (8 + 4 + 4 + 4 + 1 + 132);
+    if (hipMalloc(&buf, need) != hipSuccess) return set_error(GSV_E_HIP, "scratch");
+    int64_t* y = (int64_t*)buf;
+    int* ny = (int*)(y + B);
+    int* steps = ny + B;
+    int* kvlen = steps + B;
+    uint32_t* seen_c = (uint32_t*)(kvlen + B);
+    uint8_t* done = (uint8_t*)(seen_c + 33 * B);
+    hipMemsetAsync(buf, 0, need, st);
+    hipMemcpyAsync(seen_c, seen, (size_t)B * 33 * 4, hipMemcpyDeviceToDevice, st);
+    std::vector<int> hs(B, step - 1);
+    hipMemcpyAsync(steps, hs.data(), B * 4, hipMemcpyHostToDevice, st);
+    SampleArgs a{};
+    a.B = B; a.logits = logits; a.ldl = 1025; a.y = y; a.ldy = 1; a.ny = ny; a.seen = seen_c;
+    a.done = done; a.stop_out = stop; a.steps = steps; a.kvlen = kvlen;
+    a.top_k = s->top_k; a.temperature = s->temperature; a.rep_penalty = s->repetition_penalty;
+    a.greedy = s->greedy; a.seed = s->seed; a.max_steps = 1 << 30; a.force_steps = 0; a.prefill = 0;
+    sample_tokens(a, st);
+    hipMemcpyAsync(tokens, y, (size_t)B * 8, hipMemcpyDeviceToDevice, st);
+    const bool ok = hipStreamSynchronize(st) == hipSuccess;
+    hipFree(buf);
+    return ok ? 0 : set_error(GSV_E_HIP, "debug sample");
 }

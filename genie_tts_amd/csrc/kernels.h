@@ -160,6 +160,7 @@ struct SampleArgs {
     int max_steps; int force_steps;
     int prefill;                       // 1: first-stage sampler (no stop, no step count)
     float* logits_out; long ldlo;      // optional copy of raw logits
+    int ablate;                        // probe only: 1 skip top-k, 2 also skip softmax, 3 loads + tail
 };
 void sample_tokens(const SampleArgs& a, hipStream_t s);
 

@@ -18,6 +18,7 @@ __global__ void k_empty(int* p) {
 // which: 0 empty(1 block) 1 empty(256 blocks) 2 gemv QKV+LN 3 gemv QKV no-LN
 //        4 gemv FFN1(+LN) 5 gemv FFN2 6 gemv out-proj 7 attention decode (kvlen as set)
 //        8 full decode step (B as given) 9 attention+out-proj 10 fused FFN 11 QKV+partials+LN
+//        14-17 sampler (14 full; ablations 15 no top-k, 16 no softmax, 17 loads + tail)
 extern "C" int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us, void* stream) {
     if (!eng || !us || iters <= 0) return set_error(GSV_E_ARG, "bad probe args");
     hipSetDevice(eng->device);
@@ -27,6 +28,23 @@ extern "C" int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us
     hipStream_t st = sc.st();
     const long sstride = (long)16 * eng->tmax * 32;
     const T2SLayerW& W = eng->layers[1];
+    // sampler probes (14-17) advance their own scratch sequence state, one token per launch
+    int64_t* probe_y = nullptr;
+    int* probe_i = nullptr;
+    uint8_t* probe_done = nullptr;
+    const long probe_cap = iters + 256;   // warm-up replay (50) + ceil(iters/50)*50 launches
+    if (which >= 14 && which <= 17) {
+        hipMalloc(&probe_y, (size_t)B * probe_cap * 8);
+        hipMalloc(&probe_i, (size_t)3 * B * 4);
+        hipMalloc(&probe_done, (size_t)B);
+        if (!probe_y || !probe_i || !probe_done) return set_error(GSV_E_HIP, "probe scratch");
+        hipMemsetAsync(probe_i, 0, (size_t)3 * B * 4, st);
+        hipMemsetAsync(probe_done, 0, (size_t)B, st);
+    }
+    struct Free {
+        void* p[3];
+        ~Free() { for (void* q : p) if (q) hipFree(q); }
+    } free_guard{{probe_y, probe_i, probe_done}};
     auto launch = [&]() {
         switch (which) {
             case 0: hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st, nullptr); break;
@@ -92,6 +110,15 @@ extern "C" int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us
                 a.mode = EPI_QKV; a.kv.k = eng->kcache[2]; a.kv.v = eng->vcache[2]; a.kv.tmax = eng->tmax;
                 a.kv.row_pos = eng->kvlen; a.kv.seq_stride = sstride; a.kv.row_skip = nullptr;
                 gemv_f16(a, st);
+            } break;
+            case 14: case 15: case 16: case 17: {
+                // scratch state (probe_y sized for every launch of this probe): never done
+                gsv_sampler sp{15, 1.0f, 1.35f, 1, 0, 1 << 30, 1 << 30};
+                SampleArgs sa = eng->sampler_args(&sp, B);
+                sa.y = probe_y; sa.ldy = probe_cap; sa.ny = probe_i; sa.steps = probe_i + B;
+                sa.kvlen = probe_i + 2 * B; sa.done = probe_done; sa.stop_out = nullptr;
+                sa.ablate = which - 14;
+                sample_tokens(sa, st);
             } break;
             default: break;
         }

@@ -493,7 +493,7 @@ void gemv_f16(const GemvArgs& a, hipStream_t s) {
 // repetition penalty over the history set, /temperature, top-k threshold
 // (k-th largest by radix select), softmax, argmax(p / q) with q = 1 (greedy)
 // or q ~ N(0,1) (Philox + Box-Muller), stop = argmax(raw)==EOS || tok==EOS.
-// One 1024-thread block per sequence.
+// One 256-thread block per sequence.
 // =====================================================================
 __device__ __forceinline__ uint32_t f2key(float f) {
     const uint32_t u = __float_as_uint(f);
@@ -525,95 +525,186 @@ __device__ void block_argmax(float& v, int& i, float* sv, int* si) {
     for (int k = 1; k < nw; ++k) argmax_merge(v, i, sv[k], si[k]);
 }
 
+// Block argmax on DPP reductions: value max, then the smallest index holding it.
+__device__ __forceinline__ void block_argmax_dpp(float& v, int& i, float* sv, int* si) {
+    const float m = wave_max_dpp(v);
+    const int mi = wave_min_dpp(v == m ? i : 0x7fffffff);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { sv[w] = m; si[w] = mi; }
+    __syncthreads();
+    v = sv[0];
+    i = si[0];
+    for (int k = 1; k < nw; ++k) argmax_merge(v, i, sv[k], si[k]);
+}
+
+// Append the token and advance the sequence state (thread 0; state read at entry).
+__device__ __forceinline__ void sample_commit(const SampleArgs& a, int b, int tok, int raw_arg, int n,
+                                              int steps, int kv, const uint32_t* seen_s) {
+    a.y[(long)b * a.ldy + n] = tok;
+    a.ny[b] = n + 1;
+    a.seen[(long)b * 33 + (tok >> 5)] = seen_s[tok >> 5] | (1u << (tok & 31));
+    if (!a.prefill) {
+        const bool stop = raw_arg == 1024 || tok == 1024;
+        if (a.stop_out) a.stop_out[b] = stop ? 1 : 0;
+        const int st = steps + 1;
+        a.steps[b] = st;
+        a.kvlen[b] = kv + 1;
+        const bool fin = a.force_steps > 0 ? st >= a.force_steps : (stop || st >= a.max_steps);
+        if (fin) a.done[b] = 1;
+    }
+}
+
 #define VOCAB 1025
-__global__ __launch_bounds__(1024) void k_sample(SampleArgs a) {
-    __shared__ float vals[VOCAB];
-    __shared__ uint32_t hist[256];
+#define SAMPLE_SLOTS 5     // ceil(1025 / 256) logits per thread
+#define SAMPLE_MAXK 64
+
+// One round of "extract the wave maximum, removing ONE instance": each lane holds
+// a descending list h[0..n) with head index hp; returns the maximum (uniform).
+template <int N>
+__device__ __forceinline__ float wave_extract(const float (&h)[N], int& hp) {
+    const int lane = threadIdx.x & 63;
+    float head = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+        if (j == hp) head = h[j];
+    const float m = wave_max_dpp(head);
+    const unsigned long long hit = __ballot(head == m && hp < N);
+    if (hit && lane == __ffsll((long long)hit) - 1) ++hp;
+    return m;
+}
+
+template <int N>
+__device__ __forceinline__ void sort_desc(float (&h)[N]) {
+#pragma unroll
+    for (int i = 1; i < N; ++i)
+#pragma unroll
+        for (int j = i; j > 0; --j)
+            if (h[j] > h[j - 1]) { const float t = h[j]; h[j] = h[j - 1]; h[j - 1] = t; }
+}
+
+// 256 threads per sequence; logits in registers.  top-k threshold = k-th largest
+// penalised logit WITH multiplicity (TopK values[:, -1], stage#1786-1790): every
+// wave extracts its own k largest (one instance per round), then wave 0 extracts
+// the k-th largest of the 4k candidates -- the global k-th largest.
+__global__ __launch_bounds__(256) void k_sample(SampleArgs a) {
+    __shared__ float cand[4][SAMPLE_MAXK];
     __shared__ float sv[16];
     __shared__ int si[16];
-    __shared__ uint32_t sel_prefix, sel_remain;
-    const int b = blockIdx.x, tid = threadIdx.x;
-    if (!a.prefill && a.done[b]) {
+    __shared__ float thr_s;
+    __shared__ uint32_t seen_s[33];
+    __shared__ int step_s;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* lg = a.logits + (long)b * a.ldl;
+    const uint32_t* seen = a.seen + (long)b * 33;
+    // every load issued before the first use (the done flag included)
+    float l[SAMPLE_SLOTS];
+    uint32_t sw[SAMPLE_SLOTS];
+#pragma unroll
+    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
+        const int i = tid + 256 * j;
+        l[j] = i < VOCAB ? lg[i] : -INFINITY;
+        sw[j] = i < VOCAB ? seen[i >> 5] : 0u;
+    }
+    // sequence state for the tail, read up front (no dependent round trips at the end)
+    int st_ny = 0, st_steps = 0, st_kv = 0;
+    if (tid == 0) {
+        st_ny = a.ny[b];
+        if (!a.prefill) { st_steps = a.steps[b]; st_kv = a.kvlen[b]; }
+    }
+    if (tid < 33) seen_s[tid] = seen[tid];
+    const bool skip = !a.prefill && a.done[b];
+    if (skip) {
         if (tid == 0 && a.stop_out) a.stop_out[b] = 0;
         return;
     }
-    const float* lg = a.logits + (long)b * a.ldl;
-    const uint32_t* seen = a.seen + (long)b * 33;
+    const int K = a.top_k;
+    float v[SAMPLE_SLOTS];
     float rv = -INFINITY;
     int ri = 0x7fffffff;
-    for (int i = tid; i < VOCAB; i += 1024) {
-        const float l = lg[i];
-        if (a.logits_out) a.logits_out[(long)b * a.ldlo + i] = l;
-        argmax_merge(rv, ri, l, i);
-        float pen = l;
-        if ((seen[i >> 5] >> (i & 31)) & 1u) pen = l < 0.f ? l * a.rep_penalty : l / a.rep_penalty;
-        vals[i] = pen / a.temperature;
+#pragma unroll
+    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
+        const int i = tid + 256 * j;
+        v[j] = -INFINITY;
+        if (i < VOCAB) {
+            if (a.logits_out) a.logits_out[(long)b * a.ldlo + i] = l[j];
+            argmax_merge(rv, ri, l[j], i);
+            float pen = l[j];
+            if ((sw[j] >> (i & 31)) & 1u) pen = l[j] < 0.f ? l[j] * a.rep_penalty : l[j] / a.rep_penalty;
+            v[j] = pen / a.temperature;
+        }
     }
-    block_argmax(rv, ri, sv, si);
+    block_argmax_dpp(rv, ri, sv, si);
     const int raw_arg = ri;
-    // ---- k-th largest (with multiplicity) by MSB-first radix select
-    if (tid == 0) { sel_prefix = 0; sel_remain = (uint32_t)a.top_k; }
-    uint32_t mask = 0;
-    for (int pass = 0; pass < 4; ++pass) {
-        const int shift = 24 - 8 * pass;
-        if (tid < 256) hist[tid] = 0;
-        __syncthreads();
-        const uint32_t prefix = sel_prefix;
-        for (int i = tid; i < VOCAB; i += 1024) {
-            const uint32_t k = f2key(vals[i]);
-            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (tid < 64) {
-            // lane l owns bins 255-4l .. 252-4l (descending)
-            uint32_t c[4], s = 0;
+    if (a.greedy) {
+        // q := 1 and softmax is monotone: argmax(p / q) is the first index of the
+        // largest penalised logit; the top-k mask cannot remove the maximum.
+        float gv = -INFINITY;
+        int gi = 0x7fffffff;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { c[j] = hist[255 - 4 * tid - j]; s += c[j]; }
-            uint32_t incl = s;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o, 64);
-                if (tid >= o) incl += t;
-            }
-            const uint32_t excl = incl - s;
-            const uint32_t rem = sel_remain;
-            const bool mine = excl < rem && incl >= rem;
-            if (mine) {
-                uint32_t cum = excl;
-                for (int j = 0; j < 4; ++j) {
-                    if (cum + c[j] >= rem) {
-                        sel_prefix = prefix | ((uint32_t)(255 - 4 * tid - j) << shift);
-                        sel_remain = rem - cum;
-                        break;
-                    }
-                    cum += c[j];
-                }
-            }
+        for (int j = 0; j < SAMPLE_SLOTS; ++j) {
+            const int i = tid + 256 * j;
+            if (i < VOCAB) argmax_merge(gv, gi, v[j], i);
         }
-        mask |= 255u << shift;
-        __syncthreads();
+        block_argmax_dpp(gv, gi, sv, si);
+        if (tid == 0) sample_commit(a, b, gi, raw_arg, st_ny, st_steps, st_kv, seen_s);
+        return;
     }
-    const float thr = key2f(sel_prefix);
+    // ---- k-th largest with multiplicity
+    if (a.ablate == 3) {
+        if (tid == 0) { a.y[(long)b * a.ldy + st_ny] = raw_arg; a.ny[b] = st_ny + 1; }
+        return;
+    }
+    if (a.ablate == 0) {
+        float h[SAMPLE_SLOTS];
+#pragma unroll
+        for (int j = 0; j < SAMPLE_SLOTS; ++j) h[j] = v[j];
+        sort_desc(h);
+        int hp = 0;
+        for (int r = 0; r < K; ++r) {
+            const float m = wave_extract(h, hp);
+            if (lane == 0) cand[w][r] = m;
+        }
+    }
+    __syncthreads();
+    if (w == 0 && a.ablate == 0) {
+        float h[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h[j] = lane < K ? cand[j][lane] : -INFINITY;
+        sort_desc(h);
+        int hp = 0;
+        float m = -INFINITY;
+        for (int r = 0; r < K; ++r) m = wave_extract(h, hp);
+        if (lane == 0) thr_s = m;
+    }
+    if (a.ablate && tid == 0) thr_s = -INFINITY;
+    __syncthreads();
+    const float thr = thr_s;
     // ---- softmax over kept entries, then argmax(p / q)
     float lmax = -INFINITY;
-    for (int i = tid; i < VOCAB; i += 1024) {
-        const float v = vals[i] < thr ? -INFINITY : vals[i];
-        vals[i] = v;
-        lmax = fmaxf(lmax, v);
+#pragma unroll
+    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
+        v[j] = v[j] < thr ? -INFINITY : v[j];
+        lmax = fmaxf(lmax, v[j]);
     }
-    const float m = block_max(lmax, sv);
+    const float m = a.ablate == 2 ? 0.f : block_max_dpp(lmax, sv);
     float lsum = 0.f;
-    for (int i = tid; i < VOCAB; i += 1024) {
-        const float e = expf(vals[i] - m);
-        vals[i] = e;
-        lsum += e;
+#pragma unroll
+    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
+        v[j] = expf(v[j] - m);
+        lsum += v[j];
     }
-    const float sum = block_sum(lsum, sv);
-    const int step = a.prefill ? 0 : a.steps[b] + 1;
+    const float sum = a.ablate == 2 ? 1.f : block_sum_dpp(lsum, sv);
+    if (tid == 0) step_s = st_steps;
+    __syncthreads();
+    const int step = a.prefill ? 0 : step_s + 1;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = tid; i < VOCAB; i += 1024) {
-        const float p = vals[i] / sum;
+#pragma unroll
+    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
+        const int i = tid + 256 * j;
+        if (i >= VOCAB) continue;
+        const float p = v[j] / sum;
         float q = 1.0f;
         if (!a.greedy) {
             const uint4 r = philox4x32(make_uint4((uint32_t)i, (uint32_t)step, (uint32_t)b, 0x51u),
@@ -623,29 +714,12 @@ __global__ __launch_bounds__(1024) void k_sample(SampleArgs a) {
         }
         argmax_merge(bv, bi, p / q, i);
     }
-    block_argmax(bv, bi, sv, si);
-    if (tid == 0) {
-        const int tok = bi;
-        const int n = a.ny[b];
-        a.y[(long)b * a.ldy + n] = tok;
-        a.ny[b] = n + 1;
-        a.seen[(long)b * 33 + (tok >> 5)] |= 1u << (tok & 31);
-        if (!a.prefill) {
-            const bool stop = raw_arg == 1024 || tok == 1024;
-            if (a.stop_out) a.stop_out[b] = stop ? 1 : 0;
-            const int st = a.steps[b] + 1;
-            a.steps[b] = st;
-            a.kvlen[b] += 1;
-            bool fin;
-            if (a.force_steps > 0) fin = st >= a.force_steps;
-            else fin = stop || st >= a.max_steps;
-            if (fin) a.done[b] = 1;
-        }
-    }
+    block_argmax_dpp(bv, bi, sv, si);
+    if (tid == 0) sample_commit(a, b, bi, raw_arg, st_ny, st_steps, st_kv, seen_s);
 }
 
 void sample_tokens(const SampleArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_sample, dim3(a.B), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_sample, dim3(a.B), dim3(256), 0, s, a);
 }
 
 __global__ __launch_bounds__(256) void k_seq_init(int b, const int64_t* prompts, int P, int L,

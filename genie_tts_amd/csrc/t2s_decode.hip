@@ -16,7 +16,6 @@ namespace gsv {
 // ---------------------------------------------------------------------------
 // Attention (one head, one sequence) + out-projection partial for that head.
 // ---------------------------------------------------------------------------
-#define DEC_KP 4          // keys per thread held in registers (len <= 1024)
 // Reduce-scatter of a 32-vector over the 64 lanes of a wave: afterwards lane l
 // holds sum over all lanes of a[l & 31].
 __device__ __forceinline__ float wave_reduce_scatter32(float (&a)[32]) {
@@ -60,36 +59,56 @@ __global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
     const float4 qv = *reinterpret_cast<const float4*>(a.q + (long)b * 512 + h * 32 + 4 * c);
     const float q0 = qv.x * sc, q1 = qv.y * sc, q2 = qv.z * sc, q3 = qv.w * sc;
     float mt = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-    constexpr int U = 4;
+    // One pass = 32 groups x U keys, every K/V row of the pass loaded before any
+    // math (one memory round trip for up to 512 keys); the per-lane softmax state
+    // is merged once per pass.
+    constexpr int U = 16;
     for (int base = 0; base < len; base += 32 * U) {
         float4 kk[U], vv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int t = min(base + u * 32 + g, len - 1);
-            kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
-            vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            float sv = q0 * (kk[u].x * sc);
-            sv += q1 * (kk[u].y * sc);
-            sv += q2 * (kk[u].z * sc);
-            sv += q3 * (kk[u].w * sc);
-            sv += __shfl_xor(sv, 1, 64);
-            sv += __shfl_xor(sv, 2, 64);
-            sv += __shfl_xor(sv, 4, 64);
-            if (base + u * 32 + g < len) {          // uniform within the 8-lane group
-                const float mn = fmaxf(mt, sv);
-                const float f = expf(mt - mn);
-                const float p = expf(sv - mn);
-                l = l * f + p;
-                o0 = o0 * f + p * vv[u].x;
-                o1 = o1 * f + p * vv[u].y;
-                o2 = o2 * f + p * vv[u].z;
-                o3 = o3 * f + p * vv[u].w;
-                mt = mn;
+            const int t = base + u * 32 + g;
+            if (t < len) {
+                kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
+                vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
+            } else {
+                kk[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                vv[u] = kk[u];
             }
         }
+        float sv[U];
+        float pm = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float x = q0 * (kk[u].x * sc);
+            x += q1 * (kk[u].y * sc);
+            x += q2 * (kk[u].z * sc);
+            x += q3 * (kk[u].w * sc);
+            x += __shfl_xor(x, 1, 64);
+            x += __shfl_xor(x, 2, 64);
+            x += __shfl_xor(x, 4, 64);
+            sv[u] = base + u * 32 + g < len ? x : -INFINITY;   // uniform within the 8-lane group
+            pm = fmaxf(pm, sv[u]);
+        }
+        if (pm == -INFINITY) continue;                          // this group has no key in the pass
+        const float mn = fmaxf(mt, pm);
+        const float f = expf(mt - mn);
+        float ls = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float p = expf(sv[u] - mn);
+            ls += p;
+            a0 += p * vv[u].x;
+            a1 += p * vv[u].y;
+            a2 += p * vv[u].z;
+            a3 += p * vv[u].w;
+        }
+        l = l * f + ls;
+        o0 = o0 * f + a0;
+        o1 = o1 * f + a1;
+        o2 = o2 * f + a2;
+        o3 = o3 * f + a3;
+        mt = mn;
     }
     // block max of the per-group maxima
     const float bm = wave_max(mt);

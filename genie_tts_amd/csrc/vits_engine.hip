@@ -576,12 +576,14 @@ extern "C" int gsv_debug_copy(gsv_engine* eng, const char* name, float* dst, int
 
 extern "C" int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout, int k,
                                 int dil, int pad, const float* bias, float* out, int tout,
-                                int in_act, float slope, void* stream) {
+                                int in_act, float slope, float* splitk_ws, int64_t splitk_cap,
+                                void* stream) {
     ConvArgs a{};
     a.x = x; a.x_cs = tin; a.x_ts = 1; a.Cin = cin; a.Tin = tin;
     a.w = w; a.Cout = cout; a.K = k; a.dil = dil; a.pad = pad; a.bias = bias;
     a.out = out; a.o_cs = tout; a.o_ts = 1; a.n_t = tout; a.o_tstride = 1; a.o_toff = 0; a.o_len = tout;
     a.in_act = in_act; a.in_slope = slope; a.mode = CV_STORE; a.phases = 1;
+    a.part = splitk_ws; a.part_cap = splitk_cap;
     conv1d(a, (hipStream_t)stream);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "debug conv");
 }

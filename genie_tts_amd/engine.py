@@ -80,7 +80,8 @@ def lib():
         L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
-                                       ctypes.c_float, vp]
+                                       ctypes.c_float, vp, ctypes.c_int64, vp]
+        L.gsv_debug_sample.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(Sampler), ctypes.c_int, vp, vp, vp]
         L.gsv_probe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_float), vp]
         L.gsv_set_timing.argtypes = [vp, ctypes.c_int]
@@ -95,7 +96,7 @@ EXPORTED = (
     "gsv_finalize_weights", "gsv_reserve", "gsv_t2s_encode", "gsv_t2s_generate", "gsv_t2s_prefill",
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
-    "gsv_probe", "gsv_get_kernel_timing",
+    "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample",
 )
 
 
@@ -120,16 +121,29 @@ def _ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
 
-def debug_conv1d(x, w, bias=None, dil=1, pad=0, in_act=False, slope=0.1):
-    """Run the engine's conv1d kernel once (tests): x [Cin,T], w [Cout,Cin,K] cuda fp32."""
+def debug_conv1d(x, w, bias=None, dil=1, pad=0, in_act=False, slope=0.1, splitk_ws=None):
+    """Run the engine's conv1d kernel once (tests): x [Cin,T], w [Cout,Cin,K] cuda fp32.
+    splitk_ws (cuda fp32 tensor) enables the split-K path for small grids."""
     torch = _torch()
     cin, tin = x.shape
     cout, _, k = w.shape
     tout = tin + 2 * pad - dil * (k - 1)
     out = torch.empty((cout, tout), dtype=torch.float32, device=x.device)
     _check(lib().gsv_debug_conv1d(_ptr(x), cin, tin, _ptr(w), cout, k, dil, pad, _ptr(bias), _ptr(out),
-                                  tout, int(in_act), ctypes.c_float(slope), _stream()), "gsv_debug_conv1d")
+                                  tout, int(in_act), ctypes.c_float(slope), _ptr(splitk_ws),
+                                  0 if splitk_ws is None else splitk_ws.numel(), _stream()), "gsv_debug_conv1d")
     return out
+
+
+def debug_sample(logits, seen, sampler: "Sampler", step: int):
+    """Run the decode sampler kernel (tests): logits [B,1025] cuda f32, seen [B,33] cuda int32 bitmaps."""
+    torch = _torch()
+    B = logits.shape[0]
+    tok = torch.empty((B,), dtype=torch.int64, device=logits.device)
+    stop = torch.empty((B,), dtype=torch.uint8, device=logits.device)
+    _check(lib().gsv_debug_sample(_ptr(logits), _ptr(seen), B, ctypes.byref(sampler), step, _ptr(tok), _ptr(stop),
+                                  _stream()), "gsv_debug_sample")
+    return tok, stop
 
 
 class Engine:

@@ -92,7 +92,7 @@ typedef struct {
 
 /* Sampler (reference constants: t2s_stage_decoder_fp32.onnx#1780-1801). */
 typedef struct {
-    int32_t top_k;               /* 15 */
+    int32_t top_k;               /* 15 (1..64) */
     float   temperature;         /* 1.0 */
     float   repetition_penalty;  /* 1.35 */
     int32_t greedy;              /* 1: RandomNormalLike := 1 (argmax of penalised logits) */
@@ -143,11 +143,17 @@ int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
 
 /* Debug hooks (tests only): copy a named VITS workspace buffer after
  * gsv_vits_decode ("ge","stats","z","y","q","te","g0","g1","spec","a");
- * run one conv1d (zero padding) on device buffers. */
+ * run one conv1d (zero padding) on device buffers; a non-NULL splitk_ws (device,
+ * splitk_cap floats) enables the split-K path for under-filled grids. */
 int gsv_debug_copy(gsv_engine* eng, const char* name, float* dst, int64_t n, void* stream);
 int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout, int k, int dil,
                      int pad, const float* bias, float* out, int tout, int in_act, float slope,
-                     void* stream);
+                     float* splitk_ws, int64_t splitk_cap, void* stream);
+/* Run the decode sampler kernel once on logits (device [B][1025]) with the
+ * token-presence bitmaps seen (device u32 [B][33]) at loop step `step`
+ * (Philox counter); tokens (device i64 [B]) and stop flags (device u8 [B]). */
+int gsv_debug_sample(const float* logits, const uint32_t* seen, int B, const gsv_sampler* s,
+                     int step, int64_t* tokens, uint8_t* stop, void* stream);
 
 /* Probe: replay one kernel configuration `iters` times (hipGraph) between HIP
  * events on the engine stream; *us = average microseconds per launch.
