@@ -21,6 +21,21 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Deterministic cross-block accumulation: partial sums converted to int64 fixed
+// point (2^-32 resolution) and added with device-scope integer atomics, which
+// are associative -- the sum is independent of arrival order.
+__device__ __forceinline__ long long to_fx(float v) { return __double2ll_rn((double)v * 4294967296.0); }
+__device__ __forceinline__ float from_fx(long long v) { return (float)((double)v * (1.0 / 4294967296.0)); }
+__device__ __forceinline__ void fx_add(long long* p, float v) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)to_fx(v));
+}
+
+// Phase timestamp (100 MHz realtime counter) of block blockIdx.x, slot i (diagnostics).
+#define GSV_STAMP(tr, i)                                                              \
+    do {                                                                              \
+        if ((tr) && threadIdx.x == 0) (tr)[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
 // DPP wave reductions (VALU latency, no LDS crossbar): quad swaps, half-row and
 // row mirrors, then row_bcast15 / row_bcast31; lane 63 holds the result, read
 // back as a wave-uniform value.

@@ -56,6 +56,7 @@ gsv_engine::~gsv_engine() {
     if (own_stream && stream) hipStreamDestroy(stream);
     if (done_host) hipHostFree(done_host);
     for (auto& e : kev) if (e) hipEventDestroy(e);
+    if (ktrace) hipFree(ktrace);
     for (auto& e : poll_ev) if (e) hipEventDestroy(e);
     for (auto& e : ev) if (e) hipEventDestroy(e);
     if (ev_in) hipEventDestroy(ev_in);
@@ -119,6 +120,12 @@ int gsv_engine::finalize_t2s() {
     pe_max = 4096;
     if (const char* e = std::getenv("GENIE_FFN_SLICES")) ffn_slices = std::atoi(e) == 32 ? 32 : 64;
     if (const char* e = std::getenv("GENIE_DECODE_FUSE")) fuse_qkv = std::atoi(e) == 2;
+    if (const char* e = std::getenv("GENIE_ACC")) use_acc = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_KTRACE"))
+        if (std::atoi(e) == 1 && !ktrace) {
+            hipMalloc(&ktrace, (size_t)3 * 256 * 8 * 8);
+            hipMemset(ktrace, 0, (size_t)3 * 256 * 8 * 8);
+        }
     std::vector<float> pe((size_t)pe_max * 512);
     for (int p = 0; p < pe_max; ++p)
         for (int i = 0; i < 256; ++i) {
@@ -216,7 +223,9 @@ int gsv_engine::reserve(int batch, int tokens) {
     pF = (float*)A((size_t)nt * 2048 * 4);
     prow_len = (int*)A((size_t)nt * 4);
     prompts_buf = (int64_t*)A((size_t)nt * 8);
-    if (!pF || !prompts_buf) return set_error(GSV_E_HIP, "state allocation failed");
+    acc64 = (long long*)A((size_t)nb * ACC_SEQ * 8);
+    if (!pF || !prompts_buf || !acc64) return set_error(GSV_E_HIP, "state allocation failed");
+    hipMemset(acc64, 0, (size_t)nb * ACC_SEQ * 8);
     std::vector<int> id(nb);
     for (int i = 0; i < nb; ++i) id[i] = i;
     hipMemcpy(ident, id.data(), nb * 4, hipMemcpyHostToDevice);
@@ -366,6 +375,10 @@ SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
 // ------------------------------------------------------------ decode step
 void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st) {
     const long sstride = (long)16 * tmax * 32;
+    // fixed-point hand-off slices of layer l (fused path): FFN output, attention output
+    const bool acc = use_acc && !fuse_qkv && B <= 8 && tmax <= 1024;
+    auto accF = [&](int l) { return acc ? acc64 + (long)(2 * l) * 512 : nullptr; };
+    auto accA = [&](int l) { return acc ? acc64 + (long)(2 * l + 1) * 512 : nullptr; };
     decode_embed(B, y, tmax, ny, emb_audio, alpha_audio, pe_tab, h, done, st);
     if (B <= 8 && tmax <= 1024) {
         // fused path: 2 launches per layer (QKV+attention+out-proj | FFN1+FFN2)
@@ -398,17 +411,23 @@ void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hi
                 a.W = W.w_in; a.bias = W.b_in; a.C = q; a.ldc = 512; a.mode = EPI_QKV;
                 a.kv.k = kcache[l]; a.kv.v = vcache[l]; a.kv.tmax = tmax; a.kv.row_pos = kvlen;
                 a.kv.seq_stride = sstride; a.kv.row_skip = done;
+                if (l > 0) { a.acc_in = accF(l - 1); a.acc_bstride = ACC_SEQ; }
+                if (l == probe_layer) a.trace = ktrace;
                 gemv_f16(a, st);
                 AttnOutArgs ao{};
                 ao.B = B; ao.q = q; ao.k = kcache[l]; ao.v = vcache[l]; ao.seq_stride = sstride;
                 ao.tmax = tmax; ao.kvlen = kvlen; ao.done = done; ao.scale = qk_scale;
                 ao.WoT = W.woT; ao.part = attn_part;
+                ao.acc_out = accA(l); ao.acc_bstride = ACC_SEQ;
+                if (l == probe_layer && ktrace) ao.trace = ktrace + 256 * 8;
                 attn_outproj(ao, st);
             }
             FfnArgs fa{};
             fa.B = B; fa.nslices = ffn_slices; fa.h = h; fa.bo = W.b_out; fa.attn_part = attn_part;
             fa.ln_g = W.n1w; fa.ln_b = W.n1b; fa.h1 = h1;
             fa.W1 = W.w1; fa.b1 = W.b1; fa.W2T = W.w2T; fa.part = ffn_part;
+            if (!fuse_qkv) { fa.acc_attn = accA(l); fa.acc_out = accF(l); fa.acc_bstride = ACC_SEQ; }
+            if (l == probe_layer && ktrace) fa.trace = ktrace + 2 * 256 * 8;
             if (probe_now && l == probe_layer) ffn_fused(fa, st, kev[0], kev[1]);
             else ffn_fused(fa, st);
         }
@@ -418,6 +437,7 @@ void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hi
         lg.part_bias = layers[23].b2; lg.part_res = h1;
         lg.ln_g = layers[23].n2w; lg.ln_b = layers[23].n2b;
         lg.W = w_pred; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
+        lg.acc_in = accF(23); lg.acc_bstride = ACC_SEQ;
         gemv_f16(lg, st);
     } else {
         // batched path: f32-MFMA GEMMs over the B rows + row LayerNorms
@@ -459,6 +479,7 @@ void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hi
     }
     SampleArgs sa = sampler_args(sp, B);
     sa.logits_out = logits_out; sa.ldlo = 1025;
+    if (acc) { sa.acc_zero = acc64; sa.acc_n = ACC_SEQ; }
     sample_tokens(sa, st);
 }
 
@@ -808,4 +829,12 @@ extern "C" int gsv_debug_sample(const float* logits, const uint32_t* seen, int B
     const bool ok = hipStreamSynchronize(st) == hipSuccess;
     hipFree(buf);
     return ok ? 0 : set_error(GSV_E_HIP, "debug sample");
+}
+
+extern "C" int gsv_debug_ktrace(gsv_engine* eng, uint64_t* host, int n) {
+    ENG_CHECK(eng);
+    if (!eng->ktrace) return set_error(GSV_E_STATE, "set GENIE_KTRACE=1 before gsv_finalize_weights");
+    n = std::min(n, 3 * 256 * 8);
+    return hipMemcpy(host, eng->ktrace, (size_t)n * 8, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0 : set_error(GSV_E_HIP, "ktrace copy");
 }

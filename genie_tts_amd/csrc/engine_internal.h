@@ -14,6 +14,7 @@
 namespace gsv {
 int set_error(int code, const std::string& msg);
 struct StreamScope;
+constexpr long ACC_SEQ = 24 * 2 * 512;   // fixed-point hand-off accumulators per sequence
 
 struct Staged {
     std::vector<int64_t> dims;
@@ -87,6 +88,9 @@ struct gsv_engine {
     int kern_n = 0;
     int kern_err = 0;        // last hipEventElapsedTime failure (reported as -samples)
     bool probe_now = false;  // eager step in flight: time the probed FFN launch
+    unsigned long long* ktrace = nullptr;
+    long long* acc64 = nullptr;   // per sequence [24 layers][FFN out, attn out][512] fixed-point hand-offs
+    bool use_acc = true;          // GENIE_ACC=0: split-K partial slabs instead   // GENIE_KTRACE: phase stamps [3][256][8] of layer probe_layer
     hipEvent_t poll_ev[2] = {};
 
     ~gsv_engine();

@@ -95,6 +95,10 @@ struct GemvArgs {
     int mode;
     const float* res; long ldr;
     KVScatter kv;
+    unsigned long long* trace;         // phase stamps [block][8] (GENIE_KTRACE diagnostics)
+    // fixed-point accumulator input (replaces part/n_part): src[b][k] :=
+    //   part_res[b][k] + (part_bias[k] + acc_in[b * acc_bstride + k] * 2^-32)
+    const long long* acc_in; long acc_bstride;
 };
 void gemv_f16(const GemvArgs& a, hipStream_t s);
 
@@ -109,6 +113,8 @@ struct AttnOutArgs {
     float scale;
     const __half* WoT;                     // [512 in][512 out]
     float* part;                           // [16][B][512]
+    unsigned long long* trace;
+    long long* acc_out; long acc_bstride;  // if set: fixed-point adds instead of part
 };
 void attn_outproj(const AttnOutArgs& a, hipStream_t s);
 
@@ -139,6 +145,8 @@ struct FfnArgs {
     const float* ln_g; const float* ln_b; float* h1;
     const __half* W1; const float* b1; const __half* W2T;      // W2T [2048][512]
     float* part;                                               // [nslices][B][512]
+    unsigned long long* trace;
+    const long long* acc_attn; long long* acc_out; long acc_bstride;  // fixed-point hand-offs
 };
 void ffn_fused(const FfnArgs& a, hipStream_t s, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
@@ -161,6 +169,7 @@ struct SampleArgs {
     int prefill;                       // 1: first-stage sampler (no stop, no step count)
     float* logits_out; long ldlo;      // optional copy of raw logits
     int ablate;                        // probe only: 1 skip top-k, 2 also skip softmax, 3 loads + tail
+    long long* acc_zero; long acc_n;   // per-sequence fixed-point accumulators zeroed for the next step
 };
 void sample_tokens(const SampleArgs& a, hipStream_t s);
 

@@ -352,22 +352,41 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int B = a.B;
     // weights first: their HBM latency overlaps the activation load + LN prologue
+    GSV_STAMP(a.trace, 0);
     const int nbase = (blockIdx.x * 4 + w) * ROWS;
     constexpr int KI = K / 512;
     uint4 wr[ROWS][KI];
+    // weights are loaded after the prologue's activation loads (vmcnt retires in
+    // order: anything issued behind the weight stream would wait for all of it)
+    auto load_weights = [&]() {
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-        const int n = min(nbase + r, a.N - 1);
-        const __half* wp = a.W + (long)n * K + lane * 8;
+        for (int r = 0; r < ROWS; ++r) {
+            const int n = min(nbase + r, a.N - 1);
+            const __half* wp = a.W + (long)n * K + lane * 8;
 #pragma unroll
-        for (int i = 0; i < KI; ++i) wr[r][i] = *reinterpret_cast<const uint4*>(wp + i * 512);
-    }
+            for (int i = 0; i < KI; ++i) wr[r][i] = *reinterpret_cast<const uint4*>(wp + i * 512);
+        }
+    };
+    // every small parameter the later phases need, loaded now (no round trip after a barrier)
+    float bias_r[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) bias_r[r] = a.bias ? a.bias[min(nbase + r, a.N - 1)] : 0.f;
+    float lng0 = 0.f, lng1 = 0.f, lnb0 = 0.f, lnb1 = 0.f;
+    if (a.ln_g) { lng0 = a.ln_g[tid]; lng1 = a.ln_g[tid + 256]; lnb0 = a.ln_b[tid]; lnb1 = a.ln_b[tid + 256]; }
+    int kvpos[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        kvpos[b] = (a.mode == EPI_QKV && b < B) ? (a.kv.row_pos ? a.kv.row_pos[b] : a.kv.pos0) : 0;
     if (a.ln_g) {
         float v0[NB], v1[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             if (b < B) {
-                if (a.part) {
+                if (a.acc_in) {
+                    const long long* ac = a.acc_in + (long)b * a.acc_bstride;
+                    v0[b] = a.part_res[(long)b * 512 + tid] + (a.part_bias[tid] + from_fx(ac[tid]));
+                    v1[b] = a.part_res[(long)b * 512 + tid + 256] + (a.part_bias[tid + 256] + from_fx(ac[tid + 256]));
+                } else if (a.part) {
                     // split-K partial reduce: res + (bias + sum_j part_j), fixed order
                     float p0 = a.part_bias[tid], p1 = a.part_bias[tid + 256];
                     for (int j0 = 0; j0 < a.n_part; j0 += 16) {
@@ -389,13 +408,15 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 }
             }
         }
+        load_weights();
         float mean[NB], den[NB];
         block_meanvar512<NB>(v0, v1, B, mean, den, red);
+        GSV_STAMP(a.trace, 1);
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             if (b >= B) break;
-            const float o0 = (v0[b] - mean[b]) / den[b] * a.ln_g[tid] + a.ln_b[tid];
-            const float o1 = (v1[b] - mean[b]) / den[b] * a.ln_g[tid + 256] + a.ln_b[tid + 256];
+            const float o0 = (v0[b] - mean[b]) / den[b] * lng0 + lnb0;
+            const float o1 = (v1[b] - mean[b]) / den[b] * lng1 + lnb1;
             xs[b * K + tid] = o0;
             xs[b * K + tid + 256] = o1;
             if (a.ln_out && blockIdx.x == 0) {
@@ -404,12 +425,14 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
         }
     } else {
+        load_weights();
         for (int b = 0; b < B; ++b)
             for (int i = tid * 4; i < K; i += 1024)
                 *reinterpret_cast<float4*>(&xs[b * K + i]) =
                     *reinterpret_cast<const float4*>(a.src + (long)b * a.lds + i);
     }
     __syncthreads();
+    GSV_STAMP(a.trace, 2);
     float acc[ROWS][NB];
 #pragma unroll
     for (int r = 0; r < ROWS; ++r)
@@ -435,15 +458,16 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
         }
     }
+    GSV_STAMP(a.trace, 3);
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
         const int n = nbase + r;
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             if (b >= B) continue;
-            const float sum = wave_sum(acc[r][b]);
+            const float sum = wave_sum_dpp(acc[r][b]);
             if (lane != 0 || n >= a.N) continue;
-            const float v = a.bias ? a.bias[n] + sum : sum;
+            const float v = a.bias ? bias_r[r] + sum : sum;
             switch (a.mode) {
                 case EPI_STORE: a.C[(long)b * a.ldc + n] = v; break;
                 case EPI_RELU: a.C[(long)b * a.ldc + n] = fmaxf(v, 0.f); break;
@@ -453,7 +477,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                         a.C[(long)b * a.ldc + n] = v;
                     } else {
                         if (a.kv.row_skip && a.kv.row_skip[b]) break;
-                        const int pos = a.kv.row_pos ? a.kv.row_pos[b] : a.kv.pos0;
+                        const int pos = kvpos[b];
                         const int c = (n - 512) & 511;
                         float* dst = (n < 1024 ? a.kv.k : a.kv.v) + (long)b * a.kv.seq_stride;
                         dst[((long)(c >> 5) * a.kv.tmax + pos) * 32 + (c & 31)] = v;
@@ -463,6 +487,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
         }
     }
+    GSV_STAMP(a.trace, 4);
 }
 
 template <int K, int ROWS>
@@ -597,6 +622,11 @@ __global__ __launch_bounds__(256) void k_sample(SampleArgs a) {
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float* lg = a.logits + (long)b * a.ldl;
     const uint32_t* seen = a.seen + (long)b * 33;
+    if (a.acc_zero) {   // this step's hand-off accumulators: every reader has run
+        long long* z = a.acc_zero + (long)b * a.acc_n;
+        for (long i = tid * 2; i < a.acc_n; i += 512)
+            *reinterpret_cast<longlong2*>(z + i) = make_longlong2(0, 0);
+    }
     // every load issued before the first use (the done flag included)
     float l[SAMPLE_SLOTS];
     uint32_t sw[SAMPLE_SLOTS];

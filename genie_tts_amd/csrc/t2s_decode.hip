@@ -44,36 +44,58 @@ __global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
     __shared__ float reda[4][32];
     __shared__ float ored[4][512];
     const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (a.done && a.done[b]) return;
-    uint4 wo[8];
-    {
-        const __half* base = a.WoT + (long)(h * 32) * 512 + 8 * lane;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wo[i] = *reinterpret_cast<const uint4*>(base + (long)(w + 4 * i) * 512);
-    }
-    const int len = a.kvlen[b] + 1;
+    GSV_STAMP(a.trace, 0);
+    // Issue order = retire order (vmcnt): done/kvlen/q first, then the first 256
+    // K/V rows speculatively (rows < tmax are allocated; rows >= len are masked by
+    // selects, so stale contents never reach the math), then -- once len is known --
+    // the rest of the first pass, then the WoT slice.
+    const uint8_t dn = a.done ? a.done[b] : 0;
+    const int lenv = a.kvlen[b];
     const float* K = a.k + (long)b * a.seq_stride + (long)h * a.tmax * 32;
     const float* V = a.v + (long)b * a.seq_stride + (long)h * a.tmax * 32;
     const float sc = a.scale;
     const int c = lane & 7, g = (w << 3) | (lane >> 3);     // chunk, key group (0..31)
     const float4 qv = *reinterpret_cast<const float4*>(a.q + (long)b * 512 + h * 32 + 4 * c);
+    constexpr int U = 16, US = 8;                            // keys per group per pass; speculative part
+    float4 kk[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < US; ++u) {
+        const int t = min(u * 32 + g, a.tmax - 1);
+        kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
+        vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
+    }
+    if (dn) return;
+    const int len = lenv + 1;
+#pragma unroll
+    for (int u = US; u < U; ++u) {
+        const int t = u * 32 + g;
+        if (t < len) {
+            kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
+            vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
+        } else {
+            kk[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            vv[u] = kk[u];
+        }
+    }
+    uint4 wo[8];
+    {
+        const __half* wb = a.WoT + (long)(h * 32) * 512 + 8 * lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wo[i] = *reinterpret_cast<const uint4*>(wb + (long)(w + 4 * i) * 512);
+    }
     const float q0 = qv.x * sc, q1 = qv.y * sc, q2 = qv.z * sc, q3 = qv.w * sc;
     float mt = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-    // One pass = 32 groups x U keys, every K/V row of the pass loaded before any
-    // math (one memory round trip for up to 512 keys); the per-lane softmax state
-    // is merged once per pass.
-    constexpr int U = 16;
+    // One pass = 32 groups x U keys, every row of the pass in registers before any
+    // math; the per-lane softmax state is merged once per pass.
     for (int base = 0; base < len; base += 32 * U) {
-        float4 kk[U], vv[U];
+        if (base > 0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int t = base + u * 32 + g;
-            if (t < len) {
-                kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
-                vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
-            } else {
-                kk[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                vv[u] = kk[u];
+            for (int u = 0; u < U; ++u) {
+                const int t = base + u * 32 + g;
+                if (t < len) {
+                    kk[u] = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
+                    vv[u] = *reinterpret_cast<const float4*>(V + (long)t * 32 + 4 * c);
+                }
             }
         }
         float sv[U];
@@ -84,10 +106,13 @@ __global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
             x += q1 * (kk[u].y * sc);
             x += q2 * (kk[u].z * sc);
             x += q3 * (kk[u].w * sc);
-            x += __shfl_xor(x, 1, 64);
-            x += __shfl_xor(x, 2, 64);
-            x += __shfl_xor(x, 4, 64);
-            sv[u] = base + u * 32 + g < len ? x : -INFINITY;   // uniform within the 8-lane group
+            // sum over the 8 lanes of the key row: quad swaps, then the half-row mirror
+            x += dpp_f<0xB1, 0xF>(x);
+            x += dpp_f<0x4E, 0xF>(x);
+            x += dpp_f<0x141, 0xF>(x);
+            const bool valid = base + u * 32 + g < len;       // uniform within the 8-lane group
+            sv[u] = valid ? x : -INFINITY;
+            if (!valid) vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             pm = fmaxf(pm, sv[u]);
         }
         if (pm == -INFINITY) continue;                          // this group has no key in the pass
@@ -110,6 +135,7 @@ __global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
         o3 = o3 * f + a3;
         mt = mn;
     }
+    GSV_STAMP(a.trace, 1);
     // block max of the per-group maxima
     const float bm = wave_max(mt);
     if (lane == 0) redm[w] = bm;
@@ -137,6 +163,7 @@ __global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
         os[tid] = ((reda[0][tid] + reda[1][tid]) + (reda[2][tid] + reda[3][tid])) / L;
     }
     __syncthreads();
+    GSV_STAMP(a.trace, 2);
     float r[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = 0.f;
@@ -151,9 +178,18 @@ __global__ __launch_bounds__(256) void k_attn_out(AttnOutArgs a) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) ored[w][8 * lane + k] = r[k];
     __syncthreads();
-    float* dst = a.part + ((long)h * a.B + b) * 512;
-    dst[tid] = (ored[0][tid] + ored[1][tid]) + (ored[2][tid] + ored[3][tid]);
-    dst[tid + 256] = (ored[0][tid + 256] + ored[1][tid + 256]) + (ored[2][tid + 256] + ored[3][tid + 256]);
+    const float r0 = (ored[0][tid] + ored[1][tid]) + (ored[2][tid] + ored[3][tid]);
+    const float r1 = (ored[0][tid + 256] + ored[1][tid + 256]) + (ored[2][tid + 256] + ored[3][tid + 256]);
+    if (a.acc_out) {
+        long long* ac = a.acc_out + (long)b * a.acc_bstride;
+        fx_add(ac + tid, r0);
+        fx_add(ac + tid + 256, r1);
+    } else {
+        float* dst = a.part + ((long)h * a.B + b) * 512;
+        dst[tid] = r0;
+        dst[tid + 256] = r1;
+    }
+    GSV_STAMP(a.trace, 3);
 }
 
 void attn_outproj(const AttnOutArgs& a, hipStream_t s) {
@@ -170,39 +206,54 @@ __global__ __launch_bounds__(256) void k_ffn(FfnArgs a) {
     __shared__ float red[4 * NB * 2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int j = blockIdx.x, B = a.B;
+    GSV_STAMP(a.trace, 0);
     constexpr int RW = RPB / 4;            // FFN1 rows per wave
-    // prefetch FFN1 rows (one 16 B chunk per lane per row) and the W2T slice
-    uint4 w1r[RW];
+    // small parameters now, not after the barriers
+    const float lng0 = a.ln_g[tid], lng1 = a.ln_g[tid + 256], lnb0 = a.ln_b[tid], lnb1 = a.ln_b[tid + 256];
+    float b1r[RW];
 #pragma unroll
-    for (int r = 0; r < RW; ++r)
-        w1r[r] = *reinterpret_cast<const uint4*>(a.W1 + (long)(j * RPB + w * RW + r) * 512 + lane * 8);
-    // W2T slice rows j*RPB + w + 4*i (i < RPB/4), columns [8*lane, +8)
-    uint4 w2r[RPB / 4];
-#pragma unroll
-    for (int i = 0; i < RPB / 4; ++i)
-        w2r[i] = *reinterpret_cast<const uint4*>(a.W2T + (long)(j * RPB + w + 4 * i) * 512 + 8 * lane);
+    for (int r = 0; r < RW; ++r) b1r[r] = a.b1[j * RPB + w * RW + r];
     // prologue: s1 = h + (bo + sum_h attn_part[h]); LN1
     float v0[NB], v1[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         if (b >= B) break;
         float p0 = a.bo[tid], p1 = a.bo[tid + 256];
+        if (a.acc_attn) {
+            const long long* ac = a.acc_attn + (long)b * a.acc_bstride;
+            p0 += from_fx(ac[tid]);
+            p1 += from_fx(ac[tid + 256]);
+        } else {
 #pragma unroll
-        for (int hh = 0; hh < 16; ++hh) {
-            const float* pp = a.attn_part + ((long)hh * B + b) * 512;
-            p0 += pp[tid];
-            p1 += pp[tid + 256];
+            for (int hh = 0; hh < 16; ++hh) {
+                const float* pp = a.attn_part + ((long)hh * B + b) * 512;
+                p0 += pp[tid];
+                p1 += pp[tid + 256];
+            }
         }
         v0[b] = a.h[(long)b * 512 + tid] + p0;
         v1[b] = a.h[(long)b * 512 + tid + 256] + p1;
     }
+    // Weight prefetch AFTER the prologue loads: vmcnt retires in order, so loads
+    // issued after the 64 KB weight stream would wait for all of it.
+    // FFN1 rows (one 16 B chunk per lane per row) and the W2T slice rows
+    // j*RPB + w + 4*i (i < RPB/4), columns [8*lane, +8)
+    uint4 w1r[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+        w1r[r] = *reinterpret_cast<const uint4*>(a.W1 + (long)(j * RPB + w * RW + r) * 512 + lane * 8);
+    uint4 w2r[RPB / 4];
+#pragma unroll
+    for (int i = 0; i < RPB / 4; ++i)
+        w2r[i] = *reinterpret_cast<const uint4*>(a.W2T + (long)(j * RPB + w + 4 * i) * 512 + 8 * lane);
     float mean[NB], den[NB];
     block_meanvar512<NB>(v0, v1, B, mean, den, red);
+    GSV_STAMP(a.trace, 1);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         if (b >= B) break;
-        const float o0 = (v0[b] - mean[b]) / den[b] * a.ln_g[tid] + a.ln_b[tid];
-        const float o1 = (v1[b] - mean[b]) / den[b] * a.ln_g[tid + 256] + a.ln_b[tid + 256];
+        const float o0 = (v0[b] - mean[b]) / den[b] * lng0 + lnb0;
+        const float o1 = (v1[b] - mean[b]) / den[b] * lng1 + lnb1;
         xs[b][tid] = o0;
         xs[b][tid + 256] = o1;
         if (j == 0) {
@@ -225,11 +276,12 @@ __global__ __launch_bounds__(256) void k_ffn(FfnArgs a) {
             float s = 0.f;
             s += wf[0] * x0.x; s += wf[1] * x0.y; s += wf[2] * x0.z; s += wf[3] * x0.w;
             s += wf[4] * x1.x; s += wf[5] * x1.y; s += wf[6] * x1.z; s += wf[7] * x1.w;
-            s = wave_sum(s);
-            if (lane == 0) fs[b][w * RW + r] = fmaxf(a.b1[row] + s, 0.f);
+            s = wave_sum_dpp(s);
+            if (lane == 0) fs[b][w * RW + r] = fmaxf(b1r[r] + s, 0.f);
         }
     }
     __syncthreads();
+    GSV_STAMP(a.trace, 2);
     // FFN2 partial: each wave sums its rows for 8 columns per lane, then LDS reduce
     __shared__ float fred[4][512];
     for (int b = 0; b < B; ++b) {
@@ -247,11 +299,20 @@ __global__ __launch_bounds__(256) void k_ffn(FfnArgs a) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) fred[w][8 * lane + k] = r8[k];
         __syncthreads();
-        float* dst = a.part + ((long)j * B + b) * 512;
-        dst[tid] = (fred[0][tid] + fred[1][tid]) + (fred[2][tid] + fred[3][tid]);
-        dst[tid + 256] = (fred[0][tid + 256] + fred[1][tid + 256]) + (fred[2][tid + 256] + fred[3][tid + 256]);
+        const float r0 = (fred[0][tid] + fred[1][tid]) + (fred[2][tid] + fred[3][tid]);
+        const float r1 = (fred[0][tid + 256] + fred[1][tid + 256]) + (fred[2][tid + 256] + fred[3][tid + 256]);
+        if (a.acc_out) {
+            long long* ac = a.acc_out + (long)b * a.acc_bstride;
+            fx_add(ac + tid, r0);
+            fx_add(ac + tid + 256, r1);
+        } else {
+            float* dst = a.part + ((long)j * B + b) * 512;
+            dst[tid] = r0;
+            dst[tid + 256] = r1;
+        }
         __syncthreads();
     }
+    GSV_STAMP(a.trace, 3);
 }
 
 // start/stop (optional): hipExtLaunchKernelGGL stamps them from the dispatch packet's
@@ -344,7 +405,7 @@ __global__ __launch_bounds__(256) void k_qkv_attn(QkvAttnArgs a) {
                 float sacc = 0.f;
                 sacc += wf[0] * x0.x; sacc += wf[1] * x0.y; sacc += wf[2] * x0.z; sacc += wf[3] * x0.w;
                 sacc += wf[4] * x1.x; sacc += wf[5] * x1.y; sacc += wf[6] * x1.z; sacc += wf[7] * x1.w;
-                sacc = wave_sum(sacc);
+                sacc = wave_sum_dpp(sacc);
                 if (lane == 0) {
                     const int row = m * 512 + h * 32 + w * 8 + r;
                     qkv[m][w * 8 + r] = a.b_in[row] + sacc;

@@ -81,6 +81,7 @@ def lib():
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_float, vp, ctypes.c_int64, vp]
+        L.gsv_debug_ktrace.argtypes = [vp, vp, ctypes.c_int]
         L.gsv_debug_sample.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(Sampler), ctypes.c_int, vp, vp, vp]
         L.gsv_probe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_float), vp]
@@ -96,7 +97,7 @@ EXPORTED = (
     "gsv_finalize_weights", "gsv_reserve", "gsv_t2s_encode", "gsv_t2s_generate", "gsv_t2s_prefill",
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
-    "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample",
+    "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
 )
 
 
@@ -327,6 +328,12 @@ class Engine:
         us, n = ctypes.c_float(), ctypes.c_int32()
         _check(lib().gsv_get_kernel_timing(self.h, ctypes.byref(us), ctypes.byref(n)), "gsv_get_kernel_timing")
         return us.value, n.value
+
+    def ktrace(self) -> np.ndarray:
+        """[3 kernels][256 blocks][8 slots] realtime stamps (GENIE_KTRACE=1 builds only)."""
+        out = np.zeros((3, 256, 8), np.uint64)
+        _check(lib().gsv_debug_ktrace(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size), "gsv_debug_ktrace")
+        return out
 
     def timing(self) -> List[float]:
         a = (ctypes.c_float * 4)()
