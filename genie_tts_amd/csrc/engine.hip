@@ -224,7 +224,8 @@ int gsv_engine::reserve(int batch, int tokens) {
     prow_len = (int*)A((size_t)nt * 4);
     prompts_buf = (int64_t*)A((size_t)nt * 8);
     acc64 = (long long*)A((size_t)nb * ACC_SEQ * 8);
-    if (!pF || !prompts_buf || !acc64) return set_error(GSV_E_HIP, "state allocation failed");
+    pSlab = (float*)A((size_t)8 * nt * 512 * 4);
+    if (!pF || !prompts_buf || !acc64 || !pSlab) return set_error(GSV_E_HIP, "state allocation failed");
     hipMemset(acc64, 0, (size_t)nb * ACC_SEQ * 8);
     std::vector<int> id(nb);
     for (int i = 0; i < nb; ++i) id[i] = i;
@@ -323,12 +324,22 @@ int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, in
         at.seq_stride = sstride; at.tmax = tmax; at.row_len = prow_len; at.out = pO; at.ldo = 512;
         at.rows = N0; at.scale = qk_scale;
         attn_rows(at, st);
+        // out-proj and FFN2 have 32 output tiles: split K over 4 / 8 blocks into slabs,
+        // reduced in fixed order (+ bias + residual) by the LayerNorm that follows
+        const bool slabs = gemm_slabs_supported(512, 512, 512) && gemm_slabs_supported(2048, 2048, 2048);
+        const long slab_stride = (long)tmax * 512;
         GemmArgs go{};
         go.M = N0; go.N = 512; go.K = 512; go.A = pO; go.lda = 512;
         go.W = W.w_out; go.ldw = 512; go.w_f16 = 1; go.bias = W.b_out;
-        go.C = pS; go.ldc = 512; go.mode = EPI_RESID; go.res = pH; go.ldr = 512;
-        gemm_nt(go, st);
-        layernorm_rows(pS, pH1, N0, W.n1w, W.n1b, st);
+        if (slabs) {
+            go.C = pSlab; go.ldc = 512; go.mode = EPI_SLAB; go.ksplit = 4; go.slab_stride = slab_stride;
+            gemm_nt(go, st);
+            layernorm_rows_slabs(pSlab, 4, slab_stride, W.b_out, pH, pH1, N0, W.n1w, W.n1b, st);
+        } else {
+            go.C = pS; go.ldc = 512; go.mode = EPI_RESID; go.res = pH; go.ldr = 512;
+            gemm_nt(go, st);
+            layernorm_rows(pS, pH1, N0, W.n1w, W.n1b, st);
+        }
         GemmArgs g1{};
         g1.M = N0; g1.N = 2048; g1.K = 512; g1.A = pH1; g1.lda = 512;
         g1.W = W.w1; g1.ldw = 512; g1.w_f16 = 1; g1.bias = W.b1;
@@ -337,9 +348,15 @@ int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, in
         GemmArgs g2{};
         g2.M = N0; g2.N = 512; g2.K = 2048; g2.A = pF; g2.lda = 2048;
         g2.W = W.w2; g2.ldw = 2048; g2.w_f16 = 1; g2.bias = W.b2;
-        g2.C = pS; g2.ldc = 512; g2.mode = EPI_RESID; g2.res = pH1; g2.ldr = 512;
-        gemm_nt(g2, st);
-        layernorm_rows(pS, pH, N0, W.n2w, W.n2b, st);
+        if (slabs) {
+            g2.C = pSlab; g2.ldc = 512; g2.mode = EPI_SLAB; g2.ksplit = 8; g2.slab_stride = slab_stride;
+            gemm_nt(g2, st);
+            layernorm_rows_slabs(pSlab, 8, slab_stride, W.b2, pH1, pH, N0, W.n2w, W.n2b, st);
+        } else {
+            g2.C = pS; g2.ldc = 512; g2.mode = EPI_RESID; g2.res = pH1; g2.ldr = 512;
+            gemm_nt(g2, st);
+            layernorm_rows(pS, pH, N0, W.n2w, W.n2b, st);
+        }
     }
     // logits of the last row (#1785-1788), first-stage sampler on prompts (#1789-1815)
     GemvArgs lg{};

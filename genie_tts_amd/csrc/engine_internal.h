@@ -89,6 +89,7 @@ struct gsv_engine {
     int kern_err = 0;        // last hipEventElapsedTime failure (reported as -samples)
     bool probe_now = false;  // eager step in flight: time the probed FFN launch
     unsigned long long* ktrace = nullptr;
+    float* pSlab = nullptr;       // prefill split-K slabs [8][tmax][512]
     long long* acc64 = nullptr;   // per sequence [24 layers][FFN out, attn out][512] fixed-point hand-offs
     bool use_acc = true;          // GENIE_ACC=0: split-K partial slabs instead   // GENIE_KTRACE: phase stamps [3][256][8] of layer probe_layer
     hipEvent_t poll_ev[2] = {};

@@ -16,6 +16,7 @@ enum EpiMode {
     EPI_QKV = 3,         // n<512 -> q[m*512+n]; n<1024 -> K cache; else V cache
     EPI_VQDIST = 4,      // C = (rowsq[m] - v) + colsq[n]   (VQ distance, encoder #30-34)
     EPI_MISH = 5,        // C = v * tanh(softplus(v))        (MelStyleEncoder spectral)
+    EPI_SLAB = 6,        // split-K: C + z*slab_stride = raw partial of K slice z (no bias)
 };
 
 struct KVScatter {
@@ -39,12 +40,19 @@ struct GemmArgs {
     const float* res; long ldr;
     const float* rowsq; const float* colsq;
     KVScatter kv;
+    int ksplit; long slab_stride;    // EPI_SLAB: K split over grid.z (fp16-weight path only)
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
+// EPI_SLAB (split-K into slabs) is available for fp16 weights with these shapes
+bool gemm_slabs_supported(int K, long lda, long ldw);
 
 // --------------------------------------------------------- row kernels
 void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,
                     hipStream_t s);   // D = 512, eps 1e-5
+// LayerNorm of res + (bias + sum_z slab[z]) (fixed order) -- the split-K GEMM's reduce
+void layernorm_rows_slabs(const float* slabs, int nsplit, long slab_stride, const float* bias,
+                          const float* res, float* out, int rows, const float* g, const float* b,
+                          hipStream_t s);
 void sumsq_rows(const float* in, long ld, int rows, int cols, float* out, hipStream_t s);
 void argmin_dist_rows(const float* dist, int rows, int cols, int64_t* out, hipStream_t s);
 

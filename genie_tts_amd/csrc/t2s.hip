@@ -6,6 +6,7 @@
 // and t2s_stage_decoder_fp32.onnx (node indices cited per kernel).
 #include "common.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace gsv {
 
@@ -14,6 +15,42 @@ namespace gsv {
 // (exact f32 FMA chain, 157 TF/s peak).  Block tile 64x64, 4 waves of 32x32,
 // K-step 32 staged through padded LDS (stride 33 -> conflict-free b32 reads).
 // =====================================================================
+// Shared GEMM epilogue: 32x32 accumulator tile of rows [row0, row0+32), column col.
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, int row0, int col, int lane, const f32x16& acc) {
+    if (col >= a.N) return;
+    const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= a.M) continue;
+        const float v = a.bias ? bv + acc[r] : acc[r];   // Add(bias, MatMul)
+        switch (a.mode) {
+            case EPI_STORE: a.C[(long)row * a.ldc + col] = v; break;
+            case EPI_RELU: a.C[(long)row * a.ldc + col] = fmaxf(v, 0.f); break;
+            case EPI_RESID: a.C[(long)row * a.ldc + col] = a.res[(long)row * a.ldr + col] + v; break;
+            case EPI_MISH: {
+                const float sp = v > 0.f ? v + log1pf(expf(-v)) : log1pf(expf(v));
+                a.C[(long)row * a.ldc + col] = v * tanhf(sp);
+            } break;
+            case EPI_VQDIST:   // (sum h^2) - (2h).c + (sum c^2); x2 is exact so (2h).c == 2(h.c)
+                a.C[(long)row * a.ldc + col] = (a.rowsq[row] - 2.0f * acc[r]) + a.colsq[col];
+                break;
+            case EPI_QKV: {
+                if (col < 512) {
+                    a.C[(long)row * a.ldc + col] = v;
+                } else {
+                    if (a.kv.row_skip && a.kv.row_skip[a.kv.row_seq ? a.kv.row_seq[row] : 0]) break;
+                    const int seq = a.kv.row_seq ? a.kv.row_seq[row] : 0;
+                    const int pos = a.kv.row_pos ? a.kv.row_pos[row] : a.kv.pos0 + row;
+                    const int c = (col - 512) & 511;
+                    float* dst = (col < 1024 ? a.kv.k : a.kv.v) + (long)seq * a.kv.seq_stride;
+                    dst[((long)(c >> 5) * a.kv.tmax + pos) * 32 + (c & 31)] = v;
+                }
+            } break;
+        }
+    }
+}
+
 template <bool F16W>
 __global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs a) {
     __shared__ float As[64][33];
@@ -66,43 +103,147 @@ __global__ __launch_bounds__(256) void k_gemm_nt(GemmArgs a) {
         }
         __syncthreads();
     }
-    const int col = n0 + wn * 32 + (lane & 31);
-    if (col >= a.N) return;
-    const float bv = a.bias ? a.bias[col] : 0.f;
+    gemm_epilogue(a, m0 + wm * 32, n0 + wn * 32 + (lane & 31), lane, acc);
+}
+
+// =====================================================================
+// GEMM NT with fp16 weights on the f16 MFMA (v_mfma_f32_32x32x16_f16, 16x the
+// f32-MFMA rate): the weights are exactly fp16 (the reference's own values), the
+// f32 activations are split a = a_hi + a_lo into two fp16 terms, so
+// sum_k a*w = sum_k a_hi*w + sum_k a_lo*w with f32 accumulation -- the dropped
+// residual is ~2^-22 |a|, i.e. f32-level accuracy.  64x64 block tile, 4 waves
+// of 32x32, K-steps of 64 staged through LDS with the next step prefetched
+// into registers while the MFMAs run.
+// =====================================================================
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+#define GX_KS 128
+__device__ __forceinline__ void split8(const float4 x0, const float4 x1, h16x8& hi, h16x8& lo) {
+    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= a.M) continue;
-        const float v = a.bias ? bv + acc[r] : acc[r];   // Add(bias, MatMul)
-        switch (a.mode) {
-            case EPI_STORE: a.C[(long)row * a.ldc + col] = v; break;
-            case EPI_RELU: a.C[(long)row * a.ldc + col] = fmaxf(v, 0.f); break;
-            case EPI_RESID: a.C[(long)row * a.ldc + col] = a.res[(long)row * a.ldr + col] + v; break;
-            case EPI_MISH: {
-                const float sp = v > 0.f ? v + log1pf(expf(-v)) : log1pf(expf(v));
-                a.C[(long)row * a.ldc + col] = v * tanhf(sp);
-            } break;
-            case EPI_VQDIST:   // (sum h^2) - (2h).c + (sum c^2); x2 is exact so (2h).c == 2(h.c)
-                a.C[(long)row * a.ldc + col] = (a.rowsq[row] - 2.0f * acc[r]) + a.colsq[col];
-                break;
-            case EPI_QKV: {
-                if (col < 512) {
-                    a.C[(long)row * a.ldc + col] = v;
-                } else {
-                    if (a.kv.row_skip && a.kv.row_skip[a.kv.row_seq ? a.kv.row_seq[row] : 0]) break;
-                    const int seq = a.kv.row_seq ? a.kv.row_seq[row] : 0;
-                    const int pos = a.kv.row_pos ? a.kv.row_pos[row] : a.kv.pos0 + row;
-                    const int c = (col - 512) & 511;
-                    float* dst = (col < 1024 ? a.kv.k : a.kv.v) + (long)seq * a.kv.seq_stride;
-                    dst[((long)(c >> 5) * a.kv.tmax + pos) * 32 + (c & 31)] = v;
-                }
-            } break;
+    for (int j = 0; j < 8; ++j) {
+        const _Float16 hj = (_Float16)v[j];
+        hi[j] = hj;
+        lo[j] = (_Float16)(v[j] - (float)hj);
+    }
+}
+
+struct GxRegs {
+    float4 a[8];   // 64 rows x 128 k f32 = 2048 float4, 8 per thread
+    uint4 w[4];    // 64 rows x 128 k f16 = 1024 uint4, 4 per thread
+};
+
+__global__ __launch_bounds__(256) void k_gemm_x2(GemmArgs a) {
+    __shared__ float As[64][GX_KS + 4];
+    __shared__ __half Ws[64][GX_KS + 8];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    const int r = lane & 31, hh = lane >> 5;
+    // K slice of this block (split-K over grid.z); slices are whole K-steps
+    const int nsplit = gridDim.z, kz = blockIdx.z;
+    const int steps_all = a.K / GX_KS;
+    const int s_lo = kz * steps_all / nsplit, s_hi = (kz + 1) * steps_all / nsplit;
+    const int nsteps = s_hi - s_lo;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    auto load = [&](GxRegs& R, int step) {
+        const int k0 = step * GX_KS;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = tid + 256 * i, row = e >> 5, kc = (e & 31) * 4;
+            const int gm = m0 + row;
+            R.a[i] = gm < a.M ? *reinterpret_cast<const float4*>(a.A + (long)gm * a.lda + k0 + kc)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + 256 * i, row = e >> 4, kc = (e & 15) * 8;
+            const int gn = n0 + row;
+            R.w[i] = gn < a.N ? *reinterpret_cast<const uint4*>(reinterpret_cast<const __half*>(a.W) +
+                                                                 (long)gn * a.ldw + k0 + kc)
+                              : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto store = [&](const GxRegs& R) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = tid + 256 * i, row = e >> 5, kc = (e & 31) * 4;
+            *reinterpret_cast<float4*>(&As[row][kc]) = R.a[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + 256 * i, row = e >> 4, kc = (e & 15) * 8;
+            *reinterpret_cast<uint4*>(&Ws[row][kc]) = R.w[i];
+        }
+    };
+    auto compute = [&]() {
+#pragma unroll
+        for (int ks = 0; ks < GX_KS / 16; ++ks) {
+            const float* ap = &As[wm * 32 + r][ks * 16 + 8 * hh];
+            const float4 x0 = *reinterpret_cast<const float4*>(ap);
+            const float4 x1 = *reinterpret_cast<const float4*>(ap + 4);
+            h16x8 ahi, alo;
+            split8(x0, x1, ahi, alo);
+            const h16x8 bw = *reinterpret_cast<const h16x8*>(&Ws[wn * 32 + r][ks * 16 + 8 * hh]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bw, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bw, acc, 0, 0, 0);
+        }
+    };
+    // two K-steps in flight: R0 holds even steps, R1 odd ones
+    GxRegs R0, R1;
+    if (nsteps > 0) load(R0, s_lo);
+    if (nsteps > 1) load(R1, s_lo + 1);
+    for (int s = 0; s < nsteps; s += 2) {
+        store(R0);
+        __syncthreads();
+        if (s + 2 < nsteps) load(R0, s_lo + s + 2);
+        compute();
+        __syncthreads();
+        if (s + 1 < nsteps) {
+            store(R1);
+            __syncthreads();
+            if (s + 3 < nsteps) load(R1, s_lo + s + 3);
+            compute();
+            __syncthreads();
         }
     }
+    if (a.mode == EPI_SLAB) {
+        const int col = n0 + wn * 32 + r;
+        if (col >= a.N) return;
+        float* C = a.C + (long)kz * a.slab_stride;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (row < a.M) C[(long)row * a.ldc + col] = acc[i];
+        }
+        return;
+    }
+    gemm_epilogue(a, m0 + wm * 32, n0 + wn * 32 + r, lane, acc);
+}
+
+static bool gemm_x2_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("GENIE_GEMM_X2");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+bool gemm_slabs_supported(int K, long lda, long ldw) {
+    return K % GX_KS == 0 && lda % 4 == 0 && ldw % 8 == 0 && gemm_x2_enabled();
 }
 
 void gemm_nt(const GemmArgs& a, hipStream_t s) {
     dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
+    // fp16 weights -> split-activation f16 MFMA; the VQ distance GEMM stays on the
+    // exact f32 path (its argmin must see the f32 dot products).
+    if (a.w_f16 && a.mode != EPI_VQDIST && a.K % GX_KS == 0 && a.lda % 4 == 0 && a.ldw % 8 == 0 &&
+        gemm_x2_enabled()) {
+        if (a.mode == EPI_SLAB) grid.z = a.ksplit;
+        hipLaunchKernelGGL(k_gemm_x2, grid, dim3(256), 0, s, a);
+        return;
+    }
     if (a.w_f16)
         hipLaunchKernelGGL(k_gemm_nt<true>, grid, dim3(256), 0, s, a);
     else
@@ -125,6 +266,34 @@ __global__ __launch_bounds__(256) void k_layernorm512(const float* in, float* ou
     const float den = sqrtf(var + 1e-5f);
     out[r * 512 + t] = d0 / den * g[t] + b[t];
     out[r * 512 + t + 256] = d1 / den * g[t + 256] + b[t + 256];
+}
+
+__global__ __launch_bounds__(256) void k_layernorm512_slabs(const float* slabs, int nsplit, long sstride,
+                                                            const float* bias, const float* res, float* out,
+                                                            const float* g, const float* b) {
+    __shared__ float red[16];
+    const long r = blockIdx.x;
+    const int t = threadIdx.x;
+    float p0 = 0.f, p1 = 0.f;
+    for (int z = 0; z < nsplit; ++z) {
+        p0 += slabs[z * sstride + r * 512 + t];
+        p1 += slabs[z * sstride + r * 512 + t + 256];
+    }
+    const float v0 = res[r * 512 + t] + (bias[t] + p0), v1 = res[r * 512 + t + 256] + (bias[t + 256] + p1);
+    const float mean = block_sum(v0 + v1, red) * (1.0f / 512.0f);
+    const float d0 = v0 - mean, d1 = v1 - mean;
+    const float var = block_sum(d0 * d0 + d1 * d1, red) * (1.0f / 512.0f);
+    const float den = sqrtf(var + 1e-5f);
+    out[r * 512 + t] = d0 / den * g[t] + b[t];
+    out[r * 512 + t + 256] = d1 / den * g[t + 256] + b[t + 256];
+}
+
+void layernorm_rows_slabs(const float* slabs, int nsplit, long slab_stride, const float* bias,
+                          const float* res, float* out, int rows, const float* g, const float* b,
+                          hipStream_t s) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_layernorm512_slabs, dim3(rows), dim3(256), 0, s, slabs, nsplit, slab_stride, bias,
+                       res, out, g, b);
 }
 
 void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,
