@@ -99,6 +99,7 @@ def main():
     d_ssl = torch.as_tensor(ssl.reshape(768, -1), device=dev)
     d_audio = torch.as_tensor(audio.reshape(-1), device=dev)
     sp = make_sampler(force_steps=FORCE_STEPS)
+    eng.set_option("persist", 1)  # whole decode loop as one launch (t2s_persist.hip)
     eng.set_timing(True)          # phase events + live dominant-kernel event pair
 
     def one_utterance():
@@ -134,8 +135,8 @@ def main():
     utt_s = world * args.steps / dt
     rtf = (dt / args.steps) / audio_s
 
-    from genie_tts_amd.probe import dominant_kernel_roofline
-    roofline = dominant_kernel_roofline(eng, B=1)
+    from genie_tts_amd.probe import persist_roofline
+    roofline = persist_roofline(eng, n0=R_PH + S_PH + H_SSL // 2, steps=FORCE_STEPS, B=1)
 
     out = {
         "metric": METRIC,

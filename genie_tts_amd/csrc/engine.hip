@@ -57,6 +57,11 @@ gsv_engine::~gsv_engine() {
     if (done_host) hipHostFree(done_host);
     for (auto& e : kev) if (e) hipEventDestroy(e);
     if (ktrace) hipFree(ktrace);
+    if (ptrace) hipFree(ptrace);
+    if (pws) hipFree(pws);
+    if (perr_host) hipHostFree(perr_host);
+    for (void* p : state_allocs) hipFree(p);
+    state_allocs.clear();
     for (auto& e : poll_ev) if (e) hipEventDestroy(e);
     for (auto& e : ev) if (e) hipEventDestroy(e);
     if (ev_in) hipEventDestroy(ev_in);
@@ -121,6 +126,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_FFN_SLICES")) ffn_slices = std::atoi(e) == 32 ? 32 : 64;
     if (const char* e = std::getenv("GENIE_DECODE_FUSE")) fuse_qkv = std::atoi(e) == 2;
     if (const char* e = std::getenv("GENIE_ACC")) use_acc = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_PERSIST")) use_persist = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_KTRACE"))
         if (std::atoi(e) == 1 && !ktrace) {
             hipMalloc(&ktrace, (size_t)3 * 256 * 8 * 8);
@@ -159,6 +165,17 @@ int gsv_engine::finalize_t2s() {
         L.n2b = up_f32(p + "norm2.bias", &err);
     }
     if (err) return err;
+    {
+        std::vector<PLayer> pl(24);
+        for (int l = 0; l < 24; ++l) {
+            const T2SLayerW& L = layers[l];
+            pl[l] = PLayer{L.w_in, L.woT, L.w1, L.w2T, L.b_in, L.b_out, L.b1, L.b2, L.n1w, L.n1b, L.n2w, L.n2b};
+        }
+        d_layers = (PLayer*)dalloc(24 * sizeof(PLayer));
+        if (!d_layers) return set_error(GSV_E_HIP, "layer table");
+        hipMemcpy(d_layers, pl.data(), 24 * sizeof(PLayer), hipMemcpyHostToDevice);
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    }
     text_emb = up_f32("encoder.ar_text_embedding.word_embeddings.weight", &err);
     bert_w = up_f32("encoder.bert_proj.weight", &err);
     bert_b = up_f32("encoder.bert_proj.bias", &err);
@@ -525,6 +542,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
+    if (use_persist && B <= 8 && persist_grid(B) <= n_cu) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -573,6 +591,59 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "decode sync");
     if (probed) {
         // one sample per decode loop: the probed step's layer-`probe_layer` FFN launch
+        float ms = 0.f;
+        const hipError_t e = hipEventElapsedTime(&ms, kev[0], kev[1]);
+        if (e == hipSuccess && ms > 0.f) {
+            kern_us_sum += ms * 1000.0;
+            ++kern_n;
+        } else {
+            kern_err = e == hipSuccess ? -1 : (int)e;
+            (void)hipGetLastError();
+        }
+    }
+    return 0;
+}
+
+int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) {
+    // One launch runs every loop step (t2s_persist.hip).  Hand-off buffers are unique
+    // per (step, layer) and zeroed here, so the step count bounds the workspace.
+    const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
+    const int smax = std::max(1, limit);
+    size_t zero = 0;
+    const size_t need = persist_ws_bytes(B, smax, &zero);
+    if (need > pws_bytes) {
+        if (pws) hipFree(pws);
+        pws = nullptr;
+        pws_bytes = 0;
+        if (hipMalloc(&pws, need) != hipSuccess) return set_error(GSV_E_HIP, "persistent workspace");
+        pws_bytes = need;
+    }
+    if (!perr_host && hipHostMalloc((void**)&perr_host, 64, hipHostMallocDefault) != hipSuccess)
+        return set_error(GSV_E_HIP, "pinned alloc");
+    PersistArgs a{};
+    a.B = B;
+    for (int l = 0; l < 24; ++l) {
+        const T2SLayerW& W = layers[l];
+        a.L[l] = PLayer{W.w_in, W.woT, W.w1, W.w2T, W.b_in, W.b_out, W.b1, W.b2, W.n1w, W.n1b, W.n2w, W.n2b};
+    }
+    a.emb = emb_audio; a.alpha = alpha_audio; a.pe = pe_tab; a.w_pred = w_pred;
+    for (int l = 0; l < 24; ++l) { a.kc[l] = kcache[l]; a.vc[l] = vcache[l]; }
+    a.sstride = (long)16 * tmax * 32; a.tmax = tmax; a.scale = qk_scale;
+    a.y = y; a.ldy = tmax; a.ny = ny; a.kvlen = kvlen; a.steps = steps; a.done = done; a.stop_out = stopf;
+    a.seen = seen;
+    a.top_k = sp->top_k; a.temperature = sp->temperature; a.rep_penalty = sp->repetition_penalty;
+    a.greedy = sp->greedy; a.seed = sp->seed; a.max_steps = sp->max_steps; a.force_steps = sp->force_steps;
+    persist_bind_ws(a, pws, B, smax);
+    a.trace = ptrace;
+    hipMemsetAsync(pws, 0, zero, st);
+    const bool probe = timing && kev[0] != nullptr;
+    if (decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr) != hipSuccess)
+        return set_error(GSV_E_HIP, "persistent decode launch");
+    hipMemcpyAsync(perr_host, a.err, 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
+    if (*perr_host != 0)
+        return set_error(GSV_E_HIP, "persistent decode: hand-off timeout (code " + std::to_string(*perr_host) + ")");
+    if (probe) {
         float ms = 0.f;
         const hipError_t e = hipEventElapsedTime(&ms, kev[0], kev[1]);
         if (e == hipSuccess && ms > 0.f) {
@@ -846,6 +917,35 @@ extern "C" int gsv_debug_sample(const float* logits, const uint32_t* seen, int B
     const bool ok = hipStreamSynchronize(st) == hipSuccess;
     hipFree(buf);
     return ok ? 0 : set_error(GSV_E_HIP, "debug sample");
+}
+
+extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
+    ENG_CHECK(eng);
+    if (!name) return set_error(GSV_E_ARG, "null option name");
+    hipSetDevice(eng->device);
+    const std::string n(name);
+    if (n == "persist") {
+        eng->use_persist = value != 0;
+    } else if (n == "ptrace") {
+        if (value && !eng->ptrace) {
+            if (hipMalloc(&eng->ptrace, (size_t)256 * 8 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");
+            hipMemset(eng->ptrace, 0, (size_t)256 * 8 * 8);
+        } else if (!value && eng->ptrace) {
+            hipFree(eng->ptrace);
+            eng->ptrace = nullptr;
+        }
+    } else {
+        return set_error(GSV_E_ARG, "unknown option " + n);
+    }
+    return 0;
+}
+
+extern "C" int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n) {
+    ENG_CHECK(eng);
+    if (!eng->ptrace) return set_error(GSV_E_STATE, "enable option ptrace first");
+    n = std::min(n, 256 * 8);
+    return hipMemcpy(host, eng->ptrace, (size_t)n * 8, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0 : set_error(GSV_E_HIP, "ptrace copy");
 }
 
 extern "C" int gsv_debug_ktrace(gsv_engine* eng, uint64_t* host, int n) {

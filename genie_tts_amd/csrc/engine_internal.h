@@ -93,6 +93,14 @@ struct gsv_engine {
     long long* acc64 = nullptr;   // per sequence [24 layers][FFN out, attn out][512] fixed-point hand-offs
     bool use_acc = true;          // GENIE_ACC=0: split-K partial slabs instead   // GENIE_KTRACE: phase stamps [3][256][8] of layer probe_layer
     hipEvent_t poll_ev[2] = {};
+    // ---- persistent decode (t2s_persist.hip)
+    gsv::PLayer* d_layers = nullptr;   // [24] device copy of the layer pointers
+    void* pws = nullptr;               // hand-off workspace
+    size_t pws_bytes = 0;
+    int* perr_host = nullptr;          // pinned error word
+    bool use_persist = true;           // GENIE_PERSIST=0: per-step graphs instead
+    int n_cu = 0;
+    unsigned long long* ptrace = nullptr;   // option "ptrace": persistent phase stamps [256][8]
 
     ~gsv_engine();
     void* dalloc(size_t bytes);
@@ -113,6 +121,7 @@ struct gsv_engine {
     void decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st);
     hipGraphExec_t step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st);
     int decode_loop(int B, const gsv_sampler* sp, hipStream_t st);
+    int decode_persistent(int B, const gsv_sampler* sp, hipStream_t st);
     int vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                     const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
                     const float* eps, float noise_scale, float* audio, hipStream_t st);

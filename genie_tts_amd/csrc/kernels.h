@@ -178,6 +178,7 @@ struct SampleArgs {
     float* logits_out; long ldlo;      // optional copy of raw logits
     int ablate;                        // probe only: 1 skip top-k, 2 also skip softmax, 3 loads + tail
     long long* acc_zero; long acc_n;   // per-sequence fixed-point accumulators zeroed for the next step
+    int threads;                       // 256 (default) or 512: block size of the sampler body
 };
 void sample_tokens(const SampleArgs& a, hipStream_t s);
 
@@ -185,5 +186,32 @@ void sample_tokens(const SampleArgs& a, hipStream_t s);
 // kvlen = L + P, steps = 0, done = 0, seen = bits(prompts).
 void seq_state_init(int b, const int64_t* prompts, int P, int L, int64_t* y, long ldy, int* ny,
                     int* kvlen, int* steps, uint8_t* done, uint32_t* seen, hipStream_t s);
+
+
+// ---------------------------------------------------------------------------
+// Persistent decode (t2s_persist.hip): the whole AR loop in one launch.
+// ---------------------------------------------------------------------------
+struct PLayer {
+    const __half *w_in, *woT, *w1, *w2T;
+    const float *b_in, *b_out, *b1, *b2, *n1w, *n1b, *n2w, *n2b;
+};
+constexpr int PERSIST_CNT_LINES = 64;   // 128-B counter lines per step (24 attn + 24 FFN + logits)
+constexpr int PERSIST_LGS = 1056;       // logits row stride (floats, 128-B multiple)
+struct PersistArgs {
+    int B;
+    PLayer L[24];                                 // by value: kernarg (scalar loads)
+    const __half* emb; const float* alpha; const float* pe; const __half* w_pred;
+    float* kc[24]; float* vc[24];
+    long sstride; int tmax; float scale;
+    int64_t* y; long ldy; int* ny; int* kvlen; int* steps; uint8_t* done; uint8_t* stop_out; uint32_t* seen;
+    int top_k; float temperature; float rep_penalty; int greedy; uint64_t seed; int max_steps; int force_steps;
+    long long* accA; long long* accF; float* lg; int* cnt; unsigned long long* gran; int* err;
+    int smax;
+    unsigned long long* trace;                    // optional [grid][8] phase stamps (step 8, layer 12)
+};
+int persist_grid(int B);
+size_t persist_ws_bytes(int B, int smax, size_t* zero_bytes);
+void persist_bind_ws(PersistArgs& a, void* base, int B, int smax);
+hipError_t decode_persist(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 
 }  // namespace gsv

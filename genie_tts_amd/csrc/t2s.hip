@@ -6,6 +6,7 @@
 // and t2s_stage_decoder_fp32.onnx (node indices cited per kernel).
 #include "common.h"
 #include "kernels.h"
+#include "sampler.h"
 #include <cstdlib>
 
 namespace gsv {
@@ -682,128 +683,19 @@ void gemv_f16(const GemvArgs& a, hipStream_t s) {
     }
 }
 
-// =====================================================================
-// Sampler (t2s_stage_decoder_fp32.onnx#1775-1821, first-stage #1789-1820):
-// repetition penalty over the history set, /temperature, top-k threshold
-// (k-th largest by radix select), softmax, argmax(p / q) with q = 1 (greedy)
-// or q ~ N(0,1) (Philox + Box-Muller), stop = argmax(raw)==EOS || tok==EOS.
-// One 256-thread block per sequence.
-// =====================================================================
-__device__ __forceinline__ uint32_t f2key(float f) {
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float key2f(uint32_t k) {
-    const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
-    return __uint_as_float(u);
-}
-
-__device__ __forceinline__ void argmax_merge(float& v, int& i, float ov, int oi) {
-    if (ov > v || (ov == v && oi < i) || (v != v && ov == ov)) { v = ov; i = oi; }
-}
-
-__device__ void block_argmax(float& v, int& i, float* sv, int* si) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const float ov = __shfl_xor(v, o, 64);
-        const int oi = __shfl_xor(i, o, 64);
-        argmax_merge(v, i, ov, oi);
-    }
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) { sv[w] = v; si[w] = i; }
-    __syncthreads();
-    v = sv[0];
-    i = si[0];
-    const int nw = blockDim.x >> 6;
-    for (int k = 1; k < nw; ++k) argmax_merge(v, i, sv[k], si[k]);
-}
-
-// Block argmax on DPP reductions: value max, then the smallest index holding it.
-__device__ __forceinline__ void block_argmax_dpp(float& v, int& i, float* sv, int* si) {
-    const float m = wave_max_dpp(v);
-    const int mi = wave_min_dpp(v == m ? i : 0x7fffffff);
-    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) { sv[w] = m; si[w] = mi; }
-    __syncthreads();
-    v = sv[0];
-    i = si[0];
-    for (int k = 1; k < nw; ++k) argmax_merge(v, i, sv[k], si[k]);
-}
-
-// Append the token and advance the sequence state (thread 0; state read at entry).
-__device__ __forceinline__ void sample_commit(const SampleArgs& a, int b, int tok, int raw_arg, int n,
-                                              int steps, int kv, const uint32_t* seen_s) {
-    a.y[(long)b * a.ldy + n] = tok;
-    a.ny[b] = n + 1;
-    a.seen[(long)b * 33 + (tok >> 5)] = seen_s[tok >> 5] | (1u << (tok & 31));
-    if (!a.prefill) {
-        const bool stop = raw_arg == 1024 || tok == 1024;
-        if (a.stop_out) a.stop_out[b] = stop ? 1 : 0;
-        const int st = steps + 1;
-        a.steps[b] = st;
-        a.kvlen[b] = kv + 1;
-        const bool fin = a.force_steps > 0 ? st >= a.force_steps : (stop || st >= a.max_steps);
-        if (fin) a.done[b] = 1;
-    }
-}
-
-#define VOCAB 1025
-#define SAMPLE_SLOTS 5     // ceil(1025 / 256) logits per thread
-#define SAMPLE_MAXK 64
-
-// One round of "extract the wave maximum, removing ONE instance": each lane holds
-// a descending list h[0..n) with head index hp; returns the maximum (uniform).
-template <int N>
-__device__ __forceinline__ float wave_extract(const float (&h)[N], int& hp) {
-    const int lane = threadIdx.x & 63;
-    float head = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < N; ++j)
-        if (j == hp) head = h[j];
-    const float m = wave_max_dpp(head);
-    const unsigned long long hit = __ballot(head == m && hp < N);
-    if (hit && lane == __ffsll((long long)hit) - 1) ++hp;
-    return m;
-}
-
-template <int N>
-__device__ __forceinline__ void sort_desc(float (&h)[N]) {
-#pragma unroll
-    for (int i = 1; i < N; ++i)
-#pragma unroll
-        for (int j = i; j > 0; --j)
-            if (h[j] > h[j - 1]) { const float t = h[j]; h[j] = h[j - 1]; h[j - 1] = t; }
-}
-
-// 256 threads per sequence; logits in registers.  top-k threshold = k-th largest
-// penalised logit WITH multiplicity (TopK values[:, -1], stage#1786-1790): every
-// wave extracts its own k largest (one instance per round), then wave 0 extracts
-// the k-th largest of the 4k candidates -- the global k-th largest.
-__global__ __launch_bounds__(256) void k_sample(SampleArgs a) {
-    __shared__ float cand[4][SAMPLE_MAXK];
-    __shared__ float sv[16];
-    __shared__ int si[16];
-    __shared__ float thr_s;
+// One NT-thread block per sequence; logits in registers.  top-k threshold = k-th
+// largest penalised logit WITH multiplicity (TopK values[:, -1], stage#1786-1790).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_sample(SampleArgs a) {
+    __shared__ SampleLds<NT> sh;
     __shared__ uint32_t seen_s[33];
-    __shared__ int step_s;
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b = blockIdx.x, tid = threadIdx.x;
     const float* lg = a.logits + (long)b * a.ldl;
     const uint32_t* seen = a.seen + (long)b * 33;
     if (a.acc_zero) {   // this step's hand-off accumulators: every reader has run
         long long* z = a.acc_zero + (long)b * a.acc_n;
-        for (long i = tid * 2; i < a.acc_n; i += 512)
+        for (long i = tid * 2; i < a.acc_n; i += 2 * NT)
             *reinterpret_cast<longlong2*>(z + i) = make_longlong2(0, 0);
-    }
-    // every load issued before the first use (the done flag included)
-    float l[SAMPLE_SLOTS];
-    uint32_t sw[SAMPLE_SLOTS];
-#pragma unroll
-    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
-        const int i = tid + 256 * j;
-        l[j] = i < VOCAB ? lg[i] : -INFINITY;
-        sw[j] = i < VOCAB ? seen[i >> 5] : 0u;
     }
     // sequence state for the tail, read up front (no dependent round trips at the end)
     int st_ny = 0, st_steps = 0, st_kv = 0;
@@ -817,108 +709,23 @@ __global__ __launch_bounds__(256) void k_sample(SampleArgs a) {
         if (tid == 0 && a.stop_out) a.stop_out[b] = 0;
         return;
     }
-    const int K = a.top_k;
-    float v[SAMPLE_SLOTS];
-    float rv = -INFINITY;
-    int ri = 0x7fffffff;
-#pragma unroll
-    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
-        const int i = tid + 256 * j;
-        v[j] = -INFINITY;
-        if (i < VOCAB) {
-            if (a.logits_out) a.logits_out[(long)b * a.ldlo + i] = l[j];
-            argmax_merge(rv, ri, l[j], i);
-            float pen = l[j];
-            if ((sw[j] >> (i & 31)) & 1u) pen = l[j] < 0.f ? l[j] * a.rep_penalty : l[j] / a.rep_penalty;
-            v[j] = pen / a.temperature;
-        }
-    }
-    block_argmax_dpp(rv, ri, sv, si);
-    const int raw_arg = ri;
-    if (a.greedy) {
-        // q := 1 and softmax is monotone: argmax(p / q) is the first index of the
-        // largest penalised logit; the top-k mask cannot remove the maximum.
-        float gv = -INFINITY;
-        int gi = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < SAMPLE_SLOTS; ++j) {
-            const int i = tid + 256 * j;
-            if (i < VOCAB) argmax_merge(gv, gi, v[j], i);
-        }
-        block_argmax_dpp(gv, gi, sv, si);
-        if (tid == 0) sample_commit(a, b, gi, raw_arg, st_ny, st_steps, st_kv, seen_s);
-        return;
-    }
-    // ---- k-th largest with multiplicity
-    if (a.ablate == 3) {
-        if (tid == 0) { a.y[(long)b * a.ldy + st_ny] = raw_arg; a.ny[b] = st_ny + 1; }
-        return;
-    }
-    if (a.ablate == 0) {
-        float h[SAMPLE_SLOTS];
-#pragma unroll
-        for (int j = 0; j < SAMPLE_SLOTS; ++j) h[j] = v[j];
-        sort_desc(h);
-        int hp = 0;
-        for (int r = 0; r < K; ++r) {
-            const float m = wave_extract(h, hp);
-            if (lane == 0) cand[w][r] = m;
-        }
-    }
-    __syncthreads();
-    if (w == 0 && a.ablate == 0) {
-        float h[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) h[j] = lane < K ? cand[j][lane] : -INFINITY;
-        sort_desc(h);
-        int hp = 0;
-        float m = -INFINITY;
-        for (int r = 0; r < K; ++r) m = wave_extract(h, hp);
-        if (lane == 0) thr_s = m;
-    }
-    if (a.ablate && tid == 0) thr_s = -INFINITY;
-    __syncthreads();
-    const float thr = thr_s;
-    // ---- softmax over kept entries, then argmax(p / q)
-    float lmax = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
-        v[j] = v[j] < thr ? -INFINITY : v[j];
-        lmax = fmaxf(lmax, v[j]);
-    }
-    const float m = a.ablate == 2 ? 0.f : block_max_dpp(lmax, sv);
-    float lsum = 0.f;
-#pragma unroll
-    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
-        v[j] = expf(v[j] - m);
-        lsum += v[j];
-    }
-    const float sum = a.ablate == 2 ? 1.f : block_sum_dpp(lsum, sv);
+    __shared__ int step_s;
     if (tid == 0) step_s = st_steps;
     __syncthreads();
     const int step = a.prefill ? 0 : step_s + 1;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int j = 0; j < SAMPLE_SLOTS; ++j) {
-        const int i = tid + 256 * j;
-        if (i >= VOCAB) continue;
-        const float p = v[j] / sum;
-        float q = 1.0f;
-        if (!a.greedy) {
-            const uint4 r = philox4x32(make_uint4((uint32_t)i, (uint32_t)step, (uint32_t)b, 0x51u),
-                                       make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
-            const float u1 = u01_open(r.x), u2 = u01_open(r.y);
-            q = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
-        }
-        argmax_merge(bv, bi, p / q, i);
+    int raw = 0;
+    const int tok = sample_block<NT>([&](int i) { return lg[i]; }, seen_s, b, step, a.top_k, a.temperature,
+                                     a.rep_penalty, a.greedy, a.seed, a.ablate,
+                                     a.logits_out ? a.logits_out + (long)b * a.ldlo : nullptr, &raw, sh);
+    if (tid == 0) {
+        if (a.ablate == 3) { a.y[(long)b * a.ldy + st_ny] = raw; a.ny[b] = st_ny + 1; return; }
+        sample_commit(a, b, tok, raw, st_ny, st_steps, st_kv, seen_s);
     }
-    block_argmax_dpp(bv, bi, sv, si);
-    if (tid == 0) sample_commit(a, b, bi, raw_arg, st_ny, st_steps, st_kv, seen_s);
 }
 
 void sample_tokens(const SampleArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_sample, dim3(a.B), dim3(256), 0, s, a);
+    if (a.threads == 512) hipLaunchKernelGGL(k_sample<512>, dim3(a.B), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(k_sample<256>, dim3(a.B), dim3(256), 0, s, a);
 }
 
 __global__ __launch_bounds__(256) void k_seq_init(int b, const int64_t* prompts, int P, int L,

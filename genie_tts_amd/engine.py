@@ -88,6 +88,8 @@ def lib():
         L.gsv_set_timing.argtypes = [vp, ctypes.c_int]
         L.gsv_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.gsv_get_kernel_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32)]
+        L.gsv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int]
+        L.gsv_debug_ptrace.argtypes = [vp, vp, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -98,6 +100,7 @@ EXPORTED = (
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
+    "gsv_set_option", "gsv_debug_ptrace",
 )
 
 
@@ -328,6 +331,16 @@ class Engine:
         us, n = ctypes.c_float(), ctypes.c_int32()
         _check(lib().gsv_get_kernel_timing(self.h, ctypes.byref(us), ctypes.byref(n)), "gsv_get_kernel_timing")
         return us.value, n.value
+
+    def set_option(self, name: str, value: int):
+        """Engine option (see gsv_set_option): "persist" decode path, "ptrace" phase stamps."""
+        _check(lib().gsv_set_option(self.h, name.encode(), int(value)), "gsv_set_option")
+
+    def ptrace(self) -> np.ndarray:
+        """[256 workgroups][8 slots] realtime stamps of the persistent decode (option ptrace)."""
+        out = np.zeros((256, 8), np.uint64)
+        _check(lib().gsv_debug_ptrace(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size), "gsv_debug_ptrace")
+        return out
 
     def ktrace(self) -> np.ndarray:
         """[3 kernels][256 blocks][8 slots] realtime stamps (GENIE_KTRACE=1 builds only)."""

@@ -1,5 +1,17 @@
 """Roofline of the dominant kernel, from the engine's live in-loop timing.
 
+Persistent decode (default, t2s_persist.hip): the dominant kernel is
+`k_decode_persist`, ONE launch per utterance that runs every decode step.  Its
+algorithmic bytes (per sequence per step): the fp16 weights read
+once, W16 = 24 layers x (1536+512+2048+2048) x 512 x 2 B + the 1025x512 fp16
+logits head = 152,044,544 B, plus the fp32 K/V cache rows read, 98,304 B per
+cached position (24 layers x K,V x 512 x 4 B), plus the new row written,
+98,304 B.  Summed over the launch's steps (key count N0 + s at step s).
+The duration is the launch's own dispatch-packet start/stop events
+(hipExtLaunchKernelGGL), averaged over the timed utterances.
+
+Per-step hipGraph path (option persist=0):
+
 Dominant kernel (rocprofv3, profiles/): the fused decode FFN (`k_ffn`, one
 launch per layer per step) -- HBM-bound weight streaming.  Its algorithmic
 bytes per launch at batch B (the unique bytes the math needs, each once):
@@ -22,6 +34,36 @@ def ffn_algorithmic_bytes(B: int = 1, slices: int = 64) -> int:
     params = 2048 * 4 + 3 * 512 * 4
     per_seq = 16 * 512 * 4 + 512 * 4 + slices * 512 * 4 + 512 * 4
     return weights + params + B * per_seq
+
+
+W16 = 24 * (1536 + 512 + 2048 + 2048) * 512 * 2 + 1025 * 512 * 2   # 152,044,544
+KV_ROW = 24 * 2 * 512 * 4                                         # 98,304
+
+
+def persist_algorithmic_bytes(n0: int, steps: int, B: int = 1) -> int:
+    """Bytes one persistent launch must move: per step W16 once + each sequence's
+    K/V rows read (n0 + s of them) and one row written."""
+    return sum(W16 + B * (KV_ROW * (n0 + s) + KV_ROW) for s in range(steps))
+
+
+def persist_roofline(eng, n0: int, steps: int, B: int = 1):
+    us, n = eng.kernel_timing()
+    if n <= 0 or us <= 0:
+        return {"error": f"no live kernel samples (hipEventElapsedTime error {-n})"}
+    bytes_ = persist_algorithmic_bytes(n0, steps, B)
+    achieved = bytes_ / (us * 1e-6) / 1e9
+    return {
+        "kernel": "k_decode_persist (whole decode loop, %d steps, N0=%d, B=%d)" % (steps, n0, B),
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": None,
+        "algorithmic_bytes_per_launch": bytes_,
+        "avg_launch_us": us,
+        "samples": n,
+    }
 
 
 def dominant_kernel_roofline(eng, B: int = 1):

@@ -177,6 +177,15 @@ int gsv_get_timing(gsv_engine* eng, float* ms4);
  * negative count is -(hipError_t) of a failed hipEventElapsedTime. */
 int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples);
 
+/* Engine options (no reference counterpart; the reference's session options are
+ * ORT's).  "persist": 1 (default) runs gsv_t2s_generate's decode loop as ONE
+ * persistent launch (B <= 8), 0 as replayed per-step hipGraphs.  "ptrace": 1
+ * allocates per-workgroup phase stamps of the persistent launch (step 8, layer 12),
+ * read back with gsv_debug_ptrace ([256 workgroups][8 slots], 100 MHz).
+ * GSV_E_ARG for an unknown name. */
+int gsv_set_option(gsv_engine* eng, const char* name, int value);
+int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,107 @@
+"""GPU: the persistent decode launch (t2s_persist.hip) against the per-step
+hipGraph path and the CPU oracle.
+
+Both decode paths sit behind gsv_t2s_generate (the reference's 500-step loop,
+Inference.py:95-109); option "persist" selects one.  Bars: greedy token ids
+identical to the oracle (bit-exact, north_star) and to the graph path; sampled
+(top-k, Philox) ids identical to the graph path -- same sampler formula and
+noise, only the block size of the sampler's reductions differs.
+"""
+import numpy as np
+import pytest
+
+from tests.common import character, t2s_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from genie_tts_amd.engine import Engine
+    w = character("v2")
+    e = Engine({"t2s_encoder": w["t2s_encoder"], "t2s": w["t2s"]}, "v2")
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def oracle_model():
+    from oracle import restate as R
+    return R.T2SModel(character("v2")["t2s"])
+
+
+def _both(eng, inps, sp):
+    eng.set_option("persist", 1)
+    a = eng.t2s_generate(inps, sp)
+    eng.set_option("persist", 0)
+    try:
+        b = eng.t2s_generate(inps, sp)
+    finally:
+        eng.set_option("persist", 1)
+    return a, b
+
+
+def _ordered(inp):
+    ref, txt, rb, tb, ssl = inp
+    return ref, rb, txt, tb, ssl
+
+
+@pytest.mark.parametrize("R_,S_,H_,steps", [(12, 10, 41, 30), (48, 45, 264, 81)])
+def test_persistent_greedy_matches_oracle(eng, oracle_model, R_, S_, H_, steps):
+    from genie_tts_amd.engine import make_sampler
+    from oracle import restate as R
+    inp = t2s_inputs(R=R_, S=S_, H=H_, tag=f"p{R_}")
+    eng.set_option("persist", 1)
+    out = eng.t2s_generate([inp], make_sampler(force_steps=steps))
+    sem, _, _ = R.t2s_generate(character("v2")["t2s_encoder"], oracle_model, *_ordered(inp), force_steps=steps)
+    assert out[0].tolist() == sem.reshape(-1).tolist()
+
+
+def test_persistent_long_context_multipass(eng, oracle_model):
+    """N0 = 93 + 300 > 384 keys: attention runs past the LDS-staged rows."""
+    from genie_tts_amd.engine import make_sampler
+    from oracle import restate as R
+    inp = t2s_inputs(R=48, S=45, H=600, tag="long")
+    steps = 12
+    eng.set_option("persist", 1)
+    out = eng.t2s_generate([inp], make_sampler(force_steps=steps))
+    sem, _, _ = R.t2s_generate(character("v2")["t2s_encoder"], oracle_model, *_ordered(inp), force_steps=steps)
+    assert out[0].tolist() == sem.reshape(-1).tolist()
+
+
+@pytest.mark.parametrize("B", [1, 3, 8])
+def test_persistent_matches_graph_path_greedy(eng, B):
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=10 + 2 * i, S=8 + i, H=30 + 4 * i, tag=f"pg{B}_{i}") for i in range(B)]
+    a, b = _both(eng, inps, make_sampler(force_steps=20))
+    for i in range(B):
+        assert a[i].tolist() == b[i].tolist(), f"utterance {i}"
+
+
+@pytest.mark.parametrize("top_k,temp", [(15, 1.0), (5, 0.8)])
+def test_persistent_matches_graph_path_sampled(eng, top_k, temp):
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=12 + i, S=9 + i, H=36 + 2 * i, tag=f"ps{i}") for i in range(4)]
+    sp = make_sampler(top_k=top_k, temperature=temp, greedy=False, seed=1234, force_steps=24)
+    a, b = _both(eng, inps, sp)
+    for i in range(len(inps)):
+        assert a[i].tolist() == b[i].tolist(), f"utterance {i}"
+
+
+def test_persistent_natural_stop_max_steps(eng):
+    """No forced length: the loop ends on max_steps (Inference.py:95 range(500)) -> idx+1 tokens."""
+    from genie_tts_amd.engine import make_sampler
+    inp = t2s_inputs(R=10, S=8, H=30, tag="ms")
+    a, b = _both(eng, [inp], make_sampler(max_steps=17))
+    assert a[0].tolist() == b[0].tolist()
+    assert len(a[0]) > 0
+
+
+def test_persistent_repeated_calls_are_deterministic(eng):
+    from genie_tts_amd.engine import make_sampler
+    inp = t2s_inputs(R=14, S=11, H=44, tag="rep")
+    sp = make_sampler(top_k=15, greedy=False, seed=7, force_steps=30)
+    eng.set_option("persist", 1)
+    first = eng.t2s_generate([inp], sp)[0].tolist()
+    for _ in range(3):
+        assert eng.t2s_generate([inp], sp)[0].tolist() == first
