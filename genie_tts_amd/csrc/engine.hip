@@ -60,6 +60,7 @@ gsv_engine::~gsv_engine() {
     if (ptrace) hipFree(ptrace);
     if (pws) hipFree(pws);
     if (perr_host) hipHostFree(perr_host);
+    if (perr) hipFree(perr);
     for (void* p : state_allocs) hipFree(p);
     state_allocs.clear();
     for (auto& e : poll_ev) if (e) hipEventDestroy(e);
@@ -165,17 +166,7 @@ int gsv_engine::finalize_t2s() {
         L.n2b = up_f32(p + "norm2.bias", &err);
     }
     if (err) return err;
-    {
-        std::vector<PLayer> pl(24);
-        for (int l = 0; l < 24; ++l) {
-            const T2SLayerW& L = layers[l];
-            pl[l] = PLayer{L.w_in, L.woT, L.w1, L.w2T, L.b_in, L.b_out, L.b1, L.b2, L.n1w, L.n1b, L.n2w, L.n2b};
-        }
-        d_layers = (PLayer*)dalloc(24 * sizeof(PLayer));
-        if (!d_layers) return set_error(GSV_E_HIP, "layer table");
-        hipMemcpy(d_layers, pl.data(), 24 * sizeof(PLayer), hipMemcpyHostToDevice);
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
-    }
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
     text_emb = up_f32("encoder.ar_text_embedding.word_embeddings.weight", &err);
     bert_w = up_f32("encoder.bert_proj.weight", &err);
     bert_b = up_f32("encoder.bert_proj.bias", &err);
@@ -542,7 +533,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (use_persist && B <= 8 && persist_grid(B) <= n_cu) return decode_persistent(B, sp, st);
+    if (use_persist && B <= 8 && persist_groups(B, n_cu) > 0) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -605,23 +596,35 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
 }
 
 int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) {
-    // One launch runs every loop step (t2s_persist.hip).  Hand-off buffers are unique
-    // per (step, layer) and zeroed here, so the step count bounds the workspace.
+    // One launch runs every loop step (t2s_persist.hip).  Hand-offs are tagged
+    // granules in a ring; the launch epoch in the tag makes the ring reusable
+    // without zeroing (re-zeroed when the epoch wraps or the layout changes).
     const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    const int smax = std::max(1, limit);
-    size_t zero = 0;
-    const size_t need = persist_ws_bytes(B, smax, &zero);
-    if (need > pws_bytes) {
-        if (pws) hipFree(pws);
-        pws = nullptr;
-        pws_bytes = 0;
-        if (hipMalloc(&pws, need) != hipSuccess) return set_error(GSV_E_HIP, "persistent workspace");
-        pws_bytes = need;
+    if (tmax > persist_max_tokens()) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
+    const size_t need = persist_ring_bytes(B);
+    if (need > pws_bytes || B != pws_batch) {
+        if (need > pws_bytes) {
+            if (pws) hipFree(pws);
+            pws = nullptr;
+            pws_bytes = 0;
+            if (hipMalloc(&pws, need) != hipSuccess) return set_error(GSV_E_HIP, "persistent ring");
+            pws_bytes = need;
+        }
+        hipMemsetAsync(pws, 0, pws_bytes, st);
+        pws_batch = B;
+        pepoch = 0;
     }
+    if (++pepoch >= (1u << 20)) {
+        hipMemsetAsync(pws, 0, pws_bytes, st);
+        pepoch = 1;
+    }
+    if (!perr && hipMalloc((void**)&perr, 64) != hipSuccess) return set_error(GSV_E_HIP, "error word");
     if (!perr_host && hipHostMalloc((void**)&perr_host, 64, hipHostMallocDefault) != hipSuccess)
         return set_error(GSV_E_HIP, "pinned alloc");
     PersistArgs a{};
     a.B = B;
+    a.groups = persist_groups(B, n_cu);
+    if (const char* e = std::getenv("GENIE_PERSIST_GROUPS")) a.groups = std::max(1, std::min(a.groups, std::atoi(e)));
     for (int l = 0; l < 24; ++l) {
         const T2SLayerW& W = layers[l];
         a.L[l] = PLayer{W.w_in, W.woT, W.w1, W.w2T, W.b_in, W.b_out, W.b1, W.b2, W.n1w, W.n1b, W.n2w, W.n2b};
@@ -633,13 +636,17 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
     a.seen = seen;
     a.top_k = sp->top_k; a.temperature = sp->temperature; a.rep_penalty = sp->repetition_penalty;
     a.greedy = sp->greedy; a.seed = sp->seed; a.max_steps = sp->max_steps; a.force_steps = sp->force_steps;
-    persist_bind_ws(a, pws, B, smax);
+    a.ring = (unsigned long long*)pws;
+    a.epoch = pepoch;
+    a.err = perr;
+    a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
-    hipMemsetAsync(pws, 0, zero, st);
+    a.trace_rep = std::getenv("GENIE_TRACE_REP") ? 1 : 0;
+    hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;
     if (decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr) != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
-    hipMemcpyAsync(perr_host, a.err, 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
     if (*perr_host != 0)
         return set_error(GSV_E_HIP, "persistent decode: hand-off timeout (code " + std::to_string(*perr_host) + ")");
@@ -928,8 +935,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist = value != 0;
     } else if (n == "ptrace") {
         if (value && !eng->ptrace) {
-            if (hipMalloc(&eng->ptrace, (size_t)256 * 8 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");
-            hipMemset(eng->ptrace, 0, (size_t)256 * 8 * 8);
+            if (hipMalloc(&eng->ptrace, (size_t)256 * 16 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");
+            hipMemset(eng->ptrace, 0, (size_t)256 * 16 * 8);
         } else if (!value && eng->ptrace) {
             hipFree(eng->ptrace);
             eng->ptrace = nullptr;
@@ -943,7 +950,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
 extern "C" int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n) {
     ENG_CHECK(eng);
     if (!eng->ptrace) return set_error(GSV_E_STATE, "enable option ptrace first");
-    n = std::min(n, 256 * 8);
+    n = std::min(n, 256 * 16);
     return hipMemcpy(host, eng->ptrace, (size_t)n * 8, hipMemcpyDeviceToHost) == hipSuccess
                ? 0 : set_error(GSV_E_HIP, "ptrace copy");
 }

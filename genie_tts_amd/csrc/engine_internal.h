@@ -94,9 +94,11 @@ struct gsv_engine {
     bool use_acc = true;          // GENIE_ACC=0: split-K partial slabs instead   // GENIE_KTRACE: phase stamps [3][256][8] of layer probe_layer
     hipEvent_t poll_ev[2] = {};
     // ---- persistent decode (t2s_persist.hip)
-    gsv::PLayer* d_layers = nullptr;   // [24] device copy of the layer pointers
-    void* pws = nullptr;               // hand-off workspace
+    void* pws = nullptr;               // granule ring
     size_t pws_bytes = 0;
+    int pws_batch = 0;                 // batch the ring is laid out for
+    unsigned pepoch = 0;               // launch epoch (granule tags)
+    int* perr = nullptr;               // device error word
     int* perr_host = nullptr;          // pinned error word
     bool use_persist = true;           // GENIE_PERSIST=0: per-step graphs instead
     int n_cu = 0;

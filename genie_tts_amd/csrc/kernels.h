@@ -195,8 +195,7 @@ struct PLayer {
     const __half *w_in, *woT, *w1, *w2T;
     const float *b_in, *b_out, *b1, *b2, *n1w, *n1b, *n2w, *n2b;
 };
-constexpr int PERSIST_CNT_LINES = 64;   // 128-B counter lines per step (24 attn + 24 FFN + logits)
-constexpr int PERSIST_LGS = 1056;       // logits row stride (floats, 128-B multiple)
+constexpr int PERSIST_LGS = 1056;       // logits granule row stride (128-B multiple)
 struct PersistArgs {
     int B;
     PLayer L[24];                                 // by value: kernarg (scalar loads)
@@ -205,13 +204,18 @@ struct PersistArgs {
     long sstride; int tmax; float scale;
     int64_t* y; long ldy; int* ny; int* kvlen; int* steps; uint8_t* done; uint8_t* stop_out; uint32_t* seen;
     int top_k; float temperature; float rep_penalty; int greedy; uint64_t seed; int max_steps; int force_steps;
-    long long* accA; long long* accF; float* lg; int* cnt; unsigned long long* gran; int* err;
-    int smax;
-    unsigned long long* trace;                    // optional [grid][8] phase stamps (step 8, layer 12)
+    unsigned long long* ring;                     // granule ring (persist_ring_bytes)
+    unsigned epoch;                               // launch epoch (tag high bits), 1 .. 2^20-1
+    int* err;                                     // zeroed per launch; non-zero: a hand-off timed out
+    int smax;                                     // step cap of the launch
+    int groups;                                   // layer groups (layer l -> group l % groups)
+    unsigned long long* trace;                    // optional [grid][16] phase stamps (step 8, layer 12)
+    int trace_rep;                                // probe only: run the probed QKV twice
 };
-int persist_grid(int B);
-size_t persist_ws_bytes(int B, int smax, size_t* zero_bytes);
-void persist_bind_ws(PersistArgs& a, void* base, int B, int smax);
+int persist_groups(int B, int n_cu);   // 0: the grid does not fit
+int persist_grid(int B, int groups);
+size_t persist_ring_bytes(int B);
+int persist_max_tokens();
 hipError_t decode_persist(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 
 }  // namespace gsv

@@ -3,41 +3,38 @@
 //
 // Why: at batch 1 a decode step is ~150 MB of fp16 weights (≈25 µs of HBM time)
 // spread over 24 layers of tiny dependent GEMVs.  As separate launches every
-// layer pays three kernel boundaries plus each kernel's own dependent prologue
-// (measured: 15.4 µs per layer).  Here every workgroup keeps a FIXED role for the
-// whole generation and the two all-reduces a post-norm layer needs are
-// hand-offs inside the launch:
+// layer pays kernel boundaries plus each kernel's own dependent prologue
+// (measured 15.4 µs per layer).  Here every workgroup keeps a FIXED role for the
+// whole generation, and the two all-reduces a post-norm layer needs are
+// hand-offs inside the launch.
 //
-//   attention role (16·B workgroups, one per (head, sequence)):
-//     x_l = LN2_{l-1}(h1_{l-1} + b2 + ΣFFN_{l-1})   (layer 0: E_audio[tok] + α·pe[n])
-//     q,k,v of the head (stage#43-51 per layer) -> K/V row appended to the cache
-//     -> attention over [0, kv] (stage#84-96) -> out-proj slice (WoT rows of the head)
-//     -> int64 fixed-point atomic adds into accA[s][l][b] -> arrival counter
-//   FFN role (64 workgroups, 32 hidden units each):
-//     h1_l = LN1_l(x_l + bo + ΣaccA) -> relu(W1 slice) -> W2 split-K slice
-//     -> fixed-point adds into accF[s][l][b] -> arrival counter
-//   after layer 23 the FFN role computes x_24 and the logits (ar_predict_layer,
-//   16 rows per workgroup, write-through stores) -> counter; the attention
-//   workgroup (head 0, b) runs the sampler (sampler.h, K10) and publishes the token
-//   as a tagged 8-byte granule that every workgroup polls.
+// Grid: G layer groups x (16·B attention + 64 FFN workgroups); group g owns the
+// layers l ≡ g (mod G) and streams its next layer's weights (registers + LDS-DMA)
+// during the G-1 layers it only tracks.  Per owned layer:
+//   attention (head h, sequence b): q,k,v rows of the head (stage#43-51) ->
+//     attention over [0, kv] (stage#84-96) -> out-proj slice (WoT rows of the head)
+//     -> 512 partial granules PA[l][b][h][*]
+//   FFN (slice j = hidden units [32 j, 32 j + 32)):
+//     reduce-A: columns [8 j, 8 j + 8) of Σ_h PA (fixed order) -> granules RA
+//     h1_l = LN1_l(x_l + bo + RA) -> relu(W1 slice) -> W2 slice -> partials PF[l][b][j][*]
+//     reduce-F: columns [8 j, 8 j + 8) of Σ_j' PF (fixed order) -> granules RF
+//   every workgroup tracks the residual stream of its sequences from RA / RF:
+//     x_l = LN2_{l-1}(h1_{l-1} + b2 + RF_{l-1}),  h1_l = LN1_l(x_l + bo + RA_l)
+//   after layer 23 the FFN workgroups of group 23 % G compute x_24 and the logits
+//   (ar_predict_layer) as granules LG; the group-0 head-0 attention workgroup of
+//   each sequence runs the sampler (sampler.h, K10) and publishes the token
+//   granule TK that every workgroup polls.
 //
-// Each role also computes the other role's LayerNorm for itself (from the same
-// immutable hand-off buffers), so no residual vector is ever published: the only
-// cross-workgroup data are the fixed-point accumulators, the logits and the token
-// granules.  Every hand-off buffer has a unique address per (step, layer) and is
-// zeroed by a memset before the launch, so a consumer can never hit a stale line;
-// counters are polled with relaxed agent-scope (sc1) loads and payloads read with
-// sc1 loads after a workgroup barrier (MI355X_MICROARCH.md hand-off table, row 3;
-// producers drain with s_waitcnt vmcnt(0) before their counter add).  Integer
-// accumulation is associative, so results do not depend on arrival order.
-//
-// Weights of the NEXT layer (and the K/V rows already in the cache) are loaded
-// into registers right after a phase's output is published, i.e. while the
-// workgroup waits for its next input: the weight stream is off the critical path.
+// Hand-offs are 8-byte {tag, value} granules written by ONE write-through (sc1)
+// store and read by relaxed agent-scope (sc1) loads that re-poll until the tag
+// matches (MI355X_MICROARCH.md, hand-offs R2: the data is the flag; no fence, no
+// counter, one round trip).  tag = (launch epoch << 12) | (step + 1), so a ring of
+// RING step slots is reused without zeroing; sums are formed by a fixed set of
+// lanes in a fixed order, so results do not depend on arrival order.
 //
 // Every spin is bounded (s_memrealtime); a timeout sets the error word and every
-// workgroup leaves.  The grid (16·B + 64 ≤ 192 workgroups, one per CU by LDS) is
-// checked against the CU count on the host.
+// workgroup leaves.  The grid (<= 256 workgroups, one per CU by LDS) is checked
+// against the CU count on the host.
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
@@ -46,35 +43,28 @@
 namespace gsv {
 
 namespace {
+typedef unsigned long long u64;
 constexpr int PT = 512;            // threads per workgroup (8 waves)
 constexpr int PWV = PT / 64;
-constexpr int KU = 6;              // K/V rows per 8-lane group per pass: 64 groups -> 384 keys
-constexpr int KVL = 64 * KU;       // K/V rows staged in LDS (LDS-DMA) ahead of the hand-off
-constexpr int NFB = 64;            // FFN workgroups (32 hidden units each)
+constexpr int KVL = 320;           // K/V rows of a head staged in LDS ahead of the hand-off
+constexpr int TMAXP = 4096;        // longest key range (pe table)
+constexpr int NFB = 64;            // FFN workgroups per group (32 hidden units each)
+constexpr int RING = 4;            // granule ring depth (steps)
 constexpr unsigned long long SPIN_TICKS = 300000000ull;   // 3 s of the 100 MHz clock
 
 __device__ __forceinline__ int ld_rlx(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ long long ld_rlx64(const long long* p) {
+__device__ __forceinline__ u64 ld_rlxu64(const u64* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ unsigned long long ld_rlxu64(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// one write-through store of {tag, value}
+__device__ __forceinline__ void st_gran(u64* p, unsigned tag, float v) {
+    __hip_atomic_store(p, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float ld_rlxf(const float* p) {
-    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_wt(float* p, float v) {   // write-through (sc1) store
-    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Loads through global (address space 1) pointers: the layer table holds generic
-// pointers, which would otherwise become flat loads (counted in lgkmcnt too, so
-// every LDS wait would also drain the weight prefetch).
+// pointers, which would otherwise become flat loads (counted in lgkmcnt too).
 #define GPTR(T, p) ((const __attribute__((address_space(1))) T*)(p))
 template <typename T>
 __device__ __forceinline__ T ldg(const T* base, long idx) { return GPTR(T, base)[idx]; }
@@ -92,68 +82,122 @@ __device__ __forceinline__ float4 ldg16f(const float* base, long idx) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// One lane: wait until *p >= target.  False on timeout or when another workgroup failed.
-__device__ bool spin_ge(const int* p, int target, int* err, int code) {
+// One lane waits for its granule.  ok := false on timeout or when another
+// workgroup failed (the caller leaves after a block-wide check).
+__device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err, bool& ok) {
+    u64 g = ld_rlxu64(p);
+    if ((unsigned)(g >> 32) == tag) return __uint_as_float((unsigned)g);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (unsigned it = 0;; ++it) {
-        if (ld_rlx(p) >= target) return true;
-        if ((it & 63) == 63) {
-            if (ld_rlx(err) != 0) return false;
+    for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        g = ld_rlxu64(p);
+        if ((unsigned)(g >> 32) == tag) return __uint_as_float((unsigned)g);
+        if ((it & 63) == 0) {
+            if (ld_rlx(err) != 0) { ok = false; return 0.f; }
             if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
-                atomicCAS(err, 0, code);
-                return false;
+                atomicCAS(err, 0, 1);
+                ok = false;
+                return 0.f;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
     }
 }
+__device__ __forceinline__ bool block_ok(bool ok) { return !__syncthreads_or(ok ? 0 : 1); }
 
-struct Ws {   // hand-off workspace addressing (all zeroed before the launch)
-    long long* accA; long long* accF; float* lg; int* cnt; unsigned long long* gran;
+// Ring of step slots of granules (u64).  Per slot: PA [24][B][16][512],
+// RA [24][B][512], PF [24][B][64][512], RF [24][B][512], LG [B][1056], TK [16].
+struct Ws {
+    u64* ring;
     int B;
-    __device__ long long* A(int s, int l, int b) const { return accA + ((long)(s * 24 + l) * B + b) * 512; }
-    __device__ long long* F(int s, int l, int b) const { return accF + ((long)(s * 24 + l) * B + b) * 512; }
-    __device__ float* L(int s, int b) const { return lg + ((long)s * B + b) * PERSIST_LGS; }
-    __device__ int* cA(int s, int l) const { return cnt + ((long)s * PERSIST_CNT_LINES + 2 * l) * 32; }
-    __device__ int* cF(int s, int l) const { return cnt + ((long)s * PERSIST_CNT_LINES + 2 * l + 1) * 32; }
-    __device__ int* cL(int s) const { return cnt + ((long)s * PERSIST_CNT_LINES + 48) * 32; }
-    __device__ unsigned long long* G(int s, int b) const { return gran + (long)s * 16 + b; }
+    unsigned epoch;
+    __device__ long oRA() const { return (long)24 * B * 16 * 512; }
+    __device__ long oPF() const { return oRA() + (long)24 * B * 512; }
+    __device__ long oRF() const { return oPF() + (long)24 * B * 64 * 512; }
+    __device__ long oLG() const { return oRF() + (long)24 * B * 512; }
+    __device__ long oTK() const { return oLG() + (long)B * PERSIST_LGS; }
+    __device__ long slot_sz() const { return oTK() + 16; }
+    __device__ u64* slot(int s) const { return ring + (long)(s % RING) * slot_sz(); }
+    __device__ unsigned tag(int s) const { return (epoch << 12) | (unsigned)(s + 1); }
+    __device__ u64* PA(int s, int l, int b, int h) const { return slot(s) + ((long)(l * B + b) * 16 + h) * 512; }
+    __device__ u64* RA(int s, int l, int b) const { return slot(s) + oRA() + (long)(l * B + b) * 512; }
+    __device__ u64* PF(int s, int l, int b, int j) const { return slot(s) + oPF() + ((long)(l * B + b) * 64 + j) * 512; }
+    __device__ u64* RF(int s, int l, int b) const { return slot(s) + oRF() + (long)(l * B + b) * 512; }
+    __device__ u64* LG(int s, int b) const { return slot(s) + oLG() + (long)b * PERSIST_LGS; }
+    __device__ u64* TK(int s, int b) const { return slot(s) + oTK() + b; }
 };
 
-// LayerNorm statistics of NB rows of 512 values, one value per thread per row
-// (Chan et al. pairwise merge of (mean, M2)), one LDS exchange.
+// N independent wave sums on the DPP path, interleaved (ILP); lane 63 holds the sums.
+template <int N>
+__device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f<0xB1, 0xF>(v[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x4E, 0xF>(v[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x141, 0xF>(v[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x140, 0xF>(v[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x142, 0xA>(v[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x143, 0xC>(v[q]);
+}
+
+// LayerNorm statistics of NB rows of 512 values, one value per thread per row:
+// Chan et al. pairwise (mean, M2) merges -- butterflies on the DPP path inside
+// 16-lane rows, the 4 rows of a wave and the 8 waves on uniform values.
 template <int NB>
 __device__ __forceinline__ void ln_stats(const float (&v)[NB], float (&mean)[NB], float (&den)[NB], float* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float mu[NB], m2[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) { mu[b] = v[b]; m2[b] = 0.f; }
+    auto merge = [&](float& a_mu, float& a_m2, float o_mu, float o_m2, float n) {   // equal counts n
+        const float dl = o_mu - a_mu;
+        a_m2 = a_m2 + o_m2 + dl * dl * (n * 0.5f);
+        a_mu = a_mu + dl * 0.5f;
+    };
+#define LN_STEP(CTRL, N)                                                                     \
+    _Pragma("unroll") for (int b = 0; b < NB; ++b) {                                         \
+        const float om = dpp_f<CTRL, 0xF>(mu[b]), o2 = dpp_f<CTRL, 0xF>(m2[b]);              \
+        merge(mu[b], m2[b], om, o2, N);                                                      \
+    }
+    LN_STEP(0xB1, 1.f)
+    LN_STEP(0x4E, 2.f)
+    LN_STEP(0x141, 4.f)
+    LN_STEP(0x140, 8.f)
+#undef LN_STEP
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        float mu = v[b], m2 = 0.f, n = 1.f;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float mu_o = __shfl_xor(mu, o, 64);
-            const float m2_o = __shfl_xor(m2, o, 64);
-            const float dl = mu_o - mu;
-            m2 = m2 + m2_o + dl * dl * (n * 0.5f);
-            mu = mu + dl * 0.5f;
-            n *= 2.f;
-        }
-        if (lane == 0) { red[(w * NB + b) * 2] = mu; red[(w * NB + b) * 2 + 1] = m2; }
+        // rows 0..3 of the wave (16 values each), merged on uniform values
+        float r_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 0));
+        float r_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 0));
+        float r1_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 16));
+        float r1_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 16));
+        float r2_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 32));
+        float r2_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 32));
+        float r3_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 48));
+        float r3_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 48));
+        merge(r_mu, r_m2, r1_mu, r1_m2, 16.f);
+        merge(r2_mu, r2_m2, r3_mu, r3_m2, 16.f);
+        merge(r_mu, r_m2, r2_mu, r2_m2, 32.f);
+        if (lane == 0) { red[(w * NB + b) * 2] = r_mu; red[(w * NB + b) * 2 + 1] = r_m2; }
     }
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        float mu = red[b * 2], m2 = red[b * 2 + 1], n = 64.f;
+        float a_mu[PWV], a_m2[PWV];
 #pragma unroll
-        for (int ww = 1; ww < PWV; ++ww) {
-            const float mo = red[(ww * NB + b) * 2], m2o = red[(ww * NB + b) * 2 + 1];
-            const float dl = mo - mu;
-            const float nt = n + 64.f;
-            mu = mu + dl * (64.f / nt);
-            m2 = m2 + m2o + dl * dl * (n * 64.f / nt);
-            n = nt;
-        }
-        mean[b] = mu;
-        den[b] = sqrtf(m2 * (1.0f / 512.0f) + 1e-5f);
+        for (int ww = 0; ww < PWV; ++ww) { a_mu[ww] = red[(ww * NB + b) * 2]; a_m2[ww] = red[(ww * NB + b) * 2 + 1]; }
+        merge(a_mu[0], a_m2[0], a_mu[1], a_m2[1], 64.f);
+        merge(a_mu[2], a_m2[2], a_mu[3], a_m2[3], 64.f);
+        merge(a_mu[4], a_m2[4], a_mu[5], a_m2[5], 64.f);
+        merge(a_mu[6], a_m2[6], a_mu[7], a_m2[7], 64.f);
+        merge(a_mu[0], a_m2[0], a_mu[2], a_m2[2], 128.f);
+        merge(a_mu[4], a_m2[4], a_mu[6], a_m2[6], 128.f);
+        merge(a_mu[0], a_m2[0], a_mu[4], a_m2[4], 256.f);
+        mean[b] = a_mu[0];
+        den[b] = sqrtf(a_m2[0] * (1.0f / 512.0f) + 1e-5f);
     }
     __syncthreads();   // red reusable
 }
@@ -169,61 +213,62 @@ __device__ __forceinline__ float dot8(const uint4 w, const float4 x0, const floa
 
 struct Shared {
     union {
-        struct {               // attention role
-            float k[KVL * 32]; // K/V rows [0, min(kv, KVL)) of the head, staged by LDS-DMA
+        struct {                    // attention role
+            float k[KVL * 32];      // K/V rows [0, min(kv, KVL)) of the head (LDS-DMA)
             float v[KVL * 32];
-            float x[512];      // x_l
-            float h1[512];     // LN1 output (residual of the next layer)
-            uint4 wo[32 * 64]; // WoT rows of the head (32 x 512 fp16), staged by LDS-DMA
+            __half wo[32 * 512];    // WoT rows of the head (LDS-DMA)
+            float p[TMAXP];         // scores, then softmax numerators
+            float x[512];           // x_l of the sequence
+            float h1[512];          // LN1 output of the sequence
+            float ov[16][32];       // P·V partial sums of 16 key groups
+            float lg[PERSIST_LGS];  // logits (sampler)
         } at;
-        struct {               // FFN role
-            float x[8][512];   // x_l per sequence
-            float h1[8][512];  // LN1 output per sequence
+        struct {                    // FFN role
+            float x[8][512];        // x_l per sequence
+            float h1[8][512];       // LN1 output per sequence
+            __half w2[32 * 512];    // W2^T rows of the slice (LDS-DMA)
+            float ra[8][16][8];     // reduce-A operands
+            float rf[64][8];        // reduce-F operands
         } ff;
     };
-    float ored[PWV][512];      // cross-wave reduction of 512-wide partials
     float qkv[96];
     float os[32];
     float fs[8][32];
     float red[2 * PWV * 8];
-    float redm[PWV];
-    float redl[PWV][8];
-    float reda[PWV][32];
+    float wred[2][PWV];
     uint32_t seen[33];
     int tok[8];
-    int act;                   // bit b: sequence b still decoding
+    int act;                        // bit b: sequence b still decoding
     int flag;
+    unsigned long long stamp[16];   // [0,8) 100 MHz realtime, [8,16) shader clock
     SampleLds<PT> samp;
 };
+
+// Phase stamps go to LDS (no vector-memory op that a later vmcnt wait would count)
+// and are flushed once per step.
+#define STAMP(i)                                                                          \
+    do {                                                                                  \
+        if (probe && threadIdx.x == 0) {                                                  \
+            sh.stamp[i] = __builtin_amdgcn_s_memrealtime();                               \
+            sh.stamp[8 + (i)] = __builtin_amdgcn_s_memtime();                             \
+        }                                                                                 \
+    } while (0)
 
 // Token granules of step s+1 for every sequence active in step s: new tokens and
 // the active set.  Block-uniform result; false on error.
 __device__ bool poll_tokens(const PersistArgs& a, const Ws& ws, int s, Shared& sh) {
     if (threadIdx.x == 0) {
-        int act = sh.act, ok = 1;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int act = sh.act;
+        bool ok = true;
         for (int b = 0; b < a.B && ok; ++b) {
             if (!((act >> b) & 1)) continue;
-            for (unsigned it = 0;; ++it) {
-                const unsigned long long g = ld_rlxu64(ws.G(s + 1, b));
-                if ((unsigned)(g >> 32) == (unsigned)(s + 1)) {
-                    sh.tok[b] = (int)(g & 0xffff);
-                    if ((g >> 16) & 1) act &= ~(1 << b);
-                    break;
-                }
-                if ((it & 63) == 63) {
-                    if (ld_rlx(a.err) != 0) { ok = 0; break; }
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
-                        atomicCAS(a.err, 0, 3);
-                        ok = 0;
-                        break;
-                    }
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
+            const float v = wait_gran(ws.TK(s + 1, b), ws.tag(s + 1), a.err, ok);
+            const unsigned u = __float_as_uint(v);
+            sh.tok[b] = (int)(u & 0xffff);
+            if ((u >> 16) & 1) act &= ~(1 << b);
         }
         sh.act = act;
-        sh.flag = ok;
+        sh.flag = ok ? 1 : 0;
     }
     __syncthreads();
     const bool ok = sh.flag != 0;
@@ -231,33 +276,56 @@ __device__ bool poll_tokens(const PersistArgs& a, const Ws& ws, int s, Shared& s
     return ok;
 }
 
-__device__ bool block_wait(const int* p, int target, int* err, int code, Shared& sh) {
-    if (threadIdx.x == 0) sh.flag = spin_ge(p, target, err, code) ? 1 : 0;
-    __syncthreads();
-    const bool ok = sh.flag != 0;
-    __syncthreads();
-    return ok;
+// LayerNorm parameters of one layer, one element per thread (loaded a layer ahead)
+struct LnP {
+    float bo, n1w, n1b, b2, n2w, n2b;
+    __device__ void load(const PLayer& P, int tid) {
+        bo = ldg(P.b_out, tid); n1w = ldg(P.n1w, tid); n1b = ldg(P.n1b, tid);
+        b2 = ldg(P.b2, tid); n2w = ldg(P.n2w, tid); n2b = ldg(P.n2b, tid);
+    }
+};
+
+// out[i] = LN(res[i] + (bias + R[b0+i])) for the tracked sequences; R from granules.
+template <int NB, typename GranF>
+__device__ __forceinline__ bool track_ln(GranF gran, unsigned tag, const float* res, float* out, int b0, int nb,
+                                         int act, float bias, float g, float be, int* err, Shared& sh) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    float v[NB], mean[NB], den[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        v[i] = 0.f;
+        if (i < nb && ((act >> (b0 + i)) & 1)) v[i] = res[i * 512 + tid] + (bias + wait_gran(gran(b0 + i) + tid, tag, err, ok));
+    }
+    if (!block_ok(ok)) return false;
+    ln_stats<NB>(v, mean, den, sh.red);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+        if (i < nb) out[i * 512 + tid] = (v[i] - mean[i]) / den[i] * g + be;
+    return true;
 }
 
-#define STAMP(i)                                                                          \
-    do {                                                                                  \
-        if (probe && threadIdx.x == 0)                                                    \
-            a.trace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();              \
-    } while (0)
-
 // --------------------------------------------------------------------------
-// attention role: head h of sequence b
+// One workgroup of role ATTN (head h, sequence ab) or FFN (slice j, NB >= B).
 // --------------------------------------------------------------------------
-__device__ void attn_role(const PersistArgs& a, const Ws& ws, int h, int b, Shared& sh) {
+template <bool ATTN, int NB>
+__device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: row offsets fold into SGPR bases
-    const int B = a.B, NA = 16 * B;
-    const int c = lane & 7, g = (w << 3) | (lane >> 3);     // 16-B chunk of a K/V row, key group
-    const long kvoff = (long)b * a.sstride + (long)h * a.tmax * 32;
-    const bool sampler = h == 0;
-    // entry state of sequence b
-    const int ny0 = a.ny[b], kv0 = a.kvlen[b], st0 = a.steps[b];
-    if (tid < 33) sh.seen[tid] = a.seen[(long)b * 33 + tid];
+    const int B = a.B, G = a.groups, NA = 16 * B, per = NA + NFB;
+    const int grp = blockIdx.x / per, r = blockIdx.x - grp * per;
+    const int h = r & 15, ab = r >> 4, j = r - NA;
+    const int b0 = ATTN ? ab : 0, nb = ATTN ? 1 : B;
+    const bool sampler = ATTN && h == 0 && grp == 0;
+    const bool logits_grp = !ATTN && grp == 23 % G;
+    float* X = ATTN ? sh.at.x : &sh.ff.x[0][0];
+    float* H1 = ATTN ? sh.at.h1 : &sh.ff.h1[0][0];
+    // entry state
+    int ny0[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) ny0[i] = i < nb ? a.ny[b0 + i] : 0;
+    const int kv0 = ATTN ? a.kvlen[ab] : 0, st0 = ATTN ? a.steps[ab] : 0;
+    if (sampler && tid < 33) sh.seen[tid] = a.seen[(long)ab * 33 + tid];
     if (tid == 0) {
         int act = 0;
         for (int bb = 0; bb < B; ++bb) {
@@ -267,469 +335,375 @@ __device__ void attn_role(const PersistArgs& a, const Ws& ws, int h, int b, Shar
         sh.act = act;
     }
     __syncthreads();
+    const long kvoff = (long)ab * a.sstride + (long)h * a.tmax * 32;
     uint4 wq[12];
     float bqv = 0.f;
-    float p_bo = 0.f, p_n1w = 0.f, p_n1b = 0.f, p_b2 = 0.f, p_n2w = 0.f, p_n2b = 0.f;
-    // loads for layer l of the step whose K/V length is kv
-    auto prefetch = [&](int l, int kv) {
+    uint4 w1r[4], wp[3];
+    float b1r[4];
+    auto prefetch = [&](int l, int kv) {   // this workgroup's operands of layer l
         const PLayer& P = a.L[l];
-        // wave w: q, k and v rows h*32 + 4w + r (r < 4) -- 1 KB apart, immediate offsets
-        const __half* wb = P.w_in + (long)(h * 32 + 4 * w) * 512;
+        if constexpr (ATTN) {
+            // wave w: q, k and v rows h*32 + 4w + q (q < 4) -- 1 KB apart, immediate offsets
+            const __half* wb = P.w_in + (long)(h * 32 + 4 * w) * 512;
 #pragma unroll
-        for (int m = 0; m < 3; ++m)
+            for (int m = 0; m < 3; ++m)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) wq[m * 4 + r] = ldg16(wb + (long)m * 512 * 512 + r * 512, lane * 8);
-        // lane m*4+r (< 12) holds the bias of row (m, r); read back with readlane
-        bqv = lane < 12 ? ldg(P.b_in, (lane >> 2) * 512 + h * 32 + 4 * w + (lane & 3)) : 0.f;
-        // WoT rows h*32 .. h*32+31 (contiguous 32 KB) -> LDS, one 1 KB row per wave instruction
-        const __half* ob = P.woT + (long)(h * 32 + 4 * w) * 512;
+                for (int q = 0; q < 4; ++q) wq[m * 4 + q] = ldg16(wb + (long)m * 512 * 512 + q * 512, lane * 8);
+            // lane m*4+q (< 12) holds the bias of row (m, q)
+            bqv = lane < 12 ? ldg(P.b_in, (lane >> 2) * 512 + h * 32 + 4 * w + (lane & 3)) : 0.f;
+            // WoT rows h*32 .. h*32+31 (contiguous 32 KB) -> LDS, one 1 KB row per wave instruction
+            const __half* ob = P.woT + (long)(h * 32 + 4 * w) * 512;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds(ob + i * 512 + lane * 8, sh.at.wo + (4 * w + i) * 64, 16, 0, 0);
-        // K/V rows [0, min(kv, KVL)) -> LDS, 1 KB (8 rows) per wave instruction.  Rows of the
-        // last chunk past kv are read (allocated: tmax >= kv + 16) and masked in the math.
-        const float* K = a.kc[l] + kvoff;
-        const float* V = a.vc[l] + kvoff;
-        const int nch = (min(kv, KVL) + 7) >> 3;
-        for (int i = w; i < nch; i += PWV) {
-            __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
-        }
-        p_bo = ldg(P.b_out, tid); p_n1w = ldg(P.n1w, tid); p_n1b = ldg(P.n1b, tid);
-        if (l > 0) {
-            const PLayer& Q = a.L[l - 1];
-            p_b2 = ldg(Q.b2, tid); p_n2w = ldg(Q.n2w, tid); p_n2b = ldg(Q.n2b, tid);
+            for (int i = 0; i < 4; ++i)
+                __builtin_amdgcn_global_load_lds(ob + i * 512 + lane * 8, sh.at.wo + (4 * w + i) * 512, 16, 0, 0);
+            // K/V rows [0, min(kv, KVL)) -> LDS, 8 rows (1 KB) per wave instruction.  Rows of the
+            // last chunk past kv are read (allocated: tmax >= kv + 16) and never used.
+            const float* K = a.kc[l] + kvoff;
+            const float* V = a.vc[l] + kvoff;
+            const int nch = (min(kv, KVL) + 7) >> 3;
+            for (int i = w; i < nch; i += PWV) {
+                __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w1r[q] = ldg16(P.w1 + (long)(j * 32 + w * 4 + q) * 512, lane * 8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b1r[q] = ldg(P.b1, j * 32 + w * 4 + q);
+            const __half* w2b = P.w2T + (long)(j * 32 + 4 * w) * 512;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                __builtin_amdgcn_global_load_lds(w2b + i * 512 + lane * 8, sh.ff.w2 + (4 * w + i) * 512, 16, 0, 0);
         }
     };
+    // logits rows (logits group): 2 per wave, + row 1024 on the last FFN workgroup's wave 0
+    const int lrow0 = j * 16 + 2 * w;
+    const bool extra = (j == NFB - 1) && w == 0;
+    const bool mine_seq = !ATTN || ((sh.act >> ab) & 1);
+    if (sh.act && mine_seq) prefetch(grp, kv0);
+    LnP lp;                                   // layer l's parameters
+    float pb2 = 0.f, pn2w = 0.f, pn2b = 0.f;  // layer l-1's LN2
+    lp.load(a.L[0], tid);
     int n_exec = 0, last_stop = 0;
-    bool alive = true;
     int kv = kv0;
-    if ((sh.act >> b) & 1) prefetch(0, kv);
-    for (int s = 0; s < a.smax && alive; ++s) {
+    for (int s = 0; s < a.smax; ++s) {
         const int act = sh.act;
         if (act == 0) break;
-        const bool mine = (act >> b) & 1;
-        if (!mine) {
-            // idle sequence: arrive on every attention counter of the step
-            if (tid == 0)
-                for (int l = 0; l < 24; ++l) __hip_atomic_fetch_add(ws.cA(s, l), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!poll_tokens(a, ws, s, sh)) { alive = false; break; }
+        const unsigned tag = ws.tag(s);
+        if (ATTN && !((act >> ab) & 1)) {     // finished sequence: nothing to publish (reducers skip it)
+            if (!poll_tokens(a, ws, s, sh)) return;
             continue;
+        }
+        // x_0 = E_audio[tok] + alpha * pe[n]
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            if (i >= nb || !((act >> (b0 + i)) & 1)) continue;
+            X[i * 512 + tid] = ldg_h(a.emb, (long)sh.tok[b0 + i] * 512 + tid) +
+                               ldg(a.alpha, 0) * ldg(a.pe, (long)(ny0[i] + s) * 512 + tid);
         }
         for (int l = 0; l < 24; ++l) {
             const bool probe = a.trace && s == 8 && l == 12;
-            const PLayer& P = a.L[l];
-            // ---- layer input x_l
-            float xv;
-            if (l == 0) {
-                const int n = ny0 + s;
-                xv = ldg_h(a.emb, (long)sh.tok[b] * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)n * 512 + tid);
-            } else {
-                if (!block_wait(ws.cF(s, l - 1), NFB, a.err, 1, sh)) { alive = false; break; }
+            const bool mine = (l - grp) % G == 0;
+            // ---- x_l (layer 0: the embedding above)
+            if (l > 0) {
                 STAMP(0);
-                const float acc = from_fx(ld_rlx64(ws.F(s, l - 1, b) + tid));
-                float v[1] = {sh.at.h1[tid] + (p_b2 + acc)}, mean[1], den[1];
-                ln_stats<1>(v, mean, den, sh.red);
-                xv = (v[0] - mean[0]) / den[0] * p_n2w + p_n2b;
+                if (!track_ln<NB>([&](int b) { return ws.RF(s, l - 1, b); }, tag, H1, X, b0, nb, act, pb2, pn2w,
+                                  pn2b, a.err, sh))
+                    return;
             }
-            sh.at.x[tid] = xv;
             __syncthreads();
             STAMP(1);
-            // ---- q, k, v of head h (12 rows per wave)
-            {
-                const float4 x0 = *reinterpret_cast<const float4*>(&sh.at.x[lane * 8]);
-                const float4 x1 = *reinterpret_cast<const float4*>(&sh.at.x[lane * 8 + 4]);
+            if constexpr (ATTN) if (mine) {
+                // ---- q, k, v of head h: 12 independent dot products per wave, reduced together
+                for (int rep = 0; rep < (probe && a.trace_rep ? 2 : 1); ++rep) {
+                    if (rep == 1) { __syncthreads(); STAMP(7); }
+                    const float4 x0 = *reinterpret_cast<const float4*>(&X[lane * 8]);
+                    const float4 x1 = *reinterpret_cast<const float4*>(&X[lane * 8 + 4]);
+                    float acc[12];
 #pragma unroll
-                for (int r = 0; r < 12; ++r) {
-                    const float sum = wave_sum_dpp(dot8(wq[r], x0, x1));
-                    const float bias = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bqv), r));
-                    if (lane == 0) sh.qkv[(r >> 2) * 32 + 4 * w + (r & 3)] = bias + sum;
-                }
-            }
-            __syncthreads();
-            STAMP(5);
-            // ---- append the new K/V row, attention over [0, kv]
-            float* Kw = a.kc[l] + kvoff;
-            float* Vw = a.vc[l] + kvoff;
-            const float sc = a.scale;
-            const float q0 = sh.qkv[4 * c] * sc, q1 = sh.qkv[4 * c + 1] * sc;
-            const float q2 = sh.qkv[4 * c + 2] * sc, q3 = sh.qkv[4 * c + 3] * sc;
-            const float4 knew = make_float4(sh.qkv[32 + 4 * c], sh.qkv[33 + 4 * c], sh.qkv[34 + 4 * c], sh.qkv[35 + 4 * c]);
-            const float4 vnew = make_float4(sh.qkv[64 + 4 * c], sh.qkv[65 + 4 * c], sh.qkv[66 + 4 * c], sh.qkv[67 + 4 * c]);
-            const int T = kv + 1;
-            float mt = -INFINITY, ls = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-            for (int base = 0; base < T; base += 64 * KU) {
-                float4 kk[KU], vv[KU];
-                if (base == 0) {
+                    for (int q = 0; q < 12; ++q) acc[q] = dot8(wq[q], x0, x1);
+                    wave_sum_n<12>(acc);
+                    float mv = 0.f;
 #pragma unroll
-                    for (int u = 0; u < KU; ++u) {
-                        const int t = u * 64 + g;
-                        kk[u] = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * c);
-                        vv[u] = *reinterpret_cast<const float4*>(sh.at.v + t * 32 + 4 * c);
+                    for (int q = 0; q < 12; ++q) {
+                        const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[q]), 63));
+                        mv = lane == q ? t : mv;
                     }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < KU; ++u) {
-                        const int t = min(base + u * 64 + g, kv - 1);
-                        kk[u] = ldg16f(Kw, (long)t * 32 + 4 * c);
-                        vv[u] = ldg16f(Vw, (long)t * 32 + 4 * c);
-                    }
+                    if (lane < 12) sh.qkv[(lane >> 2) * 32 + 4 * w + (lane & 3)] = bqv + mv;
+                    if (rep == 0 && probe && a.trace_rep) { __syncthreads(); STAMP(6); }
                 }
-                float sv[KU];
-                float pm = -INFINITY;
-#pragma unroll
-                for (int u = 0; u < KU; ++u) {
-                    const int t = base + u * 64 + g;
-                    if (t == kv) { kk[u] = knew; vv[u] = vnew; }
-                    float x = q0 * (kk[u].x * sc);
-                    x += q1 * (kk[u].y * sc);
-                    x += q2 * (kk[u].z * sc);
-                    x += q3 * (kk[u].w * sc);
-                    x += dpp_f<0xB1, 0xF>(x);
-                    x += dpp_f<0x4E, 0xF>(x);
-                    x += dpp_f<0x141, 0xF>(x);
-                    const bool valid = t < T;
-                    sv[u] = valid ? x : -INFINITY;
-                    if (!valid) vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    pm = fmaxf(pm, sv[u]);
-                }
-                if (pm == -INFINITY) continue;
-                const float mn = fmaxf(mt, pm);
-                const float f = expf(mt - mn);
-                float lsum = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-                for (int u = 0; u < KU; ++u) {
-                    const float p = expf(sv[u] - mn);
-                    lsum += p;
-                    a0 += p * vv[u].x; a1 += p * vv[u].y; a2 += p * vv[u].z; a3 += p * vv[u].w;
-                }
-                ls = ls * f + lsum;
-                o0 = o0 * f + a0; o1 = o1 * f + a1; o2 = o2 * f + a2; o3 = o3 * f + a3;
-                mt = mn;
-            }
-            STAMP(6);
-            {
-                const float bm = wave_max(mt);
-                if (lane == 0) sh.redm[w] = bm;
                 __syncthreads();
-                float m = sh.redm[0];
+                STAMP(2);
+                // ---- scores (q*s)·(k*s) over [0, kv]: keys t = pass*512 + tid
+                float* Kw = a.kc[l] + kvoff;
+                float* Vw = a.vc[l] + kvoff;
+                const float sc = a.scale;
+                const int T = kv + 1;
+                float lmax = -INFINITY;
+                for (int t = tid; t < T; t += PT) {
+                    float4 kr[8];
+                    if (t < kv && t < KVL) {
 #pragma unroll
-                for (int ww = 1; ww < PWV; ++ww) m = fmaxf(m, sh.redm[ww]);
-                const float fsc = mt == -INFINITY ? 0.f : expf(mt - m);
-                ls *= fsc; o0 *= fsc; o1 *= fsc; o2 *= fsc; o3 *= fsc;
+                        for (int i = 0; i < 8; ++i) kr[i] = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * i);
+                    } else if (t < kv) {
 #pragma unroll
-                for (int x = 8; x < 64; x <<= 1) {
-                    ls += __shfl_xor(ls, x, 64);
-                    o0 += __shfl_xor(o0, x, 64);
-                    o1 += __shfl_xor(o1, x, 64);
-                    o2 += __shfl_xor(o2, x, 64);
-                    o3 += __shfl_xor(o3, x, 64);
+                        for (int i = 0; i < 8; ++i) kr[i] = ldg16f(Kw, (long)t * 32 + 4 * i);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) kr[i] = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * i);
+                    }
+                    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float4 qd = *reinterpret_cast<const float4*>(sh.qkv + 4 * i);
+                        part[i & 3] += (qd.x * sc) * (kr[i].x * sc);
+                        part[i & 3] += (qd.y * sc) * (kr[i].y * sc);
+                        part[i & 3] += (qd.z * sc) * (kr[i].z * sc);
+                        part[i & 3] += (qd.w * sc) * (kr[i].w * sc);
+                    }
+                    const float sv = (part[0] + part[1]) + (part[2] + part[3]);
+                    sh.at.p[t] = sv;
+                    lmax = fmaxf(lmax, sv);
                 }
-                if (lane < 8) {
-                    sh.reda[w][4 * lane] = o0; sh.reda[w][4 * lane + 1] = o1;
-                    sh.reda[w][4 * lane + 2] = o2; sh.reda[w][4 * lane + 3] = o3;
-                    sh.redl[w][lane] = ls;
+                const float wm = wave_max_dpp(lmax);
+                if (lane == 0) sh.wred[0][w] = wm;
+                __syncthreads();
+                float M = sh.wred[0][0];
+#pragma unroll
+                for (int ww = 1; ww < PWV; ++ww) M = fmaxf(M, sh.wred[0][ww]);
+                float lsum = 0.f;
+                for (int t = tid; t < T; t += PT) {
+                    const float e = expf(sh.at.p[t] - M);
+                    sh.at.p[t] = e;
+                    lsum += e;
+                }
+                const float ws_ = wave_sum_dpp(lsum);
+                if (lane == 0) sh.wred[1][w] = ws_;
+                __syncthreads();
+                STAMP(3);
+                // ---- P·V: 16 key groups x 32 dims
+                {
+                    const int kg = tid >> 5, d = tid & 31;
+                    float o = 0.f;
+                    for (int t = kg; t < T; t += 16) {
+                        const float vv = t < kv ? (t < KVL ? sh.at.v[t * 32 + d] : ldg(Vw, (long)t * 32 + d))
+                                                : sh.qkv[64 + d];
+                        o += sh.at.p[t] * vv;
+                    }
+                    sh.at.ov[kg][d] = o;
                 }
                 __syncthreads();
                 if (tid < 32) {
-                    const float L = ((sh.redl[0][0] + sh.redl[1][0]) + (sh.redl[2][0] + sh.redl[3][0])) +
-                                    ((sh.redl[4][0] + sh.redl[5][0]) + (sh.redl[6][0] + sh.redl[7][0]));
-                    const float O = ((sh.reda[0][tid] + sh.reda[1][tid]) + (sh.reda[2][tid] + sh.reda[3][tid])) +
-                                    ((sh.reda[4][tid] + sh.reda[5][tid]) + (sh.reda[6][tid] + sh.reda[7][tid]));
+                    float O = 0.f, L = 0.f;
+#pragma unroll
+                    for (int kg = 0; kg < 16; ++kg) O += sh.at.ov[kg][tid];
+#pragma unroll
+                    for (int ww = 0; ww < PWV; ++ww) L += sh.wred[1][ww];
                     sh.os[tid] = O / L;
                 }
                 __syncthreads();
-            }
-            STAMP(2);
-            // ---- out-projection slice of this head -> fixed-point hand-off
-            {
-                float r[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) r[k] = 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float wf[8];
-                    h8_to_f8(sh.at.wo[(w + 8 * i) * 64 + lane], wf);
-                    const float ov = sh.os[w + 8 * i];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) r[k] += wf[k] * ov;
-                }
-#pragma unroll
-                for (int k = 0; k < 8; ++k) sh.ored[w][8 * lane + k] = r[k];
-                __syncthreads();
-                const float val = ((sh.ored[0][tid] + sh.ored[1][tid]) + (sh.ored[2][tid] + sh.ored[3][tid])) +
-                                  ((sh.ored[4][tid] + sh.ored[5][tid]) + (sh.ored[6][tid] + sh.ored[7][tid]));
-                // the new K/V row (read by this workgroup only, next step), then the hand-off
-                if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
-                else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
-                fx_add(ws.A(s, l, b) + tid, val);
-                drain();
-                __syncthreads();
-                if (tid == 0) __hip_atomic_fetch_add(ws.cA(s, l), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            STAMP(3);
-            // ---- next layer's weights and K/V rows while the others finish
-            const float bo = p_bo, n1w = p_n1w, n1b = p_n1b;
-            if (l < 23) prefetch(l + 1, kv);
-            else prefetch(0, kv + 1);
-            // ---- h1_l = LN1(x_l + bo + Σ heads) for the next layer's input (not needed after 23)
-            if (l < 23) {
-                if (!block_wait(ws.cA(s, l), NA, a.err, 2, sh)) { alive = false; break; }
-                const float acc = from_fx(ld_rlx64(ws.A(s, l, b) + tid));
-                float v[1] = {sh.at.x[tid] + (bo + acc)}, mean[1], den[1];
-                ln_stats<1>(v, mean, den, sh.red);
-                sh.at.h1[tid] = (v[0] - mean[0]) / den[0] * n1w + n1b;
                 STAMP(4);
+                // ---- out-projection slice of this head (column tid) -> partial granule
+                {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int d = 0; d < 32; ++d) acc += __half2float(sh.at.wo[d * 512 + tid]) * sh.os[d];
+                    st_gran(ws.PA(s, l, ab, h) + tid, tag, acc);
+                    // the new K/V row (read by this workgroup only, next step)
+                    if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
+                    else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
+                }
+                STAMP(5);
+                __syncthreads();   // LDS operands consumed before the next layer's LDS-DMA lands
+                // ---- next layer of this group (or of the next step) while the others work
+                if (l + G < 24) prefetch(l + G, kv);
+                else prefetch(l + G - 24, kv + 1);
+            }
+            if constexpr (!ATTN) if (mine) {
+                // ---- reduce-A: columns [8j, 8j+8) of Σ_h PA, fixed order
+                bool ok = true;
+                if (tid < 128) {
+                    const int hh = tid >> 3, c = tid & 7;
+#pragma unroll
+                    for (int i = 0; i < NB; ++i)
+                        if (i < nb && ((act >> i) & 1))
+                            sh.ff.ra[i][hh][c] = wait_gran(ws.PA(s, l, i, hh) + 8 * j + c, tag, a.err, ok);
+                }
+                if (!block_ok(ok)) return;
+                if (tid < 8 * NB) {
+                    const int i = tid >> 3, c = tid & 7;
+                    if (i < nb && ((act >> i) & 1)) {
+                        float sum = 0.f;
+#pragma unroll
+                        for (int hh = 0; hh < 16; ++hh) sum += sh.ff.ra[i][hh][c];
+                        st_gran(ws.RA(s, l, i) + 8 * j + c, tag, sum);
+                    }
+                }
+                STAMP(2);
+            }
+            // ---- h1_l = LN1(x_l + bo + RA_l)  (not needed after layer 23 unless this workgroup computes the logits)
+            if (l < 23 || logits_grp) {
+                if (!track_ln<NB>([&](int b) { return ws.RA(s, l, b); }, tag, X, H1, b0, nb, act, lp.bo, lp.n1w,
+                                  lp.n1b, a.err, sh))
+                    return;
+                __syncthreads();
+                STAMP(6);
+            }
+            pb2 = lp.b2; pn2w = lp.n2w; pn2b = lp.n2b;
+            lp.load(a.L[l < 23 ? l + 1 : 0], tid);
+            if constexpr (!ATTN) if (mine) {
+                // ---- FFN1 rows of this slice (4 per wave), ReLU
+#pragma unroll
+                for (int i = 0; i < NB; ++i) {
+                    if (i >= nb || !((act >> i) & 1)) continue;
+                    const float4 x0 = *reinterpret_cast<const float4*>(&H1[i * 512 + lane * 8]);
+                    const float4 x1 = *reinterpret_cast<const float4*>(&H1[i * 512 + lane * 8 + 4]);
+                    float acc[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = dot8(w1r[q], x0, x1);
+                    wave_sum_n<4>(acc);
+                    if (lane == 63) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) sh.fs[i][w * 4 + q] = fmaxf(b1r[q] + acc[q], 0.f);
+                    }
+                }
+                __syncthreads();
+                STAMP(3);
+                // ---- FFN2 slice (column tid) -> partial granules
+                {
+                    float acc[NB];
+#pragma unroll
+                    for (int i = 0; i < NB; ++i) acc[i] = 0.f;
+#pragma unroll 8
+                    for (int q = 0; q < 32; ++q) {
+                        const float wv = __half2float(sh.ff.w2[q * 512 + tid]);
+#pragma unroll
+                        for (int i = 0; i < NB; ++i) acc[i] += wv * sh.fs[i][q];
+                    }
+#pragma unroll
+                    for (int i = 0; i < NB; ++i)
+                        if (i < nb && ((act >> i) & 1)) st_gran(ws.PF(s, l, i, j) + tid, tag, acc[i]);
+                }
+                STAMP(4);
+                // ---- reduce-F: columns [8j, 8j+8) of Σ_j' PF, fixed order
+                {
+                    const int jj = tid >> 3, c = tid & 7;
+#pragma unroll
+                    for (int i = 0; i < NB; ++i) {
+                        if (i >= nb || !((act >> i) & 1)) continue;
+                        bool ok = true;
+                        sh.ff.rf[jj][c] = wait_gran(ws.PF(s, l, i, jj) + 8 * j + c, tag, a.err, ok);
+                        if (!block_ok(ok)) return;
+                        if (tid < 8) {
+                            float sum = 0.f;
+#pragma unroll 16
+                            for (int q = 0; q < 64; ++q) sum += sh.ff.rf[q][tid];
+                            st_gran(ws.RF(s, l, i) + 8 * j + tid, tag, sum);
+                        }
+                        __syncthreads();
+                    }
+                }
+                STAMP(5);
+                if (l + G >= 24 && logits_grp) {
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) wp[q] = ldg16(a.w_pred + (long)(lrow0 + q) * 512, lane * 8);
+                    wp[2] = ldg16(a.w_pred + (long)1024 * 512, lane * 8);
+                }
+                if (l + G < 24) prefetch(l + G, 0);
+                else prefetch(l + G - 24, 0);
             }
         }
-        if (!alive) break;
-        // ---- sampler (head-0 workgroup of the sequence)
+        if (logits_grp) {
+            // ---- x_24 = LN2_23(h1_23 + b2 + RF_23), logits rows (ar_predict_layer, no bias)
+            if (!track_ln<NB>([&](int b) { return ws.RF(s, 23, b); }, tag, H1, X, 0, nb, act, pb2, pn2w, pn2b, a.err,
+                              sh))
+                return;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                if (i >= nb || !((act >> i) & 1)) continue;
+                const float4 x0 = *reinterpret_cast<const float4*>(&X[i * 512 + lane * 8]);
+                const float4 x1 = *reinterpret_cast<const float4*>(&X[i * 512 + lane * 8 + 4]);
+                float acc[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) acc[q] = dot8(wp[q], x0, x1);
+                wave_sum_n<3>(acc);
+                if (lane == 63) {
+                    u64* lg = ws.LG(s, i);
+                    st_gran(lg + lrow0, tag, acc[0]);
+                    st_gran(lg + lrow0 + 1, tag, acc[1]);
+                    if (extra) st_gran(lg + 1024, tag, acc[2]);
+                }
+            }
+        }
+        // ---- sampler (group 0, head-0 workgroup of the sequence)
         if (sampler) {
-            if (!block_wait(ws.cL(s), NFB, a.err, 4, sh)) { alive = false; break; }
-            const float* lg = ws.L(s, b);
+            bool ok = true;
+            const u64* lgg = ws.LG(s, ab);
+            for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok);
+            if (!block_ok(ok)) return;
             const int st = st0 + s;                 // loop steps already executed
             int raw = 0;
-            const int tok = sample_block<PT>([&](int i) { return ld_rlxf(lg + i); }, sh.seen, b, st + 1, a.top_k,
+            const int tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, ab, st + 1, a.top_k,
                                              a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw,
                                              sh.samp);
             if (tid == 0) {
-                a.y[(long)b * a.ldy + ny0 + s] = tok;
+                a.y[(long)ab * a.ldy + ny0[0] + s] = tok;
                 sh.seen[tok >> 5] |= 1u << (tok & 31);
                 const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
                 const int nst = st + 1;
                 const bool fin = a.force_steps > 0 ? nst >= a.force_steps : (stop || nst >= a.max_steps);
                 last_stop = stop;
-                __hip_atomic_store(ws.G(s + 1, b),
-                                   ((unsigned long long)(s + 1) << 32) | (unsigned)tok | (fin ? 1u << 16 : 0u),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                st_gran(ws.TK(s + 1, ab), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
             }
         }
+        if (a.trace && s == 8 && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         ++n_exec;
         ++kv;
-        if (!poll_tokens(a, ws, s, sh)) { alive = false; break; }
+        if (!poll_tokens(a, ws, s, sh)) return;
     }
-    // ---- write back the sequence state (head-0 workgroup)
+    // ---- write back the sequence state (sampler workgroup)
     if (sampler && n_exec > 0) {
         __syncthreads();
-        if (tid < 33) a.seen[(long)b * 33 + tid] = sh.seen[tid];
+        if (tid < 33) a.seen[(long)ab * 33 + tid] = sh.seen[tid];
         if (tid == 0) {
-            a.ny[b] = ny0 + n_exec;
-            a.steps[b] = st0 + n_exec;
-            a.kvlen[b] = kv0 + n_exec;
-            a.done[b] = ((sh.act >> b) & 1) ? 0 : 1;
-            if (a.stop_out) a.stop_out[b] = (uint8_t)last_stop;
+            a.ny[ab] = ny0[0] + n_exec;
+            a.steps[ab] = st0 + n_exec;
+            a.kvlen[ab] = kv0 + n_exec;
+            a.done[ab] = ((sh.act >> ab) & 1) ? 0 : 1;
+            if (a.stop_out) a.stop_out[ab] = (uint8_t)last_stop;
         }
-    }
-}
-
-// --------------------------------------------------------------------------
-// FFN role: hidden units [32 j, 32 j + 32) for every sequence; logits rows
-// [16 j, 16 j + 16) (+ row 1024 on the last workgroup)
-// --------------------------------------------------------------------------
-template <int NB>
-__device__ void ffn_role(const PersistArgs& a, const Ws& ws, int j, Shared& sh) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: row offsets fold into SGPR bases
-    const int B = a.B, NA = 16 * B;
-    int ny0[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) ny0[b] = b < B ? a.ny[b] : 0;
-    if (tid == 0) {
-        int act = 0;
-        for (int bb = 0; bb < B; ++bb) {
-            if (!a.done[bb]) act |= 1 << bb;
-            sh.tok[bb] = (int)a.y[(long)bb * a.ldy + a.ny[bb] - 1];
-        }
-        sh.act = act;
-    }
-    __syncthreads();
-    uint4 w1r[4], w2r[4];
-    float b1r[4];
-    float p_bo = 0.f, p_n1w = 0.f, p_n1b = 0.f, p_b2 = 0.f, p_n2w = 0.f, p_n2b = 0.f;
-    auto prefetch = [&](int l) {
-        const PLayer& P = a.L[l];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            w1r[r] = ldg16(P.w1, (long)(j * 32 + w * 4 + r) * 512 + lane * 8);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            w2r[i] = ldg16(P.w2T, (long)(j * 32 + w + 8 * i) * 512 + lane * 8);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) b1r[r] = ldg(P.b1, j * 32 + w * 4 + r);
-        p_bo = ldg(P.b_out, tid); p_n1w = ldg(P.n1w, tid); p_n1b = ldg(P.n1b, tid);
-        p_b2 = ldg(P.b2, tid); p_n2w = ldg(P.n2w, tid); p_n2b = ldg(P.n2b, tid);
-    };
-    // logits rows of this workgroup: 2 per wave, + row 1024 on the last workgroup's wave 0
-    const int lrow0 = j * 16 + 2 * w;
-    const bool extra = (j == NFB - 1) && w == 0;
-    bool alive = true;
-    if (sh.act) prefetch(0);
-    for (int s = 0; s < a.smax && alive; ++s) {
-        const int act = sh.act;
-        if (act == 0) break;
-        // x_0 = E_audio[tok] + alpha * pe[n]
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            if (b >= B || !((act >> b) & 1)) continue;
-            sh.ff.x[b][tid] = ldg_h(a.emb, (long)sh.tok[b] * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)(ny0[b] + s) * 512 + tid);
-        }
-        for (int l = 0; l < 24; ++l) {
-            const bool probe = a.trace && s == 8 && l == 12;
-            // ---- wait for the attention sum of layer l, h1 = LN1(x + bo + Σ)
-            if (!block_wait(ws.cA(s, l), NA, a.err, 5, sh)) { alive = false; break; }
-            STAMP(0);
-            {
-                float v[NB], mean[NB], den[NB];
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    v[b] = 0.f;
-                    if (b < B && ((act >> b) & 1)) v[b] = sh.ff.x[b][tid] + (p_bo + from_fx(ld_rlx64(ws.A(s, l, b) + tid)));
-                }
-                ln_stats<NB>(v, mean, den, sh.red);
-#pragma unroll
-                for (int b = 0; b < NB; ++b)
-                    if (b < B) sh.ff.h1[b][tid] = (v[b] - mean[b]) / den[b] * p_n1w + p_n1b;
-            }
-            __syncthreads();
-            STAMP(1);
-            // ---- FFN1 rows of this slice (4 per wave), ReLU
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                if (b >= B || !((act >> b) & 1)) continue;
-                const float4 x0 = *reinterpret_cast<const float4*>(&sh.ff.h1[b][lane * 8]);
-                const float4 x1 = *reinterpret_cast<const float4*>(&sh.ff.h1[b][lane * 8 + 4]);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float sum = wave_sum_dpp(dot8(w1r[r], x0, x1));
-                    if (lane == 0) sh.fs[b][w * 4 + r] = fmaxf(b1r[r] + sum, 0.f);
-                }
-            }
-            __syncthreads();
-            STAMP(2);
-            // ---- FFN2 split-K slice -> fixed-point hand-off
-            float w2f[4][8];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) h8_to_f8(w2r[i], w2f[i]);
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                if (b >= B || !((act >> b) & 1)) continue;
-                float r8[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) r8[k] = 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float fv = sh.fs[b][w + 8 * i];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) r8[k] += w2f[i][k] * fv;
-                }
-#pragma unroll
-                for (int k = 0; k < 8; ++k) sh.ored[w][8 * lane + k] = r8[k];
-                __syncthreads();
-                const float val = ((sh.ored[0][tid] + sh.ored[1][tid]) + (sh.ored[2][tid] + sh.ored[3][tid])) +
-                                  ((sh.ored[4][tid] + sh.ored[5][tid]) + (sh.ored[6][tid] + sh.ored[7][tid]));
-                fx_add(ws.F(s, l, b) + tid, val);
-                __syncthreads();
-            }
-            drain();
-            __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add(ws.cF(s, l), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            STAMP(3);
-            const float b2 = p_b2, n2w = p_n2w, n2b = p_n2b;
-            uint4 wp[3];
-            if (l < 23) {
-                prefetch(l + 1);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    wp[r] = ldg16(a.w_pred, (long)(lrow0 + r) * 512 + lane * 8);
-                wp[2] = ldg16(a.w_pred, (long)1024 * 512 + lane * 8);
-            }
-            // ---- x_{l+1} = LN2(h1 + b2 + Σ FFN)
-            if (!block_wait(ws.cF(s, l), NFB, a.err, 6, sh)) { alive = false; break; }
-            {
-                float v[NB], mean[NB], den[NB];
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    v[b] = 0.f;
-                    if (b < B && ((act >> b) & 1)) v[b] = sh.ff.h1[b][tid] + (b2 + from_fx(ld_rlx64(ws.F(s, l, b) + tid)));
-                }
-                ln_stats<NB>(v, mean, den, sh.red);
-#pragma unroll
-                for (int b = 0; b < NB; ++b)
-                    if (b < B) sh.ff.x[b][tid] = (v[b] - mean[b]) / den[b] * n2w + n2b;
-            }
-            __syncthreads();
-            STAMP(4);
-            if (l == 23) {
-                // ---- logits rows (ar_predict_layer, no bias), write-through stores
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    if (b >= B || !((act >> b) & 1)) continue;
-                    const float4 x0 = *reinterpret_cast<const float4*>(&sh.ff.x[b][lane * 8]);
-                    const float4 x1 = *reinterpret_cast<const float4*>(&sh.ff.x[b][lane * 8 + 4]);
-                    float* lg = ws.L(s, b);
-#pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        const float sum = wave_sum_dpp(dot8(wp[r], x0, x1));
-                        if (lane == 0) st_wt(lg + lrow0 + r, sum);
-                    }
-                    if (extra) {
-                        const float sum = wave_sum_dpp(dot8(wp[2], x0, x1));
-                        if (lane == 0) st_wt(lg + 1024, sum);
-                    }
-                }
-                drain();
-                __syncthreads();
-                if (tid == 0) __hip_atomic_fetch_add(ws.cL(s), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                prefetch(0);
-            }
-        }
-        if (!alive) break;
-        if (!poll_tokens(a, ws, s, sh)) { alive = false; break; }
     }
 }
 
 template <int NB>
 __global__ __launch_bounds__(PT) void k_decode_persist(PersistArgs a) {
     __shared__ Shared sh;
-    const Ws ws{a.accA, a.accF, a.lg, a.cnt, a.gran, a.B};
-    const int NA = 16 * a.B;
-    if ((int)blockIdx.x < NA) attn_role(a, ws, blockIdx.x & 15, blockIdx.x >> 4, sh);
-    else ffn_role<NB>(a, ws, blockIdx.x - NA, sh);
+    const Ws ws{a.ring, a.B, a.epoch};
+    const int per = 16 * a.B + NFB;
+    if ((int)(blockIdx.x % per) < 16 * a.B) run_block<true, 1>(a, ws, sh);
+    else run_block<false, NB>(a, ws, sh);
 }
 
 }  // namespace
 
-int persist_grid(int B) { return 16 * B + NFB; }
-
-size_t persist_ws_bytes(int B, int smax, size_t* zero_bytes) {
-    // [counters | granules] (zeroed) then [accA | accF] (zeroed) then logits
-    const size_t cnt = (size_t)smax * PERSIST_CNT_LINES * 128;
-    const size_t gran = (size_t)(smax + 1) * 16 * 8;
-    const size_t acc = (size_t)smax * 24 * B * 512 * 8;
-    const size_t lg = (size_t)smax * B * PERSIST_LGS * 4;
-    if (zero_bytes) *zero_bytes = cnt + gran + 2 * acc + 4;   // + error word
-    return cnt + gran + 2 * acc + 16 + lg;
+int persist_groups(int B, int n_cu) {
+    for (int g = 3; g >= 1; --g)
+        if (24 % g == 0 && g * (16 * B + NFB) <= n_cu) return g;
+    return 0;
 }
 
-void persist_bind_ws(PersistArgs& a, void* base, int B, int smax) {
-    char* p = (char*)base;
-    a.cnt = (int*)p;
-    p += (size_t)smax * PERSIST_CNT_LINES * 128;
-    a.gran = (unsigned long long*)p;
-    p += (size_t)(smax + 1) * 16 * 8;
-    a.accA = (long long*)p;
-    p += (size_t)smax * 24 * B * 512 * 8;
-    a.accF = (long long*)p;
-    p += (size_t)smax * 24 * B * 512 * 8;
-    a.err = (int*)p;
-    p += 16;
-    a.lg = (float*)p;
-    a.smax = smax;
+int persist_grid(int B, int groups) { return groups * (16 * B + NFB); }
+
+size_t persist_ring_bytes(int B) {
+    const size_t slot = (size_t)24 * B * (16 + 1 + 64 + 1) * 512 + (size_t)B * PERSIST_LGS + 16;
+    return slot * RING * 8;
 }
+
+int persist_max_tokens() { return TMAXP; }
 
 hipError_t decode_persist(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
-    const dim3 g(persist_grid(a.B)), blk(PT);
+    const dim3 g(persist_grid(a.B, a.groups)), blk(PT);
     if (a.B <= 1) hipExtLaunchKernelGGL(k_decode_persist<1>, g, blk, 0, s, start, stop, 0, a);
     else if (a.B <= 2) hipExtLaunchKernelGGL(k_decode_persist<2>, g, blk, 0, s, start, stop, 0, a);
     else if (a.B <= 4) hipExtLaunchKernelGGL(k_decode_persist<4>, g, blk, 0, s, start, stop, 0, a);

@@ -337,8 +337,9 @@ class Engine:
         _check(lib().gsv_set_option(self.h, name.encode(), int(value)), "gsv_set_option")
 
     def ptrace(self) -> np.ndarray:
-        """[256 workgroups][8 slots] realtime stamps of the persistent decode (option ptrace)."""
-        out = np.zeros((256, 8), np.uint64)
+        """[256 workgroups][16 slots] stamps of the persistent decode (option ptrace):
+        slots 0-7 the 100 MHz clock, 8-15 the shader clock at the same points."""
+        out = np.zeros((256, 16), np.uint64)
         _check(lib().gsv_debug_ptrace(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size), "gsv_debug_ptrace")
         return out
 

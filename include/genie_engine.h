@@ -181,7 +181,8 @@ int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples);
  * ORT's).  "persist": 1 (default) runs gsv_t2s_generate's decode loop as ONE
  * persistent launch (B <= 8), 0 as replayed per-step hipGraphs.  "ptrace": 1
  * allocates per-workgroup phase stamps of the persistent launch (step 8, layer 12),
- * read back with gsv_debug_ptrace ([256 workgroups][8 slots], 100 MHz).
+ * read back with gsv_debug_ptrace ([256 workgroups][16 slots]: 8 stamps of the
+ * 100 MHz clock, then the same 8 of the shader clock).
  * GSV_E_ARG for an unknown name. */
 int gsv_set_option(gsv_engine* eng, const char* name, int value);
 int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);
