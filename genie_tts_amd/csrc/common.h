@@ -39,10 +39,12 @@ __device__ __forceinline__ void fx_add(long long* p, float v) {
 // DPP wave reductions (VALU latency, no LDS crossbar): quad swaps, half-row and
 // row mirrors, then row_bcast15 / row_bcast31; lane 63 holds the result, read
 // back as a wave-uniform value.
+// mov_dpp with bound_ctrl: the compiler folds it into the consuming VALU op
+// (v_add_f32_dpp ...), one instruction per reduction step instead of three.
+// Lanes of rows outside ROW_MASK are undefined: callers read lane 63 only.
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROW_MASK,
-                                                      0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, ROW_MASK, 0xF, true));
 }
 template <typename Op>
 __device__ __forceinline__ float wave_reduce_dpp(float v, Op op) {

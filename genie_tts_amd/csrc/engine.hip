@@ -641,7 +641,6 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
     a.err = perr;
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
-    a.trace_rep = std::getenv("GENIE_TRACE_REP") ? 1 : 0;
     hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;
     if (decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr) != hipSuccess)

@@ -210,7 +210,6 @@ struct PersistArgs {
     int smax;                                     // step cap of the launch
     int groups;                                   // layer groups (layer l -> group l % groups)
     unsigned long long* trace;                    // optional [grid][16] phase stamps (step 8, layer 12)
-    int trace_rep;                                // probe only: run the probed QKV twice
 };
 int persist_groups(int B, int n_cu);   // 0: the grid does not fit
 int persist_grid(int B, int groups);

@@ -102,7 +102,38 @@ __device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err,
         }
     }
 }
-__device__ __forceinline__ bool block_ok(bool ok) { return !__syncthreads_or(ok ? 0 : 1); }
+
+// One lane waits for N granules p + k*stride (k < N), all N loads in flight at
+// once; re-polls only the ones whose tag is still stale.
+template <int N>
+__device__ __forceinline__ void wait_gran_n(const u64* p, long stride, unsigned tag, float (&out)[N], int* err,
+                                            bool& ok) {
+    u64 g[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) g[k] = ld_rlxu64(p + k * stride);
+    unsigned long long t0 = 0;
+    for (unsigned it = 0;; ++it) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < N; ++k) all &= (unsigned)(g[k] >> 32) == tag;
+        if (all) break;
+        if (it == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if ((unsigned)(g[k] >> 32) != tag) g[k] = ld_rlxu64(p + k * stride);
+        if ((it & 63) == 63) {
+            if (ld_rlx(err) != 0) { ok = false; break; }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+                atomicCAS(err, 0, 1);
+                ok = false;
+                break;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = __uint_as_float((unsigned)g[k]);
+}
 
 // Ring of step slots of granules (u64).  Per slot: PA [24][B][16][512],
 // RA [24][B][512], PF [24][B][64][512], RF [24][B][512], LG [B][1056], TK [16].
@@ -143,63 +174,43 @@ __device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
     for (int q = 0; q < N; ++q) v[q] += dpp_f<0x143, 0xC>(v[q]);
 }
 
-// LayerNorm statistics of NB rows of 512 values, one value per thread per row:
-// Chan et al. pairwise (mean, M2) merges -- butterflies on the DPP path inside
-// 16-lane rows, the 4 rows of a wave and the 8 waves on uniform values.
+// LayerNorm of NB rows of 512 values, one value per thread per row, as the graph
+// computes it (LayerNormalization: mean, then mean of squared deviations):
+// DPP wave sums (folded into v_add_f32_dpp), one LDS exchange per pass.
 template <int NB>
 __device__ __forceinline__ void ln_stats(const float (&v)[NB], float (&mean)[NB], float (&den)[NB], float* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float mu[NB], m2[NB];
+    float t[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) { mu[b] = v[b]; m2[b] = 0.f; }
-    auto merge = [&](float& a_mu, float& a_m2, float o_mu, float o_m2, float n) {   // equal counts n
-        const float dl = o_mu - a_mu;
-        a_m2 = a_m2 + o_m2 + dl * dl * (n * 0.5f);
-        a_mu = a_mu + dl * 0.5f;
-    };
-#define LN_STEP(CTRL, N)                                                                     \
-    _Pragma("unroll") for (int b = 0; b < NB; ++b) {                                         \
-        const float om = dpp_f<CTRL, 0xF>(mu[b]), o2 = dpp_f<CTRL, 0xF>(m2[b]);              \
-        merge(mu[b], m2[b], om, o2, N);                                                      \
-    }
-    LN_STEP(0xB1, 1.f)
-    LN_STEP(0x4E, 2.f)
-    LN_STEP(0x141, 4.f)
-    LN_STEP(0x140, 8.f)
-#undef LN_STEP
+    for (int b = 0; b < NB; ++b) t[b] = v[b];
+    wave_sum_n<NB>(t);
+    if (lane == 63) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        // rows 0..3 of the wave (16 values each), merged on uniform values
-        float r_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 0));
-        float r_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 0));
-        float r1_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 16));
-        float r1_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 16));
-        float r2_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 32));
-        float r2_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 32));
-        float r3_mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mu[b]), 48));
-        float r3_m2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m2[b]), 48));
-        merge(r_mu, r_m2, r1_mu, r1_m2, 16.f);
-        merge(r2_mu, r2_m2, r3_mu, r3_m2, 16.f);
-        merge(r_mu, r_m2, r2_mu, r2_m2, 32.f);
-        if (lane == 0) { red[(w * NB + b) * 2] = r_mu; red[(w * NB + b) * 2 + 1] = r_m2; }
+        for (int b = 0; b < NB; ++b) red[w * NB + b] = t[b];
     }
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        float a_mu[PWV], a_m2[PWV];
+        float s0 = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < PWV; ++ww) { a_mu[ww] = red[(ww * NB + b) * 2]; a_m2[ww] = red[(ww * NB + b) * 2 + 1]; }
-        merge(a_mu[0], a_m2[0], a_mu[1], a_m2[1], 64.f);
-        merge(a_mu[2], a_m2[2], a_mu[3], a_m2[3], 64.f);
-        merge(a_mu[4], a_m2[4], a_mu[5], a_m2[5], 64.f);
-        merge(a_mu[6], a_m2[6], a_mu[7], a_m2[7], 64.f);
-        merge(a_mu[0], a_m2[0], a_mu[2], a_m2[2], 128.f);
-        merge(a_mu[4], a_m2[4], a_mu[6], a_m2[6], 128.f);
-        merge(a_mu[0], a_m2[0], a_mu[4], a_m2[4], 256.f);
-        mean[b] = a_mu[0];
-        den[b] = sqrtf(a_m2[0] * (1.0f / 512.0f) + 1e-5f);
+        for (int ww = 0; ww < PWV; ++ww) s0 += red[ww * NB + b];
+        mean[b] = s0 * (1.0f / 512.0f);
+        const float d = v[b] - mean[b];
+        t[b] = d * d;
     }
-    __syncthreads();   // red reusable
+    wave_sum_n<NB>(t);
+    if (lane == 63) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) red[PWV * NB + w * NB + b] = t[b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        float s1 = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < PWV; ++ww) s1 += red[PWV * NB + ww * NB + b];
+        den[b] = sqrtf(s1 * (1.0f / 512.0f) + 1e-5f);
+    }
 }
 
 __device__ __forceinline__ float dot8(const uint4 w, const float4 x0, const float4 x1) {
@@ -227,7 +238,6 @@ struct Shared {
             float x[8][512];        // x_l per sequence
             float h1[8][512];       // LN1 output per sequence
             __half w2[32 * 512];    // W2^T rows of the slice (LDS-DMA)
-            float ra[8][16][8];     // reduce-A operands
             float rf[64][8];        // reduce-F operands
         } ff;
     };
@@ -235,6 +245,7 @@ struct Shared {
     float os[32];
     float fs[8][32];
     float red[2 * PWV * 8];
+    int fail;                       // set once by any thread whose hand-off failed
     float wred[2][PWV];
     uint32_t seen[33];
     int tok[8];
@@ -253,6 +264,13 @@ struct Shared {
             sh.stamp[8 + (i)] = __builtin_amdgcn_s_memtime();                             \
         }                                                                                 \
     } while (0)
+
+// Block-wide "every hand-off of this phase arrived": one barrier; a failure is sticky.
+__device__ __forceinline__ bool block_ok(bool ok, Shared& sh) {
+    if (!ok) sh.fail = 1;
+    __syncthreads();
+    return sh.fail == 0;
+}
 
 // Token granules of step s+1 for every sequence active in step s: new tokens and
 // the active set.  Block-uniform result; false on error.
@@ -297,7 +315,7 @@ __device__ __forceinline__ bool track_ln(GranF gran, unsigned tag, const float* 
         v[i] = 0.f;
         if (i < nb && ((act >> (b0 + i)) & 1)) v[i] = res[i * 512 + tid] + (bias + wait_gran(gran(b0 + i) + tid, tag, err, ok));
     }
-    if (!block_ok(ok)) return false;
+    if (!block_ok(ok, sh)) return false;
     ln_stats<NB>(v, mean, den, sh.red);
 #pragma unroll
     for (int i = 0; i < NB; ++i)
@@ -333,24 +351,28 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
             sh.tok[bb] = (int)a.y[(long)bb * a.ldy + a.ny[bb] - 1];
         }
         sh.act = act;
+        sh.fail = 0;
     }
     __syncthreads();
     const long kvoff = (long)ab * a.sstride + (long)h * a.tmax * 32;
     uint4 wq[12];
-    float bqv = 0.f;
+    float bq[3] = {0.f, 0.f, 0.f};
     uint4 w1r[4], wp[3];
     float b1r[4];
     auto prefetch = [&](int l, int kv) {   // this workgroup's operands of layer l
         const PLayer& P = a.L[l];
         if constexpr (ATTN) {
-            // wave w: q, k and v rows h*32 + 4w + q (q < 4) -- 1 KB apart, immediate offsets
-            const __half* wb = P.w_in + (long)(h * 32 + 4 * w) * 512;
+            // wave w, lane group r4 = lane >> 4: rows (m, h*32 + 4w + r4) of W_in for m = q, k, v;
+            // lane i16 = lane & 15 holds columns 8*i16 + 128*c (c < 4) of each: a row is reduced
+            // over 16 lanes (4 DPP steps, no cross-row broadcast)
+            const int r4 = lane >> 4, i16 = lane & 15;
+            const __half* wb = P.w_in + (long)(h * 32 + 4 * w + r4) * 512 + 8 * i16;
 #pragma unroll
             for (int m = 0; m < 3; ++m)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) wq[m * 4 + q] = ldg16(wb + (long)m * 512 * 512 + q * 512, lane * 8);
-            // lane m*4+q (< 12) holds the bias of row (m, q)
-            bqv = lane < 12 ? ldg(P.b_in, (lane >> 2) * 512 + h * 32 + 4 * w + (lane & 3)) : 0.f;
+                for (int c = 0; c < 4; ++c) wq[m * 4 + c] = ldg16(wb + (long)m * 512 * 512 + c * 128, 0);
+#pragma unroll
+            for (int m = 0; m < 3; ++m) bq[m] = ldg(P.b_in, m * 512 + h * 32 + 4 * w + r4);
             // WoT rows h*32 .. h*32+31 (contiguous 32 KB) -> LDS, one 1 KB row per wave instruction
             const __half* ob = P.woT + (long)(h * 32 + 4 * w) * 512;
 #pragma unroll
@@ -414,56 +436,71 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
             __syncthreads();
             STAMP(1);
             if constexpr (ATTN) if (mine) {
-                // ---- q, k, v of head h: 12 independent dot products per wave, reduced together
-                for (int rep = 0; rep < (probe && a.trace_rep ? 2 : 1); ++rep) {
-                    if (rep == 1) { __syncthreads(); STAMP(7); }
-                    const float4 x0 = *reinterpret_cast<const float4*>(&X[lane * 8]);
-                    const float4 x1 = *reinterpret_cast<const float4*>(&X[lane * 8 + 4]);
-                    float acc[12];
+                // ---- q, k, v of head h: 3 rows per lane group, 16 lanes per row
+                {
+                    const int r4 = lane >> 4, i16 = lane & 15;
+                    float acc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int q = 0; q < 12; ++q) acc[q] = dot8(wq[q], x0, x1);
-                    wave_sum_n<12>(acc);
-                    float mv = 0.f;
+                    for (int c = 0; c < 4; ++c) {
+                        const float4 x0 = *reinterpret_cast<const float4*>(&X[8 * i16 + 128 * c]);
+                        const float4 x1 = *reinterpret_cast<const float4*>(&X[8 * i16 + 128 * c + 4]);
 #pragma unroll
-                    for (int q = 0; q < 12; ++q) {
-                        const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[q]), 63));
-                        mv = lane == q ? t : mv;
+                        for (int m = 0; m < 3; ++m) acc[m] += dot8(wq[m * 4 + c], x0, x1);
                     }
-                    if (lane < 12) sh.qkv[(lane >> 2) * 32 + 4 * w + (lane & 3)] = bqv + mv;
-                    if (rep == 0 && probe && a.trace_rep) { __syncthreads(); STAMP(6); }
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0xB1, 0xF>(acc[m]);
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x4E, 0xF>(acc[m]);
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x141, 0xF>(acc[m]);
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x140, 0xF>(acc[m]);
+                    if (i16 == 0) {
+#pragma unroll
+                        for (int m = 0; m < 3; ++m) sh.qkv[m * 32 + 4 * w + r4] = bq[m] + acc[m];
+                    }
                 }
                 __syncthreads();
                 STAMP(2);
-                // ---- scores (q*s)·(k*s) over [0, kv]: keys t = pass*512 + tid
+                // ---- scores (q*s)·(k*s) over [0, kv]: 8 lanes per key row (16 B each, conflict-free
+                // LDS reads), keys t = base + 64 u + g
                 float* Kw = a.kc[l] + kvoff;
                 float* Vw = a.vc[l] + kvoff;
                 const float sc = a.scale;
                 const int T = kv + 1;
+                const int c8 = lane & 7, g = (w << 3) | (lane >> 3);
+                const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
+                const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
                 float lmax = -INFINITY;
-                for (int t = tid; t < T; t += PT) {
-                    float4 kr[8];
-                    if (t < kv && t < KVL) {
+                for (int base = 0; base < T; base += 512) {
+                    float sv[8];
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) kr[i] = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * i);
-                    } else if (t < kv) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) kr[i] = ldg16f(Kw, (long)t * 32 + 4 * i);
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) kr[i] = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * i);
+                    for (int u = 0; u < 8; ++u) {
+                        const int t = base + 64 * u + g;
+                        float4 kr;
+                        if (t < kv && t < KVL) kr = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * c8);
+                        else if (t < kv) kr = ldg16f(Kw, (long)t * 32 + 4 * c8);
+                        else kr = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
+                        float x = q0 * (kr.x * sc);
+                        x += q1 * (kr.y * sc);
+                        x += q2 * (kr.z * sc);
+                        x += q3 * (kr.w * sc);
+                        sv[u] = x;
                     }
-                    float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const float4 qd = *reinterpret_cast<const float4*>(sh.qkv + 4 * i);
-                        part[i & 3] += (qd.x * sc) * (kr[i].x * sc);
-                        part[i & 3] += (qd.y * sc) * (kr[i].y * sc);
-                        part[i & 3] += (qd.z * sc) * (kr[i].z * sc);
-                        part[i & 3] += (qd.w * sc) * (kr[i].w * sc);
+                    for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int t = base + 64 * u + g;
+                        if (t < T) {
+                            if (c8 == 0) sh.at.p[t] = sv[u];
+                            lmax = fmaxf(lmax, sv[u]);
+                        }
                     }
-                    const float sv = (part[0] + part[1]) + (part[2] + part[3]);
-                    sh.at.p[t] = sv;
-                    lmax = fmaxf(lmax, sv);
                 }
                 const float wm = wave_max_dpp(lmax);
                 if (lane == 0) sh.wred[0][w] = wm;
@@ -481,16 +518,20 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 if (lane == 0) sh.wred[1][w] = ws_;
                 __syncthreads();
                 STAMP(3);
-                // ---- P·V: 16 key groups x 32 dims
+                // ---- P·V: 16 key groups x 32 dims; LDS rows unrolled by 4 with independent sums
                 {
                     const int kg = tid >> 5, d = tid & 31;
-                    float o = 0.f;
-                    for (int t = kg; t < T; t += 16) {
-                        const float vv = t < kv ? (t < KVL ? sh.at.v[t * 32 + d] : ldg(Vw, (long)t * 32 + d))
-                                                : sh.qkv[64 + d];
-                        o += sh.at.p[t] * vv;
+                    const int tl = min(kv, KVL);
+                    float o4[4] = {0.f, 0.f, 0.f, 0.f};
+                    int t = kg;
+                    for (; t + 48 < tl; t += 64) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) o4[u] += sh.at.p[t + 16 * u] * sh.at.v[(t + 16 * u) * 32 + d];
                     }
-                    sh.at.ov[kg][d] = o;
+                    for (; t < tl; t += 16) o4[0] += sh.at.p[t] * sh.at.v[t * 32 + d];
+                    for (; t < kv; t += 16) o4[1] += sh.at.p[t] * ldg(Vw, (long)t * 32 + d);
+                    if (t == kv) o4[2] += sh.at.p[t] * sh.qkv[64 + d];
+                    sh.at.ov[kg][d] = (o4[0] + o4[1]) + (o4[2] + o4[3]);
                 }
                 __syncthreads();
                 if (tid < 32) {
@@ -519,30 +560,36 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 if (l + G < 24) prefetch(l + G, kv);
                 else prefetch(l + G - 24, kv + 1);
             }
-            if constexpr (!ATTN) if (mine) {
-                // ---- reduce-A: columns [8j, 8j+8) of Σ_h PA, fixed order
+            // ---- h1_l = LN1(x_l + bo + Σ_h attention partials)
+            if (!ATTN && mine) {
+                // owner FFN workgroups sum the 16 head partials of every column themselves
+                // (fixed order, one hop), and publish the sums of their 8 columns (RA) for
+                // every other workgroup that tracks the residual stream
                 bool ok = true;
-                if (tid < 128) {
-                    const int hh = tid >> 3, c = tid & 7;
+                float v[NB], mean[NB], den[NB];
 #pragma unroll
-                    for (int i = 0; i < NB; ++i)
-                        if (i < nb && ((act >> i) & 1))
-                            sh.ff.ra[i][hh][c] = wait_gran(ws.PA(s, l, i, hh) + 8 * j + c, tag, a.err, ok);
-                }
-                if (!block_ok(ok)) return;
-                if (tid < 8 * NB) {
-                    const int i = tid >> 3, c = tid & 7;
+                for (int i = 0; i < NB; ++i) {
+                    v[i] = 0.f;
                     if (i < nb && ((act >> i) & 1)) {
+                        float pa[16];
+                        wait_gran_n<16>(ws.PA(s, l, i, 0) + tid, 512, tag, pa, a.err, ok);
                         float sum = 0.f;
 #pragma unroll
-                        for (int hh = 0; hh < 16; ++hh) sum += sh.ff.ra[i][hh][c];
-                        st_gran(ws.RA(s, l, i) + 8 * j + c, tag, sum);
+                        for (int hh = 0; hh < 16; ++hh) sum += pa[hh];
+                        if ((tid >> 3) == j) st_gran(ws.RA(s, l, i) + tid, tag, sum);
+                        v[i] = X[i * 512 + tid] + (lp.bo + sum);
                     }
                 }
+                if (!block_ok(ok, sh)) return;
                 STAMP(2);
-            }
-            // ---- h1_l = LN1(x_l + bo + RA_l)  (not needed after layer 23 unless this workgroup computes the logits)
-            if (l < 23 || logits_grp) {
+                ln_stats<NB>(v, mean, den, sh.red);
+#pragma unroll
+                for (int i = 0; i < NB; ++i)
+                    if (i < nb) H1[i * 512 + tid] = (v[i] - mean[i]) / den[i] * lp.n1w + lp.n1b;
+                __syncthreads();
+                STAMP(6);
+            } else if (l < 23 || logits_grp) {
+                // (not needed after layer 23 unless this workgroup computes the logits)
                 if (!track_ln<NB>([&](int b) { return ws.RA(s, l, b); }, tag, X, H1, b0, nb, act, lp.bo, lp.n1w,
                                   lp.n1b, a.err, sh))
                     return;
@@ -593,11 +640,12 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                         if (i >= nb || !((act >> i) & 1)) continue;
                         bool ok = true;
                         sh.ff.rf[jj][c] = wait_gran(ws.PF(s, l, i, jj) + 8 * j + c, tag, a.err, ok);
-                        if (!block_ok(ok)) return;
+                        if (!block_ok(ok, sh)) return;
                         if (tid < 8) {
-                            float sum = 0.f;
-#pragma unroll 16
-                            for (int q = 0; q < 64; ++q) sum += sh.ff.rf[q][tid];
+                            float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                            for (int q = 0; q < 64; ++q) s4[q & 3] += sh.ff.rf[q][tid];
+                            const float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
                             st_gran(ws.RF(s, l, i) + 8 * j + tid, tag, sum);
                         }
                         __syncthreads();
@@ -641,7 +689,7 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
             bool ok = true;
             const u64* lgg = ws.LG(s, ab);
             for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok);
-            if (!block_ok(ok)) return;
+            if (!block_ok(ok, sh)) return;
             const int st = st0 + s;                 // loop steps already executed
             int raw = 0;
             const int tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, ab, st + 1, a.top_k,

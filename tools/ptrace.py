@@ -1,9 +1,10 @@
 """Phase timeline of the persistent decode launch (step 8, layer 12), option ptrace.
 
-Group 0 (owns layer 12).  attention workgroups (0..15): 0 cF(l-1) seen, 1 x_l ready,
-5 qkv ready, 6 attention loop done, 2 attention merged, 3 accA published, 4 h1 ready.
-FFN workgroups (16..79): 0 cF(l-1) seen, 1 x_l ready, 4 h1 ready (cA seen + LN1),
-5 FFN1 done, 6 accF published.  Microseconds from the first stamp."""
+Group 0 (owns layer 12).  attention workgroups (0..15): 0 before the x_l wait, 1 x_l
+ready, 2 q/k/v ready, 3 softmax numerators ready, 4 head output ready, 5 partials
+published, 6 h1 ready.  FFN workgroups (16..79): 0 before the x_l wait, 1 x_l ready,
+2 head partials summed, 6 h1 ready, 3 FFN1 done, 4 FFN2 partials published,
+5 reduce-F published.  Microseconds from the first stamp."""
 import sys
 sys.path.insert(0, ".")
 import numpy as np
