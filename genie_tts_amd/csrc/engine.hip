@@ -627,7 +627,7 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
     if (const char* e = std::getenv("GENIE_PERSIST_GROUPS")) a.groups = std::max(1, std::min(a.groups, std::atoi(e)));
     for (int l = 0; l < 24; ++l) {
         const T2SLayerW& W = layers[l];
-        a.L[l] = PLayer{W.w_in, W.woT, W.w1, W.w2T, W.b_in, W.b_out, W.b1, W.b2, W.n1w, W.n1b, W.n2w, W.n2b};
+        a.L[l] = PLayer{W.w_in, W.w_out, W.w1, W.w2, W.b_in, W.b_out, W.b1, W.b2, W.n1w, W.n1b, W.n2w, W.n2b};
     }
     a.emb = emb_audio; a.alpha = alpha_audio; a.pe = pe_tab; a.w_pred = w_pred;
     for (int l = 0; l < 24; ++l) { a.kc[l] = kcache[l]; a.vc[l] = vcache[l]; }

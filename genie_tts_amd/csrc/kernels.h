@@ -192,7 +192,7 @@ void seq_state_init(int b, const int64_t* prompts, int P, int L, int64_t* y, lon
 // Persistent decode (t2s_persist.hip): the whole AR loop in one launch.
 // ---------------------------------------------------------------------------
 struct PLayer {
-    const __half *w_in, *woT, *w1, *w2T;
+    const __half *w_in, *w_out, *w1, *w2;   // fp16, the graph's [out][in] layouts
     const float *b_in, *b_out, *b1, *b2, *n1w, *n1b, *n2w, *n2b;
 };
 constexpr int PERSIST_LGS = 1056;       // logits granule row stride (128-B multiple)

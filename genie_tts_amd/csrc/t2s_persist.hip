@@ -227,7 +227,6 @@ struct Shared {
         struct {                    // attention role
             float k[KVL * 32];      // K/V rows [0, min(kv, KVL)) of the head (LDS-DMA)
             float v[KVL * 32];
-            __half wo[32 * 512];    // WoT rows of the head (LDS-DMA)
             float p[TMAXP];         // scores, then softmax numerators
             float x[512];           // x_l of the sequence
             float h1[512];          // LN1 output of the sequence
@@ -237,7 +236,6 @@ struct Shared {
         struct {                    // FFN role
             float x[8][512];        // x_l per sequence
             float h1[8][512];       // LN1 output per sequence
-            __half w2[32 * 512];    // W2^T rows of the slice (LDS-DMA)
             float rf[64][8];        // reduce-F operands
         } ff;
     };
@@ -355,9 +353,9 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
     }
     __syncthreads();
     const long kvoff = (long)ab * a.sstride + (long)h * a.tmax * 32;
-    uint4 wq[12];
+    uint4 wq[12], wo[4];
     float bq[3] = {0.f, 0.f, 0.f};
-    uint4 w1r[4], wp[3];
+    uint4 w1r[4], w2r[4], wp[3];
     float b1r[4];
     auto prefetch = [&](int l, int kv) {   // this workgroup's operands of layer l
         const PLayer& P = a.L[l];
@@ -373,11 +371,9 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 for (int c = 0; c < 4; ++c) wq[m * 4 + c] = ldg16(wb + (long)m * 512 * 512 + c * 128, 0);
 #pragma unroll
             for (int m = 0; m < 3; ++m) bq[m] = ldg(P.b_in, m * 512 + h * 32 + 4 * w + r4);
-            // WoT rows h*32 .. h*32+31 (contiguous 32 KB) -> LDS, one 1 KB row per wave instruction
-            const __half* ob = P.woT + (long)(h * 32 + 4 * w) * 512;
+            // out-projection: thread tid owns output column tid, W_out[tid][h*32 .. h*32+32)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                __builtin_amdgcn_global_load_lds(ob + i * 512 + lane * 8, sh.at.wo + (4 * w + i) * 512, 16, 0, 0);
+            for (int k = 0; k < 4; ++k) wo[k] = ldg16(P.w_out + (long)tid * 512 + h * 32 + 8 * k, 0);
             // K/V rows [0, min(kv, KVL)) -> LDS, 8 rows (1 KB) per wave instruction.  Rows of the
             // last chunk past kv are read (allocated: tmax >= kv + 16) and never used.
             const float* K = a.kc[l] + kvoff;
@@ -392,10 +388,9 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
             for (int q = 0; q < 4; ++q) w1r[q] = ldg16(P.w1 + (long)(j * 32 + w * 4 + q) * 512, lane * 8);
 #pragma unroll
             for (int q = 0; q < 4; ++q) b1r[q] = ldg(P.b1, j * 32 + w * 4 + q);
-            const __half* w2b = P.w2T + (long)(j * 32 + 4 * w) * 512;
+            // FFN2: thread tid owns output column tid, W2[tid][j*32 .. j*32+32)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                __builtin_amdgcn_global_load_lds(w2b + i * 512 + lane * 8, sh.ff.w2 + (4 * w + i) * 512, 16, 0, 0);
+            for (int k = 0; k < 4; ++k) w2r[k] = ldg16(P.w2 + (long)tid * 2048 + j * 32 + 8 * k, 0);
         }
     };
     // logits rows (logits group): 2 per wave, + row 1024 on the last FFN workgroup's wave 0
@@ -548,7 +543,11 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 {
                     float acc = 0.f;
 #pragma unroll
-                    for (int d = 0; d < 32; ++d) acc += __half2float(sh.at.wo[d * 512 + tid]) * sh.os[d];
+                    for (int k = 0; k < 4; ++k) {
+                        const float4 oa = *reinterpret_cast<const float4*>(sh.os + 8 * k);
+                        const float4 ob = *reinterpret_cast<const float4*>(sh.os + 8 * k + 4);
+                        acc += dot8(wo[k], oa, ob);
+                    }
                     st_gran(ws.PA(s, l, ab, h) + tid, tag, acc);
                     // the new K/V row (read by this workgroup only, next step)
                     if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
@@ -618,18 +617,18 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 STAMP(3);
                 // ---- FFN2 slice (column tid) -> partial granules
                 {
-                    float acc[NB];
 #pragma unroll
-                    for (int i = 0; i < NB; ++i) acc[i] = 0.f;
-#pragma unroll 8
-                    for (int q = 0; q < 32; ++q) {
-                        const float wv = __half2float(sh.ff.w2[q * 512 + tid]);
+                    for (int i = 0; i < NB; ++i) {
+                        if (i >= nb || !((act >> i) & 1)) continue;
+                        float acc = 0.f;
 #pragma unroll
-                        for (int i = 0; i < NB; ++i) acc[i] += wv * sh.fs[i][q];
+                        for (int k = 0; k < 4; ++k) {
+                            const float4 fa = *reinterpret_cast<const float4*>(&sh.fs[i][8 * k]);
+                            const float4 fb = *reinterpret_cast<const float4*>(&sh.fs[i][8 * k + 4]);
+                            acc += dot8(w2r[k], fa, fb);
+                        }
+                        st_gran(ws.PF(s, l, i, j) + tid, tag, acc);
                     }
-#pragma unroll
-                    for (int i = 0; i < NB; ++i)
-                        if (i < nb && ((act >> i) & 1)) st_gran(ws.PF(s, l, i, j) + tid, tag, acc[i]);
                 }
                 STAMP(4);
                 // ---- reduce-F: columns [8j, 8j+8) of Σ_j' PF, fixed order

@@ -20,10 +20,15 @@ for rep in range(3):
     e.t2s_generate([(ref, txt, None, None, ssl)], make_sampler(force_steps=81))
 print("decode ms", e.timing()[2], "kernel us", e.kernel_timing())
 tr = e.ptrace().astype(np.int64)
-rt, ck = tr[:16, 1], tr[:16, 9]
-rt2, ck2 = tr[:16, 2], tr[:16, 10]
-print("shader clock MHz (attention, stamp 1->2):", np.median((ck2 - ck) / ((rt2 - rt) * 10e-3)))
-att, ffn = tr[:16, :8], tr[16:80, :8]
+# owners of the probed layer: attention workgroups stamp q/k/v (slot 2) and the FFN owners FFN1 (slot 3)
+per = 16 + 64   # B=1: 16 attention + 64 FFN workgroups per layer group
+grp = [g for g in range(256 // per) if (tr[g * per:(g + 1) * per, :8] > 0).any()]
+G = len(grp)
+og = 12 % G
+att, ffn = tr[og * per:og * per + 16, :8], tr[og * per + 16:(og + 1) * per, :8]
+ck = tr[og * per:og * per + 16, 8:16]
+print(f"groups {G}, owner group {og}")
+print("shader clock MHz (attention, stamp 1->2):", np.median((ck[:, 2] - ck[:, 1]) / ((att[:, 2] - att[:, 1]) * 10e-3)))
 t0 = att[:, 0].min()
 for nm, t in (("attn", att), ("ffn", ffn)):
     t = (t - t0) * 10 / 1000.0
