@@ -321,6 +321,52 @@ __device__ __forceinline__ bool track_ln(GranF gran, unsigned tag, const float* 
     return true;
 }
 
+// Scores of the general case (more than 512 keys or rows beyond the LDS stage),
+// out of line so the common path keeps its registers.  Returns the lane's max.
+__device__ __noinline__ float scores_general(Shared& sh, const float* Kw, int kv, int T, float q0, float q1, float q2,
+                                             float q3, float sc, float4 knew, int c8, int g) {
+    float lmax = -INFINITY;
+    for (int base = 0; base < T; base += 512) {
+        float sv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = base + 64 * u + g;
+            float4 kr;
+            if (t < kv && t < KVL) kr = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * c8);
+            else if (t < kv) kr = ldg16f(Kw, (long)t * 32 + 4 * c8);
+            else kr = knew;
+            float x = q0 * (kr.x * sc);
+            x += q1 * (kr.y * sc);
+            x += q2 * (kr.z * sc);
+            x += q3 * (kr.w * sc);
+            sv[u] = x;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = base + 64 * u + g;
+            if (t < T) {
+                if (c8 == 0) sh.at.p[t] = sv[u];
+                lmax = fmaxf(lmax, sv[u]);
+            }
+        }
+    }
+    return lmax;
+}
+
+// The sampler body (sampler.h) out of line: it runs once per step and would
+// otherwise share the register allocation of the decode loop.
+__device__ __forceinline__ int run_sampler(Shared& sh, int b, int step, int top_k, float temperature, float rep_penalty,
+                                        int greedy, uint64_t seed, int* raw) {
+    return sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, b, step, top_k, temperature, rep_penalty,
+                            greedy, seed, 0, nullptr, raw, sh.samp);
+}
+
 // --------------------------------------------------------------------------
 // One workgroup of role ATTN (head h, sequence ab) or FFN (slice j, NB >= B).
 // --------------------------------------------------------------------------
@@ -467,35 +513,42 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
                 const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
                 float lmax = -INFINITY;
-                for (int base = 0; base < T; base += 512) {
-                    float sv[8];
+                const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
+                if (T <= 512 && kv <= KVL) {
+                    // common case, branch-free: every cached row is in LDS, 8 keys per lane in two halves
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int t = base + 64 * u + g;
-                        float4 kr;
-                        if (t < kv && t < KVL) kr = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * c8);
-                        else if (t < kv) kr = ldg16f(Kw, (long)t * 32 + 4 * c8);
-                        else kr = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
-                        float x = q0 * (kr.x * sc);
-                        x += q1 * (kr.y * sc);
-                        x += q2 * (kr.z * sc);
-                        x += q3 * (kr.w * sc);
-                        sv[u] = x;
-                    }
+                    for (int hf = 0; hf < 2; ++hf) {
+                        float sv[4];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+                        for (int u = 0; u < 4; ++u) {
+                            const int t = 64 * (4 * hf + u) + g;
+                            float4 kr = *reinterpret_cast<const float4*>(sh.at.k + min(t, KVL - 1) * 32 + 4 * c8);
+                            if (t == kv) { kr.x = knew.x; kr.y = knew.y; kr.z = knew.z; kr.w = knew.w; }
+                            float x = q0 * (kr.x * sc);
+                            x += q1 * (kr.y * sc);
+                            x += q2 * (kr.z * sc);
+                            x += q3 * (kr.w * sc);
+                            sv[u] = x;
+                        }
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+                        for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+                        for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int t = base + 64 * u + g;
-                        if (t < T) {
-                            if (c8 == 0) sh.at.p[t] = sv[u];
+                        for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int t = 64 * (4 * hf + u) + g;
+                            sv[u] = t < T ? sv[u] : -INFINITY;
                             lmax = fmaxf(lmax, sv[u]);
                         }
+                        if (c8 == 0) {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) sh.at.p[64 * (4 * hf + u) + g] = sv[u];   // p[t >= T] is never read
+                        }
                     }
+                } else {
+                    lmax = scores_general(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
                 }
                 const float wm = wave_max_dpp(lmax);
                 if (lane == 0) sh.wred[0][w] = wm;
@@ -556,8 +609,7 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 STAMP(5);
                 __syncthreads();   // LDS operands consumed before the next layer's LDS-DMA lands
                 // ---- next layer of this group (or of the next step) while the others work
-                if (l + G < 24) prefetch(l + G, kv);
-                else prefetch(l + G - 24, kv + 1);
+                prefetch(l + G < 24 ? l + G : l + G - 24, l + G < 24 ? kv : kv + 1);
             }
             // ---- h1_l = LN1(x_l + bo + Σ_h attention partials)
             if (!ATTN && mine) {
@@ -656,8 +708,7 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                     for (int q = 0; q < 2; ++q) wp[q] = ldg16(a.w_pred + (long)(lrow0 + q) * 512, lane * 8);
                     wp[2] = ldg16(a.w_pred + (long)1024 * 512, lane * 8);
                 }
-                if (l + G < 24) prefetch(l + G, 0);
-                else prefetch(l + G - 24, 0);
+                prefetch(l + G < 24 ? l + G : l + G - 24, 0);
             }
         }
         if (logits_grp) {
@@ -691,9 +742,7 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
             if (!block_ok(ok, sh)) return;
             const int st = st0 + s;                 // loop steps already executed
             int raw = 0;
-            const int tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, ab, st + 1, a.top_k,
-                                             a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw,
-                                             sh.samp);
+            const int tok = run_sampler(sh, ab, st + 1, a.top_k, a.temperature, a.rep_penalty, a.greedy, a.seed, &raw);
             if (tid == 0) {
                 a.y[(long)ab * a.ldy + ny0[0] + s] = tok;
                 sh.seen[tok >> 5] |= 1u << (tok & 31);
