@@ -128,6 +128,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_DECODE_FUSE")) fuse_qkv = std::atoi(e) == 2;
     if (const char* e = std::getenv("GENIE_ACC")) use_acc = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST")) use_persist = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_PERSIST1")) use_persist1 = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_KTRACE"))
         if (std::atoi(e) == 1 && !ktrace) {
             hipMalloc(&ktrace, (size_t)3 * 256 * 8 * 8);
@@ -601,8 +602,10 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
     // without zeroing (re-zeroed when the epoch wraps or the layout changes).
     const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     if (tmax > persist_max_tokens()) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
-    const size_t need = persist_ring_bytes(B);
-    if (need > pws_bytes || B != pws_batch) {
+    const bool one = B == 1 && use_persist1 && n_cu >= persist1_grid();
+    const size_t need = one ? persist1_ring_bytes() : persist_ring_bytes(B);
+    const int layout = one ? -1 : B;   // ring layout key: the two kernels slot the ring differently
+    if (need > pws_bytes || layout != pws_batch) {
         if (need > pws_bytes) {
             if (pws) hipFree(pws);
             pws = nullptr;
@@ -611,7 +614,7 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
             pws_bytes = need;
         }
         hipMemsetAsync(pws, 0, pws_bytes, st);
-        pws_batch = B;
+        pws_batch = layout;
         pepoch = 0;
     }
     if (++pepoch >= (1u << 20)) {
@@ -643,7 +646,9 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
     a.trace = ptrace;
     hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;
-    if (decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr) != hipSuccess)
+    const hipError_t le = one ? decode_persist1(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr)
+                              : decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr);
+    if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
@@ -932,6 +937,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     const std::string n(name);
     if (n == "persist") {
         eng->use_persist = value != 0;
+    } else if (n == "persist1") {
+        eng->use_persist1 = value != 0;
     } else if (n == "ptrace") {
         if (value && !eng->ptrace) {
             if (hipMalloc(&eng->ptrace, (size_t)256 * 16 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");

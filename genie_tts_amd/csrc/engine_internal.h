@@ -100,6 +100,7 @@ struct gsv_engine {
     unsigned pepoch = 0;               // launch epoch (granule tags)
     int* perr = nullptr;               // device error word
     int* perr_host = nullptr;          // pinned error word
+    bool use_persist1 = true;          // GENIE_PERSIST1=0: the general kernel at B=1 too
     bool use_persist = true;           // GENIE_PERSIST=0: per-step graphs instead
     int n_cu = 0;
     unsigned long long* ptrace = nullptr;   // option "ptrace": persistent phase stamps [256][8]

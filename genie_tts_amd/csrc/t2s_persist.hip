@@ -38,102 +38,19 @@
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
+#include "persist.h"
 #include <hip/hip_ext.h>
 
 namespace gsv {
 
 namespace {
-typedef unsigned long long u64;
+using namespace pk;
 constexpr int PT = 512;            // threads per workgroup (8 waves)
 constexpr int PWV = PT / 64;
 constexpr int KVL = 320;           // K/V rows of a head staged in LDS ahead of the hand-off
 constexpr int TMAXP = 4096;        // longest key range (pe table)
 constexpr int NFB = 64;            // FFN workgroups per group (32 hidden units each)
 constexpr int RING = 4;            // granule ring depth (steps)
-constexpr unsigned long long SPIN_TICKS = 300000000ull;   // 3 s of the 100 MHz clock
-
-__device__ __forceinline__ int ld_rlx(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u64 ld_rlxu64(const u64* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// one write-through store of {tag, value}
-__device__ __forceinline__ void st_gran(u64* p, unsigned tag, float v) {
-    __hip_atomic_store(p, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Loads through global (address space 1) pointers: the layer table holds generic
-// pointers, which would otherwise become flat loads (counted in lgkmcnt too).
-#define GPTR(T, p) ((const __attribute__((address_space(1))) T*)(p))
-template <typename T>
-__device__ __forceinline__ T ldg(const T* base, long idx) { return GPTR(T, base)[idx]; }
-__device__ __forceinline__ float ldg_h(const __half* base, long idx) {
-    return __half2float(__ushort_as_half(*GPTR(unsigned short, base + idx)));
-}
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ldg16(const __half* base, long idx) {   // 8 halves at base[idx]
-    const u32x4_t v = *GPTR(u32x4_t, base + idx);   // native vector: no generic-ref copy constructor
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float4 ldg16f(const float* base, long idx) {
-    const f32x4_t v = *GPTR(f32x4_t, base + idx);
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-
-// One lane waits for its granule.  ok := false on timeout or when another
-// workgroup failed (the caller leaves after a block-wide check).
-__device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err, bool& ok) {
-    u64 g = ld_rlxu64(p);
-    if ((unsigned)(g >> 32) == tag) return __uint_as_float((unsigned)g);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (unsigned it = 1;; ++it) {
-        __builtin_amdgcn_s_sleep(1);
-        g = ld_rlxu64(p);
-        if ((unsigned)(g >> 32) == tag) return __uint_as_float((unsigned)g);
-        if ((it & 63) == 0) {
-            if (ld_rlx(err) != 0) { ok = false; return 0.f; }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
-                atomicCAS(err, 0, 1);
-                ok = false;
-                return 0.f;
-            }
-        }
-    }
-}
-
-// One lane waits for N granules p + k*stride (k < N), all N loads in flight at
-// once; re-polls only the ones whose tag is still stale.
-template <int N>
-__device__ __forceinline__ void wait_gran_n(const u64* p, long stride, unsigned tag, float (&out)[N], int* err,
-                                            bool& ok) {
-    u64 g[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k) g[k] = ld_rlxu64(p + k * stride);
-    unsigned long long t0 = 0;
-    for (unsigned it = 0;; ++it) {
-        bool all = true;
-#pragma unroll
-        for (int k = 0; k < N; ++k) all &= (unsigned)(g[k] >> 32) == tag;
-        if (all) break;
-        if (it == 0) t0 = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (int k = 0; k < N; ++k)
-            if ((unsigned)(g[k] >> 32) != tag) g[k] = ld_rlxu64(p + k * stride);
-        if ((it & 63) == 63) {
-            if (ld_rlx(err) != 0) { ok = false; break; }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
-                atomicCAS(err, 0, 1);
-                ok = false;
-                break;
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < N; ++k) out[k] = __uint_as_float((unsigned)g[k]);
-}
 
 // Ring of step slots of granules (u64).  Per slot: PA [24][B][16][512],
 // RA [24][B][512], PF [24][B][64][512], RF [24][B][512], LG [B][1056], TK [16].
@@ -156,71 +73,6 @@ struct Ws {
     __device__ u64* LG(int s, int b) const { return slot(s) + oLG() + (long)b * PERSIST_LGS; }
     __device__ u64* TK(int s, int b) const { return slot(s) + oTK() + b; }
 };
-
-// N independent wave sums on the DPP path, interleaved (ILP); lane 63 holds the sums.
-template <int N>
-__device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f<0xB1, 0xF>(v[q]);
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x4E, 0xF>(v[q]);
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x141, 0xF>(v[q]);
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x140, 0xF>(v[q]);
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x142, 0xA>(v[q]);
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f<0x143, 0xC>(v[q]);
-}
-
-// LayerNorm of NB rows of 512 values, one value per thread per row, as the graph
-// computes it (LayerNormalization: mean, then mean of squared deviations):
-// DPP wave sums (folded into v_add_f32_dpp), one LDS exchange per pass.
-template <int NB>
-__device__ __forceinline__ void ln_stats(const float (&v)[NB], float (&mean)[NB], float (&den)[NB], float* red) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float t[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) t[b] = v[b];
-    wave_sum_n<NB>(t);
-    if (lane == 63) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) red[w * NB + b] = t[b];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        float s0 = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < PWV; ++ww) s0 += red[ww * NB + b];
-        mean[b] = s0 * (1.0f / 512.0f);
-        const float d = v[b] - mean[b];
-        t[b] = d * d;
-    }
-    wave_sum_n<NB>(t);
-    if (lane == 63) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) red[PWV * NB + w * NB + b] = t[b];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        float s1 = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < PWV; ++ww) s1 += red[PWV * NB + ww * NB + b];
-        den[b] = sqrtf(s1 * (1.0f / 512.0f) + 1e-5f);
-    }
-}
-
-__device__ __forceinline__ float dot8(const uint4 w, const float4 x0, const float4 x1) {
-    float wf[8];
-    h8_to_f8(w, wf);
-    float s = 0.f;
-    s += wf[0] * x0.x; s += wf[1] * x0.y; s += wf[2] * x0.z; s += wf[3] * x0.w;
-    s += wf[4] * x1.x; s += wf[5] * x1.y; s += wf[6] * x1.z; s += wf[7] * x1.w;
-    return s;
-}
 
 struct Shared {
     union {

@@ -1,0 +1,603 @@
+// Persistent decode for ONE sequence (the single-stream case): the whole AR loop
+// of the stage decoder (t2s_stage_decoder_fp32.onnx, loop Inference.py:95-106)
+// in one launch, with TWO hand-offs per layer.
+//
+// A post-norm layer (stage#43-120) is a chain  x_l -> q,k,v -> attention -> out-proj
+// -> LN1 -> FFN1 -> FFN2 -> LN2 -> x_{l+1}.  Spread over many CUs it needs an
+// all-to-all after the out-projection and one after FFN2; nothing else has to
+// cross workgroups:
+//   attention workgroup (head h, 16 per layer): reads the 16 FFN2 partials of the
+//     previous layer plus its LN1 output h1_{l-1}, forms x_l = LN2(h1 + b2 + sum)
+//     itself, then q/k/v of head h, attention over the cached keys, and the
+//     head's out-projection slice -> 512 partial granules PA[l][h].
+//   FFN workgroup (slice j = hidden units [128 j, 128 j + 128), 16 per layer):
+//     forms x_l the same way (off the critical path, while attention runs), then
+//     h1_l = LN1(x_l + bo + sum_h PA[l][h]), publishes h1_l (32 columns per
+//     slice), FFN1 rows of the slice (ReLU), FFN2 partial -> granules PF[l][j].
+// So a token costs 2 hand-offs per layer + logits + sampler + token = 50 hops
+// (the general kernel, t2s_persist.hip, needs 3 per layer because every
+// workgroup tracks the residual stream).  Everything else is local.
+//
+// Grid: 8 layer groups x 32 workgroups = 256 (one per CU; LDS forces it).  Group
+// g owns layers g, g+8, g+16 and keeps its weights of the owned layer it works on
+// next in registers (q/k/v rows 48, out-proj column 16; W1 rows 64, W2 column 64
+// VGPRs) with the head's K/V rows in LDS, all loaded during the 7 layers it
+// waits; a waiting workgroup sleeps on one wake-up granule (the output of the
+// layer two before its own) and polls its real inputs only then.  Group 1's FFN
+// workgroups also hold the logits rows (ar_predict_layer, 64 + 1 per workgroup)
+// in LDS for the whole launch and compute the logits after layer 23; group 2's
+// head-0 attention workgroup runs the sampler (sampler.h, K10) and publishes the
+// token granule TK that group 0 waits on.
+//
+// Hand-offs: 8-byte {tag, value} granules (persist.h), tag = (epoch << 12) |
+// (step + 1) in a ring of RING1 step slots.  Every sum is formed in a fixed
+// order, so results do not depend on arrival order.  Every spin is bounded; a
+// timeout sets the error word and every workgroup leaves.
+#include "common.h"
+#include "kernels.h"
+#include "sampler.h"
+#include "persist.h"
+#include <hip/hip_ext.h>
+
+namespace gsv {
+
+namespace {
+using namespace pk;
+constexpr int PT = 512;            // threads per workgroup (8 waves)
+constexpr int PWV = PT / 64;
+constexpr int NG = 8;              // layer groups: layer l -> group l % NG
+constexpr int GW = 32;             // workgroups per group: 16 attention + 16 FFN
+constexpr int NF = 16;             // FFN slices per layer (128 hidden units each)
+constexpr int KVL1 = 448;          // K/V rows of a head staged in LDS
+constexpr int TMAX1 = 4096;        // longest key range (pe table)
+constexpr int RING1 = 4;           // granule ring depth (steps)
+constexpr int LOGIT_GRP = 1;       // FFN workgroups of this group compute the logits
+constexpr int SAMPLER_GRP = 2;     // head-0 attention workgroup of this group samples
+constexpr int LROWS = 64;          // logits rows per FFN workgroup (16 x 64 = 1024, + EOS row)
+
+// Granule ring.  Per step slot: PA [24][16][512], PFH [24][17][512] (rows 0..15 FFN2
+// partials, row 16 = h1), LG [PERSIST_LGS], TK [16].
+struct Ws1 {
+    u64* ring;
+    unsigned epoch;
+    static constexpr long oPFH = 24L * 16 * 512;
+    static constexpr long oLG = oPFH + 24L * 17 * 512;
+    static constexpr long oTK = oLG + PERSIST_LGS;
+    static constexpr long SLOT = oTK + 16;
+    __device__ u64* slot(int s) const { return ring + (long)(s % RING1) * SLOT; }
+    __device__ unsigned tag(int s) const { return (epoch << 12) | (unsigned)(s + 1); }
+    __device__ u64* PA(int s, int l, int h) const { return slot(s) + ((long)l * 16 + h) * 512; }
+    __device__ u64* PFH(int s, int l, int j) const { return slot(s) + oPFH + ((long)l * 17 + j) * 512; }
+    __device__ u64* LG(int s) const { return slot(s) + oLG; }
+    __device__ u64* TK(int s) const { return slot(s) + oTK; }
+};
+
+struct Shared1 {
+    union {
+        struct {                    // attention role
+            float k[KVL1 * 32];     // K/V rows [0, min(kv, KVL1)) of the head (LDS-DMA)
+            float v[KVL1 * 32];
+            float p[TMAX1];         // scores, then softmax numerators
+            float ov[16][32];       // P.V partial sums of 16 key groups
+            float lg[PERSIST_LGS];  // logits (sampler)
+        } at;
+        struct {                    // FFN role
+            uint4 wp[LROWS + 1][64];   // logits rows (group LOGIT_GRP), resident for the launch
+        } ff;
+    };
+    float x[512];                   // x_l (attention), h1_l (FFN), x_24 (logits)
+    float qkv[96];
+    float os[32];
+    float fs[128];                  // FFN1 output of the slice
+    float b1[128];                  // FFN1 bias of the slice
+    float red[2 * PWV];
+    float wred[2][PWV];
+    uint32_t seen[33];
+    int tok, fin, fail;
+    unsigned long long stamp[16];   // [0,8) 100 MHz realtime, [8,16) shader clock
+    SampleLds<PT> samp;
+};
+
+#define STAMP1(i)                                                                         \
+    do {                                                                                  \
+        if (probe && threadIdx.x == 0) {                                                  \
+            sh.stamp[i] = __builtin_amdgcn_s_memrealtime();                               \
+            sh.stamp[8 + (i)] = __builtin_amdgcn_s_memtime();                             \
+        }                                                                                 \
+    } while (0)
+
+__device__ __forceinline__ bool block_ok1(bool ok, Shared1& sh) {
+    if (!ok) sh.fail = 1;
+    __syncthreads();
+    return sh.fail == 0;
+}
+
+// Scores of the general case (more than 512 keys or rows beyond the LDS stage),
+// out of line so the common path keeps its registers.  Returns the lane's max.
+__device__ __noinline__ float scores_general1(Shared1& sh, const float* Kw, int kv, int T, float q0, float q1,
+                                              float q2, float q3, float sc, float4 knew, int c8, int g) {
+    float lmax = -INFINITY;
+    for (int base = 0; base < T; base += 512) {
+        float sv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = base + 64 * u + g;
+            float4 kr;
+            if (t < kv && t < KVL1) kr = *reinterpret_cast<const float4*>(sh.at.k + t * 32 + 4 * c8);
+            else if (t < kv) kr = ldg16f(Kw, (long)t * 32 + 4 * c8);
+            else kr = knew;
+            float x = q0 * (kr.x * sc);
+            x += q1 * (kr.y * sc);
+            x += q2 * (kr.z * sc);
+            x += q3 * (kr.w * sc);
+            sv[u] = x;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = base + 64 * u + g;
+            if (t < T) {
+                if (c8 == 0) sh.at.p[t] = sv[u];
+                lmax = fmaxf(lmax, sv[u]);
+            }
+        }
+    }
+    return lmax;
+}
+
+// Step start: thread 0 learns the token of step s (s >= 1: granule TK(s), whose
+// bit 16 says the previous step finished the sequence).  Group 0 needs the token
+// at once (its layer 0 starts from it) and sleeps on the layer-23 output of the
+// previous step first; the other groups only need the stop bit and poll slowly.
+// Returns false when the loop is over (or on error: sh.fail).
+__device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0, Shared1& sh) {
+    if (threadIdx.x == 0) {
+        bool ok = true;
+        if (s > 0) {
+            float v;
+            if (grp0) {
+                wait_tag_slow(ws.PFH(s - 1, 23, 0), ws.tag(s - 1), a.err, ok);
+                v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok) : 0.f;
+            } else {
+                wait_tag_slow(ws.TK(s), ws.tag(s), a.err, ok);
+                v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok) : 0.f;
+            }
+            const unsigned u = __float_as_uint(v);
+            sh.tok = (int)(u & 0xffff);
+            sh.fin = ok ? (int)((u >> 16) & 1) : 1;
+        }
+        if (!ok) sh.fail = 1;
+    }
+    __syncthreads();
+    const bool go = sh.fail == 0 && sh.fin == 0;
+    __syncthreads();
+    return go;
+}
+
+// x_l for column tid: layer 0 from the token (E_audio[tok] + alpha * pe[n]),
+// otherwise LN2_{l-1}(h1_{l-1} + (b2 + sum_j PF[l-1][j])), the partials summed in
+// slice order.  A sleeping lane waits for the wake-up granule (layer l-2's output)
+// before every thread polls its 17 granules.
+__device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, float b2p,
+                                       float n2w, float n2b, float& xv, Shared1& sh) {
+    const int tid = threadIdx.x;
+    if (l == 0) {
+        xv = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
+        return true;
+    }
+    const unsigned tag = ws.tag(s);
+    bool ok = true;
+    if (l >= 2) {
+        if (tid == 0) wait_tag_slow(ws.PFH(s, l - 2, 0), tag, a.err, ok);
+        if (!block_ok1(ok, sh)) return false;
+    }
+    float g[17];
+    wait_gran_n<17>(ws.PFH(s, l - 1, 0) + tid, 512, tag, g, a.err, ok);
+    float f = g[0];
+#pragma unroll
+    for (int j = 1; j < NF; ++j) f += g[j];
+    float v[1] = {g[16] + (b2p + f)}, mean[1], den[1];
+    if (!block_ok1(ok, sh)) return false;
+    ln_stats<1>(v, mean, den, sh.red);
+    xv = (v[0] - mean[0]) / den[0] * n2w + n2b;
+    return true;
+}
+
+// --------------------------------------------------------------------------
+// Attention workgroup: head h of layers grp, grp + 8, grp + 16.
+// --------------------------------------------------------------------------
+__device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int grp, int h) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool sampler = grp == SAMPLER_GRP && h == 0;
+    const int ny0 = a.ny[0], kv0 = a.kvlen[0], st0 = a.steps[0];
+    if (tid == 0) {
+        sh.tok = (int)a.y[ny0 - 1];
+        sh.fin = a.done[0] ? 1 : 0;
+        sh.fail = 0;
+    }
+    if (sampler && tid < 33) sh.seen[tid] = a.seen[tid];
+    const long kvoff = (long)h * a.tmax * 32;
+    uint4 wq[12], wo[4];
+    float bq[3] = {0.f, 0.f, 0.f};
+    float b2p = 0.f, n2w = 0.f, n2b = 0.f;   // LN2 of layer l-1
+    auto prefetch = [&](int l, int kv) {
+        const PLayer& P = a.L[l];
+        // wave w, lane group r4 = lane >> 4: rows (m, h*32 + 4w + r4) of W_in for m = q, k, v;
+        // lane i16 = lane & 15 holds columns 8*i16 + 128*c (c < 4): a row is reduced over 16 lanes
+        const int r4 = lane >> 4, i16 = lane & 15;
+        const __half* wb = P.w_in + (long)(h * 32 + 4 * w + r4) * 512 + 8 * i16;
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wq[m * 4 + c] = ldg16(wb + (long)m * 512 * 512 + c * 128, 0);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) bq[m] = ldg(P.b_in, m * 512 + h * 32 + 4 * w + r4);
+        // out-projection: thread tid owns output column tid, W_out[tid][h*32 .. h*32+32)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wo[k] = ldg16(P.w_out + (long)tid * 512 + h * 32 + 8 * k, 0);
+        if (l > 0) {
+            const PLayer& Q = a.L[l - 1];
+            b2p = ldg(Q.b2, tid); n2w = ldg(Q.n2w, tid); n2b = ldg(Q.n2b, tid);
+        }
+        // K/V rows [0, min(kv, KVL1)) -> LDS, 8 rows (1 KB) per wave instruction.  Rows of
+        // the last chunk past kv are read (allocated: tmax >= kv + 16) and never used.
+        const float* K = a.kc[l] + kvoff;
+        const float* V = a.vc[l] + kvoff;
+        const int nch = (min(kv, KVL1) + 7) >> 3;
+        for (int i = w; i < nch; i += PWV) {
+            __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
+        }
+    };
+    __syncthreads();
+    if (sh.fin) return;
+    prefetch(grp, kv0);
+    int n_exec = 0, last_stop = 0, last_fin = 0;
+    for (int s = 0; s < a.smax; ++s) {
+        if (!step_start(a, ws, s, grp == 0, sh)) break;
+        const unsigned tag = ws.tag(s);
+        const int kv = kv0 + s;
+        for (int l = grp; l < 24; l += NG) {
+            const bool probe = a.trace && s == 8 && l == 12;
+            STAMP1(0);
+            float xv;
+            if (!form_x(a, ws, s, l, ny0 + s, b2p, n2w, n2b, xv, sh)) return;
+            sh.x[tid] = xv;
+            __syncthreads();
+            STAMP1(1);
+            // ---- q, k, v of head h: 3 rows per lane group, 16 lanes per row
+            {
+                const int r4 = lane >> 4, i16 = lane & 15;
+                float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[8 * i16 + 128 * c]);
+                    const float4 x1 = *reinterpret_cast<const float4*>(&sh.x[8 * i16 + 128 * c + 4]);
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) acc[m] += dot8(wq[m * 4 + c], x0, x1);
+                }
+#pragma unroll
+                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0xB1, 0xF>(acc[m]);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x4E, 0xF>(acc[m]);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x141, 0xF>(acc[m]);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x140, 0xF>(acc[m]);
+                if (i16 == 0) {
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) sh.qkv[m * 32 + 4 * w + r4] = bq[m] + acc[m];
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
+            __syncthreads();
+            STAMP1(2);
+            // ---- scores (q*s).(k*s) over [0, kv]: 8 lanes per key row (16 B each,
+            // conflict-free LDS reads), keys t = base + 64 u + g
+            float* Kw = a.kc[l] + kvoff;
+            float* Vw = a.vc[l] + kvoff;
+            const float sc = a.scale;
+            const int T = kv + 1;
+            const int c8 = lane & 7, g = (w << 3) | (lane >> 3);
+            const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
+            const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
+            float lmax = -INFINITY;
+            const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
+            if (T <= 512 && kv <= KVL1) {
+                // common case, branch-free: every cached row is in LDS, 8 keys per lane in two halves
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    float sv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = 64 * (4 * hf + u) + g;
+                        float4 kr = *reinterpret_cast<const float4*>(sh.at.k + min(t, KVL1 - 1) * 32 + 4 * c8);
+                        if (t == kv) { kr.x = knew.x; kr.y = knew.y; kr.z = knew.z; kr.w = knew.w; }
+                        float x = q0 * (kr.x * sc);
+                        x += q1 * (kr.y * sc);
+                        x += q2 * (kr.z * sc);
+                        x += q3 * (kr.w * sc);
+                        sv[u] = x;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = 64 * (4 * hf + u) + g;
+                        sv[u] = t < T ? sv[u] : -INFINITY;
+                        lmax = fmaxf(lmax, sv[u]);
+                    }
+                    if (c8 == 0) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) sh.at.p[64 * (4 * hf + u) + g] = sv[u];   // p[t >= T] is never read
+                    }
+                }
+            } else {
+                lmax = scores_general1(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
+            }
+            const float wm = wave_max_dpp(lmax);
+            if (lane == 0) sh.wred[0][w] = wm;
+            __syncthreads();
+            float M = sh.wred[0][0];
+#pragma unroll
+            for (int ww = 1; ww < PWV; ++ww) M = fmaxf(M, sh.wred[0][ww]);
+            float lsum = 0.f;
+            for (int t = tid; t < T; t += PT) {
+                const float e = expf(sh.at.p[t] - M);
+                sh.at.p[t] = e;
+                lsum += e;
+            }
+            const float ws_ = wave_sum_dpp(lsum);
+            if (lane == 0) sh.wred[1][w] = ws_;
+            __syncthreads();
+            STAMP1(3);
+            // ---- P.V: 16 key groups x 32 dims; LDS rows unrolled by 4 with independent sums
+            {
+                const int kg = tid >> 5, d = tid & 31;
+                const int tl = min(kv, KVL1);
+                float o4[4] = {0.f, 0.f, 0.f, 0.f};
+                int t = kg;
+                for (; t + 48 < tl; t += 64) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) o4[u] += sh.at.p[t + 16 * u] * sh.at.v[(t + 16 * u) * 32 + d];
+                }
+                for (; t < tl; t += 16) o4[0] += sh.at.p[t] * sh.at.v[t * 32 + d];
+                for (; t < kv; t += 16) o4[1] += sh.at.p[t] * ldg(Vw, (long)t * 32 + d);
+                if (t == kv) o4[2] += sh.at.p[t] * sh.qkv[64 + d];
+                sh.at.ov[kg][d] = (o4[0] + o4[1]) + (o4[2] + o4[3]);
+            }
+            __syncthreads();
+            if (tid < 32) {
+                float O = 0.f, L = 0.f;
+#pragma unroll
+                for (int kg = 0; kg < 16; ++kg) O += sh.at.ov[kg][tid];
+#pragma unroll
+                for (int ww = 0; ww < PWV; ++ww) L += sh.wred[1][ww];
+                sh.os[tid] = O / L;
+            }
+            __syncthreads();
+            STAMP1(4);
+            // ---- out-projection slice of this head (column tid) -> partial granule
+            {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 oa = *reinterpret_cast<const float4*>(sh.os + 8 * k);
+                    const float4 ob = *reinterpret_cast<const float4*>(sh.os + 8 * k + 4);
+                    acc += dot8(wo[k], oa, ob);
+                }
+                st_gran(ws.PA(s, l, h) + tid, tag, acc);
+                // the new K/V row (read by this workgroup only, next step)
+                if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
+                else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
+            }
+            STAMP1(5);
+            __syncthreads();   // LDS operands consumed before the next layer's LDS-DMA lands
+            // ---- next owned layer (this step) or the first one of the next step
+            const int ln = l + NG < 24 ? l + NG : grp;
+            prefetch(ln, l + NG < 24 ? kv : kv + 1);
+            if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
+        }
+        // ---- sampler: logits granules of this step -> token -> TK(s + 1)
+        if (sampler) {
+            bool ok = true;
+            if (tid == 0) wait_tag_slow(ws.PFH(s, 23, 0), tag, a.err, ok);
+            if (!block_ok1(ok, sh)) return;
+            const u64* lgg = ws.LG(s);
+            for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok);
+            if (!block_ok1(ok, sh)) return;
+            const int st = st0 + s;   // loop steps already executed
+            int raw = 0;
+            const int tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, 0, st + 1, a.top_k,
+                                             a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw,
+                                             sh.samp);
+            if (tid == 0) {
+                a.y[ny0 + s] = tok;
+                sh.seen[tok >> 5] |= 1u << (tok & 31);
+                const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
+                const int nst = st + 1;
+                const bool fin = a.force_steps > 0 ? nst >= a.force_steps : (stop || nst >= a.max_steps);
+                last_stop = stop;
+                last_fin = fin ? 1 : 0;
+                st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+            }
+        }
+        ++n_exec;
+    }
+    // ---- sequence state write-back (sampler workgroup)
+    if (sampler && n_exec > 0 && sh.fail == 0) {
+        __syncthreads();
+        if (tid < 33) a.seen[tid] = sh.seen[tid];
+        if (tid == 0) {
+            a.ny[0] = ny0 + n_exec;
+            a.steps[0] = st0 + n_exec;
+            a.kvlen[0] = kv0 + n_exec;
+            a.done[0] = (uint8_t)last_fin;
+            if (a.stop_out) a.stop_out[0] = (uint8_t)last_stop;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// FFN workgroup: hidden slice j of layers grp, grp + 8, grp + 16 (+ logits rows
+// [64 j, 64 j + 64) in group LOGIT_GRP).
+// --------------------------------------------------------------------------
+__device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int grp, int j) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool logits = grp == LOGIT_GRP;
+    const int ny0 = a.ny[0];
+    if (tid == 0) {
+        sh.tok = (int)a.y[ny0 - 1];
+        sh.fin = a.done[0] ? 1 : 0;
+        sh.fail = 0;
+    }
+    float lb2 = 0.f, ln2w = 0.f, ln2b = 0.f;   // LN2 of layer 23 (logits)
+    if (logits) {
+        // rows 64 j + r (r < 64) and, on the last slice, the EOS row 1024 -- resident for the launch
+        for (int e = tid; e < (LROWS + 1) * 64; e += PT) {
+            const int r = e >> 6, c = e & 63;
+            const int row = r < LROWS ? j * LROWS + r : 1024;
+            sh.ff.wp[r][c] = (r < LROWS || j == NF - 1) ? ldg16(a.w_pred, (long)row * 512 + 8 * c)
+                                                        : make_uint4(0u, 0u, 0u, 0u);
+        }
+        lb2 = ldg(a.L[23].b2, tid); ln2w = ldg(a.L[23].n2w, tid); ln2b = ldg(a.L[23].n2b, tid);
+    }
+    uint4 w1r[16], w2r[16];
+    float b2p = 0.f, n2w = 0.f, n2b = 0.f;   // LN2 of layer l-1
+    float bo = 0.f, n1w = 0.f, n1b = 0.f;    // out-proj bias and LN1 of layer l
+    float b1v = 0.f;                         // FFN1 bias of hidden unit 128 j + tid (tid < 128)
+    auto prefetch = [&](int l) {
+        const PLayer& P = a.L[l];
+        // FFN1: wave w holds rows 128 j + 16 w + q (q < 16), lane columns [8 lane, 8 lane + 8)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w1r[q] = ldg16(P.w1 + (long)(j * 128 + w * 16 + q) * 512, lane * 8);
+        // FFN2: thread tid owns output column tid, W2[tid][128 j .. 128 j + 128)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w2r[k] = ldg16(P.w2 + (long)tid * 2048 + j * 128 + 8 * k, 0);
+        b1v = tid < 128 ? ldg(P.b1, j * 128 + tid) : 0.f;
+        bo = ldg(P.b_out, tid); n1w = ldg(P.n1w, tid); n1b = ldg(P.n1b, tid);
+        if (l > 0) {
+            const PLayer& Q = a.L[l - 1];
+            b2p = ldg(Q.b2, tid); n2w = ldg(Q.n2w, tid); n2b = ldg(Q.n2b, tid);
+        }
+    };
+    __syncthreads();
+    if (sh.fin) return;
+    prefetch(grp);
+    for (int s = 0; s < a.smax; ++s) {
+        if (!step_start(a, ws, s, grp == 0, sh)) break;
+        const unsigned tag = ws.tag(s);
+        for (int l = grp; l < 24; l += NG) {
+            const bool probe = a.trace && s == 8 && l == 12;
+            STAMP1(0);
+            float xv;
+            if (!form_x(a, ws, s, l, ny0 + s, b2p, n2w, n2b, xv, sh)) return;
+            STAMP1(1);
+            // ---- h1_l = LN1(x_l + (bo + sum_h PA[l][h])), heads summed in order
+            {
+                bool ok = true;
+                float pa[16];
+                wait_gran_n<16>(ws.PA(s, l, 0) + tid, 512, tag, pa, a.err, ok);
+                float sum = pa[0];
+#pragma unroll
+                for (int hh = 1; hh < 16; ++hh) sum += pa[hh];
+                float v[1] = {xv + (bo + sum)}, mean[1], den[1];
+                if (!block_ok1(ok, sh)) return;
+                STAMP1(2);
+                ln_stats<1>(v, mean, den, sh.red);
+                const float h1 = (v[0] - mean[0]) / den[0] * n1w + n1b;
+                if ((tid >> 5) == j) st_gran(ws.PFH(s, l, 16) + tid, tag, h1);
+                sh.x[tid] = h1;
+                if (tid < 128) sh.b1[tid] = b1v;
+            }
+            __syncthreads();
+            STAMP1(6);
+            // ---- FFN1 rows of this slice (16 per wave), ReLU
+            {
+                const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[lane * 8]);
+                const float4 x1 = *reinterpret_cast<const float4*>(&sh.x[lane * 8 + 4]);
+                float acc[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[q] = dot8(w1r[q], x0, x1);
+                wave_sum_n<16>(acc);
+                if (lane == 63) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) sh.fs[w * 16 + q] = fmaxf(sh.b1[w * 16 + q] + acc[q], 0.f);
+                }
+            }
+            __syncthreads();
+            STAMP1(3);
+            // ---- FFN2 slice (column tid) -> partial granule
+            {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const float4 fa = *reinterpret_cast<const float4*>(&sh.fs[8 * k]);
+                    const float4 fb = *reinterpret_cast<const float4*>(&sh.fs[8 * k + 4]);
+                    acc += dot8(w2r[k], fa, fb);
+                }
+                st_gran(ws.PFH(s, l, j) + tid, tag, acc);
+            }
+            STAMP1(4);
+            __syncthreads();   // fs / b1 consumed before the next prefetch lands
+            prefetch(l + NG < 24 ? l + NG : grp);
+            if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
+        }
+        if (logits) {
+            // ---- x_24 = LN2_23(h1_23 + b2 + sum PF_23), logits rows (ar_predict_layer, no bias)
+            float xv;
+            if (!form_x(a, ws, s, 24, 0, lb2, ln2w, ln2b, xv, sh)) return;
+            sh.x[tid] = xv;
+            __syncthreads();
+            const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[lane * 8]);
+            const float4 x1 = *reinterpret_cast<const float4*>(&sh.x[lane * 8 + 4]);
+            float acc[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = dot8(sh.ff.wp[w * 8 + q][lane], x0, x1);
+            wave_sum_n<8>(acc);
+            u64* lg = ws.LG(s);
+            if (lane == 63) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) st_gran(lg + j * LROWS + w * 8 + q, tag, acc[q]);
+            }
+            if (j == NF - 1 && w == 0) {
+                float e[1] = {dot8(sh.ff.wp[LROWS][lane], x0, x1)};
+                wave_sum_n<1>(e);
+                if (lane == 63) st_gran(lg + 1024, tag, e[0]);
+            }
+            __syncthreads();   // x consumed before the next step's writes
+        }
+    }
+}
+
+__global__ __launch_bounds__(PT) void k_decode_persist1(PersistArgs a) {
+    __shared__ Shared1 sh;
+    const Ws1 ws{a.ring, a.epoch};
+    const int grp = blockIdx.x / GW, r = blockIdx.x - grp * GW;
+    if (r < 16) run_attn(a, ws, sh, grp, r);
+    else run_ffn(a, ws, sh, grp, r - 16);
+}
+
+}  // namespace
+
+int persist1_grid() { return NG * GW; }
+
+size_t persist1_ring_bytes() { return (size_t)Ws1::SLOT * RING1 * 8; }
+
+hipError_t decode_persist1(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_decode_persist1, dim3(NG * GW), dim3(PT), 0, s, start, stop, 0, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsv
