@@ -46,12 +46,30 @@ def persist_algorithmic_bytes(n0: int, steps: int, B: int = 1) -> int:
     return sum(W16 + B * (KV_ROW * (n0 + s) + KV_ROW) for s in range(steps))
 
 
+def pmc_traffic(kernel_sub: str):
+    """HBM bytes per launch of the named kernel from the committed PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    for k, v in d.get("kernels", {}).items():
+        if kernel_sub in k:
+            return float(v["traffic_bytes"]), f"{d.get('source')}: {k}"
+    return None, None
+
+
 def persist_roofline(eng, n0: int, steps: int, B: int = 1):
     us, n = eng.kernel_timing()
     if n <= 0 or us <= 0:
         return {"error": f"no live kernel samples (hipEventElapsedTime error {-n})"}
     bytes_ = persist_algorithmic_bytes(n0, steps, B)
     achieved = bytes_ / (us * 1e-6) / 1e9
+    traffic, tsrc = pmc_traffic("k_decode_persist")
     return {
         "kernel": "k_decode_persist (whole decode loop, %d steps, N0=%d, B=%d)" % (steps, n0, B),
         "bound": "hbm",
@@ -59,7 +77,8 @@ def persist_roofline(eng, n0: int, steps: int, B: int = 1):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_source": tsrc,
         "algorithmic_bytes_per_launch": bytes_,
         "avg_launch_us": us,
         "samples": n,

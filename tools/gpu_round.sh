@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
-    tests) timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
+    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
            tail -3 gpurun_out/${TAG}_tests.log ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }
            tail -2 gpurun_out/${TAG}_smoke.log ;;
@@ -17,5 +17,10 @@ for s in $STEPS; do
     prof)  rm -rf gpurun_out/prof_${TAG}
            timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o bench -- python3 bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench_under_rocprof.log 2>&1 || { tail -30 gpurun_out/${TAG}_bench_under_rocprof.log; exit 1; }
            python tools/prof_summary.py gpurun_out/prof_${TAG} > gpurun_out/${TAG}_kernel_stats.txt 2>&1; head -25 gpurun_out/${TAG}_kernel_stats.txt ;;
+    pmc)   for c in FETCH_SIZE WRITE_SIZE; do
+             rm -rf gpurun_out/pmc_${TAG}_$c
+             timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$c -o pmc -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/${TAG}_pmc_$c.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_$c.log; exit 1; }
+             python tools/pmc_summary.py gpurun_out/pmc_${TAG}_$c --gfx950-fetch-x2 --json gpurun_out/${TAG}_pmc_$c.json > gpurun_out/${TAG}_pmc_$c.txt 2>&1; grep -i "persist\|conv1d<11" gpurun_out/${TAG}_pmc_$c.txt | head -5 || true
+           done ;;
   esac
 done
