@@ -60,6 +60,8 @@ gsv_engine::~gsv_engine() {
     if (ptrace) hipFree(ptrace);
     if (pws) hipFree(pws);
     if (perr_host) hipHostFree(perr_host);
+    if (vovf_host) hipHostFree(vovf_host);
+    if (vovf) hipFree(vovf);
     if (perr) hipFree(perr);
     for (void* p : state_allocs) hipFree(p);
     state_allocs.clear();
@@ -129,6 +131,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_ACC")) use_acc = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST")) use_persist = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST1")) use_persist1 = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_KTRACE"))
         if (std::atoi(e) == 1 && !ktrace) {
             hipMalloc(&ktrace, (size_t)3 * 256 * 8 * 8);
@@ -939,6 +942,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist = value != 0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;
+    } else if (n == "convh") {
+        eng->use_convh = value != 0;
     } else if (n == "ptrace") {
         if (value && !eng->ptrace) {
             if (hipMalloc(&eng->ptrace, (size_t)256 * 16 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");

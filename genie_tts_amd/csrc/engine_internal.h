@@ -102,6 +102,10 @@ struct gsv_engine {
     int* perr_host = nullptr;          // pinned error word
     bool use_persist1 = true;          // GENIE_PERSIST1=0: the general kernel at B=1 too
     bool use_persist = true;           // GENIE_PERSIST=0: per-step graphs instead
+    bool use_convh = true;             // GENIE_CONVH=0: MRF convs on the f32 MFMA path
+    int* vovf = nullptr;               // f16-split conv overflow flag (device)
+    int* vovf_host = nullptr;          // pinned copy
+    int vits_f32_reruns = 0;           // utterances re-run on the f32 path after an overflow
     int n_cu = 0;
     unsigned long long* ptrace = nullptr;   // option "ptrace": persistent phase stamps [256][8]
 
@@ -128,6 +132,9 @@ struct gsv_engine {
     int vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                     const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
                     const float* eps, float noise_scale, float* audio, hipStream_t st);
+    int vits_decode_pass(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
+                         const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
+                         const float* eps, float noise_scale, float* audio, hipStream_t st, bool f16);
     int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                       float* ge_adv, hipStream_t st);
 };

@@ -49,8 +49,15 @@ struct ConvArgs {
     // under-filled grids over grid.z into partial slabs [split][Cout][n_t] and a
     // second kernel sums them in fixed order and applies the epilogue.
     float* part; long part_cap;
+    // f16-split MFMA path (vits_convh.hip): weights fp16 [Cout][K][Cin] (the
+    // fp16 values of the reference's weight_v / weight), per-output-channel
+    // scale (weight norm g/||v||, 1 without it), overflow flag set when an
+    // input does not fit fp16.  wh == nullptr -> f32 path.
+    const __half* wh; const float* wscale; int* ovf;
 };
 void conv1d(const ConvArgs& a, hipStream_t s);
+// f16-split path; returns false (nothing launched) when the shape is not covered.
+bool conv1d_h(const ConvArgs& a, hipStream_t s);
 
 // LayerNorm over channels per t: out = LN(x + y) (y may be null), eps 1e-5
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
@@ -91,6 +98,8 @@ struct Conv {
     float* w = nullptr;   // [Cout][Cin][K] (or [phases][Cout][Cin][K] for ConvT)
     float* b = nullptr;
     int cout = 0, cin = 0, k = 0, phases = 1;
+    __half* wh = nullptr;      // fp16 [Cout][K][Cin] when every weight value is fp16-exact
+    float* wscale = nullptr;   // [Cout] weight-norm scale applied to the f16 path's sums
 };
 
 struct AttnLayer {

@@ -10,6 +10,7 @@
 // `stride` polyphase convs of the same kernel (blockIdx.z = phase).
 #include "common.h"
 #include "vits.h"
+#include "vits_epi.h"
 #include <algorithm>
 
 namespace gsv {
@@ -22,39 +23,6 @@ template <int KT> struct ConvCfg {
 #define CONV_BN 64
 #define CONV_BM 64
 #define CONV_XW_MAX 128
-
-// Output epilogue shared by the direct and the split-K paths: output column t of
-// phase ph -> time tp; bias; the ConvMode fusion.
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int co, int t, int ph, float acc) {
-    const int tp = t * a.o_tstride + a.o_toff + ph;
-    if (tp < 0 || tp >= a.o_len) return;
-    const float v = a.bias ? a.bias[co] + acc : acc;
-    const long oi = (long)co * a.o_cs + (long)tp * a.o_ts;
-    switch (a.mode) {
-        case CV_STORE: a.out[oi] = v; break;
-        case CV_RELU: a.out[oi] = fmaxf(v, 0.f); break;
-        case CV_RESID: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
-        case CV_VEC: a.out[oi] = v + a.vec[co]; break;
-        case CV_SUB: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] - v; break;
-        case CV_TANH: a.out[oi] = tanhf(v); break;
-        case CV_ACC_FIRST: a.acc[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
-        case CV_ACC_ADD: a.acc[oi] = a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v); break;
-        case CV_ACC_MEAN:
-            a.out[oi] = (a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v)) / a.div;
-            break;
-        case CV_RESID_VEC:
-            a.out[oi] = (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v) + a.vec[co];
-            break;
-        case CV_SPLIT_RESID:
-            if (co < a.split) {
-                a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v;
-            } else {
-                const long o2 = (long)(co - a.split) * a.o_cs + (long)tp * a.o_ts;
-                a.out2[o2] = a.res2[o2] + v;
-            }
-            break;
-    }
-}
 
 // Software pipeline: the next K-chunk (input halo tile + weight tile) is loaded
 // into registers while the MFMAs consume the current chunk from LDS; LDS is
@@ -176,11 +144,10 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
         }
         return;
     }
+    float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co < a.Cout) conv_epilogue(a, co, t, ph, acc[r]);
-    }
+    for (int r = 0; r < 16; ++r) v[r] = acc[r];
+    conv_epilogue16(a, co0 + wm * 32 + 4 * h, t, ph, v);
 }
 
 // Fixed-order sum of the split-K slabs + the conv epilogue (one thread per output).
@@ -223,6 +190,7 @@ static int conv_ci(int K) {
 }
 
 void conv1d(const ConvArgs& a, hipStream_t s) {
+    if (a.wh && conv1d_h(a, s)) return;
     dim3 grid((a.n_t + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM,
               a.phases > 0 ? a.phases : 1);
     // Under-filled grids (the T=2G / S-frame encoder, MRTE and flow convs) split

@@ -1,0 +1,269 @@
+// HiFi-GAN MRF conv1d on the f16 MFMA (v_mfma_f32_32x32x16_f16) with split
+// fp32 activations: x = hi + lo, hi = fp16(x), lo = fp16(x - hi), so
+//   sum_k w_k x_k = sum_k w_k hi_k + sum_k w_k lo_k      (f32 accumulate)
+// carries ~22 bits of every activation.  The weights need no split: every value
+// of vits_fp16.bin is fp16 (ModelManager.py:59-114 upcasts fp16 -> fp32), and
+// weight norm (vits(v2) ReduceL2 -> Div -> Mul on weight_v/weight_g) is a
+// per-output-channel scale g/||v|| applied to the f32 sums in the epilogue.
+// Reference ops: the resblocks' Conv nodes of vits_fp32.onnx (dec.resblocks.*),
+// 130 of the 135.5 GFLOP per utterance.
+//
+// Implicit GEMM: M = Cout, N = time, K = (tap, Cin).  A K-chunk is CC input
+// channels x KT taps.  LDS holds the chunk's input tile time-major,
+// [t][ci] in fp16 hi and lo planes (a lane's B fragment = 8 consecutive
+// channels at one time = one ds_read_b128), and the weight tile [co][tap][ci]
+// (A fragment = one ds_read_b128); row strides are odd multiples of 16 B, so
+// the reads are conflict-free.  The next chunk is loaded into registers while
+// the MFMAs consume the current one.  Block = 4 waves laid out WM x WN x KS:
+// each wave owns a 32 x 64 output tile (two 32x32 accumulators); KS > 1 splits
+// the chunk's MFMA steps over waves and sums the partials in fixed order.
+//
+// Range guard: an input of magnitude > 65504 has no fp16 hi part; the kernel
+// then sets *a.ovf and the host re-runs the utterance on the f32 path.
+#include "common.h"
+#include "vits.h"
+#include "vits_epi.h"
+#include <cstdlib>
+
+namespace gsv {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+constexpr int DMAX = 5;   // largest dilation of the MRF convs (rb_d)
+
+template <int KT, int CC, int WM, int WN, int KS>
+struct HCfg {
+    static constexpr int BM = 32 * WM, BN = 64 * WN;
+    static constexpr int G8 = CC / 8;                   // 8-channel groups per tap
+    static constexpr int NG = KT * G8;                  // groups per chunk
+    static constexpr int NSTEP = (NG + 1) / 2;          // MFMA K-steps (2 groups each)
+    static constexpr int XW = BN + (KT - 1) * DMAX;     // input rows (time) per tile
+    static constexpr int XR = CC == 8 ? 24 : CC + 8;    // halves per X row (odd x 16 B)
+    static constexpr int WR = KT * CC + (CC == 8 ? 16 : 8);   // halves per W row (odd x 16 B)
+    static constexpr int NXI = (XW * G8 + 255) / 256;   // X items (time, group) per thread
+    static constexpr int NWI = (BM * NG + 255) / 256;   // W 16-B items per thread
+    static constexpr int X_BYTES = XW * XR * 2;
+    static constexpr int W_BYTES = BM * WR * 2;
+    static constexpr int RED_BYTES = KS > 1 ? (KS - 1) * WM * WN * 2 * 16 * 64 * 4 : 0;
+    static constexpr int MAIN_BYTES = 2 * X_BYTES + W_BYTES;
+    static constexpr int LDS = MAIN_BYTES > RED_BYTES ? MAIN_BYTES : RED_BYTES;
+};
+
+__device__ __forceinline__ void split8(const float (&v)[8], uint4& hi, uint4& lo) {
+    _Float16 h[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        h[j] = (_Float16)v[j];
+        l[j] = (_Float16)(v[j] - (float)h[j]);
+    }
+    hi = *reinterpret_cast<const uint4*>(h);
+    lo = *reinterpret_cast<const uint4*>(l);
+}
+
+template <int KT, int CC, int WM, int WN, int KS>
+__global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
+    using C = HCfg<KT, CC, WM, WN, KS>;
+    __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+    _Float16* Xh = reinterpret_cast<_Float16*>(smem);
+    _Float16* Xl = reinterpret_cast<_Float16*>(smem + C::X_BYTES);
+    _Float16* Ws = reinterpret_cast<_Float16*>(smem + 2 * C::X_BYTES);
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ks = w % KS, wn = (w / KS) % WN, wm = w / (KS * WN);
+    const int t0 = blockIdx.x * C::BN, co0 = blockIdx.y * C::BM;
+    const int dil = a.dil;
+    const int xw = C::BN + (KT - 1) * dil;
+    const int nch = a.Cin / CC;
+    const _Float16* __restrict__ Wg = reinterpret_cast<const _Float16*>(a.wh);
+    const float* __restrict__ X = a.x;
+
+    // per-thread staging items (loop invariant): X item e -> (group c8, row u)
+    int xu[C::NXI], xc[C::NXI];
+#pragma unroll
+    for (int i = 0; i < C::NXI; ++i) {
+        const int e = tid + i * 256;
+        xc[i] = e / xw;
+        xu[i] = e - xc[i] * xw;
+        if (xc[i] >= C::G8) xc[i] = -1;
+    }
+    float xr[C::NXI][8];
+    uint4 wr[C::NWI];
+    bool ovf = false;
+
+    auto load = [&](int ci0) {
+#pragma unroll
+        for (int i = 0; i < C::NXI; ++i) {
+            const int tin = t0 - a.pad + xu[i];
+            const bool ok = xc[i] >= 0 && tin >= 0 && tin < a.Tin;
+            const float* src = X + (long)(ci0 + xc[i] * 8) * a.x_cs + tin;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v = ok ? src[(long)j * a.x_cs] : 0.f;
+                if (a.in_act) v = v >= 0.f ? v : v * a.in_slope;
+                xr[i][j] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < C::NWI; ++i) {
+            const int e = tid + i * 256;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (e < C::BM * C::NG) {
+                const int r = e / C::NG, g = e - r * C::NG;
+                const int tap = g / C::G8, c8 = g - tap * C::G8;
+                const int co = co0 + r;
+                if (co < a.Cout)
+                    v = *reinterpret_cast<const uint4*>(Wg + ((long)co * KT + tap) * a.Cin + ci0 + c8 * 8);
+            }
+            wr[i] = v;
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int i = 0; i < C::NXI; ++i) {
+            if (xc[i] < 0) continue;
+            float m = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(xr[i][j]));
+            ovf |= m > 65504.f;
+            uint4 hi, lo;
+            split8(xr[i], hi, lo);
+            *reinterpret_cast<uint4*>(Xh + xu[i] * C::XR + xc[i] * 8) = hi;
+            *reinterpret_cast<uint4*>(Xl + xu[i] * C::XR + xc[i] * 8) = lo;
+        }
+#pragma unroll
+        for (int i = 0; i < C::NWI; ++i) {
+            const int e = tid + i * 256;
+            if (e < C::BM * C::NG) {
+                const int r = e / C::NG, g = e - r * C::NG;
+                const int tap = g / C::G8, c8 = g - tap * C::G8;
+                *reinterpret_cast<uint4*>(Ws + r * C::WR + tap * CC + c8 * 8) = wr[i];
+            }
+        }
+    };
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[f][i] = 0.f;
+
+    const int r32 = lane & 31, hsel = lane >> 5;
+    const _Float16* wrow = Ws + (wm * 32 + r32) * C::WR;
+    load(0);
+    store();
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load((c + 1) * CC);
+#pragma unroll
+        for (int j = ks; j < C::NSTEP; j += KS) {
+            const int g = 2 * j + hsel;                 // this lane's 8-channel group
+            const bool gv = g < C::NG;
+            const int tap = gv ? g / C::G8 : 0, c8 = gv ? g - tap * C::G8 : 0;
+            h8 A = *reinterpret_cast<const h8*>(wrow + tap * CC + c8 * 8);
+            if (!gv) A = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const int row = wn * 64 + f * 32 + r32 + tap * dil;
+                const h8 Bl = *reinterpret_cast<const h8*>(Xl + row * C::XR + c8 * 8);
+                const h8 Bh = *reinterpret_cast<const h8*>(Xh + row * C::XR + c8 * 8);
+                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bl, acc[f], 0, 0, 0);
+                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bh, acc[f], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+        if (c + 1 < nch) {
+            store();
+            __syncthreads();
+        }
+    }
+    if (ovf) atomicOr(a.ovf, 1);
+
+    if (KS > 1) {
+        // waves ks > 0 park their partials; ks == 0 adds them in ks order
+        float* red = reinterpret_cast<float*>(smem);
+        const int tile = wm * WN + wn;
+        if (ks > 0) {
+            float* p = red + ((long)((ks - 1) * WM * WN + tile) * 2 * 16) * 64;
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) p[(f * 16 + i) * 64 + lane] = acc[f][i];
+        }
+        __syncthreads();
+        if (ks > 0) return;
+#pragma unroll
+        for (int s = 1; s < KS; ++s) {
+            const float* p = red + ((long)((s - 1) * WM * WN + tile) * 2 * 16) * 64;
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[f][i] += p[(f * 16 + i) * 64 + lane];
+        }
+    }
+    const int cobase = co0 + wm * 32 + 4 * hsel;
+    float sc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int co = cobase + (r & 3) + 8 * (r >> 2);
+        sc[r] = co < a.Cout ? a.wscale[co] : 0.f;
+    }
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int t = t0 + wn * 64 + f * 32 + r32;
+        if (t >= a.n_t) continue;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[f][r] * sc[r];
+        conv_epilogue16(a, cobase, t, 0, v);
+    }
+}
+
+template <int KT, int CC>
+bool launch_h(const ConvArgs& a, hipStream_t s) {
+    // (WM, WN, KS) by estimated time: block rounds at 2 blocks per CU x tile area
+    // (4 waves share a block's work whatever KS), a small price per K-split way
+    // (fits tools/convh_prof.sh on the generator's stage shapes).
+    struct Cand { int wm, wn, ks; };
+    static const Cand cands[4] = {{2, 2, 1}, {1, 2, 2}, {1, 1, 4}, {1, 4, 1}};
+    int best = -1;
+    double best_cost = 1e30;
+    for (int i = 0; i < 4; ++i) {
+        const int bm = 32 * cands[i].wm, bn = 64 * cands[i].wn;
+        const long blocks = (long)((a.n_t + bn - 1) / bn) * ((a.Cout + bm - 1) / bm);
+        const long rounds = (blocks + 511) / 512;
+        const double cost = (double)rounds * bm * bn * (1.0 + 0.1 * (cands[i].ks - 1));
+        if (cost < best_cost) { best_cost = cost; best = i; }
+    }
+    static const int forced = [] { const char* e = std::getenv("GENIE_CONVH_CFG"); return e ? std::atoi(e) : -1; }();
+    if (forced >= 0 && forced < 4) best = forced;
+    const Cand c = cands[best];
+    const dim3 grid((a.n_t + 64 * c.wn - 1) / (64 * c.wn), (a.Cout + 32 * c.wm - 1) / (32 * c.wm));
+    if (c.wm == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1>), grid, dim3(256), 0, s, a);
+    else if (c.ks == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 2, 2>), grid, dim3(256), 0, s, a);
+    else if (c.ks == 4) hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 1, 4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 4, 1>), grid, dim3(256), 0, s, a);
+    return true;
+}
+
+template <int KT>
+bool launch_kt(const ConvArgs& a, hipStream_t s) {
+    if (a.Cin % 32 == 0) return launch_h<KT, 32>(a, s);
+    if (a.Cin % 8 == 0) return launch_h<KT, 8>(a, s);
+    return false;
+}
+
+}  // namespace
+
+bool conv1d_h(const ConvArgs& a, hipStream_t s) {
+    if (!a.wh || !a.wscale || !a.ovf) return false;
+    if (a.phases > 1 || a.x_ts != 1 || a.dil < 1 || a.dil > DMAX || a.o_tstride != 1) return false;
+    if ((reinterpret_cast<uintptr_t>(a.wh) & 15) != 0) return false;
+    switch (a.K) {
+        case 3: return launch_kt<3>(a, s);
+        case 7: return launch_kt<7>(a, s);
+        case 11: return launch_kt<11>(a, s);
+        default: return false;
+    }
+}
+
+}  // namespace gsv

@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -39,7 +40,30 @@ static float* up_vec(gsv_engine* e, const std::vector<float>& v) {
     return d;
 }
 
-static int load_conv(gsv_engine* e, const std::string& base, Conv& c, bool wn, bool bias = true) {
+// fp16 copy [Cout][K][Cin] of a conv weight [Cout][Cin][K] for the f16-split path
+// (vits_convh.hip), or nullptr when some value is not fp16-exact (then the conv
+// stays on the f32 path).  scale[co] = g/||v|| (weight norm) or 1.
+static bool upload_f16(gsv_engine* e, const std::vector<float>& v, int cout, int cin, int k,
+                       const std::vector<float>& scale, Conv& c) {
+    std::vector<__half> h((size_t)cout * cin * k);
+    for (int co = 0; co < cout; ++co)
+        for (int ci = 0; ci < cin; ++ci)
+            for (int j = 0; j < k; ++j) {
+                const float x = v[((size_t)co * cin + ci) * k + j];
+                const __half hx = __float2half(x);
+                if (__half2float(hx) != x) return false;
+                h[((size_t)co * k + j) * cin + ci] = hx;
+            }
+    c.wh = (__half*)e->dalloc(h.size() * 2);
+    c.wscale = (float*)e->dalloc((size_t)cout * 4);
+    if (!c.wh || !c.wscale) return false;
+    hipMemcpy(c.wh, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    hipMemcpy(c.wscale, scale.data(), (size_t)cout * 4, hipMemcpyHostToDevice);
+    return true;
+}
+
+static int load_conv(gsv_engine* e, const std::string& base, Conv& c, bool wn, bool bias = true,
+                     bool f16 = false) {
     std::vector<float> w;
     const Staged* s = nullptr;
     if (wn) {
@@ -48,6 +72,18 @@ static int load_conv(gsv_engine* e, const std::string& base, Conv& c, bool wn, b
         if (!v || !g) return set_error(GSV_E_WEIGHT, "missing weight " + base + ".weight_v/g");
         w = fold_wn(v, g);
         s = v;
+        if (f16) {
+            // the same g/||v|| as fold_wn, applied to the f32 sums instead of the weights
+            const long o = v->dims[0], per = (long)v->data.size() / o;
+            std::vector<float> sc(o);
+            for (long i = 0; i < o; ++i) {
+                double q = 0;
+                for (long j = 0; j < per; ++j) q += (double)v->data[i * per + j] * v->data[i * per + j];
+                sc[i] = g->data[i] / (float)std::sqrt(q);
+            }
+            upload_f16(e, v->data, (int)v->dims[0], (int)v->dims[1], v->dims.size() > 2 ? (int)v->dims[2] : 1,
+                       sc, c);
+        }
     } else {
         s = e->find(base + ".weight");
         if (!s) return set_error(GSV_E_WEIGHT, "missing weight " + base + ".weight");
@@ -215,7 +251,7 @@ int gsv_engine::finalize_vits() {
             for (int m = 0; m < 3; ++m) {
                 const std::string n = D + "resblocks." + std::to_string(j) + (c == 0 ? ".convs1." : ".convs2.") +
                                       std::to_string(m);
-                if (int r = load_conv(this, n, V.rb[j][c][m], true)) return r;
+                if (int r = load_conv(this, n, V.rb[j][c][m], true, true, true)) return r;
             }
     if (!pp)
         if (int r = load_ref_enc(this, "vq_model.ref_enc.", V.ref)) return r;
@@ -241,6 +277,7 @@ int gsv_engine::finalize_prompt_encoder() {
 // this thread (set by SplitkScope; conv1d splits only when it is set).
 static thread_local float* tls_splitk = nullptr;
 static thread_local long tls_splitk_cap = 0;
+static thread_local int* tls_ovf = nullptr;   // set while the f16-split MRF path is enabled
 struct SplitkScope {
     SplitkScope(float* p, long cap) { tls_splitk = p; tls_splitk_cap = cap; }
     ~SplitkScope() { tls_splitk = nullptr; tls_splitk_cap = 0; }
@@ -255,6 +292,7 @@ static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode
     a.out = out; a.o_cs = T; a.o_ts = 1; a.n_t = T; a.o_tstride = 1; a.o_toff = 0; a.o_len = T;
     a.mode = mode; a.r_cs = T; a.r_ts = 1;
     a.phases = 1;
+    if (tls_ovf && c.wh) { a.wh = c.wh; a.wscale = c.wscale; a.ovf = tls_ovf; }
     return a;
 }
 
@@ -366,10 +404,38 @@ static int ensure_vits_ws(gsv_engine* e, int T, int S, int n_audio) {
     return 0;
 }
 
+// The MRF convs run on the f16-split MFMA path when enabled; an activation too
+// large for fp16 sets the overflow flag, and the utterance is then decoded again
+// on the f32 path (same kernels otherwise), so the output never depends on the
+// fp16 range.  The flag check is a host sync on the caller's stream.
 int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int G,
                             const float* ref_audio, int n_audio, const float* ge_in,
                             const float* ge_adv_in, const float* eps, float noise_scale, float* audio,
                             hipStream_t s) {
+    if (use_convh && !vovf) {
+        if (hipMalloc(&vovf, 64) != hipSuccess || hipHostMalloc((void**)&vovf_host, 64, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "overflow flag alloc");
+        hipMemset(vovf, 0, 64);
+    }
+    if (!use_convh)
+        return vits_decode_pass(text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_scale,
+                                audio, s, false);
+    if (int r = vits_decode_pass(text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_scale,
+                                 audio, s, true))
+        return r;
+    hipMemcpyAsync(vovf_host, vovf, 4, hipMemcpyDeviceToHost, s);
+    if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vits sync");
+    if (*vovf_host == 0) return 0;
+    hipMemsetAsync(vovf, 0, 4, s);
+    ++vits_f32_reruns;
+    return vits_decode_pass(text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_scale, audio,
+                            s, false);
+}
+
+int gsv_engine::vits_decode_pass(const int64_t* text_seq, int n_text, const int64_t* sem, int G,
+                                 const float* ref_audio, int n_audio, const float* ge_in,
+                                 const float* ge_adv_in, const float* eps, float noise_scale, float* audio,
+                                 hipStream_t s, bool f16) {
     const VitsWeights& V = vits;
     if (!V.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
     if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
@@ -380,6 +446,8 @@ int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* 
     if (int r = ensure_vits_ws(this, T, S, pp ? 0 : n_audio)) return r;
     VitsWorkspace& W = vws;
     SplitkScope sk(W.splitk, W.splitk_cap);
+    tls_ovf = f16 ? vovf : nullptr;
+    struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timing) hipEventRecord(ev[4], s);
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
@@ -586,4 +654,17 @@ extern "C" int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w
     a.part = splitk_ws; a.part_cap = splitk_cap;
     conv1d(a, (hipStream_t)stream);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "debug conv");
+}
+
+extern "C" int gsv_debug_conv1d_h(const float* x, int cin, int tin, const void* wh, const float* scale,
+                                  int cout, int k, int dil, int pad, const float* bias, float* out, int tout,
+                                  int in_act, float slope, int* ovf, void* stream) {
+    ConvArgs a{};
+    a.x = x; a.x_cs = tin; a.x_ts = 1; a.Cin = cin; a.Tin = tin;
+    a.Cout = cout; a.K = k; a.dil = dil; a.pad = pad; a.bias = bias;
+    a.out = out; a.o_cs = tout; a.o_ts = 1; a.n_t = tout; a.o_tstride = 1; a.o_toff = 0; a.o_len = tout;
+    a.in_act = in_act; a.in_slope = slope; a.mode = CV_STORE; a.phases = 1;
+    a.wh = (const __half*)wh; a.wscale = scale; a.ovf = ovf;
+    if (!conv1d_h(a, (hipStream_t)stream)) return set_error(GSV_E_ARG, "conv shape not covered by the f16 path");
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "debug conv h");
 }

@@ -81,6 +81,9 @@ def lib():
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_float, vp, ctypes.c_int64, vp]
+        L.gsv_debug_conv1d_h.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_float, vp, vp]
         L.gsv_debug_ktrace.argtypes = [vp, vp, ctypes.c_int]
         L.gsv_debug_sample.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(Sampler), ctypes.c_int, vp, vp, vp]
         L.gsv_probe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -100,7 +103,7 @@ EXPORTED = (
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
-    "gsv_set_option", "gsv_debug_ptrace",
+    "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h",
 )
 
 
@@ -137,6 +140,23 @@ def debug_conv1d(x, w, bias=None, dil=1, pad=0, in_act=False, slope=0.1, splitk_
                                   tout, int(in_act), ctypes.c_float(slope), _ptr(splitk_ws),
                                   0 if splitk_ws is None else splitk_ws.numel(), _stream()), "gsv_debug_conv1d")
     return out
+
+
+def debug_conv1d_h(x, v, scale, bias=None, dil=1, pad=0, in_act=False, slope=0.1):
+    """Run the f16-split MFMA conv once (tests): x [Cin,T] cuda fp32, v [Cout,Cin,K] fp16-valued,
+    scale [Cout] (weight = v * scale).  Returns (out, overflow flag)."""
+    torch = _torch()
+    cin, tin = x.shape
+    cout, _, k = v.shape
+    tout = tin + 2 * pad - dil * (k - 1)
+    wh = v.to(torch.float16).permute(0, 2, 1).contiguous().to(x.device)     # [Cout][K][Cin]
+    sc = scale.to(torch.float32).contiguous().to(x.device)
+    out = torch.empty((cout, tout), dtype=torch.float32, device=x.device)
+    ovf = torch.zeros(1, dtype=torch.int32, device=x.device)
+    _check(lib().gsv_debug_conv1d_h(_ptr(x), cin, tin, _ptr(wh), _ptr(sc), cout, k, dil, pad, _ptr(bias), _ptr(out),
+                                    tout, int(in_act), ctypes.c_float(slope), _ptr(ovf), _stream()),
+           "gsv_debug_conv1d_h")
+    return out, int(ovf.item())
 
 
 def debug_sample(logits, seen, sampler: "Sampler", step: int):

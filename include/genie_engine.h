@@ -149,6 +149,14 @@ int gsv_debug_copy(gsv_engine* eng, const char* name, float* dst, int64_t n, voi
 int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout, int k, int dil,
                      int pad, const float* bias, float* out, int tout, int in_act, float slope,
                      float* splitk_ws, int64_t splitk_cap, void* stream);
+/* The same conv on the f16-split MFMA path (vits_convh.hip, the MRF convs of
+ * dec.resblocks.* in vits_fp32.onnx): wh = fp16 weights [cout][k][cin], scale =
+ * per-output-channel f32 factor on the sums (weight norm g/||v||); *ovf (device
+ * int) is OR-ed with 1 when an input exceeds the fp16 range.  GSV_E_ARG when the
+ * shape is not covered (k in {3,7,11}, cin % 8 == 0, dil <= 5). */
+int gsv_debug_conv1d_h(const float* x, int cin, int tin, const void* wh, const float* scale, int cout,
+                       int k, int dil, int pad, const float* bias, float* out, int tout, int in_act,
+                       float slope, int* ovf, void* stream);
 /* Run the decode sampler kernel once on logits (device [B][1025]) with the
  * token-presence bitmaps seen (device u32 [B][33]) at loop step `step`
  * (Philox counter); tokens (device i64 [B]) and stop flags (device u8 [B]). */

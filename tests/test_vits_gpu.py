@@ -51,6 +51,25 @@ def test_vits_waveform(setup, G, S, noise):
     assert np.abs(out - ref).max() < 2e-3
 
 
+@pytest.mark.parametrize("convh", [0, 1])
+def test_vits_waveform_conv_paths(setup, convh):
+    """MRF convs on the f32 MFMA path (convh=0) and on the f16-split path (1, default)."""
+    ver, e, vm, _ = setup
+    G, S = 40, 30
+    txt = synth.synth_phones(S, f"vt{S}")
+    sem = ((np.arange(G, dtype=np.int64) * 53 + 7) % 1024).reshape(1, 1, G)
+    eps = synth.rng_for(f"eps{G}").standard_normal((1, 192, 2 * G)).astype(np.float32)
+    kw = _cond(ver)
+    ref = vm(txt, sem, eps=eps, **kw).numpy()
+    e.set_option("convh", convh)
+    try:
+        out = e.vits_decode(txt, sem, eps=eps, **kw).cpu().numpy()
+    finally:
+        e.set_option("convh", 1)
+    rms = float(np.sqrt(np.mean((out - ref) ** 2)))
+    assert rms <= RMS_TOL, f"rms {rms:.3e}"
+
+
 def test_prompt_encoder(setup):
     ver, e, _, w = setup
     if ver == "v2":
