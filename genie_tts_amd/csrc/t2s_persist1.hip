@@ -264,7 +264,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         const unsigned tag = ws.tag(s);
         const int kv = kv0 + s;
         for (int l = grp; l < 24; l += NG) {
-            const bool probe = a.trace && s == 8 && l == 12;
+            const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
             float xv;
             if (!form_x(a, ws, s, l, ny0 + s, b2p, n2w, n2b, xv, sh)) return;
@@ -499,11 +499,12 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
         if (!step_start(a, ws, s, grp == 0, sh)) break;
         const unsigned tag = ws.tag(s);
         for (int l = grp; l < 24; l += NG) {
-            const bool probe = a.trace && s == 8 && l == 12;
+            const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
             float xv;
             if (!form_x(a, ws, s, l, ny0 + s, b2p, n2w, n2b, xv, sh)) return;
             STAMP1(1);
+            float h1_pub = 0.f;
             // ---- h1_l = LN1(x_l + (bo + sum_h PA[l][h])), heads summed in order
             {
                 bool ok = true;
@@ -517,7 +518,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 STAMP1(2);
                 ln_stats<1>(v, mean, den, sh.red);
                 const float h1 = (v[0] - mean[0]) / den[0] * n1w + n1b;
-                if ((tid >> 5) == j) st_gran(ws.PFH(s, l, 16) + tid, tag, h1);
+                h1_pub = h1;   // published with the FFN2 partials: no store in flight during FFN1/FFN2
                 sh.x[tid] = h1;
                 if (tid < 128) sh.b1[tid] = b1v;
             }
@@ -549,6 +550,9 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 }
                 st_gran(ws.PFH(s, l, j) + tid, tag, acc);
             }
+            // h1 slice of this workgroup (the next layer's residual input), after the
+            // partials: a store in flight stalls every later vmcnt(0) (spill reloads)
+            if ((tid >> 5) == j) st_gran(ws.PFH(s, l, 16) + tid, tag, h1_pub);
             STAMP1(4);
             __syncthreads();   // fs / b1 consumed before the next prefetch lands
             prefetch(l + NG < 24 ? l + NG : grp);
