@@ -72,8 +72,29 @@ struct Ws1 {
     __device__ u64* TK(int s) const { return slot(s) + oTK; }
 };
 
+// Small arrays first: their LDS offsets stay below 64 KB, so an access is the
+// lane's tid-based address plus an instruction offset (no extra address
+// registers live across the layer loop -- the kernel sits at the 256-VGPR limit).
 struct Shared1 {
+    float x[512];                   // x_l (attention), x_24 (logits)
+    float qkv[96];
+    float os[32];
+    float b1[128];                  // FFN1 bias of the slice
+    float lnb[2][512];              // LayerNorm inputs: [0] x_l (form_x), [1] LN1 (FFN)
+    _Float16 xh[512], xl[512];      // MFMA row operand: h1 split hi + lo (FFN1)
+    _Float16 fh[128], fl[128];      // MFMA row operand: FFN1 output split hi + lo (FFN2)
+    float p2[3][512];               // LN2 of layer l-1 (b2, scale, shift) for form_x (LDS-DMA)
+    float red[2 * PWV];
+    float wred[2][PWV];
+    uint32_t seen[33];
+    int tok, fin, fail;
+    unsigned long long stamp[16];   // [0,8) 100 MHz realtime, [8,16) shader clock
+    SampleLds<PT> samp;
     union {
+        struct {                    // FFN role
+            uint4 wp[LROWS + 1][64];   // logits rows (group LOGIT_GRP), resident for the launch
+            float lp23[3][512];        // LN2 of layer 23 (b2, scale, shift), logits group
+        } ff;
         struct {                    // attention role
             float k[KVL1 * 32];     // K/V rows [0, min(kv, KVL1)) of the head (LDS-DMA)
             float v[KVL1 * 32];
@@ -81,21 +102,7 @@ struct Shared1 {
             float ov[16][32];       // P.V partial sums of 16 key groups
             float lg[PERSIST_LGS];  // logits (sampler)
         } at;
-        struct {                    // FFN role
-            uint4 wp[LROWS + 1][64];   // logits rows (group LOGIT_GRP), resident for the launch
-        } ff;
     };
-    float x[512];                   // x_l (attention), h1_l (FFN), x_24 (logits)
-    float qkv[96];
-    float os[32];
-    float fs[128];                  // FFN1 output of the slice
-    float b1[128];                  // FFN1 bias of the slice
-    float red[2 * PWV];
-    float wred[2][PWV];
-    uint32_t seen[33];
-    int tok, fin, fail;
-    unsigned long long stamp[16];   // [0,8) 100 MHz realtime, [8,16) shader clock
-    SampleLds<PT> samp;
 };
 
 #define STAMP1(i)                                                                         \
@@ -111,6 +118,57 @@ __device__ __forceinline__ bool block_ok1(bool ok, Shared1& sh) {
     __syncthreads();
     return sh.fail == 0;
 }
+
+// LayerNorm statistics (mean, then mean of squared deviations, as the graph's
+// LayerNormalization) of a 512-value row already in LDS, computed by EVERY wave
+// over the whole row: 8 values per lane, the same order in every wave and every
+// workgroup.  One barrier (the caller's, after the row is written) per LayerNorm.
+__device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, float& den) {
+    const int lane = threadIdx.x & 63;
+    const float4 a = *reinterpret_cast<const float4*>(buf + 8 * lane);
+    const float4 b = *reinterpret_cast<const float4*>(buf + 8 * lane + 4);
+    const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const float s = ((v8[0] + v8[1]) + (v8[2] + v8[3])) + ((v8[4] + v8[5]) + (v8[6] + v8[7]));
+    mean = wave_sum_dpp(s) * (1.0f / 512.0f);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float d = v8[k] - mean;
+        q += d * d;
+    }
+    den = sqrtf(wave_sum_dpp(q) * (1.0f / 512.0f) + 1e-5f);
+}
+
+// Batch-1 GEMV on the 16x16x32 f16 MFMA (v_mfma_f32_16x16x32_f16).  The weights
+// are exactly fp16; the f32 activation vector is split x = hi + lo into two fp16
+// rows (A rows 0 and 1, rows 2..15 zero), so C row 0 + C row 1 = W.x with the
+// dropped residual ~2^-22 |x| (f32-level, as the prefill GEMM).  Lane l holds
+// A[row l & 15][k = 8 (l >> 4) + i], B[k = 8 (l >> 4) + i][col l & 15] and
+// C[row 4 (l >> 4) + r][col l & 15]: the result of column l (l < 16) is
+// c[0] + c[1].  Replaces 2 VALU ops per MAC (cvt + fma) and the DPP row sums.
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ h8v bfrag(const uint4 w) { return __builtin_bit_cast(h8v, w); }
+// This lane's A-operand base: row 0 reads hi, row 1 lo; chunk c is one
+// ds_read_b128 at base + 32 c (an instruction offset).  Rows 2..15 are zero and
+// read nothing: only 8 lanes of the wave touch LDS (128 B per fragment, not 1 KB).
+__device__ __forceinline__ const _Float16* abase(const _Float16* hi, const _Float16* lo, int lane) {
+    return ((lane & 15) == 0 ? hi : lo) + 8 * (lane >> 4);
+}
+__device__ __forceinline__ h8v afrag(const _Float16* base, int k0, bool row01) {
+    uint4 u = make_uint4(0u, 0u, 0u, 0u);
+    if (row01) u = *reinterpret_cast<const uint4*>(base + k0);
+    return __builtin_bit_cast(h8v, u);
+}
+__device__ __forceinline__ f32x4 mfma16(h8v a, h8v b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// fp16 split of an f32 activation; false when |v| is beyond the fp16 range
+__device__ __forceinline__ bool split_h(float v, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)v;
+    lo = (_Float16)(v - (float)hi);
+    return fabsf(v) < 65504.f;
+}
+constexpr int ERR_F16_RANGE = 2;   // error word: an activation left the fp16 range (host re-runs)
 
 // Scores of the general case (more than 512 keys or rows beyond the LDS stage),
 // out of line so the common path keeps its registers.  Returns the lane's max.
@@ -179,12 +237,26 @@ __device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0
     return go;
 }
 
+// 512 floats src -> LDS dst by LDS-DMA, half h (256 floats, one 1-KB wave
+// instruction).  Per-layer vectors travel this way: no registers are held for
+// them across the layers a workgroup waits; every reader is behind a barrier.
+__device__ __forceinline__ void dma_half(const float* src, float* dst, int h, int lane) {
+    __builtin_amdgcn_global_load_lds(src + 256 * h + lane * 4, dst + 256 * h, 16, 0, 0);
+}
+// LN2 of layer l - 1 -> sh.p2, by waves 0..5 (call from every wave; l > 0)
+__device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int lane) {
+    if (w < 2) dma_half(Q.b2, sh.p2[0], w & 1, lane);
+    else if (w < 4) dma_half(Q.n2w, sh.p2[1], w & 1, lane);
+    else if (w < 6) dma_half(Q.n2b, sh.p2[2], w & 1, lane);
+}
+
 // x_l for column tid: layer 0 from the token (E_audio[tok] + alpha * pe[n]),
 // otherwise LN2_{l-1}(h1_{l-1} + (b2 + sum_j PF[l-1][j])), the partials summed in
-// slice order.  A sleeping lane waits for the wake-up granule (layer l-2's output)
-// before every thread polls its 17 granules.
-__device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, float b2p,
-                                       float n2w, float n2b, float& xv, Shared1& sh) {
+// slice order; lp2 = LDS rows {b2, scale, shift} of LN2_{l-1}.  A sleeping lane
+// waits for the wake-up granule (layer l-2's output) before every thread polls
+// its 17 granules.
+__device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, const float* lp2,
+                                       float& xv, Shared1& sh) {
     const int tid = threadIdx.x;
     if (l == 0) {
         xv = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
@@ -201,10 +273,12 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
     float f = g[0];
 #pragma unroll
     for (int j = 1; j < NF; ++j) f += g[j];
-    float v[1] = {g[16] + (b2p + f)}, mean[1], den[1];
+    const float v = g[16] + (lp2[tid] + f);
+    sh.lnb[0][tid] = v;
     if (!block_ok1(ok, sh)) return false;
-    ln_stats<1>(v, mean, den, sh.red);
-    xv = (v[0] - mean[0]) / den[0] * n2w + n2b;
+    float mean, den;
+    ln_row_stats(sh.lnb[0], mean, den);
+    xv = (v - mean) / den * lp2[512 + tid] + lp2[1024 + tid];
     return true;
 }
 
@@ -225,7 +299,6 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
     const long kvoff = (long)h * a.tmax * 32;
     uint4 wq[12], wo[4];
     float bq[3] = {0.f, 0.f, 0.f};
-    float b2p = 0.f, n2w = 0.f, n2b = 0.f;   // LN2 of layer l-1
     auto prefetch = [&](int l, int kv) {
         const PLayer& P = a.L[l];
         // wave w, lane group r4 = lane >> 4: rows (m, h*32 + 4w + r4) of W_in for m = q, k, v;
@@ -241,10 +314,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         // out-projection: thread tid owns output column tid, W_out[tid][h*32 .. h*32+32)
 #pragma unroll
         for (int k = 0; k < 4; ++k) wo[k] = ldg16(P.w_out + (long)tid * 512 + h * 32 + 8 * k, 0);
-        if (l > 0) {
-            const PLayer& Q = a.L[l - 1];
-            b2p = ldg(Q.b2, tid); n2w = ldg(Q.n2w, tid); n2b = ldg(Q.n2b, tid);
-        }
+        if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
         // K/V rows [0, min(kv, KVL1)) -> LDS, 8 rows (1 KB) per wave instruction.  Rows of
         // the last chunk past kv are read (allocated: tmax >= kv + 16) and never used.
         const float* K = a.kc[l] + kvoff;
@@ -267,7 +337,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
             float xv;
-            if (!form_x(a, ws, s, l, ny0 + s, b2p, n2w, n2b, xv, sh)) return;
+            if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
             sh.x[tid] = xv;
             __syncthreads();
             STAMP1(1);
@@ -462,7 +532,6 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
         sh.fin = a.done[0] ? 1 : 0;
         sh.fail = 0;
     }
-    float lb2 = 0.f, ln2w = 0.f, ln2b = 0.f;   // LN2 of layer 23 (logits)
     if (logits) {
         // rows 64 j + r (r < 64) and, on the last slice, the EOS row 1024 -- resident for the launch
         for (int e = tid; e < (LROWS + 1) * 64; e += PT) {
@@ -471,26 +540,29 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             sh.ff.wp[r][c] = (r < LROWS || j == NF - 1) ? ldg16(a.w_pred, (long)row * 512 + 8 * c)
                                                         : make_uint4(0u, 0u, 0u, 0u);
         }
-        lb2 = ldg(a.L[23].b2, tid); ln2w = ldg(a.L[23].n2w, tid); ln2b = ldg(a.L[23].n2b, tid);
+        sh.ff.lp23[0][tid] = ldg(a.L[23].b2, tid);
+        sh.ff.lp23[1][tid] = ldg(a.L[23].n2w, tid);
+        sh.ff.lp23[2][tid] = ldg(a.L[23].n2b, tid);
     }
     uint4 w1r[16], w2r[16];
-    float b2p = 0.f, n2w = 0.f, n2b = 0.f;   // LN2 of layer l-1
     float bo = 0.f, n1w = 0.f, n1b = 0.f;    // out-proj bias and LN1 of layer l
     float b1v = 0.f;                         // FFN1 bias of hidden unit 128 j + tid (tid < 128)
     auto prefetch = [&](int l) {
         const PLayer& P = a.L[l];
-        // FFN1: wave w holds rows 128 j + 16 w + q (q < 16), lane columns [8 lane, 8 lane + 8)
+        // MFMA B fragments (lane: column lane & 15, k 8 (lane >> 4) .. + 8 of each 32-chunk)
+        // FFN1: wave w -> hidden rows 128 j + 16 w + (lane & 15), K chunks c < 16
+        const int n16 = lane & 15, k8 = 8 * (lane >> 4);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) w1r[q] = ldg16(P.w1 + (long)(j * 128 + w * 16 + q) * 512, lane * 8);
-        // FFN2: thread tid owns output column tid, W2[tid][128 j .. 128 j + 128)
+        for (int c = 0; c < 16; ++c) w1r[c] = ldg16(P.w1 + (long)(j * 128 + w * 16 + n16) * 512 + 32 * c + k8, 0);
+        // FFN2: wave w -> output columns 64 w + 16 t + (lane & 15), hidden chunks 128 j + 32 c
 #pragma unroll
-        for (int k = 0; k < 16; ++k) w2r[k] = ldg16(P.w2 + (long)tid * 2048 + j * 128 + 8 * k, 0);
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + n16) * 2048 + j * 128 + 32 * c + k8, 0);
         b1v = tid < 128 ? ldg(P.b1, j * 128 + tid) : 0.f;
         bo = ldg(P.b_out, tid); n1w = ldg(P.n1w, tid); n1b = ldg(P.n1b, tid);
-        if (l > 0) {
-            const PLayer& Q = a.L[l - 1];
-            b2p = ldg(Q.b2, tid); n2w = ldg(Q.n2w, tid); n2b = ldg(Q.n2b, tid);
-        }
+        if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
     };
     __syncthreads();
     if (sh.fin) return;
@@ -502,7 +574,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
             float xv;
-            if (!form_x(a, ws, s, l, ny0 + s, b2p, n2w, n2b, xv, sh)) return;
+            if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
             STAMP1(1);
             float h1_pub = 0.f;
             // ---- h1_l = LN1(x_l + (bo + sum_h PA[l][h])), heads summed in order
@@ -513,42 +585,65 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 float sum = pa[0];
 #pragma unroll
                 for (int hh = 1; hh < 16; ++hh) sum += pa[hh];
-                float v[1] = {xv + (bo + sum)}, mean[1], den[1];
+                const float v = xv + (bo + sum);
+                sh.lnb[1][tid] = v;
+                if (tid < 128) sh.b1[tid] = b1v;
                 if (!block_ok1(ok, sh)) return;
                 STAMP1(2);
-                ln_stats<1>(v, mean, den, sh.red);
-                const float h1 = (v[0] - mean[0]) / den[0] * n1w + n1b;
+                float mean, den;
+                ln_row_stats(sh.lnb[1], mean, den);
+                const float h1 = (v - mean) / den * n1w + n1b;
                 h1_pub = h1;   // published with the FFN2 partials: no store in flight during FFN1/FFN2
-                sh.x[tid] = h1;
-                if (tid < 128) sh.b1[tid] = b1v;
+                split_h(h1, sh.xh[tid], sh.xl[tid]);   // LayerNorm output: always in fp16 range
             }
             __syncthreads();
             STAMP1(6);
-            // ---- FFN1 rows of this slice (16 per wave), ReLU
+            // ---- FFN1 rows of this slice on the MFMA (16 per wave), ReLU -> fh/fl
             {
-                const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[lane * 8]);
-                const float4 x1 = *reinterpret_cast<const float4*>(&sh.x[lane * 8 + 4]);
-                float acc[16];
+                const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                const bool r01 = (lane & 15) < 2;
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int q = 0; q < 16; ++q) acc[q] = dot8(w1r[q], x0, x1);
-                wave_sum_n<16>(acc);
-                if (lane == 63) {
+                for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
+                    h8v af[8];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) sh.fs[w * 16 + q] = fmaxf(sh.b1[w * 16 + q] + acc[q], 0.f);
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i), r01);
+#pragma unroll
+                    for (int i = 0; i < 8; i += 2) {
+                        c0 = mfma16(af[i], bfrag(w1r[cb + i]), c0);
+                        c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
+                    }
+                }
+                if (lane < 16) {
+                    const float f = fmaxf(sh.b1[w * 16 + lane] + ((c0[0] + c1[0]) + (c0[1] + c1[1])), 0.f);
+                    if (!split_h(f, sh.fh[w * 16 + lane], sh.fl[w * 16 + lane])) {
+                        atomicCAS(a.err, 0, ERR_F16_RANGE);
+                        sh.fail = 1;
+                    }
                 }
             }
             __syncthreads();
+            if (sh.fail) return;
             STAMP1(3);
-            // ---- FFN2 slice (column tid) -> partial granule
+            // ---- FFN2 slice on the MFMA (64 output columns per wave) -> partial granules
             {
-                float acc = 0.f;
+                f32x4 acc[4];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const float4 fa = *reinterpret_cast<const float4*>(&sh.fs[8 * k]);
-                    const float4 fb = *reinterpret_cast<const float4*>(&sh.fs[8 * k + 4]);
-                    acc += dot8(w2r[k], fa, fb);
+                for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const _Float16* ab = abase(sh.fh, sh.fl, lane);
+                const bool r01 = (lane & 15) < 2;
+                h8v af[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) af[c] = afrag(ab, 32 * c, r01);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[t] = mfma16(af[c], bfrag(w2r[4 * t + c]), acc[t]);
+                if (lane < 16) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        st_gran(ws.PFH(s, l, j) + 64 * w + 16 * t + lane, tag, acc[t][0] + acc[t][1]);
                 }
-                st_gran(ws.PFH(s, l, j) + tid, tag, acc);
             }
             // h1 slice of this workgroup (the next layer's residual input), after the
             // partials: a store in flight stalls every later vmcnt(0) (spill reloads)
@@ -561,7 +656,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
         if (logits) {
             // ---- x_24 = LN2_23(h1_23 + b2 + sum PF_23), logits rows (ar_predict_layer, no bias)
             float xv;
-            if (!form_x(a, ws, s, 24, 0, lb2, ln2w, ln2b, xv, sh)) return;
+            if (!form_x(a, ws, s, 24, 0, &sh.ff.lp23[0][0], xv, sh)) return;
             sh.x[tid] = xv;
             __syncthreads();
             const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[lane * 8]);

@@ -15,7 +15,9 @@ import numpy as np
 
 from . import weights as W
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libgenie_engine.so")
+# GENIE_ENGINE_LIB: an alternative build of the same library (A/B timing of a kernel variant)
+_LIB_PATH = os.environ.get("GENIE_ENGINE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                                "libgenie_engine.so")
 _lib = None
 
 GSV_F32, GSV_F16 = 0, 1
