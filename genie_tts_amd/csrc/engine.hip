@@ -600,12 +600,16 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
 }
 
 int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) {
+    return decode_persistent_as(B, sp, st, B == 1 && use_persist1 && n_cu >= persist1_grid());
+}
+
+// one: the single-sequence kernel (t2s_persist1.hip) instead of the general one.
+int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one) {
     // One launch runs every loop step (t2s_persist.hip).  Hand-offs are tagged
     // granules in a ring; the launch epoch in the tag makes the ring reusable
     // without zeroing (re-zeroed when the epoch wraps or the layout changes).
     const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     if (tmax > persist_max_tokens()) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
-    const bool one = B == 1 && use_persist1 && n_cu >= persist1_grid();
     const size_t need = one ? persist1_ring_bytes() : persist_ring_bytes(B);
     const int layout = one ? -1 : B;   // ring layout key: the two kernels slot the ring differently
     if (need > pws_bytes || layout != pws_batch) {
@@ -655,6 +659,14 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
+    // code 2: the single-sequence kernel met an activation beyond the fp16 range of
+    // its split-operand MFMA GEMVs.  It stopped before writing the sequence state
+    // back (KV rows and tokens of the partial run are rewritten), so the same
+    // steps run again on the general kernel (f32 VALU arithmetic).
+    if (*perr_host == 2 && one) {
+        ++persist1_f16_reruns;
+        return decode_persistent_as(B, sp, st, false);
+    }
     if (*perr_host != 0)
         return set_error(GSV_E_HIP, "persistent decode: hand-off timeout (code " + std::to_string(*perr_host) + ")");
     if (probe) {
