@@ -78,7 +78,7 @@ struct Ws1 {
 struct Shared1 {
     float x[512];                   // x_l (attention), x_24 (logits)
     float qkv[96];
-    float os[32];
+    _Float16 osh[32], osl[32];      // MFMA row operand: head output split hi + lo (out-projection)
     float b1[128];                  // FFN1 bias of the slice
     float lnb[2][512];              // LayerNorm inputs: [0] x_l (form_x), [1] LN1 (FFN)
     _Float16 xh[512], xl[512];      // MFMA row operand: h1 split hi + lo (FFN1)
@@ -297,23 +297,22 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
     }
     if (sampler && tid < 33) sh.seen[tid] = a.seen[tid];
     const long kvoff = (long)h * a.tmax * 32;
-    uint4 wq[12], wo[4];
-    float bq[3] = {0.f, 0.f, 0.f};
+    uint4 wq[16], wo[4];
+    float bqv = 0.f;
     auto prefetch = [&](int l, int kv) {
         const PLayer& P = a.L[l];
-        // wave w, lane group r4 = lane >> 4: rows (m, h*32 + 4w + r4) of W_in for m = q, k, v;
-        // lane i16 = lane & 15 holds columns 8*i16 + 128*c (c < 4): a row is reduced over 16 lanes
-        const int r4 = lane >> 4, i16 = lane & 15;
-        const __half* wb = P.w_in + (long)(h * 32 + 4 * w + r4) * 512 + 8 * i16;
+        // MFMA B fragments (lane: column lane & 15, k 8 (lane >> 4) .. + 8 of each 32-chunk).
+        // q/k/v: wave w < 6 -> rows (m = w >> 1, dims 16 (w & 1) + (lane & 15)) of head h, K chunks c < 16
+        const int n16 = lane & 15, k8 = 8 * (lane >> 4);
+        if (w < 6) {
+            const int row = (w >> 1) * 512 + h * 32 + 16 * (w & 1) + n16;
 #pragma unroll
-        for (int m = 0; m < 3; ++m)
+            for (int c = 0; c < 16; ++c) wq[c] = ldg16(P.w_in + (long)row * 512 + 32 * c + k8, 0);
+            bqv = ldg(P.b_in, row);
+        }
+        // out-projection: wave w -> output columns 64 w + 16 t + (lane & 15), K = the head's 32 dims
 #pragma unroll
-            for (int c = 0; c < 4; ++c) wq[m * 4 + c] = ldg16(wb + (long)m * 512 * 512 + c * 128, 0);
-#pragma unroll
-        for (int m = 0; m < 3; ++m) bq[m] = ldg(P.b_in, m * 512 + h * 32 + 4 * w + r4);
-        // out-projection: thread tid owns output column tid, W_out[tid][h*32 .. h*32+32)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) wo[k] = ldg16(P.w_out + (long)tid * 512 + h * 32 + 8 * k, 0);
+        for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + h * 32 + k8, 0);
         if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
         // K/V rows [0, min(kv, KVL1)) -> LDS, 8 rows (1 KB) per wave instruction.  Rows of
         // the last chunk past kv are read (allocated: tmax >= kv + 16) and never used.
@@ -338,32 +337,26 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             STAMP1(0);
             float xv;
             if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
-            sh.x[tid] = xv;
+            split_h(xv, sh.xh[tid], sh.xl[tid]);   // LayerNorm output: always in fp16 range
             __syncthreads();
             STAMP1(1);
-            // ---- q, k, v of head h: 3 rows per lane group, 16 lanes per row
-            {
-                const int r4 = lane >> 4, i16 = lane & 15;
-                float acc[3] = {0.f, 0.f, 0.f};
+            // ---- q, k, v of head h on the MFMA: wave w < 6 -> 16 rows (C row 0 + row 1)
+            if (w < 6) {
+                const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                const bool r01 = (lane & 15) < 2;
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[8 * i16 + 128 * c]);
-                    const float4 x1 = *reinterpret_cast<const float4*>(&sh.x[8 * i16 + 128 * c + 4]);
+                for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
+                    h8v af[8];
 #pragma unroll
-                    for (int m = 0; m < 3; ++m) acc[m] += dot8(wq[m * 4 + c], x0, x1);
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i), r01);
+#pragma unroll
+                    for (int i = 0; i < 8; i += 2) {
+                        c0 = mfma16(af[i], bfrag(wq[cb + i]), c0);
+                        c1 = mfma16(af[i + 1], bfrag(wq[cb + i + 1]), c1);
+                    }
                 }
-#pragma unroll
-                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0xB1, 0xF>(acc[m]);
-#pragma unroll
-                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x4E, 0xF>(acc[m]);
-#pragma unroll
-                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x141, 0xF>(acc[m]);
-#pragma unroll
-                for (int m = 0; m < 3; ++m) acc[m] += dpp_f<0x140, 0xF>(acc[m]);
-                if (i16 == 0) {
-#pragma unroll
-                    for (int m = 0; m < 3; ++m) sh.qkv[m * 32 + 4 * w + r4] = bq[m] + acc[m];
-                }
+                if (lane < 16) sh.qkv[16 * w + lane] = bqv + ((c0[0] + c1[0]) + (c0[1] + c1[1]));
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
             __syncthreads();
@@ -453,20 +446,20 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 for (int kg = 0; kg < 16; ++kg) O += sh.at.ov[kg][tid];
 #pragma unroll
                 for (int ww = 0; ww < PWV; ++ww) L += sh.wred[1][ww];
-                sh.os[tid] = O / L;
+                split_h(O / L, sh.osh[tid], sh.osl[tid]);   // a convex combination of V rows
             }
             __syncthreads();
             STAMP1(4);
             // ---- out-projection slice of this head (column tid) -> partial granule
             {
-                float acc = 0.f;
+                const h8v af = afrag(abase(sh.osh, sh.osl, lane), 0, (lane & 15) < 2);
+                f32x4 acc[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float4 oa = *reinterpret_cast<const float4*>(sh.os + 8 * k);
-                    const float4 ob = *reinterpret_cast<const float4*>(sh.os + 8 * k + 4);
-                    acc += dot8(wo[k], oa, ob);
+                for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bfrag(wo[t]), f32x4{0.f, 0.f, 0.f, 0.f});
+                if (lane < 16) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) st_gran(ws.PA(s, l, h) + 64 * w + 16 * t + lane, tag, acc[t][0] + acc[t][1]);
                 }
-                st_gran(ws.PA(s, l, h) + tid, tag, acc);
                 // the new K/V row (read by this workgroup only, next step)
                 if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
                 else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
