@@ -651,6 +651,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.err = perr;
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
+    a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;
     const hipError_t le = one ? decode_persist1(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr)
@@ -954,6 +955,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist = value != 0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;
+    } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback
+        eng->persist1_f16_limit = value;
     } else if (n == "convh") {
         eng->use_convh = value != 0;
     } else if (n == "ptrace") {

@@ -210,6 +210,8 @@ struct PersistArgs {
     int smax;                                     // step cap of the launch
     int groups;                                   // layer groups (layer l -> group l % groups)
     unsigned long long* trace;                    // optional [grid][16] phase stamps (step 8, layer 12)
+    float f16_limit;                              // single-sequence kernel: largest |activation| its fp16
+                                                  // split accepts (65504; tests lower it)
 };
 int persist_groups(int B, int n_cu);   // 0: the grid does not fit
 int persist_grid(int B, int groups);

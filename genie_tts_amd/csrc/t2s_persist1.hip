@@ -609,7 +609,8 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 }
                 if (lane < 16) {
                     const float f = fmaxf(sh.b1[w * 16 + lane] + ((c0[0] + c1[0]) + (c0[1] + c1[1])), 0.f);
-                    if (!split_h(f, sh.fh[w * 16 + lane], sh.fl[w * 16 + lane])) {
+                    split_h(f, sh.fh[w * 16 + lane], sh.fl[w * 16 + lane]);
+                    if (!(fabsf(f) < a.f16_limit)) {
                         atomicCAS(a.err, 0, ERR_F16_RANGE);
                         sh.fail = 1;
                     }

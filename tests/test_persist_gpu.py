@@ -97,6 +97,25 @@ def test_persistent_natural_stop_max_steps(eng):
     assert len(a[0]) > 0
 
 
+def test_persistent_fp16_range_fallback(eng, oracle_model):
+    """An FFN activation beyond the fp16 range of the single-sequence kernel's split
+    MFMA operands stops it (error code 2) and the host re-runs the steps on the general
+    kernel.  The hook lowers the limit to 1.0 so that the fallback fires; the tokens
+    stay bit-exact vs the oracle."""
+    from genie_tts_amd.engine import make_sampler
+    from oracle import restate as R
+    inp = t2s_inputs(R=12, S=10, H=41, tag="p12")
+    steps = 30
+    eng.set_option("persist", 1)
+    eng.set_option("persist1_f16_limit", 1)
+    try:
+        out = eng.t2s_generate([inp], make_sampler(force_steps=steps))
+    finally:
+        eng.set_option("persist1_f16_limit", 0)
+    sem, _, _ = R.t2s_generate(character("v2")["t2s_encoder"], oracle_model, *_ordered(inp), force_steps=steps)
+    assert out[0].tolist() == sem.reshape(-1).tolist()
+
+
 def test_persistent_repeated_calls_are_deterministic(eng):
     from genie_tts_amd.engine import make_sampler
     inp = t2s_inputs(R=14, S=11, H=44, tag="rep")
