@@ -2,19 +2,28 @@
 """Benchmark: GPT-SoVITS inference (Genie hot path) on MI355X.
 
 Metric (BASELINE.json): real-time factor + utterances/sec, 20-char JP, V2 speaker.
-Workload (configs[1]): one V2 utterance through the whole path -- T2S encoder,
-prefill, greedy decode (forced to 81 loop steps -> 80 semantic tokens, since
-random weights never emit EOS), VITS (ref STFT + MelStyleEncoder, TextEncoder,
-flow, HiFi-GAN) -> 102,400 samples = 3.2 s of 32 kHz audio.  Nominal shapes
-(SURVEY §8): reference phones R=48, target phones S=45, HuBERT frames H=264
-(P=132 prompts), reference audio 5.3 s.  Synthetic weights/inputs (no
-checkpoints offline).  A "step" = one utterance; inputs are resident in HBM.
 
-Multi-GPU: one process per GPU (torchrun), independent replicas, no
-collective on the data path; barrier + max-over-ranks timing; value = all
-utterances / max time (weak scaling).
+Workloads (genie_tts_amd/workloads.py; synthetic seeded inputs and synthetic
+fp16-valued weights -- no checkpoints offline; random weights never emit EOS,
+so every utterance runs a forced number of loop steps):
+  single   (default, the headline line) configs[1]: one V2 utterance through the
+           whole path -- T2S encoder, prefill, greedy decode (81 loop steps ->
+           80 semantic tokens), VITS (ref STFT + MelStyleEncoder, TextEncoder,
+           flow, HiFi-GAN) -> 102,400 samples = 3.2 s of 32 kHz audio.  R=48,
+           S=45, H=264 (P=132 prompts), 5.3 s reference.  A step = one utterance.
+  batch64  configs[2]: 64 mixed-length JP sentences (S~U[30,60], G~U[50,110]),
+           top-k 5 sampled, ONE ragged batched decode + the vocoder per
+           utterance.  A step = the 64-sentence batch.
+  mixed100 configs[3]: V2ProPlus EN+ZH 100-sentence set, LPT-sharded over the
+           ranks (genie_tts_amd/replicas.py), each rank batching its shard.  A
+           step = the whole set (weak scaling does not apply: total work fixed).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+Inputs are resident in HBM before the timed region.  Multi-GPU: one process per
+GPU (torchrun), independent replicas, no collective on the data path; the
+barrier and the max-over-ranks time use a gloo (host) group -- no RCCL.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload single|batch64|mixed100]
+                       [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -30,27 +39,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "real-time factor + utterances/sec, 20-char JP, V2 speaker, 1/2/4/8 MI355X"
-R_PH, S_PH, H_SSL = 48, 45, 264
-FORCE_STEPS = 81                 # loop steps -> 80 kept tokens (Inference.py:108-109 trim)
-REF_AUDIO_S = 5.3
 SR = 32000
-HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
-F32_MFMA_PEAK_TFS = 157.3        # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 
 
-def build_inputs():
-    from genie_tts_amd import synth
-    ref = synth.synth_phones(R_PH, "bench-ref")
-    txt = synth.synth_phones(S_PH, "bench-text")
-    rb = np.zeros((R_PH, 1024), np.float32)          # JP: BERT features are zeros
-    tb = np.zeros((S_PH, 1024), np.float32)
-    ssl = synth.synth_ssl(H_SSL, "bench")
-    audio = synth.synth_ref_audio(int(REF_AUDIO_S * SR), "bench")
-    return ref, txt, rb, tb, ssl, audio
-
-
-def cpu_baseline(inputs, threads: int):
-    """Oracle restatement of Genie's ONNX-CPU path on the host cores (torch fp32)."""
+def cpu_baseline(wl, threads: int):
+    """Oracle restatement of Genie's ONNX-CPU path on the host cores (torch fp32),
+    one utterance of the workload (bounded sample)."""
     import torch
     from genie_tts_amd import synth
     from oracle import restate as R
@@ -58,12 +52,61 @@ def cpu_baseline(inputs, threads: int):
     w = synth.synthetic_character("v2")
     m = R.T2SModel(w["t2s"])
     vm = R.VitsModel(w["vits"], "v2")
-    ref, txt, rb, tb, ssl, audio = inputs
+    ref, it = wl.reference, wl.items[0]
+    tb = np.zeros((it.text_seq.shape[1], 1024), np.float32)
     t0 = time.perf_counter()
-    sem, _, _ = R.t2s_generate(w["t2s_encoder"], m, ref, rb, txt, tb, ssl, force_steps=FORCE_STEPS)
-    wav = vm(txt, sem, ref_audio=audio)
+    sem, _, _ = R.t2s_generate(w["t2s_encoder"], m, ref.ref_seq, ref.ref_bert, it.text_seq, tb, ref.ssl,
+                               force_steps=it.force_steps)
+    wav = vm(it.text_seq, sem, ref_audio=ref.audio_32k)
     dt = time.perf_counter() - t0
     return dt, int(wav.numel())
+
+
+class Runner:
+    """One replica: engine + device-resident inputs of its share of the workload."""
+
+    def __init__(self, wl, items, dev, device_index):
+        import torch
+        from genie_tts_amd import synth
+        from genie_tts_amd.engine import Engine, make_sampler
+        self.torch = torch
+        self.wl = wl
+        self.items = items
+        self.eng = Engine(synth.synthetic_character(wl.version), wl.version, device=device_index)
+        ref = wl.reference
+        T = lambda a, dt=None: torch.as_tensor(np.ascontiguousarray(a), device=dev)
+        self.d_ref = T(ref.ref_seq.reshape(-1))
+        self.d_ssl = T(ref.ssl.reshape(768, -1))
+        self.d_audio = T(ref.audio_32k.reshape(-1))
+        self.d_ref_bert = None if not np.any(ref.ref_bert) else T(ref.ref_bert)
+        self.d_txt = [T(it.text_seq.reshape(-1)) for it in items]
+        self.d_bert = [None if it.text_bert is None else T(it.text_bert) for it in items]
+        self.sp = make_sampler(top_k=wl.top_k, greedy=wl.greedy)
+        self.ge = self.ge_adv = None
+        if wl.version != "v2":
+            self.ge, self.ge_adv = self.eng.prompt_encode(self.d_audio, T(ref.sv_emb.reshape(-1)))
+        self.eng.set_option("persist", 1)
+        self.phase = {"t2s": 0.0, "vits": 0.0}
+
+    def step(self):
+        torch = self.torch
+        t0 = time.perf_counter()
+        utts = [(self.d_ref, t, self.d_ref_bert, b, self.d_ssl, it.force_steps)
+                for t, b, it in zip(self.d_txt, self.d_bert, self.items)]
+        sems = self.eng.t2s_generate(utts, self.sp)        # returns host tokens: synchronous
+        t1 = time.perf_counter()
+        n = 0
+        for t, sem in zip(self.d_txt, sems):
+            if self.ge is None:
+                wav = self.eng.vits_decode(t, sem, ref_audio=self.d_audio)
+            else:
+                wav = self.eng.vits_decode(t, sem, ge=self.ge, ge_advanced=self.ge_adv)
+            n += int(wav.numel())
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        self.phase["t2s"] += t1 - t0
+        self.phase["vits"] += t2 - t1
+        return sems, n
 
 
 def main():
@@ -71,6 +114,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=("single", "batch64", "mixed100"), default="single")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -82,38 +126,32 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")      # host group: barrier + max time only (no RCCL)
     else:
         torch.cuda.set_device(0)
-
-    from genie_tts_amd import synth
-    from genie_tts_amd.engine import Engine, make_sampler
-    w = synth.synthetic_character("v2")
-    eng = Engine(w, "v2", device=local if world > 1 else 0)
-    inputs = build_inputs()
-    ref, txt, rb, tb, ssl, audio = inputs
     dev = torch.device("cuda", local if world > 1 else 0)
-    # inputs resident in HBM before the timed region (warmup triggers the graph captures)
-    d_ref = torch.as_tensor(ref.reshape(-1), device=dev)
-    d_txt = torch.as_tensor(txt.reshape(-1), device=dev)
-    d_ssl = torch.as_tensor(ssl.reshape(768, -1), device=dev)
-    d_audio = torch.as_tensor(audio.reshape(-1), device=dev)
-    sp = make_sampler(force_steps=FORCE_STEPS)
-    eng.set_option("persist", 1)  # whole decode loop as one launch (t2s_persist.hip)
-    eng.set_timing(True)          # phase events + live dominant-kernel event pair
 
-    def one_utterance():
-        sem = eng.t2s_generate([(d_ref, d_txt, None, None, d_ssl)], sp)[0]
-        wav = eng.vits_decode(d_txt, sem, ref_audio=d_audio)
-        return sem, wav
+    from genie_tts_amd import workloads, replicas
+    from genie_tts_amd.probe import persist_roofline, composite_roofline
+    wl = {"single": workloads.single, "batch64": workloads.batch64, "mixed100": workloads.mixed100}[args.workload]()
+    if args.workload == "mixed100":
+        reqs = [replicas.Request(i, it.text_seq, it.text_bert, it.force_steps) for i, it in enumerate(wl.items)]
+        shard = replicas.lpt_assign([replicas.predicted_cost(r) for r in reqs], world)[rank]
+        items = [wl.items[i] for i in shard]
+        units_per_step = len(wl.items)            # the whole set per step, over all ranks
+    else:
+        items = wl.items
+        units_per_step = world * len(items)       # every replica runs the workload (weak scaling)
+    run = Runner(wl, items, dev, local if world > 1 else 0)
+    timed_single = args.workload == "single"
+    run.eng.set_timing(timed_single)              # phase events + live dominant-kernel events (B = 1)
 
     for _ in range(args.warmup):
-        sem, wav = one_utterance()
+        sems, n_samples = run.step()
     torch.cuda.synchronize()
-    eng.set_timing(True)          # reset live-kernel samples: only the timed region counts
-    n_tokens = int(sem.size)
-    n_samples = int(wav.numel())
-    audio_s = n_samples / SR
+    run.phase = {"t2s": 0.0, "vits": 0.0}
+    if timed_single:
+        run.eng.set_timing(True)                  # reset live-kernel samples: only the timed region counts
 
     phase_ms = []
     if dist is not None:
@@ -121,22 +159,24 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        one_utterance()
-        phase_ms.append(eng.timing())
+        sems, n_samples = run.step()
+        if timed_single:
+            phase_ms.append(run.eng.timing())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
     ms_per_step = dt / args.steps * 1e3
-    utt_s = world * args.steps / dt
+    utt_s = units_per_step * args.steps / dt
+    audio_s = n_samples / SR                                  # this rank's audio per step
     rtf = (dt / args.steps) / audio_s
-
-    from genie_tts_amd.probe import persist_roofline
-    roofline = persist_roofline(eng, n0=R_PH + S_PH + H_SSL // 2, steps=FORCE_STEPS, B=1)
+    tokens = [int(s.size) for s in sems]
+    R_, H_ = wl.reference.ref_seq.shape[1], wl.reference.ssl.shape[2]
+    n0s = [R_ + it.text_seq.shape[1] + H_ // 2 for it in items]
 
     out = {
         "metric": METRIC,
@@ -147,27 +187,42 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.workload == "mixed100" else "weak",
         "vs_baseline": None,
-        "dtype": "f32 (fp16-valued weights)",
+        "dtype": "f32 activations (fp16-valued weights; split-fp16 MFMA GEMMs)",
         "data": "synthetic (seeded inputs, synthetic fp16-valued weights; no checkpoints offline)",
         "rtf": rtf,
         "x_realtime": 1.0 / rtf,
-        "audio_s_per_utt": audio_s,
-        "tokens_per_utt": n_tokens,
-        "config": {"workload": "configs[1]: V2 speaker, single utterance, greedy, 1 utt per replica",
-                   "ref_phones": R_PH, "text_phones": S_PH, "ssl_frames": H_SSL,
-                   "loop_steps": FORCE_STEPS, "semantic_tokens": n_tokens,
-                   "samples": n_samples, "parallelism": f"replicas x{world}"},
-        "roofline": roofline,
+        "audio_s_per_step": audio_s,
+        "tokens_per_step": sum(tokens),
     }
-    if phase_ms:
-        pm = np.mean(np.asarray(phase_ms), axis=0)
-        out["phase_ms"] = {"encode": float(pm[0]), "prefill": float(pm[1]), "decode": float(pm[2]),
-                           "vits": float(pm[3])}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.workload == "single":
+        it = items[0]
+        out["config"] = {"workload": "configs[1]: V2 speaker, single utterance, greedy, 1 utt per replica",
+                         "ref_phones": R_, "text_phones": it.text_seq.shape[1], "ssl_frames": H_,
+                         "loop_steps": it.force_steps, "semantic_tokens": tokens[0],
+                         "samples": n_samples, "parallelism": f"replicas x{world}"}
+        out["roofline"] = persist_roofline(run.eng, n0=n0s[0], steps=it.force_steps, B=1)
+        if phase_ms:
+            pm = np.mean(np.asarray(phase_ms), axis=0)
+            out["phase_ms"] = {"encode": float(pm[0]), "prefill": float(pm[1]), "decode": float(pm[2]),
+                               "vits": float(pm[3])}
+            out["roofline_utterance"] = composite_roofline(
+                ms_per_step, n0s, [it.force_steps], tokens, wl.version,
+                {"decode": float(pm[2]), "prefill": float(pm[1]), "vits": float(pm[3])})
+    else:
+        out["config"] = {"workload": wl.name + (" (top-k %d sampled)" % wl.top_k if not wl.greedy else " (greedy)"),
+                         "version": wl.version, "sentences": len(wl.items), "sentences_this_rank": len(items),
+                         "text_phones": [int(i.text_seq.shape[1]) for i in items][:8] + ["..."],
+                         "semantic_tokens_this_rank": sum(tokens), "parallelism": f"replicas x{world}" +
+                         (" (LPT shards)" if args.workload == "mixed100" else "")}
+        ph = {k: v / args.steps * 1e3 for k, v in run.phase.items()}
+        out["phase_ms"] = ph
+        out["roofline_utterance"] = composite_roofline(ms_per_step, n0s, [it.force_steps for it in items], tokens,
+                                                       wl.version)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "single":
         threads = min(16, len(os.sched_getaffinity(0)))
-        cdt, cs = cpu_baseline(inputs, threads)
+        cdt, cs = cpu_baseline(wl, threads)
         model = ""
         try:
             with open("/proc/cpuinfo") as f:
@@ -182,7 +237,7 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
-    eng.close()
+    run.eng.close()
 
 
 if __name__ == "__main__":

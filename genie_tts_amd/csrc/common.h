@@ -146,8 +146,12 @@ __device__ __forceinline__ uint4 philox4x32(uint4 ctr, uint2 key) {
     return ctr;
 }
 
-__device__ __forceinline__ float u01_open(uint32_t x) {   // (0, 1]
-    return (float)((x >> 8) + 1) * (1.0f / 16777216.0f);
+// (k + 1/2) / 2^23 for the top 23 bits k, exact in f32 and strictly inside (0, 1)
+// (largest 1 - 2^-24): the Box-Muller radius sqrt(-2 ln u1) is never 0 and
+// cos(2 pi u2) never exactly 0 (u2 != 1/4, 3/4), so q ~ N(0,1) is never +-0 and
+// argmax(p / q) never meets 0/0.
+__device__ __forceinline__ float u01_open(uint32_t x) {
+    return ((float)(x >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
 
 // ----------------------------------------------------------------------

@@ -216,6 +216,7 @@ int gsv_engine::reserve(int batch, int tokens) {
     done = (uint8_t*)A(nb);
     stopf = (uint8_t*)A(nb);
     seen = (uint32_t*)A((size_t)nb * 33 * 4);
+    forceb = (int*)A(nb * 4);
     h = (float*)A((size_t)nb * 512 * 4);
     h1 = (float*)A((size_t)nb * 512 * 4);
     s1 = (float*)A((size_t)nb * 512 * 4);
@@ -243,6 +244,7 @@ int gsv_engine::reserve(int batch, int tokens) {
     for (int i = 0; i < nb; ++i) id[i] = i;
     hipMemcpy(ident, id.data(), nb * 4, hipMemcpyHostToDevice);
     hipMemset(done, 1, nb);
+    hipMemset(forceb, 0, nb * 4);
     max_batch = nb;
     tmax = nt;
     return 0;
@@ -380,6 +382,7 @@ int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, in
     sa.y = y + (size_t)b * tmax; sa.ny = ny + b; sa.seen = seen + (size_t)b * 33;
     sa.done = done + b; sa.stop_out = nullptr; sa.steps = steps + b; sa.kvlen = kvlen + b;
     sa.prefill = 1; sa.logits_out = logits_out; sa.ldlo = 1025;
+    sa.b0 = b;   // Philox counter: the slot's own noise for its first-stage token
     sample_tokens(sa, st);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "prefill launch");
 }
@@ -397,6 +400,7 @@ SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
     sa.seed = sp ? sp->seed : 0;
     sa.max_steps = sp ? sp->max_steps : 500;
     sa.force_steps = sp ? sp->force_steps : 0;
+    sa.force_b = forceb;
     sa.prefill = 0;
     return sa;
 }
@@ -536,7 +540,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
     // Steps are launched as replayed hipGraphs (chunk of 8 steps, tail by 1-step
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
-    const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
+    const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     if (use_persist && B <= 8 && persist_groups(B, n_cu) > 0) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
@@ -608,7 +612,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     // One launch runs every loop step (t2s_persist.hip).  Hand-offs are tagged
     // granules in a ring; the launch epoch in the tag makes the ring reusable
     // without zeroing (re-zeroed when the epoch wraps or the layout changes).
-    const int limit = sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
+    const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     if (tmax > persist_max_tokens()) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
     const size_t need = one ? persist1_ring_bytes() : persist_ring_bytes(B);
     const int layout = one ? -1 : B;   // ring layout key: the two kernels slot the ring differently
@@ -646,6 +650,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.seen = seen;
     a.top_k = sp->top_k; a.temperature = sp->temperature; a.rep_penalty = sp->repetition_penalty;
     a.greedy = sp->greedy; a.seed = sp->seed; a.max_steps = sp->max_steps; a.force_steps = sp->force_steps;
+    a.force_b = forceb;
     a.ring = (unsigned long long*)pws;
     a.epoch = pepoch;
     a.err = perr;
@@ -797,6 +802,7 @@ extern "C" int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int nsteps, const 
     if (sp.top_k < 1 || sp.top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
     sp.force_steps = 1 << 30;   // session semantics: the caller owns the stop decision
     hipMemsetAsync(eng->done, 0, 1, st);
+    hipMemsetAsync(eng->forceb, 0, 4, st);
     for (int i = 0; i < nsteps; ++i) {
         eng->decode_step(1, &sp, logits_out ? logits_out + (size_t)i * 1025 : nullptr, st);
         if (stop) hipMemcpyAsync(stop + i, eng->stopf, 1, hipMemcpyDeviceToDevice, st);
@@ -842,14 +848,21 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (sp.top_k < 1 || sp.top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
     if (sp.max_steps <= 0) sp.max_steps = 500;
     const int steps_cap = sp.force_steps > 0 ? sp.force_steps : sp.max_steps;
-    int need = 0;
+    int need = 0, limit = 0;
+    std::vector<int> hforce(batch);
     for (int b = 0; b < batch; ++b) {
+        if (utts[b].force_steps < 0) return set_error(GSV_E_ARG, "negative force_steps");
+        hforce[b] = utts[b].force_steps;
+        const int cap_b = hforce[b] > 0 ? hforce[b] : steps_cap;
         const int n0 = utts[b].n_ref + utts[b].n_text + utts[b].n_ssl / 2;
-        need = std::max(need, n0 + steps_cap + 16);
+        need = std::max(need, n0 + cap_b + 16);
+        limit = std::max(limit, cap_b);
     }
     if (int e = eng->reserve(batch, need)) return e;
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
+    hipMemcpyAsync(eng->forceb, hforce.data(), batch * 4, hipMemcpyHostToDevice, st);
+    eng->loop_limit = limit;
     if (eng->timing) hipEventRecord(eng->ev[0], st);
     hipMemsetAsync(eng->done, 1, eng->max_batch, st);
     for (int b = 0; b < batch; ++b) {
@@ -860,7 +873,9 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
         if (int e = eng->prefill_slot(b, eng->pH, L, eng->prompts_buf, P, &sp, nullptr, st)) return e;
     }
     if (eng->timing) hipEventRecord(eng->ev[2], st);
-    if (int e = eng->decode_loop(batch, &sp, st)) return e;
+    const int rc = eng->decode_loop(batch, &sp, st);
+    eng->loop_limit = 0;
+    if (rc) return rc;
     if (eng->timing) hipEventRecord(eng->ev[3], st);
     // trim on host (Inference.py:108-109, then :41-44)
     std::vector<int> hny(batch), hsteps(batch);

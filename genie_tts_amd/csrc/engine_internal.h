@@ -56,6 +56,8 @@ struct gsv_engine {
     int *ny = nullptr, *kvlen = nullptr, *steps = nullptr, *ident = nullptr;
     uint8_t *done = nullptr, *stopf = nullptr;
     uint32_t* seen = nullptr;
+    int* forceb = nullptr;            // per-slot forced loop length (gsv_utt.force_steps; 0 = sampler rule)
+    int loop_limit = 0;               // >0: loop-step bound of the current generate (max over its slots)
     float *h = nullptr, *h1 = nullptr, *s1 = nullptr, *s2 = nullptr, *q = nullptr, *o = nullptr;
     float *f = nullptr, *logits = nullptr;
     float *attn_part = nullptr, *ffn_part = nullptr;

@@ -158,6 +158,15 @@ struct FfnArgs {
 };
 void ffn_fused(const FfnArgs& a, hipStream_t s, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
+// Loop-end rule of K10 + Inference.py:95-106 for sequence b after `st` executed
+// steps: a per-sequence forced length, else the launch-wide one, else EOS / 500.
+__host__ __device__ __forceinline__ bool seq_finished(const int* force_b, int b, int force_steps, int max_steps,
+                                                      int st, bool stop) {
+    const int fb = force_b ? force_b[b] : 0;
+    const int fs = fb > 0 ? fb : force_steps;
+    return fs > 0 ? st >= fs : (stop || st >= max_steps);
+}
+
 // Decode embedding: for active b: tok = y[b][ny[b]-1]; h[b] = E[tok] + alpha*pe[ny[b]]
 void decode_embed(int B, const int64_t* y, long ldy, const int* ny, const __half* emb,
                   const float* alpha, const float* pe, float* h, const uint8_t* done,
@@ -174,7 +183,9 @@ struct SampleArgs {
     int top_k; float temperature; float rep_penalty;
     int greedy; uint64_t seed;
     int max_steps; int force_steps;
+    const int* force_b;                // optional per-sequence force_steps (>0 overrides force_steps)
     int prefill;                       // 1: first-stage sampler (no stop, no step count)
+    int b0;                            // Philox sequence id of block 0 (prefill of slot b0)
     float* logits_out; long ldlo;      // optional copy of raw logits
     int ablate;                        // probe only: 1 skip top-k, 2 also skip softmax, 3 loads + tail
     long long* acc_zero; long acc_n;   // per-sequence fixed-point accumulators zeroed for the next step
@@ -204,6 +215,7 @@ struct PersistArgs {
     long sstride; int tmax; float scale;
     int64_t* y; long ldy; int* ny; int* kvlen; int* steps; uint8_t* done; uint8_t* stop_out; uint32_t* seen;
     int top_k; float temperature; float rep_penalty; int greedy; uint64_t seed; int max_steps; int force_steps;
+    const int* force_b;                           // optional per-sequence force_steps (>0 overrides)
     unsigned long long* ring;                     // granule ring (persist_ring_bytes)
     unsigned epoch;                               // launch epoch (tag high bits), 1 .. 2^20-1
     int* err;                                     // zeroed per launch; non-zero: a hand-off timed out

@@ -67,7 +67,7 @@ __device__ __forceinline__ void sample_commit(const SampleArgs& a, int b, int to
         const int st = steps + 1;
         a.steps[b] = st;
         a.kvlen[b] = kv + 1;
-        const bool fin = a.force_steps > 0 ? st >= a.force_steps : (stop || st >= a.max_steps);
+        const bool fin = seq_finished(a.force_b, b, a.force_steps, a.max_steps, st, stop);
         if (fin) a.done[b] = 1;
     }
 }

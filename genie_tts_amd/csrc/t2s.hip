@@ -828,7 +828,7 @@ __global__ __launch_bounds__(NT) void k_sample(SampleArgs a) {
     __syncthreads();
     const int step = a.prefill ? 0 : step_s + 1;
     int raw = 0;
-    const int tok = sample_block<NT>([&](int i) { return lg[i]; }, seen_s, b, step, a.top_k, a.temperature,
+    const int tok = sample_block<NT>([&](int i) { return lg[i]; }, seen_s, a.b0 + b, step, a.top_k, a.temperature,
                                      a.rep_penalty, a.greedy, a.seed, a.ablate,
                                      a.logits_out ? a.logits_out + (long)b * a.ldlo : nullptr, &raw, sh);
     if (tid == 0) {

@@ -600,7 +600,7 @@ __device__ void run_block(const PersistArgs& a, const Ws& ws, Shared& sh) {
                 sh.seen[tok >> 5] |= 1u << (tok & 31);
                 const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
                 const int nst = st + 1;
-                const bool fin = a.force_steps > 0 ? nst >= a.force_steps : (stop || nst >= a.max_steps);
+                const bool fin = seq_finished(a.force_b, ab, a.force_steps, a.max_steps, nst, stop);
                 last_stop = stop;
                 st_gran(ws.TK(s + 1, ab), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
             }

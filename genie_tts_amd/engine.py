@@ -22,6 +22,7 @@ _lib = None
 
 GSV_F32, GSV_F16 = 0, 1
 GSV_V2, GSV_V2PP = 0, 1
+MAX_BATCH = 64           # gsv_reserve: sequences decoded together
 
 
 class EngineError(RuntimeError):
@@ -34,6 +35,7 @@ class Utt(ctypes.Structure):
         ("text_seq", ctypes.c_void_p), ("n_text", ctypes.c_int32),
         ("ref_bert", ctypes.c_void_p), ("text_bert", ctypes.c_void_p),
         ("ssl", ctypes.c_void_p), ("n_ssl", ctypes.c_int32),
+        ("force_steps", ctypes.c_int32),
     ]
 
 
@@ -225,7 +227,7 @@ class Engine:
             return x.to(device=self.dev, dtype=dtype).contiguous()
         return t.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=self.dev).contiguous()
 
-    def make_utt(self, ref_seq, text_seq, ref_bert, text_bert, ssl):
+    def make_utt(self, ref_seq, text_seq, ref_bert, text_bert, ssl, force_steps: int = 0):
         t = self.torch
         flat = lambda a: a.reshape(-1) if isinstance(a, t.Tensor) else np.asarray(a).reshape(-1)
         keep = [self._dev(flat(ref_seq), t.int64),
@@ -236,7 +238,7 @@ class Engine:
         u = Utt(keep[0].data_ptr(), keep[0].numel(), keep[1].data_ptr(), keep[1].numel(),
                 0 if keep[2] is None else keep[2].data_ptr(),
                 0 if keep[3] is None else keep[3].data_ptr(),
-                keep[4].data_ptr(), keep[4].shape[1])
+                keep[4].data_ptr(), keep[4].shape[1], int(force_steps))
         return u, keep
 
     def reserve(self, batch: int, tokens: int):
@@ -255,7 +257,13 @@ class Engine:
 
     def t2s_generate(self, utts: Sequence[Tuple], sampler: Optional[Sampler] = None,
                      out_stride: int = 1024) -> List[np.ndarray]:
-        """utts: sequence of (ref_seq, text_seq, ref_bert, text_bert, ssl)."""
+        """utts: sequence of (ref_seq, text_seq, ref_bert, text_bert, ssl[, force_steps]);
+        force_steps > 0 runs that utterance for exactly that many loop steps (EOS ignored)."""
+        if len(utts) > MAX_BATCH:   # the engine decodes up to 64 sequences together
+            out = []
+            for i in range(0, len(utts), MAX_BATCH):
+                out += self.t2s_generate(utts[i:i + MAX_BATCH], sampler, out_stride)
+            return out
         arr = (Utt * len(utts))()
         keep = []
         for i, u in enumerate(utts):

@@ -131,23 +131,24 @@ class GENIE:
 
     def tts_batch(self, items: Sequence[tuple], prompt_audio: ReferenceAudio, model, sampler: Sampler) -> List[np.ndarray]:
         """Batched synthesis for one character and reference: items are
-        (text_seq, text_bert|None).  All sequences decode together (one batched
-        hipGraph step per token); the vocoder runs per utterance."""
+        (text_seq, text_bert|None[, force_steps]).  All sequences decode together
+        (one batched step per token, ragged: a finished sequence drops out); the
+        vocoder runs per utterance."""
         eng = model.ENGINE
         ssl = np.asarray(prompt_audio.ssl_content, np.float32).reshape(768, -1)
-        utts = [(prompt_audio.phonemes_seq, ts, prompt_audio.text_bert, tb, ssl) for ts, tb in items]
+        utts = [(prompt_audio.phonemes_seq, it[0], prompt_audio.text_bert, it[1], ssl,
+                 it[2] if len(it) > 2 else 0) for it in items]
         toks = eng.t2s_generate(utts, sampler)
+        if model.PROMPT_ENCODER is not None:
+            prompt_audio.update_global_emb(model.PROMPT_ENCODER)
         out = []
-        for (ts, _), tok in zip(items, toks):
+        for it, tok in zip(items, toks):
+            feed = {"text_seq": it[0], "pred_semantic": tok.reshape(1, 1, -1)}
             if model.PROMPT_ENCODER is None:
-                a = model.VITS.run(None, {"text_seq": ts, "pred_semantic": tok.reshape(1, 1, -1),
-                                          "ref_audio": prompt_audio.audio_32k})[0]
+                feed["ref_audio"] = prompt_audio.audio_32k
             else:
-                prompt_audio.update_global_emb(model.PROMPT_ENCODER)
-                a = model.VITS.run(None, {"text_seq": ts, "pred_semantic": tok.reshape(1, 1, -1),
-                                          "ge": prompt_audio.global_emb,
-                                          "ge_advanced": prompt_audio.global_emb_advanced})[0]
-            out.append(a)
+                feed.update(ge=prompt_audio.global_emb, ge_advanced=prompt_audio.global_emb_advanced)
+            out.append(model.VITS.run(None, feed)[0])
         return out
 
 

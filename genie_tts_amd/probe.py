@@ -103,3 +103,43 @@ def dominant_kernel_roofline(eng, B: int = 1):
         "avg_launch_us": us,
         "samples": n,
     }
+
+
+# ------------------------------------------------------------------ composite
+# roofline.achieved of the whole utterance = sum over phases of the
+# phase's minimum time on its own bound, over the measured time.
+#   decode : algorithmic bytes (above) / HBM peak
+#   prefill: 2 N0 x 24 x 3,145,728 (q/k/v, out, FFN1, FFN2 weights) + 4 N0^2 x 512 x 24
+#            (dense scores and P.V) FLOP / the FP32 peak (the reference computes in
+#            fp32; our split-fp16 MFMA GEMMs reproduce fp32 products)
+#   vits   : 135.5 GFLOP (V2) / 298 GFLOP (V2ProPlus) per 80 tokens, linear in the
+#            token count (the generator, 96 % of it, is linear in G) / the FP32 peak
+F32_PEAK_TFS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak
+VITS_FLOP_PER_TOKEN = {"v2": 135.5e9 / 80, "v2ProPlus": 298.0e9 / 80}
+
+
+def prefill_flop(n0: int) -> float:
+    return 2.0 * n0 * 24 * 3145728 + 4.0 * n0 * n0 * 512 * 24
+
+
+def batch_decode_bytes(n0s, steps) -> int:
+    """Algorithmic bytes of a ragged batched decode: per loop step the fp16 weights
+    once + each still-active sequence's K/V rows read and its new row written."""
+    total = 0
+    for s in range(max(steps)):
+        act = [n0 for n0, st in zip(n0s, steps) if s < st]
+        total += W16 + sum(KV_ROW * (n0 + s + 1) for n0 in act)
+    return total
+
+
+def composite_roofline(ms_total: float, n0s, steps, tokens, version: str = "v2", phase_ms=None):
+    """Sum of per-phase minimum times / measured time for one job (ms_total)."""
+    t_dec = batch_decode_bytes(n0s, steps) / (HBM_PEAK_GBS * 1e9) * 1e3
+    t_pre = sum(prefill_flop(n0) for n0 in n0s) / (F32_PEAK_TFS * 1e12) * 1e3
+    t_voc = sum(VITS_FLOP_PER_TOKEN[version] * g for g in tokens) / (F32_PEAK_TFS * 1e12) * 1e3
+    out = {"t_min_ms": {"decode_hbm": t_dec, "prefill_f32": t_pre, "vits_f32": t_voc},
+           "t_measured_ms": ms_total, "frac": (t_dec + t_pre + t_voc) / ms_total}
+    if phase_ms:
+        mins = {"decode": t_dec, "prefill": t_pre, "vits": t_voc}
+        out["phase_frac"] = {k: mins[k] / v for k, v in phase_ms.items() if k in mins and v > 0}
+    return out

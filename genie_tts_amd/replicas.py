@@ -84,12 +84,12 @@ def run_sharded(requests: Sequence[Request], synth: Callable[[List[Request]], Li
 
 
 def engine_synth(model, reference, sampler_factory) -> Callable[[List[Request]], List[object]]:
-    """synth() over one engine-backed GSVModel: one batched T2S for the shard,
-    then the vocoder per utterance (inference.GENIE.tts_batch)."""
+    """synth() over one engine-backed GSVModel: one batched T2S for the shard
+    (each request's own forced length, if any), then the vocoder per utterance
+    (inference.GENIE.tts_batch).  sampler_factory() -> engine.Sampler."""
     from .inference import tts_client
 
     def synth(reqs: List[Request]):
-        fs = max(r.force_steps for r in reqs)
-        items = [(r.text_seq, r.text_bert) for r in reqs]
-        return tts_client.tts_batch(items, reference, model, sampler_factory(fs))
+        items = [(r.text_seq, r.text_bert, r.force_steps) for r in reqs]
+        return tts_client.tts_batch(items, reference, model, sampler_factory())
     return synth

@@ -106,15 +106,25 @@ JP_PHONE_IDS = (
     322, 323, 95, 1, 3,                            # '[' ']' '_' ',' '.'
 )
 DOT_ID = 3
+# English (ARPAbet) and Chinese (pinyin initials + toned finals) phone ids of the
+# same table (g/G2P/SymbolsV2.py: symbol_to_id_v2 over ARPABET_SYMBOLS and
+# PINYIN_INITIALS / PINYIN_FINALS_BASE x tones 1-5), for the EN+ZH workload.
+EN_PHONE_IDS = tuple(list(range(6, 28)) + list(range(34, 44)) + [49, 50, 51] + list(range(53, 66)) +
+                     list(range(67, 77)) + [80, 81] + list(range(83, 86)) + list(range(87, 95)))
+ZH_PHONE_IDS = tuple([5] + list(range(28, 34)) + list(range(44, 49)) + [66] + list(range(97, 123)) +
+                     [124, 125, 127] + list(range(130, 157)) + [158] + list(range(161, 223)) +
+                     [224, 225, 227] + list(range(230, 246)) + [247, 248, 250, 251, 252] +
+                     list(range(255, 295)) + list(range(296, 321)))
 
 
 def rng_for(tag: str, seed: int = INPUT_SEED) -> np.random.Generator:
     return np.random.default_rng([seed, fnv1a64(tag) & 0xFFFFFFFF])
 
 
-def synth_phones(n: int, tag: str, seed: int = INPUT_SEED) -> np.ndarray:
+def synth_phones(n: int, tag: str, seed: int = INPUT_SEED, lang: str = "ja") -> np.ndarray:
     r = rng_for("phones:" + tag, seed)
-    ids = r.choice(np.array(JP_PHONE_IDS, dtype=np.int64), size=n)
+    table = {"ja": JP_PHONE_IDS, "en": EN_PHONE_IDS, "zh": ZH_PHONE_IDS}[lang]
+    ids = r.choice(np.array(table, dtype=np.int64), size=n)
     ids[0] = DOT_ID
     return ids.reshape(1, n)
 

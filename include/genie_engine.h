@@ -88,6 +88,10 @@ typedef struct {
     const float*   ref_bert;                    /* [n_ref, 1024]  or NULL = zeros  */
     const float*   text_bert;                   /* [n_text, 1024] or NULL = zeros  */
     const float*   ssl;       int32_t n_ssl;    /* ssl_content [768, n_ssl]        */
+    int32_t force_steps;                        /* >0: this utterance ignores EOS and runs
+                                                   exactly this many loop steps (overrides
+                                                   gsv_sampler.force_steps; benchmarks and
+                                                   ragged-batch tests); 0: the sampler's rule */
 } gsv_utt;
 
 /* Sampler (reference constants: t2s_stage_decoder_fp32.onnx#1780-1801). */

@@ -1,6 +1,6 @@
 """numpy restatement of the engine's sampler noise (genie_tts_amd/csrc/common.h):
 Philox4x32-10 (Salmon et al. 2011) keyed by the 64-bit seed, counter
-(token id, loop step, sequence, 0x51), then Box-Muller on (0,1] uniforms.
+(token id, loop step, sequence, 0x51), then Box-Muller on (0,1) uniforms.
 The reference draws its N(0,1) from onnxruntime's RandomNormalLike
 (stage#1799); ours is this stream -- equal in distribution, not in bits."""
 import numpy as np
@@ -25,7 +25,8 @@ def philox4x32(c0, c1, c2, c3, k0, k1):
 
 
 def u01_open(x):
-    return (((x >> np.uint32(8)) + np.uint32(1)).astype(np.float32)) * np.float32(1.0 / 16777216.0)
+    """(k + 1/2) / 2^23 of the top 23 bits: exact in f32, strictly inside (0, 1), so q is never +-0."""
+    return ((x >> np.uint32(9)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 8388608.0)
 
 
 def sampler_noise(vocab: int, step: int, b: int, seed: int) -> np.ndarray:

@@ -1,0 +1,66 @@
+"""configs[2] on the GPU: 64 mixed-length JP sentences in ONE batched decode
+(S~U[30,60], forced G~U[50,110]; genie_tts_amd.workloads.batch64) through the
+C ABI (gsv_t2s_generate with per-utterance force_steps), against the oracle's
+tokens in tests/golden/t2s_batch64.npz (tests/golden/make_batch64.py; pinned
+to oracle/restate.py by tests/test_batch64_oracle.py):
+
+  greedy   per-utterance token ids bit-exact (the north_star's bar);
+  top-k 5  per-utterance token ids identical to the oracle loop fed the same
+           Philox N(0,1) noise (tests/philox.py) -- the sampled formula
+           argmax(softmax(top-k(penalised logits)) / q) of
+           t2s_stage_decoder_fp32.onnx#1775-1806.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from tests.common import character
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "t2s_batch64.npz")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from genie_tts_amd.engine import Engine
+    w = character("v2")
+    e = Engine({"t2s_encoder": w["t2s_encoder"], "t2s": w["t2s"]}, "v2")
+    yield e
+    e.close()
+
+
+def _utts(wl):
+    ref = wl.reference
+    return [(ref.ref_seq, it.text_seq, None, None, ref.ssl.reshape(768, -1), it.force_steps) for it in wl.items]
+
+
+@pytest.mark.parametrize("mode", ["greedy", "topk"])
+def test_batch64_matches_oracle(eng, mode):
+    from genie_tts_amd import workloads
+    from genie_tts_amd.engine import make_sampler
+    g = np.load(GOLD)
+    wl = workloads.batch64()
+    assert [it.tokens for it in wl.items] == g["G"].tolist()
+    sp = make_sampler(top_k=int(g["top_k"]) if mode == "topk" else 15, greedy=(mode == "greedy"),
+                      seed=int(g["seed"]))
+    out = eng.t2s_generate(_utts(wl), sp)
+    bad = []
+    for b, tok in enumerate(out):
+        ref = g[mode][b, :g[mode + "_len"][b]].astype(np.int64)
+        if tok.tolist() != ref.tolist():
+            n = min(tok.size, ref.size)
+            i = next((j for j in range(n) if tok[j] != ref[j]), n)
+            bad.append((b, i, tok[max(0, i - 2):i + 3].tolist(), ref[max(0, i - 2):i + 3].tolist()))
+    assert not bad, f"{mode}: (utterance, first differing token, engine, oracle) {bad}"
+
+
+def test_batch64_ragged_lengths(eng):
+    """Each utterance stops at its own forced length; finished rows are skipped
+    by the rest of the batch (ragged KV), so lengths equal G exactly."""
+    from genie_tts_amd import workloads
+    from genie_tts_amd.engine import make_sampler
+    wl = workloads.batch64(16, tag="b64r")
+    out = eng.t2s_generate(_utts(wl), make_sampler())
+    assert [o.size for o in out] == [it.tokens for it in wl.items]
