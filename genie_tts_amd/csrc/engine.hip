@@ -132,6 +132,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_PERSIST")) use_persist = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST1")) use_persist1 = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
         if (std::atoi(e) == 1 && !ktrace) {
             hipMalloc(&ktrace, (size_t)3 * 256 * 8 * 8);
@@ -656,6 +657,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.err = perr;
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
+    a.pf_delay = persist1_pf_delay;
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;

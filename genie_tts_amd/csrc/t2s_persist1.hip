@@ -78,7 +78,8 @@ struct Ws1 {
 struct Shared1 {
     float x[512];                   // x_l (attention), x_24 (logits)
     float qkv[96];
-    _Float16 osh[32], osl[32];      // MFMA row operand: head output split hi + lo (out-projection)
+    _Float16 osh[PWV][32], osl[PWV][32];   // MFMA row operand: head output split hi + lo (out-projection),
+                                           // one copy per wave (each wave merges the head itself)
     float b1[128];                  // FFN1 bias of the slice
     float lnb[2][512];              // LayerNorm inputs: [0] x_l (form_x), [1] LN1 (FFN)
     _Float16 xh[512], xl[512];      // MFMA row operand: h1 split hi + lo (FFN1)
@@ -99,7 +100,8 @@ struct Shared1 {
             float k[KVL1 * 32];     // K/V rows [0, min(kv, KVL1)) of the head (LDS-DMA)
             float v[KVL1 * 32];
             float p[TMAX1];         // scores, then softmax numerators
-            float ov[16][32];       // P.V partial sums of 16 key groups
+            float ov[16][32];       // P.V partial sums of 16 key groups (general path)
+            float ov4[PWV][32];     // P.V partial of each wave (fast path)
             float lg[PERSIST_LGS];  // logits (sampler)
         } at;
     };
@@ -208,6 +210,160 @@ __device__ __noinline__ float scores_general1(Shared1& sh, const float* Kw, int 
     return lmax;
 }
 
+// One wave's share of the head's attention (the common case: T <= 512 keys, all
+// cached rows in LDS): keys t = 64 u + g (u < NU, g = 8 w + lane / 8), 8 lanes x 4
+// dims per key row (conflict-free 16-B LDS reads), every K and V read of the NU
+// rounds issued up front.  Online softmax within the wave: m_w = max s, p = exp(s -
+// m_w), l_w = sum p, o_w = sum p v (rows of 16 lanes summed by row_ror 8) -> LDS
+// sh.wred[0/1][w], sh.at.ov4[w][row]; the caller merges the 8 waves after a barrier.
+// x + (x of the other 16-lane row of the pair) / (of the other 32-lane half), every lane
+__device__ __forceinline__ float swap_sum16(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_sum32(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Head output from the 8 wave partials (m_w, l_w in sh.wred, o_w in sh.at.ov4),
+// merged by EVERY wave into its own operand copy (no barrier after): lane j < 8
+// weighs wave j, e_j = exp(m_j - M); O = sum e_j o_j / sum e_j l_j.
+__device__ __forceinline__ void merge_waves1(Shared1& sh, int w, int lane) {
+    const int j = lane & 7;
+    const float mj = sh.wred[0][j];
+    float M = mj;
+    M = fmaxf(M, dpp_f<0xB1, 0xF>(M));
+    M = fmaxf(M, dpp_f<0x4E, 0xF>(M));
+    M = fmaxf(M, dpp_f<0x141, 0xF>(M));
+    const float e = mj == -INFINITY ? 0.f : expf(mj - M);
+    float L = e * sh.wred[1][j];
+    L += dpp_f<0xB1, 0xF>(L);
+    L += dpp_f<0x4E, 0xF>(L);
+    L += dpp_f<0x141, 0xF>(L);
+    const int d = lane & 31;
+    float O = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < PWV; ++ww)
+        O += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), ww)) * sh.at.ov4[ww][d];
+    if (lane < 32) split_h(O / L, sh.osh[w][d], sh.osl[w][d]);   // a convex combination of V rows
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int NU>
+__device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, float q2, float q3, float sc, float4 knew,
+                                           int kv, int T, int c8, int g, int w, int lane) {
+    float4 kr[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+        kr[u] = *reinterpret_cast<const float4*>(sh.at.k + min(64 * u + g, KVL1 - 1) * 32 + 4 * c8);
+    float sv[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        float4 k4 = kr[u];
+        if (64 * u + g == kv) k4 = knew;
+        float x = q0 * (k4.x * sc);
+        x += q1 * (k4.y * sc);
+        x += q2 * (k4.z * sc);
+        x += q3 * (k4.w * sc);
+        sv[u] = x;
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+    float4 vr[NU];   // V reads in flight during the max reduction
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+        vr[u] = *reinterpret_cast<const float4*>(sh.at.v + min(64 * u + g, KVL1 - 1) * 32 + 4 * c8);
+    float wm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        sv[u] = 64 * u + g < T ? sv[u] : -INFINITY;
+        wm = fmaxf(wm, sv[u]);
+    }
+    const float m_w = wave_max_dpp(wm);
+    const float4 vnew = *reinterpret_cast<const float4*>(sh.qkv + 64 + 4 * c8);
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f, lsum = 0.f;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int t = 64 * u + g;
+        const float pu = sv[u] == -INFINITY ? 0.f : expf(sv[u] - m_w);
+        float4 v4 = vr[u];
+        if (t == kv) v4 = vnew;
+        if (t > kv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);   // rows past the cache: unloaded LDS
+        o0 += pu * v4.x;
+        o1 += pu * v4.y;
+        o2 += pu * v4.z;
+        o3 += pu * v4.w;
+        lsum += pu;
+    }
+    // sum over the wave's 8 key groups (lanes c8 + 8 k): row_ror 8 within each 16-lane
+    // row, then the gfx950 row / half swaps (VALU, no LDS round trip)
+    o0 += dpp_f<0x128, 0xF>(o0);
+    o1 += dpp_f<0x128, 0xF>(o1);
+    o2 += dpp_f<0x128, 0xF>(o2);
+    o3 += dpp_f<0x128, 0xF>(o3);
+    o0 = swap_sum16(o0); o1 = swap_sum16(o1); o2 = swap_sum16(o2); o3 = swap_sum16(o3);
+    o0 = swap_sum32(o0); o1 = swap_sum32(o1); o2 = swap_sum32(o2); o3 = swap_sum32(o3);
+    const float l_w = wave_sum_dpp(c8 == 0 ? lsum : 0.f);
+    if (lane < 8) *reinterpret_cast<float4*>(&sh.at.ov4[w][4 * lane]) = make_float4(o0, o1, o2, o3);
+    if (lane == 0) {
+        sh.wred[0][w] = m_w;
+        sh.wred[1][w] = l_w;
+    }
+}
+
+// The general case (more than 512 keys or rows beyond the LDS stage): scores into
+// sh.at.p, block softmax, P.V over 16 key groups, head output -> sh.osh/osl.  Out
+// of line so the common path keeps its registers.
+__device__ __noinline__ void attn_general1(Shared1& sh, const float* Kw, const float* Vw, int kv, int T, float q0,
+                                           float q1, float q2, float q3, float sc, float4 knew, int c8, int g, int w,
+                                           int lane, int tid) {
+    const float lmax = scores_general1(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
+    const float wm = wave_max_dpp(lmax);
+    if (lane == 0) sh.wred[0][w] = wm;
+    __syncthreads();
+    float M = sh.wred[0][0];
+#pragma unroll
+    for (int ww = 1; ww < PWV; ++ww) M = fmaxf(M, sh.wred[0][ww]);
+    float lsum = 0.f;
+    for (int t = tid; t < T; t += PT) {
+        const float e = expf(sh.at.p[t] - M);
+        sh.at.p[t] = e;
+        lsum += e;
+    }
+    const float ws_ = wave_sum_dpp(lsum);
+    if (lane == 0) sh.wred[1][w] = ws_;
+    __syncthreads();
+    {
+        const int kg = tid >> 5, d = tid & 31;
+        const int tl = min(kv, KVL1);
+        float o4[4] = {0.f, 0.f, 0.f, 0.f};
+        int t = kg;
+        for (; t + 48 < tl; t += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o4[u] += sh.at.p[t + 16 * u] * sh.at.v[(t + 16 * u) * 32 + d];
+        }
+        for (; t < tl; t += 16) o4[0] += sh.at.p[t] * sh.at.v[t * 32 + d];
+        for (; t < kv; t += 16) o4[1] += sh.at.p[t] * ldg(Vw, (long)t * 32 + d);
+        if (t == kv) o4[2] += sh.at.p[t] * sh.qkv[64 + d];
+        sh.at.ov[kg][d] = (o4[0] + o4[1]) + (o4[2] + o4[3]);
+    }
+    __syncthreads();
+    if (lane < 32) {   // every wave its own operand copy
+        float O = 0.f, L = 0.f;
+#pragma unroll
+        for (int kg = 0; kg < 16; ++kg) O += sh.at.ov[kg][lane];
+#pragma unroll
+        for (int ww = 0; ww < PWV; ++ww) L += sh.wred[1][ww];
+        split_h(O / L, sh.osh[w][lane], sh.osl[w][lane]);   // a convex combination of V rows
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Step start: thread 0 learns the token of step s (s >= 1: granule TK(s), whose
 // bit 16 says the previous step finished the sequence).  Group 0 needs the token
 // at once (its layer 0 starts from it) and sleeps on the layer-23 output of the
@@ -242,6 +398,13 @@ __device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0
 // them across the layers a workgroup waits; every reader is behind a barrier.
 __device__ __forceinline__ void dma_half(const float* src, float* dst, int h, int lane) {
     __builtin_amdgcn_global_load_lds(src + 256 * h + lane * 4, dst + 256 * h, 16, 0, 0);
+}
+// Idle a workgroup between publishing a layer's output and streaming the weights
+// of its next owned layer (needed 7 layers later): the consumers' gather of the
+// hand-off is not queued behind this CU's refill burst (MI355X_MICROARCH.md,
+// gather-pass / handoff-1to1 endpoint classes).
+__device__ __forceinline__ void pf_wait(int ticks) {
+    for (int i = 0; i < ticks; ++i) __builtin_amdgcn_s_sleep(32);
 }
 // LN2 of layer l - 1 -> sh.p2, by waves 0..5 (call from every wave; l > 0)
 __device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int lane) {
@@ -370,89 +533,27 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             const int c8 = lane & 7, g = (w << 3) | (lane >> 3);
             const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
             const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
-            float lmax = -INFINITY;
             const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
             if (T <= 512 && kv <= KVL1) {
-                // common case, branch-free: every cached row is in LDS, 8 keys per lane in two halves
-#pragma unroll
-                for (int hf = 0; hf < 2; ++hf) {
-                    float sv[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int t = 64 * (4 * hf + u) + g;
-                        float4 kr = *reinterpret_cast<const float4*>(sh.at.k + min(t, KVL1 - 1) * 32 + 4 * c8);
-                        if (t == kv) { kr.x = knew.x; kr.y = knew.y; kr.z = knew.z; kr.w = knew.w; }
-                        float x = q0 * (kr.x * sc);
-                        x += q1 * (kr.y * sc);
-                        x += q2 * (kr.z * sc);
-                        x += q3 * (kr.w * sc);
-                        sv[u] = x;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int t = 64 * (4 * hf + u) + g;
-                        sv[u] = t < T ? sv[u] : -INFINITY;
-                        lmax = fmaxf(lmax, sv[u]);
-                    }
-                    if (c8 == 0) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) sh.at.p[64 * (4 * hf + u) + g] = sv[u];   // p[t >= T] is never read
-                    }
-                }
+                // common case: every cached row is in LDS (per-wave online softmax,
+                // wave_attn1); the round count is specialised so every LDS read of a
+                // round is issued up front.
+                const int nu = (T + 63) >> 6;
+                if (nu <= 2) wave_attn1<2>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
+                else if (nu <= 4) wave_attn1<4>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
+                else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
+                else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
+                else wave_attn1<8>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
+                __syncthreads();
+                STAMP1(3);
+                merge_waves1(sh, w, lane);
             } else {
-                lmax = scores_general1(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
+                attn_general1(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, g, w, lane, tid);
             }
-            const float wm = wave_max_dpp(lmax);
-            if (lane == 0) sh.wred[0][w] = wm;
-            __syncthreads();
-            float M = sh.wred[0][0];
-#pragma unroll
-            for (int ww = 1; ww < PWV; ++ww) M = fmaxf(M, sh.wred[0][ww]);
-            float lsum = 0.f;
-            for (int t = tid; t < T; t += PT) {
-                const float e = expf(sh.at.p[t] - M);
-                sh.at.p[t] = e;
-                lsum += e;
-            }
-            const float ws_ = wave_sum_dpp(lsum);
-            if (lane == 0) sh.wred[1][w] = ws_;
-            __syncthreads();
-            STAMP1(3);
-            // ---- P.V: 16 key groups x 32 dims; LDS rows unrolled by 4 with independent sums
-            {
-                const int kg = tid >> 5, d = tid & 31;
-                const int tl = min(kv, KVL1);
-                float o4[4] = {0.f, 0.f, 0.f, 0.f};
-                int t = kg;
-                for (; t + 48 < tl; t += 64) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) o4[u] += sh.at.p[t + 16 * u] * sh.at.v[(t + 16 * u) * 32 + d];
-                }
-                for (; t < tl; t += 16) o4[0] += sh.at.p[t] * sh.at.v[t * 32 + d];
-                for (; t < kv; t += 16) o4[1] += sh.at.p[t] * ldg(Vw, (long)t * 32 + d);
-                if (t == kv) o4[2] += sh.at.p[t] * sh.qkv[64 + d];
-                sh.at.ov[kg][d] = (o4[0] + o4[1]) + (o4[2] + o4[3]);
-            }
-            __syncthreads();
-            if (tid < 32) {
-                float O = 0.f, L = 0.f;
-#pragma unroll
-                for (int kg = 0; kg < 16; ++kg) O += sh.at.ov[kg][tid];
-#pragma unroll
-                for (int ww = 0; ww < PWV; ++ww) L += sh.wred[1][ww];
-                split_h(O / L, sh.osh[tid], sh.osl[tid]);   // a convex combination of V rows
-            }
-            __syncthreads();
             STAMP1(4);
             // ---- out-projection slice of this head (column tid) -> partial granule
             {
-                const h8v af = afrag(abase(sh.osh, sh.osl, lane), 0, (lane & 15) < 2);
+                const h8v af = afrag(abase(sh.osh[w], sh.osl[w], lane), 0, (lane & 15) < 2);
                 f32x4 acc[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bfrag(wo[t]), f32x4{0.f, 0.f, 0.f, 0.f});
@@ -468,6 +569,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             __syncthreads();   // LDS operands consumed before the next layer's LDS-DMA lands
             // ---- next owned layer (this step) or the first one of the next step
             const int ln = l + NG < 24 ? l + NG : grp;
+            pf_wait(a.pf_delay);   // let the hand-off leave before this CU streams again
             prefetch(ln, l + NG < 24 ? kv : kv + 1);
             if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         }
@@ -644,6 +746,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             if ((tid >> 5) == j) st_gran(ws.PFH(s, l, 16) + tid, tag, h1_pub);
             STAMP1(4);
             __syncthreads();   // fs / b1 consumed before the next prefetch lands
+            pf_wait(a.pf_delay);
             prefetch(l + NG < 24 ? l + NG : grp);
             if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         }
