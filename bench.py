@@ -86,7 +86,7 @@ class Runner:
         if wl.version != "v2":
             self.ge, self.ge_adv = self.eng.prompt_encode(self.d_audio, T(ref.sv_emb.reshape(-1)))
         self.eng.set_option("persist", 1)
-        self.phase = {"t2s": 0.0, "vits": 0.0}
+        self.phase = {"t2s": 0.0, "vits": 0.0, "encode+prefill": 0.0, "decode": 0.0}
 
     def step(self):
         torch = self.torch
@@ -95,6 +95,9 @@ class Runner:
                 for t, b, it in zip(self.d_txt, self.d_bert, self.items)]
         sems = self.eng.t2s_generate(utts, self.sp)        # returns host tokens: synchronous
         t1 = time.perf_counter()
+        tm = self.eng.timing()                              # device phases of this generate (ms)
+        self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
+        self.phase["decode"] += tm[2] * 1e-3
         n = 0
         for t, sem in zip(self.d_txt, sems):
             if self.ge is None:
@@ -144,12 +147,12 @@ def main():
         units_per_step = world * len(items)       # every replica runs the workload (weak scaling)
     run = Runner(wl, items, dev, local if world > 1 else 0)
     timed_single = args.workload == "single"
-    run.eng.set_timing(timed_single)              # phase events + live dominant-kernel events (B = 1)
+    run.eng.set_timing(True)                      # phase events (+ live dominant-kernel events at B = 1)
 
     for _ in range(args.warmup):
         sems, n_samples = run.step()
     torch.cuda.synchronize()
-    run.phase = {"t2s": 0.0, "vits": 0.0}
+    run.phase = {k: 0.0 for k in run.phase}
     if timed_single:
         run.eng.set_timing(True)                  # reset live-kernel samples: only the timed region counts
 

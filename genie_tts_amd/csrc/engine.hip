@@ -53,6 +53,9 @@ void gsv_engine::release_all() {
 
 gsv_engine::~gsv_engine() {
     release_all();
+    for (void* p : pk_allocs) hipFree(p);
+    pk_allocs.clear();
+    if (pk_tiles) hipFree(pk_tiles);
     if (own_stream && stream) hipStreamDestroy(stream);
     if (done_host) hipHostFree(done_host);
     for (auto& e : kev) if (e) hipEventDestroy(e);
@@ -218,6 +221,7 @@ int gsv_engine::reserve(int batch, int tokens) {
     stopf = (uint8_t*)A(nb);
     seen = (uint32_t*)A((size_t)nb * 33 * 4);
     forceb = (int*)A(nb * 4);
+    dslab = (float*)A((size_t)8 * nb * 2048 * 4);   // batched-decode split-K slabs (2 regions)
     h = (float*)A((size_t)nb * 512 * 4);
     h1 = (float*)A((size_t)nb * 512 * 4);
     s1 = (float*)A((size_t)nb * 512 * 4);
@@ -272,10 +276,11 @@ int gsv_engine::ensure_enc_ws(int P, int L) {
     return 0;
 }
 
-int gsv_engine::encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st) {
+int gsv_engine::encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st, bool do_prompts) {
     const int L = u->n_ref + u->n_text, P = u->n_ssl / 2;
     if (L <= 0 || P <= 0) return set_error(GSV_E_ARG, "empty utterance");
     if (int e = ensure_enc_ws(P, L)) return e;
+    if (do_prompts) {
     // K2: ssl_proj Conv1d(768,768,k2,s2) as GEMM over im2col, then VQ argmin (#2-48)
     ssl_im2col(u->ssl, u->n_ssl, e_im2col, st);
     GemmArgs g{};
@@ -291,6 +296,7 @@ int gsv_engine::encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t
     d.C = e_dist; d.ldc = 1024; d.mode = EPI_VQDIST; d.rowsq = e_hh; d.colsq = cb_sumsq;
     gemm_nt(d, st);
     argmin_dist_rows(e_dist, P, 1024, prompts, st);
+    }
     // K1: text embedding + bert projection + PE (#49-83)
     const float* bproj = nullptr;
     if (u->ref_bert || u->text_bert) {
@@ -388,6 +394,187 @@ int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, in
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "prefill launch");
 }
 
+// ------------------------------------------------------------ packed prefill
+// Prefill of a whole batch as ONE row set: the N0_b = L_b + P_b rows of every
+// utterance are packed back to back (row r -> sequence row_seq[r], position
+// row_pos[r]), so each layer is one GEMM per weight over sum_b N0_b rows (the
+// weights are read once per layer, not once per utterance), the QKV epilogue
+// scatters K/V into each sequence's own cache slot, and attention rows see
+// their own sequence's keys [0, row_len[r]) with the first-stage prefix-LM mask
+// (t2s_first_stage_decoder_fp32.onnx#29-56: x rows see the L x keys, prompt
+// row j sees L + j + 1).  Arithmetic per row is the single-sequence path's.
+static __global__ void k_gather_rows512(const float* src, const int* rows, float* dst, int n) {
+    const int b = blockIdx.x;
+    if (b >= n) return;
+    const float* s = src + (long)rows[b] * 512;
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) dst[(long)b * 512 + i] = s[i];
+}
+
+int gsv_engine::ensure_packed(int rows, int B) {
+    if (rows <= pk_rows && B <= pk_batch) return 0;
+    const int nr = std::max(rows, pk_rows), nb = std::max(B, pk_batch);
+    for (void* p : pk_allocs) hipFree(p);
+    pk_allocs.clear();
+    auto A = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
+        pk_allocs.push_back(p);
+        return p;
+    };
+    pk_H = (float*)A((size_t)nr * 512 * 4);
+    pk_Q = (float*)A((size_t)nr * 512 * 4);
+    pk_O = (float*)A((size_t)nr * 512 * 4);
+    pk_S = (float*)A((size_t)nr * 512 * 4);
+    pk_H1 = (float*)A((size_t)nr * 512 * 4);
+    pk_F = (float*)A((size_t)nr * 2048 * 4);
+    pk_slab = (float*)A((size_t)8 * nr * 512 * 4);
+    pk_rowinfo = (int*)A((size_t)3 * nr * 4);
+    pk_prompts = (int64_t*)A((size_t)nr * 8);
+    pk_last = (int*)A((size_t)nb * 4);
+    pk_xlast = (float*)A((size_t)nb * 512 * 4);
+    if (!pk_H || !pk_F || !pk_slab || !pk_rowinfo || !pk_prompts || !pk_last || !pk_xlast) {
+        pk_rows = pk_batch = 0;
+        return set_error(GSV_E_HIP, "packed prefill allocation failed");
+    }
+    pk_rows = nr;
+    pk_batch = nb;
+    return 0;
+}
+
+int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp, hipStream_t st) {
+    std::vector<int> off(B + 1, 0), Ls(B), Ps(B), poff(B + 1, 0);
+    for (int b = 0; b < B; ++b) {
+        Ls[b] = utts[b].n_ref + utts[b].n_text;
+        Ps[b] = utts[b].n_ssl / 2;
+        if (Ls[b] <= 0 || Ps[b] <= 0) return set_error(GSV_E_ARG, "empty utterance");
+        if (Ls[b] + Ps[b] + 1 > tmax) return set_error(GSV_E_CAPACITY, "prefill exceeds reserved tokens");
+        off[b + 1] = off[b] + Ls[b] + Ps[b];
+        poff[b + 1] = poff[b] + Ps[b];
+    }
+    const int R = off[B];
+    if (int e = ensure_packed(R, B)) return e;
+    // host row tables: sequence, position, visible keys; last row of each sequence
+    // tiles of <= 16 rows of one sequence for the LDS-staged attention
+    int ntiles = 0, maxn0 = 0;
+    for (int b = 0; b < B; ++b) {
+        ntiles += (off[b + 1] - off[b] + 15) / 16;
+        maxn0 = std::max(maxn0, off[b + 1] - off[b]);
+    }
+    pk_host.resize((size_t)3 * R + B + 3 * (size_t)ntiles);
+    int* hs = pk_host.data();
+    int* hp = hs + R;
+    int* hl = hs + 2 * R;
+    int* hlast = hs + 3 * R;
+    int* htile = hlast + B;
+    int ti = 0;
+    for (int b = 0; b < B; ++b) {
+        for (int j = 0; j < Ls[b] + Ps[b]; ++j) {
+            const int r = off[b] + j;
+            hs[r] = b;
+            hp[r] = j;
+            hl[r] = j < Ls[b] ? Ls[b] : j + 1;
+        }
+        hlast[b] = off[b + 1] - 1;
+        for (int r0 = off[b]; r0 < off[b + 1]; r0 += 16, ++ti) {
+            htile[3 * ti] = b;
+            htile[3 * ti + 1] = r0;
+            htile[3 * ti + 2] = std::min(16, off[b + 1] - r0);
+        }
+    }
+    hipMemcpyAsync(pk_rowinfo, hs, (size_t)3 * R * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(pk_last, hlast, (size_t)B * 4, hipMemcpyHostToDevice, st);
+    if (ntiles > pk_tile_cap) {
+        if (pk_tiles) hipFree(pk_tiles);
+        pk_tiles = nullptr;
+        pk_tile_cap = 0;
+        if (hipMalloc((void**)&pk_tiles, (size_t)3 * ntiles * 4) != hipSuccess)
+            return set_error(GSV_E_HIP, "packed prefill tile table");
+        pk_tile_cap = ntiles;
+    }
+    hipMemcpyAsync(pk_tiles, htile, (size_t)3 * ntiles * 4, hipMemcpyHostToDevice, st);
+    // the LDS-staged tile kernel measured slower here (prefill 62.5 vs 45.4 ms at B=64):
+    // kept behind GENIE_PACKED_TILE for A/B
+    static const bool tile_opt = [] { const char* e = std::getenv("GENIE_PACKED_TILE"); return e && std::atoi(e); }();
+    const bool tiled = tile_opt && maxn0 <= ATTN_TILE_MAXK;
+    const int* row_seq = pk_rowinfo;
+    const int* row_pos = pk_rowinfo + R;
+    const int* row_len = pk_rowinfo + 2 * R;
+    // encoder per utterance (prompts computed once per distinct ssl_content buffer)
+    for (int b = 0; b < B; ++b) {
+        const gsv_utt& u = utts[b];
+        int64_t* pr = pk_prompts + poff[b];
+        int src = -1;
+        for (int c = 0; c < b && src < 0; ++c)
+            if (utts[c].ssl == u.ssl && utts[c].n_ssl == u.n_ssl) src = c;
+        if (int e = encode(&u, pk_H + (size_t)off[b] * 512, pr, st, src < 0)) return e;
+        if (src >= 0) hipMemcpyAsync(pr, pk_prompts + poff[src], (size_t)Ps[b] * 8, hipMemcpyDeviceToDevice, st);
+        if (timing && b == 0) hipEventRecord(ev[1], st);
+        seq_state_init(b, pr, Ps[b], Ls[b], y, tmax, ny, kvlen, steps, done, seen, st);
+        audio_embed_prompts(pr, Ps[b], emb_audio, alpha_audio, pe_tab, pk_H + (size_t)(off[b] + Ls[b]) * 512, st);
+    }
+    const long sstride = (long)16 * tmax * 32;
+    const long slab_stride = (long)R * 512;
+    const bool slabs = gemm_slabs_supported(512, 512, 512) && gemm_slabs_supported(2048, 2048, 2048);
+    for (int l = 0; l < 24; ++l) {
+        const T2SLayerW& W = layers[l];
+        GemmArgs g{};
+        g.M = R; g.N = 1536; g.K = 512; g.A = pk_H; g.lda = 512;
+        g.W = W.w_in; g.ldw = 512; g.w_f16 = 1; g.bias = W.b_in;
+        g.C = pk_Q; g.ldc = 512; g.mode = EPI_QKV;
+        g.kv.k = kcache[l]; g.kv.v = vcache[l]; g.kv.tmax = tmax; g.kv.seq_stride = sstride;
+        g.kv.row_seq = row_seq; g.kv.row_pos = row_pos;
+        gemm_nt(g, st);
+        AttnArgs at{};
+        at.q = pk_Q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l];
+        at.seq_stride = sstride; at.tmax = tmax; at.row_len = row_len; at.row_seq = row_seq;
+        at.out = pk_O; at.ldo = 512; at.rows = R; at.scale = qk_scale;
+        if (tiled) {
+            at.tiles = pk_tiles;
+            at.ntiles = ntiles;
+            attn_rows_tiled(at, st);
+        } else {
+            attn_rows(at, st);
+        }
+        GemmArgs go{};
+        go.M = R; go.N = 512; go.K = 512; go.A = pk_O; go.lda = 512;
+        go.W = W.w_out; go.ldw = 512; go.w_f16 = 1; go.bias = W.b_out;
+        GemmArgs g1{};
+        g1.M = R; g1.N = 2048; g1.K = 512; g1.A = pk_H1; g1.lda = 512;
+        g1.W = W.w1; g1.ldw = 512; g1.w_f16 = 1; g1.bias = W.b1;
+        g1.C = pk_F; g1.ldc = 2048; g1.mode = EPI_RELU;
+        GemmArgs g2{};
+        g2.M = R; g2.N = 512; g2.K = 2048; g2.A = pk_F; g2.lda = 2048;
+        g2.W = W.w2; g2.ldw = 2048; g2.w_f16 = 1; g2.bias = W.b2;
+        if (slabs) {
+            go.C = pk_slab; go.ldc = 512; go.mode = EPI_SLAB; go.ksplit = 4; go.slab_stride = slab_stride;
+            gemm_nt(go, st);
+            layernorm_rows_slabs(pk_slab, 4, slab_stride, W.b_out, pk_H, pk_H1, R, W.n1w, W.n1b, st);
+            gemm_nt(g1, st);
+            g2.C = pk_slab; g2.ldc = 512; g2.mode = EPI_SLAB; g2.ksplit = 8; g2.slab_stride = slab_stride;
+            gemm_nt(g2, st);
+            layernorm_rows_slabs(pk_slab, 8, slab_stride, W.b2, pk_H1, pk_H, R, W.n2w, W.n2b, st);
+        } else {
+            go.C = pk_S; go.ldc = 512; go.mode = EPI_RESID; go.res = pk_H; go.ldr = 512;
+            gemm_nt(go, st);
+            layernorm_rows(pk_S, pk_H1, R, W.n1w, W.n1b, st);
+            gemm_nt(g1, st);
+            g2.C = pk_S; g2.ldc = 512; g2.mode = EPI_RESID; g2.res = pk_H1; g2.ldr = 512;
+            gemm_nt(g2, st);
+            layernorm_rows(pk_S, pk_H, R, W.n2w, W.n2b, st);
+        }
+    }
+    // logits of each sequence's last row (#1785-1788), first-stage sampler (#1789-1815)
+    hipLaunchKernelGGL(k_gather_rows512, dim3(B), dim3(256), 0, st, pk_H, pk_last, pk_xlast, B);
+    GemmArgs lg{};
+    lg.M = B; lg.N = 1025; lg.K = 512; lg.A = pk_xlast; lg.lda = 512; lg.W = w_pred; lg.ldw = 512;
+    lg.w_f16 = 1; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
+    gemm_nt(lg, st);
+    SampleArgs sa = sampler_args(sp, B);
+    sa.prefill = 1;
+    sample_tokens(sa, st);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "packed prefill launch");
+}
+
 SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
     SampleArgs sa{};
     sa.B = B;
@@ -474,38 +661,45 @@ void gsv_engine::decode_step(int B, const gsv_sampler* sp, float* logits_out, hi
         lg.acc_in = accF(23); lg.acc_bstride = ACC_SEQ;
         gemv_f16(lg, st);
     } else {
-        // batched path: f32-MFMA GEMMs over the B rows + row LayerNorms
+        // batched path (B > 8): split-fp16 MFMA GEMMs over the B rows with the K
+        // dimension split over grid.z into f32 slabs (>= 96 workgroups per GEMM at
+        // B = 64 instead of N / 64), each reduction fused into its consumer: the
+        // attention prologue sums the QKV slabs (+ bias, K/V row append), the
+        // LayerNorms sum the out-projection / FFN2 slabs (+ bias + residual), and
+        // FFN2's operand load sums the FFN1 slabs (+ bias, ReLU).  Slab sums run in
+        // a fixed order: results do not depend on scheduling.
+        const long sq = (long)B * 1536, sf = (long)B * 2048, so = (long)B * 512;
+        float* slabA = dslab;                       // QKV slabs, then FFN1 slabs
+        float* slabB = dslab + (long)4 * max_batch * 2048;   // out-proj slabs, then FFN2 slabs
         for (int l = 0; l < 24; ++l) {
             const T2SLayerW& W = layers[l];
-            if (l > 0) layernorm_rows(s2, h, B, layers[l - 1].n2w, layers[l - 1].n2b, st);
             GemmArgs g{};
             g.M = B; g.N = 1536; g.K = 512; g.A = h; g.lda = 512;
-            g.W = W.w_in; g.ldw = 512; g.w_f16 = 1; g.bias = W.b_in; g.C = q; g.ldc = 512;
-            g.mode = EPI_QKV; g.kv.k = kcache[l]; g.kv.v = vcache[l]; g.kv.tmax = tmax;
-            g.kv.row_pos = kvlen; g.kv.row_seq = ident; g.kv.seq_stride = sstride; g.kv.row_skip = done;
+            g.W = W.w_in; g.ldw = 512; g.w_f16 = 1;
+            g.C = slabA; g.ldc = 1536; g.mode = EPI_SLAB; g.ksplit = 4; g.slab_stride = sq;
             gemm_nt(g, st);
-            AttnArgs at{};
-            at.q = q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l]; at.seq_stride = sstride;
-            at.tmax = tmax; at.row_len = kvlen; at.row_seq = ident; at.out = o; at.ldo = 512;
-            at.rows = B; at.scale = qk_scale; at.row_skip = done;
-            attn_rows_plus(at, 1, st);
+            AttnDecArgs at{};
+            at.slabs = slabA; at.nslab = 4; at.slab_stride = sq; at.b_in = W.b_in;
+            at.k = kcache[l]; at.v = vcache[l]; at.seq_stride = sstride; at.tmax = tmax;
+            at.kvlen = kvlen; at.done = done; at.out = o; at.B = B; at.scale = qk_scale;
+            attn_decode_slabs(at, st);
             GemmArgs go{};
             go.M = B; go.N = 512; go.K = 512; go.A = o; go.lda = 512; go.W = W.w_out; go.ldw = 512;
-            go.w_f16 = 1; go.bias = W.b_out; go.C = s1; go.ldc = 512; go.mode = EPI_RESID;
-            go.res = h; go.ldr = 512;
+            go.w_f16 = 1; go.C = slabB; go.ldc = 512; go.mode = EPI_SLAB; go.ksplit = 4; go.slab_stride = so;
             gemm_nt(go, st);
-            layernorm_rows(s1, h1, B, W.n1w, W.n1b, st);
+            layernorm_rows_slabs(slabB, 4, so, W.b_out, h, h1, B, W.n1w, W.n1b, st);
             GemmArgs g1{};
             g1.M = B; g1.N = 2048; g1.K = 512; g1.A = h1; g1.lda = 512; g1.W = W.w1; g1.ldw = 512;
-            g1.w_f16 = 1; g1.bias = W.b1; g1.C = f; g1.ldc = 2048; g1.mode = EPI_RELU;
+            g1.w_f16 = 1; g1.C = slabA; g1.ldc = 2048; g1.mode = EPI_SLAB; g1.ksplit = 4; g1.slab_stride = sf;
             gemm_nt(g1, st);
             GemmArgs g2{};
-            g2.M = B; g2.N = 512; g2.K = 2048; g2.A = f; g2.lda = 2048; g2.W = W.w2; g2.ldw = 2048;
-            g2.w_f16 = 1; g2.bias = W.b2; g2.C = s2; g2.ldc = 512; g2.mode = EPI_RESID;
-            g2.res = h1; g2.ldr = 512;
+            g2.M = B; g2.N = 512; g2.K = 2048; g2.A = slabA; g2.lda = 2048;
+            g2.a_nslab = 4; g2.a_slab_stride = sf; g2.a_bias = W.b1; g2.a_relu = 1;
+            g2.W = W.w2; g2.ldw = 2048; g2.w_f16 = 1;
+            g2.C = slabB; g2.ldc = 512; g2.mode = EPI_SLAB; g2.ksplit = 16; g2.slab_stride = so;
             gemm_nt(g2, st);
+            layernorm_rows_slabs(slabB, 16, so, W.b2, h1, h, B, W.n2w, W.n2b, st);
         }
-        layernorm_rows(s2, h, B, layers[23].n2w, layers[23].n2b, st);
         GemmArgs lg{};
         lg.M = B; lg.N = 1025; lg.K = 512; lg.A = h; lg.lda = 512; lg.W = w_pred; lg.ldw = 512;
         lg.w_f16 = 1; lg.C = logits; lg.ldc = 1025; lg.mode = EPI_STORE;
@@ -867,12 +1061,16 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     eng->loop_limit = limit;
     if (eng->timing) hipEventRecord(eng->ev[0], st);
     hipMemsetAsync(eng->done, 1, eng->max_batch, st);
-    for (int b = 0; b < batch; ++b) {
-        const gsv_utt& u = utts[b];
-        const int L = u.n_ref + u.n_text, P = u.n_ssl / 2;
-        if (int e = eng->encode(&u, eng->pH, eng->prompts_buf, st)) return e;
-        if (eng->timing && b == 0) hipEventRecord(eng->ev[1], st);
-        if (int e = eng->prefill_slot(b, eng->pH, L, eng->prompts_buf, P, &sp, nullptr, st)) return e;
+    if (batch > 1 && eng->use_packed) {
+        if (int e = eng->prefill_packed(batch, utts, &sp, st)) return e;
+    } else {
+        for (int b = 0; b < batch; ++b) {
+            const gsv_utt& u = utts[b];
+            const int L = u.n_ref + u.n_text, P = u.n_ssl / 2;
+            if (int e = eng->encode(&u, eng->pH, eng->prompts_buf, st)) return e;
+            if (eng->timing && b == 0) hipEventRecord(eng->ev[1], st);
+            if (int e = eng->prefill_slot(b, eng->pH, L, eng->prompts_buf, P, &sp, nullptr, st)) return e;
+        }
     }
     if (eng->timing) hipEventRecord(eng->ev[2], st);
     const int rc = eng->decode_loop(batch, &sp, st);
@@ -968,7 +1166,9 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     if (!name) return set_error(GSV_E_ARG, "null option name");
     hipSetDevice(eng->device);
     const std::string n(name);
-    if (n == "persist") {
+    if (n == "packed") {          // batched generate: one packed prefill over all utterances
+        eng->use_packed = value != 0;
+    } else if (n == "persist") {
         eng->use_persist = value != 0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;

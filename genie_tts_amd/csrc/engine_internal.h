@@ -56,6 +56,7 @@ struct gsv_engine {
     int *ny = nullptr, *kvlen = nullptr, *steps = nullptr, *ident = nullptr;
     uint8_t *done = nullptr, *stopf = nullptr;
     uint32_t* seen = nullptr;
+    float* dslab = nullptr;           // batched decode: [2][4][B][2048] split-K slabs
     int* forceb = nullptr;            // per-slot forced loop length (gsv_utt.force_steps; 0 = sampler rule)
     int loop_limit = 0;               // >0: loop-step bound of the current generate (max over its slots)
     float *h = nullptr, *h1 = nullptr, *s1 = nullptr, *s2 = nullptr, *q = nullptr, *o = nullptr;
@@ -123,7 +124,20 @@ struct gsv_engine {
     int finalize_prompt_encoder();
     int reserve(int batch, int tokens);
     int ensure_enc_ws(int P, int L);
-    int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st);
+    int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st, bool do_prompts = true);
+    // packed (multi-utterance) prefill
+    bool use_packed = true;            // option "packed"
+    int pk_rows = 0, pk_batch = 0;
+    std::vector<void*> pk_allocs;
+    float *pk_H = nullptr, *pk_Q = nullptr, *pk_O = nullptr, *pk_S = nullptr, *pk_H1 = nullptr, *pk_F = nullptr;
+    float *pk_slab = nullptr, *pk_xlast = nullptr;
+    int *pk_rowinfo = nullptr, *pk_last = nullptr;
+    int64_t* pk_prompts = nullptr;
+    int* pk_tiles = nullptr;
+    int pk_tile_cap = 0;
+    std::vector<int> pk_host;
+    int ensure_packed(int rows, int B);
+    int prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp, hipStream_t st);
     int prefill_slot(int b, const float* x, int L, const int64_t* pr, int P, const gsv_sampler* sp,
                      float* logits_out, hipStream_t st);
     gsv::SampleArgs sampler_args(const gsv_sampler* sp, int B);

@@ -41,6 +41,8 @@ struct GemmArgs {
     const float* rowsq; const float* colsq;
     KVScatter kv;
     int ksplit; long slab_stride;    // EPI_SLAB: K split over grid.z (fp16-weight path only)
+    // optional A prologue (fp16-weight path): A(m,k) = relu?(a_bias[k] + sum_z A[z * a_slab_stride + m*lda + k])
+    int a_nslab; long a_slab_stride; const float* a_bias; int a_relu;
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 // EPI_SLAB (split-K into slabs) is available for fp16 weights with these shapes
@@ -81,8 +83,25 @@ struct AttnArgs {
     int rows;
     float scale;                       // sqrt(1/sqrt(32)) applied to q and k separately
     const uint8_t* row_skip;
+    const int* tiles;                  // packed prefill: [ntiles][3] {seq, row0, nrows<=16}, rows of one seq
+    int ntiles;
 };
+constexpr int ATTN_TILE_MAXK = 448;   // keys a k_attn_tile block stages in LDS
 void attn_rows(const AttnArgs& a, hipStream_t s);
+// Tiled prefill attention over a.tiles (all rows' keys <= ATTN_TILE_MAXK).
+void attn_rows_tiled(const AttnArgs& a, hipStream_t s);
+// Batched decode attention (one block per head x sequence) whose prologue reduces
+// the split-K QKV slabs of its head: q/k/v = b_in + sum_z slab[z][b][...] (fixed
+// order), appends the new K/V row at position kvlen[b], attends over [0, kvlen[b]].
+struct AttnDecArgs {
+    const float* slabs; int nslab; long slab_stride;   // [nslab][B][1536]
+    const float* b_in;
+    float* k; float* v; long seq_stride; int tmax;     // caches (sequence 0 base)
+    const int* kvlen; const uint8_t* done;
+    float* out;                                        // [B][512]
+    int B; float scale;
+};
+void attn_decode_slabs(const AttnDecArgs& a, hipStream_t s);
 // same, with len(row) = row_len[r] + len_add (decode: kvlen + 1)
 void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s);
 

@@ -154,8 +154,26 @@ __global__ __launch_bounds__(256) void k_gemm_x2(GemmArgs a) {
         for (int i = 0; i < 8; ++i) {
             const int e = tid + 256 * i, row = e >> 5, kc = (e & 31) * 4;
             const int gm = m0 + row;
-            R.a[i] = gm < a.M ? *reinterpret_cast<const float4*>(a.A + (long)gm * a.lda + k0 + kc)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.a_nslab > 0) {
+                // A = relu?(bias + sum of the producer's split-K slabs), summed in slab order
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (gm < a.M) {
+                    const float* src = a.A + (long)gm * a.lda + k0 + kc;
+                    v = *reinterpret_cast<const float4*>(src);
+                    for (int z = 1; z < a.a_nslab; ++z) {
+                        const float4 u = *reinterpret_cast<const float4*>(src + z * a.a_slab_stride);
+                        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+                    }
+                    const float4 bb = *reinterpret_cast<const float4*>(a.a_bias + k0 + kc);
+                    v = make_float4(bb.x + v.x, bb.y + v.y, bb.z + v.z, bb.w + v.w);
+                    if (a.a_relu)
+                        v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                }
+                R.a[i] = v;
+            } else {
+                R.a[i] = gm < a.M ? *reinterpret_cast<const float4*>(a.A + (long)gm * a.lda + k0 + kc)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -500,6 +518,89 @@ __global__ __launch_bounds__(256) void k_attn_rows(AttnArgs a, int len_add) {
     }
 }
 
+// Batched decode attention with the QKV split-K reduction in its prologue: block
+// (head h, sequence b).  q/k/v of the head = b_in + sum_z slab[z] (z ascending,
+// the same order for every block), the new K/V row goes to cache position
+// kvlen[b] and is used from LDS; then (q s)(k s) over [0, kvlen[b]] (stage#91-94),
+// softmax (#95), P.V (#96) as k_attn_rows.
+__global__ __launch_bounds__(256) void k_attn_dec_slabs(AttnDecArgs a) {
+    __shared__ float p[ATTN_MAXT];
+    __shared__ float qs[32], kn[32], vn[32];
+    __shared__ float red[16];
+    __shared__ float part[8][33];
+    const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    if (a.done[b]) return;
+    const int pos = a.kvlen[b], len = pos + 1;
+    float* K = a.k + (long)b * a.seq_stride + (long)h * a.tmax * 32;
+    float* V = a.v + (long)b * a.seq_stride + (long)h * a.tmax * 32;
+    const float sc = a.scale;
+    if (tid < 96) {
+        const int part_ = tid >> 5, d = tid & 31, col = part_ * 512 + h * 32 + d;
+        const float* src = a.slabs + (long)b * 1536 + col;
+        float v = src[0];
+        for (int z = 1; z < a.nslab; ++z) v += src[z * a.slab_stride];
+        v = a.b_in[col] + v;   // Add(bias, MatMul)
+        if (part_ == 0) qs[d] = v * sc;
+        else if (part_ == 1) { kn[d] = v; K[(long)pos * 32 + d] = v; }
+        else { vn[d] = v; V[(long)pos * 32 + d] = v; }
+    }
+    __syncthreads();
+    float lmax = -INFINITY;
+    for (int t0 = 0; t0 < len; t0 += 512) {
+        const int ta = t0 + tid, tb = t0 + 256 + tid;
+        float4 ka[8], kb[8];
+        const float4* kra = reinterpret_cast<const float4*>(ta < pos ? K + (long)ta * 32 : kn);
+        const float4* krb = reinterpret_cast<const float4*>(tb < pos ? K + (long)tb * 32 : kn);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { ka[i] = kra[i]; kb[i] = krb[i]; }
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            sa += qs[4 * i] * (ka[i].x * sc); sa += qs[4 * i + 1] * (ka[i].y * sc);
+            sa += qs[4 * i + 2] * (ka[i].z * sc); sa += qs[4 * i + 3] * (ka[i].w * sc);
+            sb += qs[4 * i] * (kb[i].x * sc); sb += qs[4 * i + 1] * (kb[i].y * sc);
+            sb += qs[4 * i + 2] * (kb[i].z * sc); sb += qs[4 * i + 3] * (kb[i].w * sc);
+        }
+        if (ta < len) { p[ta] = sa; lmax = fmaxf(lmax, sa); }
+        if (tb < len) { p[tb] = sb; lmax = fmaxf(lmax, sb); }
+    }
+    const float m = block_max(lmax, red);
+    float lsum = 0.f;
+    for (int t = tid; t < len; t += 256) {
+        const float e = expf(p[t] - m);
+        p[t] = e;
+        lsum += e;
+    }
+    const float sum = block_sum(lsum, red);
+    for (int t = tid; t < len; t += 256) p[t] = p[t] / sum;
+    __syncthreads();
+    const int g = tid >> 5, d = tid & 31;
+    float acc = 0.f;
+    int t = g;
+    for (; t + 56 < pos; t += 64) {
+        float vv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vv[i] = V[(long)(t + 8 * i) * 32 + d];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += p[t + 8 * i] * vv[i];
+    }
+    for (; t < pos; t += 8) acc += p[t] * V[(long)t * 32 + d];
+    if (t == pos) acc += p[t] * vn[d];
+    part[g][d] = acc;
+    __syncthreads();
+    if (tid < 32) {
+        float o = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o += part[i][tid];
+        a.out[(long)b * 512 + h * 32 + tid] = o;
+    }
+}
+
+void attn_decode_slabs(const AttnDecArgs& a, hipStream_t s) {
+    if (a.B <= 0) return;
+    hipLaunchKernelGGL(k_attn_dec_slabs, dim3(16, a.B), dim3(256), 0, s, a);
+}
+
 // Prefill attention, one sequence: a block = one head x 16 query rows, one row
 // per wave (1024 threads).  The head's keys/values [0, max row_len of the block)
 // are staged in LDS once (36-float rows: conflict-free 16-B reads by 16 lanes);
@@ -516,16 +617,27 @@ __global__ __launch_bounds__(1024) void k_attn_tile(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) float Ks[AT_MAXK * AT_KS];
     __shared__ __attribute__((aligned(16))) float Vs[AT_MAXK * AT_KS];
     __shared__ int rl[AT_ROWS];
-    const int h = blockIdx.x, r0 = blockIdx.y * AT_ROWS, tid = threadIdx.x;
+    const int h = blockIdx.x, tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
-    const int nr = min(AT_ROWS, a.rows - r0);
+    // one sequence's rows: a tile of the packed prefill, or rows [16 y, 16 y + 16) of sequence 0
+    int r0, nr;
+    long seq_off = 0;
+    if (a.tiles) {
+        const int* tl = a.tiles + 3 * blockIdx.y;
+        seq_off = (long)tl[0] * a.seq_stride;
+        r0 = tl[1];
+        nr = tl[2];
+    } else {
+        r0 = blockIdx.y * AT_ROWS;
+        nr = min(AT_ROWS, a.rows - r0);
+    }
     if (tid < AT_ROWS) rl[tid] = tid < nr ? a.row_len[r0 + tid] : 0;
     __syncthreads();
     int kmax = 0;
 #pragma unroll
     for (int i = 0; i < AT_ROWS; ++i) kmax = max(kmax, rl[i]);
-    const float* K = a.k + (long)h * a.tmax * 32;
-    const float* V = a.v + (long)h * a.tmax * 32;
+    const float* K = a.k + seq_off + (long)h * a.tmax * 32;
+    const float* V = a.v + seq_off + (long)h * a.tmax * 32;
     for (int e = tid; e < kmax * 8; e += 1024) {            // 16-B pieces: row e/8, piece e%8
         const int t = e >> 3, c = e & 7;
         const float4 kv = *reinterpret_cast<const float4*>(K + (long)t * 32 + 4 * c);
@@ -617,6 +729,12 @@ void attn_rows(const AttnArgs& a, hipStream_t s) {
         return;
     }
     hipLaunchKernelGGL(k_attn_rows, dim3(16, a.rows), dim3(256), 0, s, a, 0);
+}
+
+void attn_rows_tiled(const AttnArgs& a, hipStream_t s) {
+    if (a.ntiles <= 0) return;
+    static_assert(AT_MAXK == ATTN_TILE_MAXK, "tile key capacity");
+    hipLaunchKernelGGL(k_attn_tile, dim3(16, a.ntiles), dim3(1024), 0, s, a);
 }
 
 void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s) {
