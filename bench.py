@@ -82,6 +82,7 @@ class Runner:
         self.d_txt = [T(it.text_seq.reshape(-1)) for it in items]
         self.d_bert = [None if it.text_bert is None else T(it.text_bert) for it in items]
         self.sp = make_sampler(top_k=wl.top_k, greedy=wl.greedy)
+        self.seed = 0x5EED
         self.ge = self.ge_adv = None
         if wl.version != "v2":
             self.ge, self.ge_adv = self.eng.prompt_encode(self.d_audio, T(ref.sv_emb.reshape(-1)))
@@ -98,13 +99,14 @@ class Runner:
         tm = self.eng.timing()                              # device phases of this generate (ms)
         self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
         self.phase["decode"] += tm[2] * 1e-3
-        n = 0
-        for t, sem in zip(self.d_txt, sems):
-            if self.ge is None:
-                wav = self.eng.vits_decode(t, sem, ref_audio=self.d_audio)
-            else:
-                wav = self.eng.vits_decode(t, sem, ge=self.ge, ge_advanced=self.ge_adv)
-            n += int(wav.numel())
+        # vocoder with the reference's z_p noise (RandomNormalLike x 0.5) from the device Philox stream
+        cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
+        if len(sems) == 1:
+            wavs = [self.eng.vits_decode(self.d_txt[0], sems[0], noise_seed=self.seed, **cond)]
+        else:   # concurrent vocoder lanes
+            wavs = self.eng.vits_decode_batch([dict(text_seq=t, pred_semantic=sem, noise_seed=self.seed + i, **cond)
+                                               for i, (t, sem) in enumerate(zip(self.d_txt, sems))])
+        n = sum(int(w.numel()) for w in wavs)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         self.phase["t2s"] += t1 - t0

@@ -65,6 +65,13 @@ gsv_engine::~gsv_engine() {
     if (perr_host) hipHostFree(perr_host);
     if (vovf_host) hipHostFree(vovf_host);
     if (vovf) hipFree(vovf);
+    for (auto& L : vlanes) {
+        if (L.st) hipStreamDestroy(L.st);
+        if (L.join) hipEventDestroy(L.join);
+    }
+    if (vfork) hipEventDestroy(vfork);
+    if (vflags) hipFree(vflags);
+    if (vflags_host) hipHostFree(vflags_host);
     if (perr) hipFree(perr);
     for (void* p : state_allocs) hipFree(p);
     state_allocs.clear();

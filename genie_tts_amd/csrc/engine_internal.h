@@ -151,10 +151,24 @@ struct gsv_engine {
     int persist1_pf_delay = 0;         // GENIE_PF_DELAY: s_sleep(32) ticks before the next-layer prefetch        // option "persist1_f16_limit" (0: the fp16 range, 65504)
     int vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                     const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
-                    const float* eps, float noise_scale, float* audio, hipStream_t st);
-    int vits_decode_pass(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
+                    const float* eps, uint64_t noise_seed, float noise_scale, float* audio, hipStream_t st);
+    int vits_decode_pass(gsv::VitsWorkspace& W, const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                          const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
-                         const float* eps, float noise_scale, float* audio, hipStream_t st, bool f16);
+                         const float* eps, uint64_t noise_seed, float noise_scale, float* audio, hipStream_t st,
+                         int* ovf, bool timed);
+    // concurrent vocoder lanes (gsv_vits_decode_batch)
+    static constexpr int VITS_LANES = 4;   // = the box's hardware queues per process
+    struct VitsLane {
+        hipStream_t st = nullptr;
+        hipEvent_t join = nullptr;
+        gsv::VitsWorkspace ws;
+    };
+    std::vector<VitsLane> vlanes;
+    hipEvent_t vfork = nullptr;
+    int* vflags = nullptr;
+    int* vflags_host = nullptr;
+    int vflag_cap = 0;
+    int vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s);
     int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                       float* ge_adv, hipStream_t st);
 };

@@ -86,6 +86,8 @@ void glu_resid(const float* h, const float* x, float* out, int C, int T, long x_
                hipStream_t s);                                                  // out = x + a*sigmoid(b)
 void noise_zp(const float* m, const float* logs, const float* eps, float scale, float* z, int n,
               hipStream_t s);
+void noise_zp_philox(const float* m, const float* logs, uint64_t seed, float scale, float* z, int n,
+                     hipStream_t s);                                              // eps ~ Philox N(0,1)
 void flip_channels(const float* in, float* out, int C, int T, hipStream_t s);
 void reflect_pad(const float* x, int n, int pad, float* out, hipStream_t s);
 void stft_mag(const float* reim, int frames, int bins, float* spec, hipStream_t s); // [F][2*bins] -> [F][bins]

@@ -447,6 +447,19 @@ void noise_zp(const float* m, const float* logs, const float* eps, float scale, 
               hipStream_t s) {
     hipLaunchKernelGGL(k_noise, dim3((n + 255) / 256), dim3(256), 0, s, m, logs, eps, scale, z, n);
 }
+// Same with eps = the engine's Philox N(0,1): element i <- Philox4x32-10(counter
+// (i, 0, 0, 0x7A), key seed), Box-Muller on the first two words (tests/philox.py
+// restates it), standing in for onnxruntime's RandomNormalLike draw.
+__global__ void k_noise_philox(const float* m, const float* logs, uint64_t seed, float sc, float* z, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 r = philox4x32(make_uint4((uint32_t)i, 0u, 0u, 0x7Au), make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const float e = sqrtf(-2.0f * logf(u01_open(r.x))) * cospif(2.0f * u01_open(r.y));
+    z[i] = m[i] + (e * expf(logs[i])) * sc;
+}
+void noise_zp_philox(const float* m, const float* logs, uint64_t seed, float scale, float* z, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_noise_philox, dim3((n + 255) / 256), dim3(256), 0, s, m, logs, seed, scale, z, n);
+}
 
 __global__ void k_flip(const float* in, float* out, int C, int T) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;

@@ -317,9 +317,8 @@ static void attn_encoder(gsv_engine* e, const std::vector<AttnLayer>& Ls, float*
 }
 
 // MelStyleEncoder on an STFT magnitude [F][704] -> ge [out_dim] (vits(v2)#79-271)
-static void run_ref_enc(gsv_engine* e, const RefEnc& R, const float* audio, int n, float* ge,
+static void run_ref_enc(VitsWorkspace& W, const RefEnc& R, const float* audio, int n, float* ge,
                         hipStream_t s) {
-    VitsWorkspace& W = e->vws;
     const int padded = n + 2 * 704;
     const int F = (padded - 2048) / 640 + 1;
     reflect_pad(audio, n, 704, W.pad, s);
@@ -368,8 +367,7 @@ static void run_ref_enc(gsv_engine* e, const RefEnc& R, const float* audio, int 
     time_mean(W.r0, F, R.out_dim, ge, s);
 }
 
-static int ensure_vits_ws(gsv_engine* e, int T, int S, int n_audio) {
-    VitsWorkspace& W = e->vws;
+static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_audio) {
     const VitsWeights& V = e->vits;
     const size_t gen = (size_t)V.upc * T * 20;    // max C*T over generator stages: upc/2^(i+1) * T*prod(u)
     const int F = n_audio > 0 ? (n_audio + 1408 - 2048) / 640 + 1 : 0;
@@ -410,32 +408,36 @@ static int ensure_vits_ws(gsv_engine* e, int T, int S, int n_audio) {
 // fp16 range.  The flag check is a host sync on the caller's stream.
 int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int G,
                             const float* ref_audio, int n_audio, const float* ge_in,
-                            const float* ge_adv_in, const float* eps, float noise_scale, float* audio,
-                            hipStream_t s) {
+                            const float* ge_adv_in, const float* eps, uint64_t noise_seed, float noise_scale,
+                            float* audio, hipStream_t s) {
     if (use_convh && !vovf) {
         if (hipMalloc(&vovf, 64) != hipSuccess || hipHostMalloc((void**)&vovf_host, 64, hipHostMallocDefault) != hipSuccess)
             return set_error(GSV_E_HIP, "overflow flag alloc");
         hipMemset(vovf, 0, 64);
     }
     if (!use_convh)
-        return vits_decode_pass(text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_scale,
-                                audio, s, false);
-    if (int r = vits_decode_pass(text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_scale,
-                                 audio, s, true))
+        return vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
+                                noise_scale, audio, s, nullptr, timing);
+    if (int r = vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
+                                 noise_scale, audio, s, vovf, timing))
         return r;
     hipMemcpyAsync(vovf_host, vovf, 4, hipMemcpyDeviceToHost, s);
     if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vits sync");
     if (*vovf_host == 0) return 0;
     hipMemsetAsync(vovf, 0, 4, s);
     ++vits_f32_reruns;
-    return vits_decode_pass(text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_scale, audio,
-                            s, false);
+    return vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed, noise_scale,
+                            audio, s, nullptr, timing);
 }
 
-int gsv_engine::vits_decode_pass(const int64_t* text_seq, int n_text, const int64_t* sem, int G,
+// One utterance on stream s with workspace W.  ovf != NULL: the MRF convs run on
+// the f16-split path and OR 1 into *ovf on an fp16-range overflow.  noise: eps
+// (device [192, 2G]) if given, else Philox N(0,1) keyed by noise_seed when it is
+// non-zero, else zeros.  timed: phase events (ms[3]) around the pass.
+int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int n_text, const int64_t* sem, int G,
                                  const float* ref_audio, int n_audio, const float* ge_in,
-                                 const float* ge_adv_in, const float* eps, float noise_scale, float* audio,
-                                 hipStream_t s, bool f16) {
+                                 const float* ge_adv_in, const float* eps, uint64_t noise_seed, float noise_scale,
+                                 float* audio, hipStream_t s, int* ovf, bool timed) {
     const VitsWeights& V = vits;
     if (!V.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
     if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
@@ -443,18 +445,17 @@ int gsv_engine::vits_decode_pass(const int64_t* text_seq, int n_text, const int6
     if (pp ? (!ge_in || !ge_adv_in) : !ref_audio) return set_error(GSV_E_ARG, "missing conditioning input");
     const int T = 2 * G, S = n_text;
     if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
-    if (int r = ensure_vits_ws(this, T, S, pp ? 0 : n_audio)) return r;
-    VitsWorkspace& W = vws;
+    if (int r = ensure_vits_ws(this, W, T, S, pp ? 0 : n_audio)) return r;
     SplitkScope sk(W.splitk, W.splitk_cap);
-    tls_ovf = f16 ? vovf : nullptr;
+    tls_ovf = ovf;
     struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
-    if (timing) hipEventRecord(ev[4], s);
+    if (timed) hipEventRecord(ev[4], s);
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
     const float* ge;
     const float* ge_m;
     if (!pp) {
-        run_ref_enc(this, V.ref, ref_audio, n_audio, W.ge, s);
+        run_ref_enc(W, V.ref, ref_audio, n_audio, W.ge, s);
         ge = W.ge;
         ge_m = W.ge;
     } else {
@@ -486,7 +487,10 @@ int gsv_engine::vits_decode_pass(const int64_t* text_seq, int n_text, const int6
     attn_encoder(this, V.enc2, W.y, T, W.qkv, W.att, W.a, W.ffn, s);
     conv1d(cargs(V.proj, W.y, T, W.stats), s);
     // ---- z_p = m_p + eps*exp(logs_p)*noise_scale
-    noise_zp(W.stats, W.stats + (size_t)192 * T, eps, noise_scale, W.z, 192 * T, s);
+    if (!eps && noise_seed != 0)
+        noise_zp_philox(W.stats, W.stats + (size_t)192 * T, noise_seed, noise_scale, W.z, 192 * T, s);
+    else
+        noise_zp(W.stats, W.stats + (size_t)192 * T, eps, noise_scale, W.z, 192 * T, s);
     // ---- reverse flow: for f = 6,4,2,0: flip, coupling (mean-only)
     for (int fi = 3; fi >= 0; --fi) {
         const auto& fl = V.flows[fi];
@@ -575,7 +579,7 @@ int gsv_engine::vits_decode_pass(const int64_t* text_seq, int n_text, const int6
         cp.in_act = 1; cp.in_slope = 0.01f;
         conv1d(cp, s);
     }
-    if (timing) {
+    if (timed) {
         hipEventRecord(ev[5], s);
         hipEventSynchronize(ev[5]);
         hipEventElapsedTime(&ms[3], ev[4], ev[5]);
@@ -583,15 +587,87 @@ int gsv_engine::vits_decode_pass(const int64_t* text_seq, int n_text, const int6
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vits launch");
 }
 
+// Several utterances at once: utterance i runs on lane i % K (its own stream and
+// workspace), so up to K vocoder chains -- each a few hundred small launches that
+// under-fill the chip -- overlap on the GPU.  Each utterance has its own overflow
+// flag; after the join, flagged utterances are decoded again on the f32 path.
+int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n == 1) {   // one utterance: the engine stream itself, no lane fork/join
+        const gsv_vits_item& u = it[0];
+        return vits_decode(u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge, u.ge_adv,
+                           u.noise_mode == 1 ? u.eps : nullptr, u.noise_mode == 2 ? u.noise_seed : 0, noise_scale,
+                           u.audio, s);
+    }
+    const int K = std::min(n, VITS_LANES);
+    for (int l = (int)vlanes.size(); l < K; ++l) {
+        VitsLane L;
+        if (hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&L.join, hipEventDisableTiming) != hipSuccess)
+            return set_error(GSV_E_HIP, "vocoder lane stream");
+        vlanes.push_back(L);
+    }
+    if (!vfork && hipEventCreateWithFlags(&vfork, hipEventDisableTiming) != hipSuccess)
+        return set_error(GSV_E_HIP, "vocoder fork event");
+    if (n > vflag_cap) {
+        if (vflags) hipFree(vflags);
+        if (vflags_host) hipHostFree(vflags_host);
+        vflags = nullptr;
+        vflags_host = nullptr;
+        vflag_cap = 0;
+        if (hipMalloc((void**)&vflags, (size_t)n * 4) != hipSuccess ||
+            hipHostMalloc((void**)&vflags_host, (size_t)n * 4, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "vocoder flags");
+        vflag_cap = n;
+    }
+    if (timing) hipEventRecord(ev[4], s);
+    hipMemsetAsync(vflags, 0, (size_t)n * 4, s);
+    hipEventRecord(vfork, s);
+    for (int l = 0; l < K; ++l) hipStreamWaitEvent(vlanes[l].st, vfork, 0);
+    for (int i = 0; i < n; ++i) {
+        VitsLane& L = vlanes[i % K];
+        const gsv_vits_item& u = it[i];
+        if (int r = vits_decode_pass(L.ws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
+                                     u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
+                                     u.noise_mode == 2 ? u.noise_seed : 0, noise_scale, u.audio, L.st,
+                                     use_convh ? vflags + i : nullptr, false))
+            return r;
+    }
+    for (int l = 0; l < K; ++l) {
+        hipEventRecord(vlanes[l].join, vlanes[l].st);
+        hipStreamWaitEvent(s, vlanes[l].join, 0);
+    }
+    if (use_convh) {
+        hipMemcpyAsync(vflags_host, vflags, (size_t)n * 4, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vocoder batch sync");
+        for (int i = 0; i < n; ++i) {
+            if (!vflags_host[i]) continue;
+            ++vits_f32_reruns;
+            const gsv_vits_item& u = it[i];
+            if (int r = vits_decode_pass(vws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
+                                         u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
+                                         u.noise_mode == 2 ? u.noise_seed : 0, noise_scale, u.audio, s, nullptr,
+                                         false))
+                return r;
+        }
+    }
+    if (timing) {
+        hipEventRecord(ev[5], s);
+        hipEventSynchronize(ev[5]);
+        hipEventElapsedTime(&ms[3], ev[4], ev[5]);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vocoder batch");
+}
+
 int gsv_engine::prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                               float* ge_adv, hipStream_t s) {
     if (!penc.ready) return set_error(GSV_E_STATE, "prompt encoder weights not loaded");
     if (n_audio < 2048) return set_error(GSV_E_ARG, "reference audio too short");
-    if (int r = ensure_vits_ws(this, 2, 2, n_audio)) return r;
+    if (int r = ensure_vits_ws(this, vws, 2, 2, n_audio)) return r;
     VitsWorkspace& W = vws;
     SplitkScope sk(W.splitk, W.splitk_cap);
     (void)hipGetLastError();
-    run_ref_enc(this, penc.ref, ref_audio, n_audio, W.pe_ge, s);
+    run_ref_enc(W, penc.ref, ref_audio, n_audio, W.pe_ge, s);
     // ge = PReLU(ref_enc + (sv_emb @ W^T + b)); ge_adv = ge @ W512^T + b  (prompt_encoder#269-280)
     GemmArgs g{};
     g.M = 1; g.N = 1024; g.K = 20480; g.A = sv_emb; g.lda = 20480;
@@ -615,8 +691,22 @@ extern "C" int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     StreamScope sc(eng, stream);
-    return eng->vits_decode(text_seq, n_text, sem, n_sem, ref_audio, n_audio, ge, ge_adv, eps,
+    return eng->vits_decode(text_seq, n_text, sem, n_sem, ref_audio, n_audio, ge, ge_adv, eps, 0,
                             noise_scale, audio, sc.st());
+}
+
+extern "C" int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_item* items, float noise_scale,
+                                     void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    if (n < 0 || (n > 0 && !items)) return set_error(GSV_E_ARG, "bad args");
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    for (int i = 0; i < n; ++i)
+        if (items[i].noise_mode < 0 || items[i].noise_mode > 2 || (items[i].noise_mode == 1 && !items[i].eps) ||
+            !items[i].audio)
+            return set_error(GSV_E_ARG, "bad vocoder item " + std::to_string(i));
+    StreamScope sc(eng, stream);
+    return eng->vits_decode_batch(n, items, noise_scale, sc.st());
 }
 
 extern "C" int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,

@@ -39,6 +39,17 @@ class Utt(ctypes.Structure):
     ]
 
 
+class VitsItem(ctypes.Structure):
+    _fields_ = [
+        ("text_seq", ctypes.c_void_p), ("n_text", ctypes.c_int32),
+        ("sem", ctypes.c_void_p), ("n_sem", ctypes.c_int32),
+        ("ref_audio", ctypes.c_void_p), ("n_audio", ctypes.c_int32),
+        ("ge", ctypes.c_void_p), ("ge_adv", ctypes.c_void_p),
+        ("eps", ctypes.c_void_p), ("noise_seed", ctypes.c_uint64), ("noise_mode", ctypes.c_int32),
+        ("audio", ctypes.c_void_p),
+    ]
+
+
 class Sampler(ctypes.Structure):
     _fields_ = [
         ("top_k", ctypes.c_int32), ("temperature", ctypes.c_float),
@@ -80,6 +91,7 @@ def lib():
         L.gsv_t2s_read_kv.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp,
                                       ctypes.POINTER(ctypes.c_int32), vp]
         L.gsv_vits_decode.argtypes = [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, ctypes.c_float, vp, vp]
+        L.gsv_vits_decode_batch.argtypes = [vp, i32, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
         L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
@@ -107,7 +119,7 @@ EXPORTED = (
     "gsv_t2s_decode_steps", "gsv_t2s_read_kv", "gsv_vits_decode", "gsv_prompt_encode",
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
-    "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h",
+    "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
 )
 
 
@@ -312,13 +324,21 @@ class Engine:
         return k[:n.value], v[:n.value]
 
     # -------------------------------------------------------------- VITS
-    def vits_decode(self, text_seq, pred_semantic, ref_audio=None, ge=None, ge_advanced=None,
-                    eps=None, noise_scale: float = 0.5):
+    def _ids(self, x):
         t = self.torch
-        ts = self._dev(np.asarray(text_seq).reshape(-1) if not isinstance(text_seq, t.Tensor)
-                       else text_seq.reshape(-1), t.int64)
-        sem = self._dev(np.asarray(pred_semantic).reshape(-1) if not isinstance(pred_semantic, t.Tensor)
-                        else pred_semantic.reshape(-1), t.int64)
+        return self._dev(np.asarray(x).reshape(-1) if not isinstance(x, t.Tensor) else x.reshape(-1), t.int64)
+
+    def vits_decode(self, text_seq, pred_semantic, ref_audio=None, ge=None, ge_advanced=None,
+                    eps=None, noise_scale: float = 0.5, noise_seed: Optional[int] = None):
+        """vits_fp32.onnx for one utterance.  Noise of z_p: eps (tensor/array [192, 2G]) if
+        given, else the engine's Philox N(0,1) stream keyed by noise_seed if given, else zeros."""
+        if noise_seed is not None and eps is None:
+            return self.vits_decode_batch([dict(text_seq=text_seq, pred_semantic=pred_semantic, ref_audio=ref_audio,
+                                                ge=ge, ge_advanced=ge_advanced, noise_seed=noise_seed)],
+                                          noise_scale)[0]
+        t = self.torch
+        ts = self._ids(text_seq)
+        sem = self._ids(pred_semantic)
         G = sem.numel()
         ra = None if ref_audio is None else self._dev(ref_audio, t.float32).reshape(-1)
         g = None if ge is None else self._dev(ge, t.float32).reshape(-1)
@@ -330,6 +350,37 @@ class Engine:
                                      ctypes.c_float(noise_scale), _ptr(audio), _stream()),
                "gsv_vits_decode")
         return audio
+
+    def vits_decode_batch(self, items: Sequence[dict], noise_scale: float = 0.5):
+        """Several vocoder calls at once (concurrent engine lanes).  Each item: text_seq,
+        pred_semantic, and ref_audio (V2) or ge + ge_advanced (V2ProPlus); optional eps or
+        noise_seed.  Returns one audio tensor [1280 G] per item."""
+        t = self.torch
+        arr = (VitsItem * len(items))()
+        keep, outs = [], []
+        for i, it in enumerate(items):
+            ts, sem = self._ids(it["text_seq"]), self._ids(it["pred_semantic"])
+            G = sem.numel()
+            ra = it.get("ref_audio")
+            ra = None if ra is None else self._dev(ra, t.float32).reshape(-1)
+            g = it.get("ge")
+            g = None if g is None else self._dev(g, t.float32).reshape(-1)
+            ga = it.get("ge_advanced")
+            ga = None if ga is None else self._dev(ga, t.float32).reshape(-1)
+            e = it.get("eps")
+            e = None if e is None else self._dev(e, t.float32).reshape(192, 2 * G)
+            seed = it.get("noise_seed")
+            mode = 1 if e is not None else (2 if seed is not None else 0)
+            audio = t.empty((1280 * G,), dtype=t.float32, device=self.dev)
+            arr[i] = VitsItem(ts.data_ptr(), ts.numel(), sem.data_ptr(), G, 0 if ra is None else ra.data_ptr(),
+                              0 if ra is None else ra.numel(), 0 if g is None else g.data_ptr(),
+                              0 if ga is None else ga.data_ptr(), 0 if e is None else e.data_ptr(),
+                              int(seed or 0) & 0xFFFFFFFFFFFFFFFF, mode, audio.data_ptr())
+            keep += [ts, sem, ra, g, ga, e]
+            outs.append(audio)
+        _check(lib().gsv_vits_decode_batch(self.h, len(items), arr, ctypes.c_float(noise_scale), _stream()),
+               "gsv_vits_decode_batch")
+        return outs
 
     def prompt_encode(self, ref_audio, sv_emb):
         t = self.torch

@@ -141,15 +141,16 @@ class GENIE:
         toks = eng.t2s_generate(utts, sampler)
         if model.PROMPT_ENCODER is not None:
             prompt_audio.update_global_emb(model.PROMPT_ENCODER)
-        out = []
-        for it, tok in zip(items, toks):
-            feed = {"text_seq": it[0], "pred_semantic": tok.reshape(1, 1, -1)}
-            if model.PROMPT_ENCODER is None:
-                feed["ref_audio"] = prompt_audio.audio_32k
-            else:
-                feed.update(ge=prompt_audio.global_emb, ge_advanced=prompt_audio.global_emb_advanced)
-            out.append(model.VITS.run(None, feed)[0])
-        return out
+        cond = ({"ref_audio": prompt_audio.audio_32k} if model.PROMPT_ENCODER is None else
+                {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced})
+        if getattr(model.VITS, "engine", None) is not eng:
+            return [model.VITS.run(None, {"text_seq": it[0], "pred_semantic": tok.reshape(1, 1, -1), **cond})[0]
+                    for it, tok in zip(items, toks)]
+        # engine-backed vocoder: all utterances on concurrent lanes (gsv_vits_decode_batch)
+        wavs = eng.vits_decode_batch([dict(text_seq=it[0], pred_semantic=tok, noise_seed=model.VITS.next_seed(),
+                                           **cond) for it, tok in zip(items, toks)],
+                                     model.VITS.noise_scale)
+        return [w.cpu().numpy() for w in wavs]
 
 
 tts_client = GENIE()

@@ -169,33 +169,48 @@ class StageDecoderSession(_DecoderBase):
 class VitsSession(_Session):
     """vits_fp32.onnx (reference calls: Inference.py:47-51 (V2), 55-60 (V2ProPlus)).
 
-    `noise_scale` and the N(0,1) draw mirror the graph's RandomNormalLike; pass
-    `eps` (device or host [192, 2G]) to fix it, else zeros (deterministic)."""
+    z_p noise: the graph draws RandomNormalLike x noise_scale (0.5) on every call
+    (vits(v2)#6490).  noise="philox" (default) draws it from the engine's device
+    Philox N(0,1) stream, a fresh seed per call; noise="zero" is the deterministic
+    test mode; `eps_fn(G) -> [192, 2G]` fixes it explicitly."""
     OUTPUTS = (NodeArg("audio", ("1280*G",), "tensor(float)"),)
 
-    def __init__(self, engine, version: str, noise_scale: float = 0.5, eps_fn=None):
+    def __init__(self, engine, version: str, noise_scale: float = 0.5, eps_fn=None, noise: str = "philox",
+                 seed: int = 0x5EED0000):
         super().__init__(engine)
+        if noise not in ("philox", "zero"):
+            raise ValueError("noise must be 'philox' or 'zero'")
         self.version = version
         self.noise_scale = noise_scale
         self.eps_fn = eps_fn
+        self.noise = noise
+        self._seed = seed
         common = (NodeArg("text_seq", (1, "S"), "tensor(int64)"), NodeArg("pred_semantic", (1, 1, "G"), "tensor(int64)"))
         self.INPUTS = common + ((NodeArg("ref_audio", (1, "N"), "tensor(float)"),) if version == "v2" else
                                 (NodeArg("ge", (1, 1024, 1), "tensor(float)"),
                                  NodeArg("ge_advanced", (1, 512, 1), "tensor(float)")))
+
+    def next_seed(self):
+        """Seed of the next call's noise (None in zero mode)."""
+        if self.noise == "zero":
+            return None
+        self._seed = (self._seed + 1) & 0xFFFFFFFFFFFFFFFF
+        return self._seed
 
     def run(self, output_names, input_feed):
         f = input_feed
         self._need(f, "text_seq", "pred_semantic")
         sem = np.asarray(f["pred_semantic"]).reshape(-1)
         eps = self.eps_fn(sem.size) if self.eps_fn else None
+        seed = None if eps is not None else self.next_seed()
         if self.version == "v2":
             self._need(f, "ref_audio")
-            audio = self.engine.vits_decode(f["text_seq"], sem, ref_audio=f["ref_audio"], eps=eps,
-                                            noise_scale=self.noise_scale)
+            cond = dict(ref_audio=f["ref_audio"])
         else:
             self._need(f, "ge", "ge_advanced")
-            audio = self.engine.vits_decode(f["text_seq"], sem, ge=f["ge"], ge_advanced=f["ge_advanced"],
-                                            eps=eps, noise_scale=self.noise_scale)
+            cond = dict(ge=f["ge"], ge_advanced=f["ge_advanced"])
+        audio = self.engine.vits_decode(f["text_seq"], sem, eps=eps, noise_scale=self.noise_scale, noise_seed=seed,
+                                        **cond)
         return self._select(output_names, {"audio": _np(audio)})
 
 

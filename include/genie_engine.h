@@ -140,6 +140,25 @@ int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
                     const float* ge, const float* ge_adv, const float* eps, float noise_scale,
                     float* audio, void* stream);
 
+/* Several vocoder calls at once (the same graph per utterance, vits_fp32.onnx):
+ * utterances run concurrently on the engine's internal streams, each with its
+ * own workspace; results are stream-ordered for the caller like gsv_vits_decode.
+ * Noise for z_p (vits(v2)#6490 RandomNormalLike x noise_scale):
+ *   noise_mode 0: zeros; 1: eps (device [192, 2*n_sem]); 2: the engine's Philox
+ *   N(0,1) stream keyed by noise_seed (counter = element index; Box-Muller). */
+typedef struct {
+    const int64_t* text_seq; int32_t n_text;   /* device */
+    const int64_t* sem;      int32_t n_sem;    /* device */
+    const float* ref_audio;  int32_t n_audio;  /* V2: device 32 kHz audio, else NULL */
+    const float* ge;         const float* ge_adv;   /* V2ProPlus: device [1024], [512] */
+    const float* eps;                          /* noise_mode 1 */
+    uint64_t noise_seed;                       /* noise_mode 2 */
+    int32_t noise_mode;
+    float* audio;                              /* device [1280 * n_sem] */
+} gsv_vits_item;
+int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_item* items, float noise_scale,
+                          void* stream);
+
 /* prompt_encoder_fp32.onnx (V2ProPlus): ref_audio (device [n_audio]),
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */
 int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,

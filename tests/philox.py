@@ -36,3 +36,13 @@ def sampler_noise(vocab: int, step: int, b: int, seed: int) -> np.ndarray:
     u1, u2 = u01_open(r[0]), u01_open(r[1])
     q = np.sqrt(np.float32(-2.0) * np.log(u1)) * np.cos(np.pi * 2.0 * u2.astype(np.float64)).astype(np.float32)
     return q.astype(np.float32)
+
+
+def vits_noise(n: int, seed: int) -> np.ndarray:
+    """eps of the vocoder's z_p (engine k_noise_philox): element i <- counter (i, 0, 0, 0x7A)."""
+    i = np.arange(n, dtype=np.uint32)
+    z = np.zeros_like(i)
+    r = philox4x32(i, z, z, np.full_like(i, 0x7A), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    u1, u2 = u01_open(r[0]), u01_open(r[1])
+    q = np.sqrt(np.float32(-2.0) * np.log(u1)) * np.cos(np.pi * 2.0 * u2.astype(np.float64)).astype(np.float32)
+    return q.astype(np.float32)

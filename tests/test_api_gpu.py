@@ -37,6 +37,7 @@ def model():
     div = np.load(os.path.join(GOLD, "pe_div_term.npy"))
     w = _eos_character()
     m = build_model(w, "v2", sampler=make_sampler(greedy=True), pe_div_term=div)
+    m.VITS.noise = "zero"          # deterministic vocoder: parity against the oracle with eps = 0
     yield m, w
     m.ENGINE.close()
 

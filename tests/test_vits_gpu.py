@@ -81,3 +81,43 @@ def test_prompt_encoder(setup):
     ge_r, ga_r = R.prompt_encoder(w["prompt_encoder"], ra, sv)
     np.testing.assert_allclose(ge.cpu().numpy(), ge_r.numpy().reshape(-1), atol=2e-4, rtol=1e-4)
     np.testing.assert_allclose(ga.cpu().numpy(), ga_r.numpy().reshape(-1), atol=2e-4, rtol=1e-4)
+
+
+def test_vits_philox_noise(setup):
+    """Device Philox eps (noise_seed, the reference's RandomNormalLike x 0.5 default) vs
+    the oracle fed the same stream restated in numpy (tests/philox.py)."""
+    from tests.philox import vits_noise
+    ver, e, vm, _ = setup
+    G, S, seed = 30, 20, 0xC0FFEE
+    txt = synth.synth_phones(S, f"vt{S}")
+    sem = ((np.arange(G, dtype=np.int64) * 29 + 5) % 1024).reshape(1, 1, G)
+    kw = _cond(ver)
+    eps = vits_noise(192 * 2 * G, seed).reshape(1, 192, 2 * G)
+    ref = vm(txt, sem, eps=eps, **kw).numpy()
+    out = e.vits_decode(txt, sem, noise_seed=seed, **kw).cpu().numpy()
+    rms = float(np.sqrt(np.mean((out - ref) ** 2)))
+    assert rms <= RMS_TOL, f"rms {rms:.3e}"
+    zero = e.vits_decode(txt, sem, **kw).cpu().numpy()
+    assert np.sqrt(np.mean((zero - out) ** 2)) > 10 * RMS_TOL      # the noise is really applied
+
+
+def test_vits_batch_lanes_match_single(setup):
+    """gsv_vits_decode_batch (utterances on concurrent lanes, own workspaces) gives
+    the single-call results bit for bit, for mixed lengths and noise modes."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    items, singles = [], []
+    for i, (G, S) in enumerate([(20, 12), (33, 25), (8, 9), (47, 31), (26, 18), (40, 40)]):
+        txt = synth.synth_phones(S, f"vb{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (7 + i) + 3 * i) % 1024).reshape(1, 1, G)
+        it = dict(text_seq=txt, pred_semantic=sem, **kw)
+        if i % 3 == 1:
+            it["noise_seed"] = 1000 + i
+        elif i % 3 == 2:
+            it["eps"] = synth.rng_for(f"vbe{i}").standard_normal((1, 192, 2 * G)).astype(np.float32)
+        items.append(it)
+        singles.append(e.vits_decode(txt, sem, eps=it.get("eps"), noise_seed=it.get("noise_seed"),
+                                     **kw).cpu().numpy())
+    outs = e.vits_decode_batch(items)
+    for i, (o, s1) in enumerate(zip(outs, singles)):
+        np.testing.assert_array_equal(o.cpu().numpy(), s1, err_msg=f"item {i}")
