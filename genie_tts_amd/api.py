@@ -1,28 +1,51 @@
 """The `genie_tts` entry points this engine serves (src/genie_tts/__init__.py:1-28,
-src/genie_tts/Internal.py:94-310), restricted to the synthesis hot path.
+src/genie_tts/Internal.py:94-330), restricted to the synthesis hot path.
 
-Same names and argument meaning as the reference; differences, all outside the
-path: reference features are supplied, not extracted from a wav
-(`set_reference_audio` takes the arrays; CN-HuBERT/SV/resampling are §8(f)),
-text needs a G2P callable (`set_g2p`, e.g. the reference's
-`get_phones_and_bert`) or phoneme ids, and there is no playback thread: `tts`
-returns the audio and optionally writes the same 16-bit mono WAV the reference's
-TTSPlayer writes (TTSPlayer.py:51-53,149-158).
+Same names, argument meaning and defaults as the reference:
+  load_character(character_name, onnx_model_dir, language)        Internal.py:94-126
+  set_reference_audio(character_name, audio_path, audio_text, language=None)
+                                                                   Internal.py:143-190
+  tts(character_name, text, play=False, split_sentence=True, save_path=None)
+                                                                   Internal.py:265-310
+  tts_async(character_name, text, play=False, split_sentence=False, save_path=None)
+      -> async iterator of 16-bit PCM bytes, one chunk per sentence Internal.py:193-262
+  unload_character, clear_reference_audio_cache, stop, wait_for_playback_done
+
+What the engine does not contain (outside the hot path) is pluggable:
+  set_g2p(fn(text, language) -> (phones i64 [1,S], bert f32 [S,1024]))   -- G2P + RoBERTa
+  set_ssl_extractor(fn(audio_16k [1,N]) -> ssl_content [1,768,H])       -- CN-HuBERT
+  set_sv_extractor(fn(audio_16k [1,N]) -> sv_emb [1,20480])             -- V2ProPlus SV model
+or the features can be passed to set_reference_audio directly (phonemes_seq=,
+text_bert=, ssl_content=, sv_emb=).  Reading/resampling the clip is audio.py
+(own WAV/AIFF reader + polyphase resampler: soundfile/soxr are absent).
+Differences: `tts` also returns the audio; `play=True` has no output device in
+this environment and is skipped with a warning, as the reference does when
+sounddevice fails (Core/TTSPlayer.py:136-146).
 """
 from __future__ import annotations
 
+import asyncio
+import logging
 import os
-import wave
-from typing import Callable, Dict, Optional, Sequence, Union
+from collections import OrderedDict
+from typing import AsyncIterator, Callable, Dict, List, Optional, Sequence, Union
 
 import numpy as np
 
+from . import audio as A
 from .inference import ReferenceAudio, tts_client
 from .model_manager import model_manager
+from .text_splitter import TextSplitter
+
+logger = logging.getLogger(__name__)
 
 SAMPLE_RATE = 32000
+SUPPORTED_AUDIO_EXTS = A.SUPPORTED_AUDIO_EXTS
 _reference_audios: Dict[str, ReferenceAudio] = {}
+_clip_cache: "OrderedDict[str, ReferenceAudio]" = OrderedDict()   # ReferenceAudio._prompt_cache (LRU 10)
 _g2p: Optional[Callable] = None
+_ssl_extractor: Optional[Callable] = None
+_sv_extractor: Optional[Callable] = None
 
 
 def _norm_language(language: Optional[str]) -> str:
@@ -34,10 +57,22 @@ def _norm_language(language: Optional[str]) -> str:
             "hybrid-chinese-english": "Hybrid-Chinese-English"}.get(l, language)
 
 
-def set_g2p(fn: Callable) -> None:
+def set_g2p(fn: Optional[Callable]) -> None:
     """fn(text, language) -> (text_seq i64 [1,S], text_bert f32 [S,1024])."""
     global _g2p
     _g2p = fn
+
+
+def set_ssl_extractor(fn: Optional[Callable]) -> None:
+    """fn(audio_16k f32 [1,N]) -> ssl_content f32 [1,768,H] (the reference's CN-HuBERT session)."""
+    global _ssl_extractor
+    _ssl_extractor = fn
+
+
+def set_sv_extractor(fn: Optional[Callable]) -> None:
+    """fn(audio_16k f32 [1,N]) -> sv_emb f32 [1,20480] (the reference's speaker-verification session)."""
+    global _sv_extractor
+    _sv_extractor = fn
 
 
 def load_character(character_name: str, onnx_model_dir: Union[str, os.PathLike], language: str) -> None:
@@ -57,10 +92,69 @@ def unload_character(character_name: str) -> None:
     model_manager.remove_character(character_name)
 
 
-def set_reference_audio(character_name: str, phonemes_seq: np.ndarray, text_bert: Optional[np.ndarray],
-                        audio_32k: np.ndarray, ssl_content: np.ndarray, sv_emb: Optional[np.ndarray] = None,
-                        audio_text: str = "") -> None:
-    """Internal.py:143-190 with the features the reference's ReferenceAudio computes."""
+def _text_features(text: str, language: str, phonemes_seq=None, text_bert=None):
+    if phonemes_seq is None:
+        if _g2p is None:
+            raise ValueError("no G2P: pass phonemes_seq (and text_bert) or call set_g2p()")
+        phonemes_seq, text_bert = _g2p(text, language)
+    ps = np.asarray(phonemes_seq, np.int64).reshape(1, -1)
+    tb = np.zeros((ps.shape[1], 1024), np.float32) if text_bert is None else np.asarray(text_bert, np.float32)
+    return ps, tb
+
+
+def set_reference_audio(character_name: str, audio_path: Union[str, os.PathLike], audio_text: str,
+                        language: Optional[str] = None, *, phonemes_seq=None, text_bert=None,
+                        ssl_content=None, sv_emb=None) -> None:
+    """Internal.py:143-190 + ReferenceAudio.py:28-57: the clip at 32 kHz (+0.3 s
+    silence) and 16 kHz, the prompt text's phones/BERT, the SSL content of the 16 kHz
+    clip; cached per clip path (LRU, Max_Cached_Reference_Audio)."""
+    path = os.fspath(audio_path)
+    ext = os.path.splitext(path)[1].lower()
+    if ext not in SUPPORTED_AUDIO_EXTS:
+        logger.error("Audio format '%s' is not supported. Only the following formats are supported: %s", ext,
+                     sorted(SUPPORTED_AUDIO_EXTS))
+        return
+    if language is None:
+        m = model_manager.get(character_name)
+        if m is None:
+            raise ValueError("No language specified")
+        language = m.LANGUAGE
+    language = _norm_language(language)
+    if language not in ("Japanese", "English", "Chinese"):
+        raise ValueError("Unknown language")
+    ref = _clip_cache.get(path)
+    if ref is None:
+        audio_32k = A.load_audio(path, 32000).reshape(1, -1)
+        audio_16k = A.resample(audio_32k[0], 32000, 16000).reshape(1, -1)
+        if ssl_content is None:
+            if _ssl_extractor is None:
+                raise ValueError("no SSL extractor (CN-HuBERT): pass ssl_content or call set_ssl_extractor()")
+            ssl_content = _ssl_extractor(audio_16k)
+        ps, tb = _text_features(audio_text, language, phonemes_seq, text_bert)
+        ref = ReferenceAudio(phonemes_seq=ps, text_bert=tb, audio_32k=audio_32k,
+                             ssl_content=np.asarray(ssl_content, np.float32).reshape(1, 768, -1),
+                             sv_emb=None if sv_emb is None else np.asarray(sv_emb, np.float32).reshape(1, -1),
+                             text=audio_text)
+        ref.audio_16k = audio_16k
+        ref.sv_fn = _sv_extractor
+        _clip_cache[path] = ref
+        while len(_clip_cache) > int(os.getenv("Max_Cached_Reference_Audio", "10")):
+            _clip_cache.popitem(last=False)
+    else:
+        _clip_cache.move_to_end(path)
+        if ref.text != audio_text or phonemes_seq is not None:      # ReferenceAudio.py:18-21 set_text
+            ref.phonemes_seq, ref.text_bert = _text_features(audio_text, language, phonemes_seq, text_bert)
+            ref.text = audio_text
+        if sv_emb is not None:
+            ref.sv_emb = np.asarray(sv_emb, np.float32).reshape(1, -1)
+            ref.global_emb = ref.global_emb_advanced = None
+    _reference_audios[character_name] = ref
+
+
+def set_reference_features(character_name: str, phonemes_seq: np.ndarray, text_bert: Optional[np.ndarray],
+                           audio_32k: np.ndarray, ssl_content: np.ndarray, sv_emb: Optional[np.ndarray] = None,
+                           audio_text: str = "") -> None:
+    """Set the reference from already-extracted features (the fields GENIE.tts reads)."""
     ps = np.asarray(phonemes_seq, np.int64).reshape(1, -1)
     tb = np.zeros((ps.shape[1], 1024), np.float32) if text_bert is None else np.asarray(text_bert, np.float32)
     _reference_audios[character_name] = ReferenceAudio(
@@ -71,37 +165,76 @@ def set_reference_audio(character_name: str, phonemes_seq: np.ndarray, text_bert
 
 def clear_reference_audio_cache() -> None:
     _reference_audios.clear()
+    _clip_cache.clear()
 
 
-def _write_wav(path: str, audio: np.ndarray) -> None:
-    parent = os.path.dirname(path)
-    if parent:
-        os.makedirs(parent, exist_ok=True)
-    with wave.open(path, "wb") as wf:
-        wf.setnchannels(1)
-        wf.setsampwidth(2)
-        wf.setframerate(SAMPLE_RATE)
-        wf.writeframes((audio.squeeze() * 32767).astype(np.int16).tobytes())
+def _sentences(text, split_sentence: bool) -> List:
+    if isinstance(text, str):
+        return TextSplitter().split(text.strip()) if split_sentence else ([text] if text else [])
+    return [np.asarray(text, np.int64)]               # phoneme ids: one utterance
 
 
-def tts(character_name: str, text: Union[str, Sequence[int], np.ndarray], play: bool = False,
-        split_sentence: bool = False, save_path: Union[str, os.PathLike, None] = None,
-        text_bert: Optional[np.ndarray] = None, sampler=None) -> np.ndarray:
-    """Internal.py:265-310, synchronous; returns audio f32 [1280*G] at 32 kHz."""
-    if play or split_sentence:
-        raise NotImplementedError("playback and sentence splitting are outside the engine (TTSPlayer)")
-    if character_name not in _reference_audios:
-        raise ValueError("Please call 'set_reference_audio' first to set the reference audio.")
+def _synthesize(character_name: str, sentence, text_bert=None, sampler=None) -> np.ndarray:
     m = model_manager.get(character_name)
     if m is None:
         raise ValueError(f"character '{character_name}' is not loaded")
-    audio = tts_client.tts(text if isinstance(text, str) else np.asarray(text, np.int64),
-                           _reference_audios[character_name], m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER,
-                           m.T2S_STAGE_DECODER, m.VITS, m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert,
-                           g2p=_g2p, sampler=sampler)
+    ref = _reference_audios[character_name]
+    if m.PROMPT_ENCODER is not None and ref.sv_emb is None and getattr(ref, "sv_fn", None) is not None:
+        ref.sv_emb = np.asarray(ref.sv_fn(ref.audio_16k), np.float32).reshape(1, -1)
+    tts_client.stop_event.clear()
+    return tts_client.tts(sentence, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER, m.VITS,
+                          m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p, sampler=sampler)
+
+
+def _play(audio: np.ndarray) -> None:
+    try:
+        import sounddevice as sd   # noqa: F401  (absent here, as on most servers)
+        sd.play(np.asarray(audio, np.float32).squeeze(), SAMPLE_RATE)
+        sd.wait()
+    except Exception as e:      # TTSPlayer.py:136-146: playback skipped, synthesis goes on
+        logger.warning("Failed to initialize sounddevice: %s. Audio playback will be skipped.", e)
+
+
+def tts(character_name: str, text: Union[str, Sequence[int], np.ndarray], play: bool = False,
+        split_sentence: bool = True, save_path: Union[str, os.PathLike, None] = None,
+        text_bert: Optional[np.ndarray] = None, sampler=None) -> Optional[np.ndarray]:
+    """Internal.py:265-310 (TTSPlayer session: split, synthesize each sentence, save the
+    concatenation as 16-bit WAV).  Returns the audio f32 [sum 1280*G_i] at 32 kHz."""
+    if character_name not in _reference_audios:
+        logger.error("Please call 'set_reference_audio' first to set the reference audio.")
+        return None
+    chunks = [_synthesize(character_name, s, text_bert, sampler) for s in _sentences(text, split_sentence)]
+    chunks = [c for c in chunks if c is not None]
+    audio = np.concatenate(chunks) if chunks else np.zeros(0, np.float32)
     if save_path:
-        _write_wav(os.fspath(save_path), audio)
+        A.write_wav(os.fspath(save_path), audio, SAMPLE_RATE)
+    if play:
+        _play(audio)
     return audio
+
+
+async def tts_async(character_name: str, text: str, play: bool = False, split_sentence: bool = False,
+                    save_path: Union[str, os.PathLike, None] = None) -> AsyncIterator[bytes]:
+    """Internal.py:193-262: yields one raw 16-bit PCM chunk per sentence as soon as it
+    is synthesized (TTSPlayer chunk callback), the engine running off the event loop."""
+    if character_name not in _reference_audios:
+        raise ValueError("Please call 'set_reference_audio' first to set the reference audio.")
+    loop = asyncio.get_running_loop()
+    chunks = []
+    for s in _sentences(text, split_sentence):
+        audio = await loop.run_in_executor(None, _synthesize, character_name, s)
+        if audio is None:
+            continue
+        chunks.append(audio)
+        if play:
+            await loop.run_in_executor(None, _play, audio)
+        yield A.to_pcm16(audio)
+    if save_path and chunks:
+        A.write_wav(os.fspath(save_path), np.concatenate(chunks), SAMPLE_RATE)
+
+
+def wait_for_playback_done() -> None:
+    """Playback is synchronous here (see `play`)."""
 
 
 def stop() -> None:

@@ -45,11 +45,15 @@ class ReferenceAudio:
     global_emb: Optional[np.ndarray] = None
     global_emb_advanced: Optional[np.ndarray] = None
     text: str = ""
+    audio_16k: Optional[np.ndarray] = None               # f32 [1, N16] (set_reference_audio)
+    sv_fn: Optional[Callable] = None                     # speaker-verification model, audio_16k -> sv_emb
 
     def update_global_emb(self, prompt_encoder) -> None:
         """ReferenceAudio.py:68-76 (cached after the first call)."""
         if self.global_emb is not None:
             return
+        if self.sv_emb is None and self.sv_fn is not None and self.audio_16k is not None:
+            self.sv_emb = np.asarray(self.sv_fn(self.audio_16k), np.float32).reshape(1, -1)
         if self.sv_emb is None:
             raise ValueError("V2ProPlus needs the speaker-verification embedding (sv_emb) of the reference")
         self.global_emb, self.global_emb_advanced = prompt_encoder.run(None, {

@@ -99,8 +99,8 @@ def test_api_tts_end_to_end(model):
     txt = synth.synth_phones(10, "api-t")
     ssl = synth.synth_ssl(41, "api-s")
     audio32 = synth.synth_ref_audio(32000 * 2, "api-a")
-    G.set_reference_audio("eos_char", ref, None, audio32, ssl)
-    out = G.tts("eos_char", txt, sampler=m.T2S_FIRST_STAGE_DECODER.sampler)
+    G.set_reference_features("eos_char", ref, None, audio32, ssl)
+    out = G.tts("eos_char", txt, split_sentence=False, sampler=m.T2S_FIRST_STAGE_DECODER.sampler)
     div = np.load(os.path.join(GOLD, "pe_div_term.npy"))
     R.set_div_term(div)
     try:

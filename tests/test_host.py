@@ -95,7 +95,6 @@ def test_session_interfaces_match_templates():
 
 def test_api_requires_reference_and_gpu():
     import genie_tts_amd as G
-    with pytest.raises(ValueError):
-        G.tts("nobody", [3, 4, 5])
+    assert G.tts("nobody", [3, 4, 5]) is None            # Internal.py:292-294: logs, returns
     with pytest.raises(ValueError):
         G.load_character("x", "/nonexistent", "klingon")
