@@ -738,12 +738,12 @@ hipGraphExec_t gsv_engine::step_graph(int B, const gsv_sampler* sp, int chunk, h
     return ex;
 }
 
-int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st) {
+int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool allow_persist) {
     // Steps are launched as replayed hipGraphs (chunk of 8 steps, tail by 1-step
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (use_persist && B <= 8 && persist_groups(B, n_cu) > 0) return decode_persistent(B, sp, st);
+    if (allow_persist && use_persist && B <= 8 && persist_groups(B, n_cu) > 0) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -859,6 +859,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
     a.pf_delay = persist1_pf_delay;
+    a.spin_ticks = persist_spin_ticks;
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;
@@ -876,8 +877,16 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
         ++persist1_f16_reruns;
         return decode_persistent_as(B, sp, st, false);
     }
+    // code 1: a hand-off waited past its bound -- the launch's workgroups were not
+    // all resident (other work on the device) or stalled.  Every workgroup left
+    // before the sequence state was written back, so the same steps run again as
+    // per-step graphs, which need no co-residency.
+    if (*perr_host == 1) {
+        ++persist_timeouts;
+        return decode_loop(B, sp, st, false);
+    }
     if (*perr_host != 0)
-        return set_error(GSV_E_HIP, "persistent decode: hand-off timeout (code " + std::to_string(*perr_host) + ")");
+        return set_error(GSV_E_HIP, "persistent decode failed (code " + std::to_string(*perr_host) + ")");
     if (probe) {
         float ms = 0.f;
         const hipError_t e = hipEventElapsedTime(&ms, kev[0], kev[1]);
@@ -1179,6 +1188,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist = value != 0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;
+    } else if (n == "persist_spin_ticks") {   // test hook: bound of a hand-off wait (100 MHz ticks)
+        eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : 300000000ull;
     } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback
         eng->persist1_f16_limit = value;
     } else if (n == "convh") {
@@ -1194,6 +1205,17 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else {
         return set_error(GSV_E_ARG, "unknown option " + n);
     }
+    return 0;
+}
+
+extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value) {
+    ENG_CHECK(eng);
+    if (!name || !value) return set_error(GSV_E_ARG, "null arg");
+    const std::string n(name);
+    if (n == "persist_timeouts") *value = eng->persist_timeouts;
+    else if (n == "persist1_f16_reruns") *value = eng->persist1_f16_reruns;
+    else if (n == "vits_f32_reruns") *value = eng->vits_f32_reruns;
+    else return set_error(GSV_E_ARG, "unknown counter " + n);
     return 0;
 }
 

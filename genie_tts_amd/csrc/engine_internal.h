@@ -143,7 +143,9 @@ struct gsv_engine {
     gsv::SampleArgs sampler_args(const gsv_sampler* sp, int B);
     void decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st);
     hipGraphExec_t step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st);
-    int decode_loop(int B, const gsv_sampler* sp, hipStream_t st);
+    int decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool allow_persist = true);
+    long persist_timeouts = 0;         // persistent launches that timed out (co-running work) and re-ran as graphs
+    unsigned long long persist_spin_ticks = 300000000ull;   // option "persist_spin_ticks" (test hook)
     int decode_persistent(int B, const gsv_sampler* sp, hipStream_t st);
     int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one);
     long persist1_f16_reruns = 0;      // single-sequence launches re-run on the general kernel (fp16 range)

@@ -241,6 +241,7 @@ struct PersistArgs {
     int smax;                                     // step cap of the launch
     int groups;                                   // layer groups (layer l -> group l % groups)
     unsigned long long* trace;                    // optional [grid][16] phase stamps (step 8, layer 12)
+    unsigned long long spin_ticks;                // single-sequence kernel: hand-off wait bound (100 MHz ticks)
     int pf_delay;                                 // single-sequence kernel: s_sleep(32) ticks between a
                                                   // workgroup's publish and its next-layer prefetch
     float f16_limit;                              // single-sequence kernel: largest |activation| its fp16

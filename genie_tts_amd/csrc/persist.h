@@ -47,7 +47,8 @@ __device__ __forceinline__ float4 ldg16f(const float* base, long idx) {
 
 // One lane waits for its granule.  ok := false on timeout or when another
 // workgroup failed (the caller leaves after a block-wide check).
-__device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err, bool& ok) {
+__device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err, bool& ok,
+                                           unsigned long long ticks = SPIN_TICKS) {
     u64 g = ld_rlxu64(p);
     if ((unsigned)(g >> 32) == tag) return __uint_as_float((unsigned)g);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -57,7 +58,7 @@ __device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err,
         if ((unsigned)(g >> 32) == tag) return __uint_as_float((unsigned)g);
         if ((it & 63) == 0) {
             if (ld_rlx(err) != 0) { ok = false; return 0.f; }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                 atomicCAS(err, 0, 1);
                 ok = false;
                 return 0.f;
@@ -68,7 +69,8 @@ __device__ __forceinline__ float wait_gran(const u64* p, unsigned tag, int* err,
 
 // One lane waits for the TAG of a granule only (a wake-up sentinel: its value is
 // never used), sleeping longer between polls -- cheap for the memory queues.
-__device__ __forceinline__ void wait_tag_slow(const u64* p, unsigned tag, int* err, bool& ok) {
+__device__ __forceinline__ void wait_tag_slow(const u64* p, unsigned tag, int* err, bool& ok,
+                                              unsigned long long ticks = SPIN_TICKS) {
     if ((unsigned)(ld_rlxu64(p) >> 32) == tag) return;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned it = 1;; ++it) {
@@ -76,7 +78,7 @@ __device__ __forceinline__ void wait_tag_slow(const u64* p, unsigned tag, int* e
         if ((unsigned)(ld_rlxu64(p) >> 32) == tag) return;
         if ((it & 15) == 0) {
             if (ld_rlx(err) != 0) { ok = false; return; }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                 atomicCAS(err, 0, 1);
                 ok = false;
                 return;
@@ -89,7 +91,7 @@ __device__ __forceinline__ void wait_tag_slow(const u64* p, unsigned tag, int* e
 // once; re-polls only the ones whose tag is still stale.
 template <int N>
 __device__ __forceinline__ void wait_gran_n(const u64* p, long stride, unsigned tag, float (&out)[N], int* err,
-                                            bool& ok) {
+                                            bool& ok, unsigned long long ticks = SPIN_TICKS) {
     u64 g[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) g[k] = ld_rlxu64(p + k * stride);
@@ -106,7 +108,7 @@ __device__ __forceinline__ void wait_gran_n(const u64* p, long stride, unsigned 
             if ((unsigned)(g[k] >> 32) != tag) g[k] = ld_rlxu64(p + k * stride);
         if ((it & 63) == 63) {
             if (ld_rlx(err) != 0) { ok = false; break; }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                 atomicCAS(err, 0, 1);
                 ok = false;
                 break;

@@ -375,11 +375,11 @@ __device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0
         if (s > 0) {
             float v;
             if (grp0) {
-                wait_tag_slow(ws.PFH(s - 1, 23, 0), ws.tag(s - 1), a.err, ok);
-                v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok) : 0.f;
+                wait_tag_slow(ws.PFH(s - 1, 23, 0), ws.tag(s - 1), a.err, ok, a.spin_ticks);
+                v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks) : 0.f;
             } else {
-                wait_tag_slow(ws.TK(s), ws.tag(s), a.err, ok);
-                v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok) : 0.f;
+                wait_tag_slow(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks);
+                v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks) : 0.f;
             }
             const unsigned u = __float_as_uint(v);
             sh.tok = (int)(u & 0xffff);
@@ -428,11 +428,11 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
     const unsigned tag = ws.tag(s);
     bool ok = true;
     if (l >= 2) {
-        if (tid == 0) wait_tag_slow(ws.PFH(s, l - 2, 0), tag, a.err, ok);
+        if (tid == 0) wait_tag_slow(ws.PFH(s, l - 2, 0), tag, a.err, ok, a.spin_ticks);
         if (!block_ok1(ok, sh)) return false;
     }
     float g[17];
-    wait_gran_n<17>(ws.PFH(s, l - 1, 0) + tid, 512, tag, g, a.err, ok);
+    wait_gran_n<17>(ws.PFH(s, l - 1, 0) + tid, 512, tag, g, a.err, ok, a.spin_ticks);
     float f = g[0];
 #pragma unroll
     for (int j = 1; j < NF; ++j) f += g[j];
@@ -576,10 +576,10 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         // ---- sampler: logits granules of this step -> token -> TK(s + 1)
         if (sampler) {
             bool ok = true;
-            if (tid == 0) wait_tag_slow(ws.PFH(s, 23, 0), tag, a.err, ok);
+            if (tid == 0) wait_tag_slow(ws.PFH(s, 23, 0), tag, a.err, ok, a.spin_ticks);
             if (!block_ok1(ok, sh)) return;
             const u64* lgg = ws.LG(s);
-            for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok);
+            for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok, a.spin_ticks);
             if (!block_ok1(ok, sh)) return;
             const int st = st0 + s;   // loop steps already executed
             int raw = 0;
@@ -676,7 +676,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             {
                 bool ok = true;
                 float pa[16];
-                wait_gran_n<16>(ws.PA(s, l, 0) + tid, 512, tag, pa, a.err, ok);
+                wait_gran_n<16>(ws.PA(s, l, 0) + tid, 512, tag, pa, a.err, ok, a.spin_ticks);
                 float sum = pa[0];
 #pragma unroll
                 for (int hh = 1; hh < 16; ++hh) sum += pa[hh];

@@ -109,6 +109,7 @@ def lib():
         L.gsv_get_kernel_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32)]
         L.gsv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int]
         L.gsv_debug_ptrace.argtypes = [vp, vp, ctypes.c_int]
+        L.gsv_get_counter.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
         _lib = L
     return _lib
 
@@ -120,6 +121,7 @@ EXPORTED = (
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
+    "gsv_get_counter",
 )
 
 
@@ -416,6 +418,12 @@ class Engine:
     def set_option(self, name: str, value: int):
         """Engine option (see gsv_set_option): "persist" decode path, "ptrace" phase stamps."""
         _check(lib().gsv_set_option(self.h, name.encode(), int(value)), "gsv_set_option")
+
+    def counter(self, name: str) -> int:
+        """Engine counter (gsv_get_counter): persist_timeouts, persist1_f16_reruns, vits_f32_reruns."""
+        v = ctypes.c_int64()
+        _check(lib().gsv_get_counter(self.h, name.encode(), ctypes.byref(v)), "gsv_get_counter")
+        return v.value
 
     def ptrace(self) -> np.ndarray:
         """[256 workgroups][16 slots] stamps of the persistent decode (option ptrace):

@@ -216,6 +216,10 @@ int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples);
  * 100 MHz clock, then the same 8 of the shader clock).
  * GSV_E_ARG for an unknown name. */
 int gsv_set_option(gsv_engine* eng, const char* name, int value);
+/* Engine counters: "persist_timeouts" (persistent decode launches whose hand-offs
+ * timed out -- e.g. other work on the device -- and re-ran as per-step graphs),
+ * "persist1_f16_reruns" (fp16-range fallbacks), "vits_f32_reruns". */
+int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value);
 int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);
 
 #ifdef __cplusplus

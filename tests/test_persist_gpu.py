@@ -124,3 +124,24 @@ def test_persistent_repeated_calls_are_deterministic(eng):
     first = eng.t2s_generate([inp], sp)[0].tolist()
     for _ in range(3):
         assert eng.t2s_generate([inp], sp)[0].tolist() == first
+
+
+def test_persistent_timeout_reruns_as_graphs(eng):
+    """A hand-off that waits past its bound (co-running work on the device) makes the
+    persistent launch leave without writing the sequence state; the same steps then
+    run as per-step graphs and the tokens stay bit-exact (forced here with a 0.5 us
+    bound)."""
+    from genie_tts_amd.engine import make_sampler
+    from oracle import restate as R
+    inp = t2s_inputs(R=12, S=10, H=41, tag="tmo")
+    before = eng.counter("persist_timeouts")
+    eng.set_option("persist_spin_ticks", 50)
+    try:
+        out = eng.t2s_generate([inp], make_sampler(force_steps=12))
+    finally:
+        eng.set_option("persist_spin_ticks", 0)
+    assert eng.counter("persist_timeouts") > before
+    ref, txt, rb, tb, ssl = inp
+    sem, _, _ = R.t2s_generate(character("v2")["t2s_encoder"], R.T2SModel(character("v2")["t2s"]), ref, rb, txt,
+                               tb, ssl, force_steps=12)
+    assert out[0].tolist() == sem.reshape(-1).tolist()
