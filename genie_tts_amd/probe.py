@@ -46,10 +46,26 @@ def persist_algorithmic_bytes(n0: int, steps: int, B: int = 1) -> int:
     return sum(W16 + B * (KV_ROW * (n0 + s) + KV_ROW) for s in range(steps))
 
 
+def kernel_source_sha() -> str:
+    """sha256 (16 hex) over the engine's HIP sources and headers: identifies the
+    kernel build a PMC measurement belongs to."""
+    import glob
+    import hashlib
+    import os
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(kernel_sub: str):
     """HBM bytes per launch of the named kernel from the committed PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench).  None when
+    there is none, or when it was measured on other kernel sources than the
+    ones built here (its csrc_sha differs): a stale count is not reported."""
     import json
     import os
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
@@ -57,9 +73,12 @@ def pmc_traffic(kernel_sub: str):
         d = json.load(open(path))
     except (OSError, ValueError):
         return None, None
+    sha = kernel_source_sha()
     for k, v in d.get("kernels", {}).items():
         if kernel_sub in k:
-            return float(v["traffic_bytes"]), f"{d.get('source')}: {k}"
+            if d.get("csrc_sha") != sha:
+                return None, f"stale: {d.get('source')} measured csrc {d.get('csrc_sha')}, built {sha}"
+            return float(v["traffic_bytes"]), f"{d.get('source')}, csrc {sha}: {k}"
     return None, None
 
 

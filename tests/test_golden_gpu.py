@@ -88,3 +88,38 @@ def test_vits_vs_reference_graphs(ver, div):
         np.testing.assert_allclose(ge.cpu().numpy(), p["ge"].reshape(-1), atol=2e-4)
         np.testing.assert_allclose(ga.cpu().numpy(), p["ge_advanced"].reshape(-1), atol=2e-4)
     e.close()
+
+
+@pytest.mark.parametrize("case", ["t2s_nominal81.npz", "t2s_sampled81.npz"])
+def test_t2s_bench_size_vs_reference_graphs(case, div):
+    """The bench workload itself (configs[1]: 81 loop steps), greedy and top-k 15
+    sampled with the Philox q the graphs were run with (make_golden_bench.py):
+    every token bit-exact, through the persistent decode of gsv_t2s_generate."""
+    from genie_tts_amd.engine import make_sampler
+    g, nom = gold(case), gold("t2s_nominal.npz")
+    w = synth.synthetic_character("v2")
+    e = _eng({"t2s_encoder": w["t2s_encoder"], "t2s": w["t2s"]}, "v2", div)
+    seed = int(g["seed"])
+    n = len(g["step_tokens"])
+    smp = make_sampler(top_k=int(g["top_k"]), greedy=seed == 0, seed=seed or 1234, force_steps=n)
+    out = e.t2s_generate([(nom["ref_seq"], nom["text_seq"], None, None, nom["ssl"])], smp)
+    np.testing.assert_array_equal(out[0], g["pred_semantic"].reshape(-1))
+    np.testing.assert_array_equal(out[0][:n - 1], g["step_tokens"][:n - 1])
+    e.close()
+
+
+@pytest.mark.parametrize("ver", ["v2", "v2ProPlus"])
+def test_vits_bench_size_vs_reference_graphs(ver, div):
+    """G=80 (102,400 samples, the bench's utterance): zero noise and the device
+    Philox eps (noise_seed) against the graphs run with the same eps."""
+    g = gold(f"vits_{ver}_g80.npz")
+    w = synth.synthetic_character(ver)
+    e = _eng({k: w[k] for k in w}, ver, div)
+    kw = dict(ref_audio=g["ref_audio"]) if ver == "v2" else dict(ge=g["ge"], ge_advanced=g["ge_advanced"])
+    a0 = e.vits_decode(g["text_seq"], g["pred_semantic"], **kw).cpu().numpy()
+    a1 = e.vits_decode(g["text_seq"], g["pred_semantic"], noise_seed=int(g["noise_seed"]), **kw).cpu().numpy()
+    for got, ref in ((a0, g["audio_zero"]), (a1, g["audio_philox"])):
+        assert got.shape == ref.shape == (102400,)
+        rms = float(np.sqrt(np.mean((got - ref) ** 2)))
+        assert rms <= 1e-4, rms
+    e.close()

@@ -111,3 +111,39 @@ def test_prompt_encoder_restatement_vs_graph():
     ge, ga = R.prompt_encoder(synth.synth_weights(W.prompt_encoder_spec()), g["ref_audio"], g["sv_emb"])
     np.testing.assert_allclose(ge.numpy(), g["ge"], atol=2e-5)
     np.testing.assert_allclose(ga.numpy(), g["ge_advanced"], atol=2e-5)
+
+
+@pytest.mark.parametrize("case", ["t2s_nominal81.npz", "t2s_sampled81.npz"])
+def test_t2s_restatement_bench_size_vs_graphs(t2s_model, case):
+    """The bench's 81-step nominal utterance, greedy and top-k 15 sampled with the
+    engine's Philox q (tests/golden/make_golden_bench.py), both pinned to the graphs."""
+    from oracle import restate as R
+    from tests.philox import sampler_noise
+    g, nom = gold(case), gold("t2s_nominal.npz")
+    w, m = t2s_model
+    seed = int(g["seed"])
+    q_fn = None if seed == 0 else (lambda idx: torch.from_numpy(sampler_noise(1025, idx + 1, 0, seed)))
+    R_, S_ = nom["ref_seq"].shape[1], nom["text_seq"].shape[1]
+    sem, st, _ = R.t2s_generate(w["t2s_encoder"], m, nom["ref_seq"], np.zeros((R_, 1024), np.float32),
+                                nom["text_seq"], np.zeros((S_, 1024), np.float32), nom["ssl"],
+                                R.SamplerCfg(top_k=int(g["top_k"])), force_steps=len(g["step_tokens"]), q_fn=q_fn)
+    P1 = g["y_prefill"].shape[1]
+    assert st.y[:P1] == g["y_prefill"].reshape(-1).tolist()
+    assert st.y[P1:] == g["step_tokens"].tolist()
+    np.testing.assert_array_equal(sem, g["pred_semantic"])
+
+
+@pytest.mark.parametrize("ver", ["v2", "v2ProPlus"])
+def test_vits_restatement_bench_size_vs_graphs(ver):
+    """G=80 (the bench's 102,400 samples), zero noise and the engine's Philox eps."""
+    from oracle import restate as R
+    from tests.philox import vits_noise
+    g = gold(f"vits_{ver}_g80.npz")
+    vm = R.VitsModel(synth.synth_weights(W.vits_spec(ver)), ver)
+    kw = dict(ref_audio=g["ref_audio"]) if ver == "v2" else dict(ge=g["ge"], ge_advanced=g["ge_advanced"])
+    G = g["pred_semantic"].shape[-1]
+    a0 = vm(g["text_seq"], g["pred_semantic"], **kw).numpy()
+    assert np.sqrt(np.mean((a0 - g["audio_zero"]) ** 2)) < 1e-5
+    eps = vits_noise(192 * 2 * G, int(g["noise_seed"])).reshape(1, 192, 2 * G)
+    a1 = vm(g["text_seq"], g["pred_semantic"], eps=eps, **kw).numpy()
+    assert np.sqrt(np.mean((a1 - g["audio_philox"]) ** 2)) < 1e-5

@@ -6,7 +6,11 @@ streaming reads, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, in bytes (KB = 1
 Usage: python tools/pmc_traffic.py TAG [kernel-substring]
 """
 import json
+import os
 import sys
+
+sys.path.insert(0, os.getcwd())
+from genie_tts_amd.probe import kernel_source_sha  # noqa: E402
 
 tag = sys.argv[1]
 sub = sys.argv[2] if len(sys.argv) > 2 else "k_decode_persist"
@@ -21,5 +25,5 @@ for k, v in f.items():
     out[k] = {"fetch_bytes_x2": fk * 1024, "write_bytes": wk * 1024, "traffic_bytes": (fk + wk) * 1024,
               "dispatches": v["FETCH_SIZE"]["dispatches"]}
 json.dump({"round": tag, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag})",
-           "kernels": out}, open("profiles/pmc_traffic.json", "w"), indent=1)
+           "csrc_sha": kernel_source_sha(), "kernels": out}, open("profiles/pmc_traffic.json", "w"), indent=1)
 print(json.dumps(out, indent=1))
