@@ -859,6 +859,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
     a.pf_delay = persist1_pf_delay;
+    for (int i = 0; i < 4; ++i) a.knob[i] = persist1_knob[i];
     a.spin_ticks = persist_spin_ticks;
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     hipMemsetAsync(perr, 0, 4, st);
@@ -1192,6 +1193,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : 300000000ull;
     } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback
         eng->persist1_f16_limit = value;
+    } else if (n.size() == 5 && n.compare(0, 4, "knob") == 0 && n[4] >= '0' && n[4] <= '3') {
+        eng->persist1_knob[n[4] - '0'] = value;   // single-sequence decode tuning variant (0 = default)
     } else if (n == "convh") {
         eng->use_convh = value != 0;
     } else if (n == "ptrace") {

@@ -150,7 +150,8 @@ struct gsv_engine {
     int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one);
     long persist1_f16_reruns = 0;      // single-sequence launches re-run on the general kernel (fp16 range)
     int persist1_f16_limit = 0;
-    int persist1_pf_delay = 0;         // GENIE_PF_DELAY: s_sleep(32) ticks before the next-layer prefetch        // option "persist1_f16_limit" (0: the fp16 range, 65504)
+    int persist1_pf_delay = 0;         // GENIE_PF_DELAY: s_sleep(32) ticks before the next-layer prefetch
+    int persist1_knob[4] = {0, 0, 0, 0};   // options "knob0".."knob3": single-sequence kernel tuning variants
     int vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                     const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
                     const float* eps, uint64_t noise_seed, float noise_scale, float* audio, hipStream_t st);

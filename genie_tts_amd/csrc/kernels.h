@@ -246,6 +246,8 @@ struct PersistArgs {
                                                   // workgroup's publish and its next-layer prefetch
     float f16_limit;                              // single-sequence kernel: largest |activation| its fp16
                                                   // split accepts (65504; tests lower it)
+    int knob[4];                                  // single-sequence kernel: tuning variants (option "knobN";
+                                                  // 0 = the default path)
 };
 int persist_groups(int B, int n_cu);   // 0: the grid does not fit
 int persist_grid(int B, int groups);
