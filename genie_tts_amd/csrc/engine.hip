@@ -1193,6 +1193,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : 300000000ull;
     } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback
         eng->persist1_f16_limit = value;
+    } else if (n == "pf_delay") {   // single-sequence decode: s_sleep(32) ticks before the next-layer prefetch
+        eng->persist1_pf_delay = std::max(0, value);
     } else if (n.size() == 5 && n.compare(0, 4, "knob") == 0 && n[4] >= '0' && n[4] <= '3') {
         eng->persist1_knob[n[4] - '0'] = value;   // single-sequence decode tuning variant (0 = default)
     } else if (n == "convh") {

@@ -121,24 +121,29 @@ __device__ __forceinline__ bool block_ok1(bool ok, Shared1& sh) {
     return sh.fail == 0;
 }
 
-// LayerNorm statistics (mean, then mean of squared deviations, as the graph's
-// LayerNormalization) of a 512-value row already in LDS, computed by EVERY wave
-// over the whole row: 8 values per lane, the same order in every wave and every
-// workgroup.  One barrier (the caller's, after the row is written) per LayerNorm.
+// LayerNorm statistics of a 512-value row already in LDS, computed by EVERY wave
+// over the whole row (8 values per lane, the same order in every wave and every
+// workgroup), in ONE interleaved DPP reduction of the shifted sum and sum of
+// squares: with c = row[0], mean = c + E[v - c] and var = E[(v - c)^2] -
+// E[v - c]^2 (the shift keeps the difference well conditioned when |mean| >> std;
+// ORT's own LayerNorm kernel is one-pass too).  One barrier (the caller's, after
+// the row is written) per LayerNorm.
 __device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, float& den) {
     const int lane = threadIdx.x & 63;
     const float4 a = *reinterpret_cast<const float4*>(buf + 8 * lane);
     const float4 b = *reinterpret_cast<const float4*>(buf + 8 * lane + 4);
-    const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const float s = ((v8[0] + v8[1]) + (v8[2] + v8[3])) + ((v8[4] + v8[5]) + (v8[6] + v8[7]));
-    mean = wave_sum_dpp(s) * (1.0f / 512.0f);
-    float q = 0.f;
+    const float c = buf[0];
+    const float v8[8] = {a.x - c, a.y - c, a.z - c, a.w - c, b.x - c, b.y - c, b.z - c, b.w - c};
+    float r[2];
+    r[0] = ((v8[0] + v8[1]) + (v8[2] + v8[3])) + ((v8[4] + v8[5]) + (v8[6] + v8[7]));
+    r[1] = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const float d = v8[k] - mean;
-        q += d * d;
-    }
-    den = sqrtf(wave_sum_dpp(q) * (1.0f / 512.0f) + 1e-5f);
+    for (int k = 0; k < 8; ++k) r[1] += v8[k] * v8[k];
+    wave_sum_n<2>(r);
+    const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[0]), 63)) * (1.0f / 512.0f);
+    const float q = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[1]), 63)) * (1.0f / 512.0f);
+    mean = c + d;
+    den = sqrtf(fmaxf(q - d * d, 0.f) + 1e-5f);
 }
 
 // Batch-1 GEMV on the 16x16x32 f16 MFMA (v_mfma_f32_16x16x32_f16).  The weights
@@ -150,16 +155,16 @@ __device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, floa
 // c[0] + c[1].  Replaces 2 VALU ops per MAC (cvt + fma) and the DPP row sums.
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ h8v bfrag(const uint4 w) { return __builtin_bit_cast(h8v, w); }
-// This lane's A-operand base: row 0 reads hi, row 1 lo; chunk c is one
-// ds_read_b128 at base + 32 c (an instruction offset).  Rows 2..15 are zero and
-// read nothing: only 8 lanes of the wave touch LDS (128 B per fragment, not 1 KB).
+// This lane's A-operand base: row 0 reads hi, rows 1..15 lo; chunk c is one
+// ds_read_b128 at base + 32 c (an instruction offset).  Rows 2..15 of C are
+// never used, so their lanes need no zeroing: they read the lo row again, which
+// the LDS serves as a broadcast (128 distinct bytes per fragment either way),
+// with no exec-masked branches around the reads.
 __device__ __forceinline__ const _Float16* abase(const _Float16* hi, const _Float16* lo, int lane) {
     return ((lane & 15) == 0 ? hi : lo) + 8 * (lane >> 4);
 }
-__device__ __forceinline__ h8v afrag(const _Float16* base, int k0, bool row01) {
-    uint4 u = make_uint4(0u, 0u, 0u, 0u);
-    if (row01) u = *reinterpret_cast<const uint4*>(base + k0);
-    return __builtin_bit_cast(h8v, u);
+__device__ __forceinline__ h8v afrag(const _Float16* base, int k0) {
+    return __builtin_bit_cast(h8v, *reinterpret_cast<const uint4*>(base + k0));
 }
 __device__ __forceinline__ f32x4 mfma16(h8v a, h8v b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -290,7 +295,7 @@ __device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, floa
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int t = 64 * u + g;
-        const float pu = sv[u] == -INFINITY ? 0.f : expf(sv[u] - m_w);
+        const float pu = sv[u] == -INFINITY ? 0.f : __expf(sv[u] - m_w);   // v_exp_f32 (ORT's MLAS exp is not libm's either)
         float4 v4 = vr[u];
         if (t == kv) v4 = vnew;
         if (t > kv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);   // rows past the cache: unloaded LDS
@@ -506,13 +511,12 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             // ---- q, k, v of head h on the MFMA: wave w < 6 -> 16 rows (C row 0 + row 1)
             if (w < 6) {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
-                const bool r01 = (lane & 15) < 2;
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
                     h8v af[8];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i), r01);
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
 #pragma unroll
                     for (int i = 0; i < 8; i += 2) {
                         c0 = mfma16(af[i], bfrag(wq[cb + i]), c0);
@@ -521,7 +525,9 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 }
                 if (lane < 16) sh.qkv[16 * w + lane] = bqv + ((c0[0] + c1[0]) + (c0[1] + c1[1]));
             }
+            STAMP1(6);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
+            STAMP1(7);
             __syncthreads();
             STAMP1(2);
             // ---- scores (q*s).(k*s) over [0, kv]: 8 lanes per key row (16 B each,
@@ -553,7 +559,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             STAMP1(4);
             // ---- out-projection slice of this head (column tid) -> partial granule
             {
-                const h8v af = afrag(abase(sh.osh[w], sh.osl[w], lane), 0, (lane & 15) < 2);
+                const h8v af = afrag(abase(sh.osh[w], sh.osl[w], lane), 0);
                 f32x4 acc[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bfrag(wo[t]), f32x4{0.f, 0.f, 0.f, 0.f});
@@ -696,13 +702,12 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             // ---- FFN1 rows of this slice on the MFMA (16 per wave), ReLU -> fh/fl
             {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
-                const bool r01 = (lane & 15) < 2;
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
                     h8v af[8];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i), r01);
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
 #pragma unroll
                     for (int i = 0; i < 8; i += 2) {
                         c0 = mfma16(af[i], bfrag(w1r[cb + i]), c0);
@@ -727,10 +732,9 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
 #pragma unroll
                 for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
                 const _Float16* ab = abase(sh.fh, sh.fl, lane);
-                const bool r01 = (lane & 15) < 2;
                 h8v af[4];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) af[c] = afrag(ab, 32 * c, r01);
+                for (int c = 0; c < 4; ++c) af[c] = afrag(ab, 32 * c);
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll

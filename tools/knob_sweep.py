@@ -1,5 +1,5 @@
 """Decode time of the single-sequence persistent kernel under tuning variants
-(engine options knob0..knob3), plus the two-layer phase trace and the shader
+(engine options knob0..knob3, pf=pf_delay), plus the two-layer phase trace and the shader
 clock of the default path.  Usage: python tools/knob_sweep.py "k1=1,k0=1" "k1=1,k0=4" ...
 (each argument one variant; the default path is always measured first and last)."""
 import sys
@@ -18,6 +18,7 @@ base = None
 def run(knobs, reps=4):
     for i in range(4):
         e.set_option(f"knob{i}", knobs.get(i, 0))
+    e.set_option("pf_delay", knobs.get("pf", 0))
     ts, toks = [], None
     for _ in range(reps):
         out = e.t2s_generate([(ref, txt, None, None, ssl)], make_sampler(force_steps=81))
@@ -50,7 +51,10 @@ base = run({})
 print(f"default: min {base[0]:.3f} ms median {base[1]:.3f}", flush=True)
 phase_trace()
 for arg in sys.argv[1:]:
-    kn = {int(kv.split("=")[0][1:]): int(kv.split("=")[1]) for kv in arg.split(",") if kv}
+    kn = {}
+    for kv in arg.split(","):
+        k, v = kv.split("=")
+        kn["pf" if k == "pf" else int(k[1:])] = int(v)
     r = run(kn)
     same = bool(np.array_equal(r[2], base[2]))
     print(f"{arg:20s}: min {r[0]:.3f} ms median {r[1]:.3f}  tokens {'same' if same else 'DIFFER'}", flush=True)
