@@ -13,8 +13,10 @@ Same names, argument meaning and defaults as the reference:
 
 What the engine does not contain (outside the hot path) is pluggable:
   set_g2p(fn(text, language) -> (phones i64 [1,S], bert f32 [S,1024]))   -- G2P + RoBERTa
-  set_ssl_extractor(fn(audio_16k [1,N]) -> ssl_content [1,768,H])       -- CN-HuBERT
+  set_ssl_extractor(fn(audio_16k [1,N]) -> ssl_content [1,768,H])       -- CN-HuBERT override
   set_sv_extractor(fn(audio_16k [1,N]) -> sv_emb [1,20480])             -- V2ProPlus SV model
+CN-HuBERT itself runs on the engine (gsv_hubert) once load_cn_hubert(dir | weights) has
+been called or $HUBERT_MODEL_DIR is set (ModelManager.py:172-195),
 or the features can be passed to set_reference_audio directly (phonemes_seq=,
 text_bert=, ssl_content=, sv_emb=).  Reading/resampling the clip is audio.py
 (own WAV/AIFF reader + polyphase resampler: soundfile/soxr are absent).
@@ -67,6 +69,12 @@ def set_ssl_extractor(fn: Optional[Callable]) -> None:
     """fn(audio_16k f32 [1,N]) -> ssl_content f32 [1,768,H] (the reference's CN-HuBERT session)."""
     global _ssl_extractor
     _ssl_extractor = fn
+
+
+def load_cn_hubert(model=None) -> None:
+    """CN-HuBERT weights: the GenieData/chinese-hubert-base directory or a dict of
+    arrays (weights.hubert_spec names); `g/ModelManager.py:172-195`."""
+    model_manager.load_cn_hubert(model)
 
 
 def set_sv_extractor(fn: Optional[Callable]) -> None:
@@ -127,9 +135,14 @@ def set_reference_audio(character_name: str, audio_path: Union[str, os.PathLike]
         audio_32k = A.load_audio(path, 32000).reshape(1, -1)
         audio_16k = A.resample(audio_32k[0], 32000, 16000).reshape(1, -1)
         if ssl_content is None:
-            if _ssl_extractor is None:
-                raise ValueError("no SSL extractor (CN-HuBERT): pass ssl_content or call set_ssl_extractor()")
-            ssl_content = _ssl_extractor(audio_16k)
+            if _ssl_extractor is not None:
+                ssl_content = _ssl_extractor(audio_16k)
+            elif model_manager.cn_hubert is not None or os.getenv("HUBERT_MODEL_DIR"):
+                model_manager.load_cn_hubert()          # ReferenceAudio.py:48-52
+                ssl_content = model_manager.cn_hubert.run(None, {"input_values": audio_16k})[0]
+            else:
+                raise ValueError("no SSL extractor (CN-HuBERT): load_cn_hubert(), pass ssl_content "
+                                 "or call set_ssl_extractor()")
         ps, tb = _text_features(audio_text, language, phonemes_seq, text_bert)
         ref = ReferenceAudio(phonemes_seq=ps, text_bert=tb, audio_32k=audio_32k,
                              ssl_content=np.asarray(ssl_content, np.float32).reshape(1, 768, -1),

@@ -27,6 +27,25 @@ struct T2SLayerW {
     float *b_in = nullptr, *b_out = nullptr, *b1 = nullptr, *b2 = nullptr;
     float *n1w = nullptr, *n1b = nullptr, *n2w = nullptr, *n2b = nullptr;
 };
+// CN-HuBERT (hubert.hip): chinese-hubert-base, transformers HubertModel layout
+struct HubertLayerW {
+    __half *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
+    float *bqkv = nullptr, *bo = nullptr, *b1 = nullptr, *b2 = nullptr;
+    float *ln1w = nullptr, *ln1b = nullptr, *ln2w = nullptr, *ln2b = nullptr;
+};
+struct HubertWeights {
+    bool ready = false;
+    float *conv0_w = nullptr, *gn_w = nullptr, *gn_b = nullptr;
+    __half* conv_w[7] = {};           // conv 1..6 as [co][tap][ci]
+    float *fp_ln_w = nullptr, *fp_ln_b = nullptr, *fp_b = nullptr;
+    __half* fp_w = nullptr;
+    __half* pos_w = nullptr;          // [768][tap 128][ci 48] (16 groups of 48 rows)
+    float *pos_b = nullptr, *enc_ln_w = nullptr, *enc_ln_b = nullptr;
+    HubertLayerW L[12];
+    float* ws = nullptr;              // workspace (grown per call)
+    size_t ws_floats = 0;
+};
+int hubert_frames(int n_samples);
 }  // namespace gsv
 
 struct gsv_engine {
@@ -77,6 +96,7 @@ struct gsv_engine {
     gsv::VitsWeights vits;
     gsv::VitsWorkspace vws;
     gsv::PromptEncWeights penc;
+    gsv::HubertWeights hubert;
 
     std::map<std::string, hipGraphExec_t> graphs;
     bool timing = false;
@@ -122,6 +142,9 @@ struct gsv_engine {
     int finalize_t2s();
     int finalize_vits();
     int finalize_prompt_encoder();
+    int finalize_hubert();
+    float* hubert_ws(size_t floats);
+    int hubert_forward(const float* audio, int n, float* out, hipStream_t st);
     int reserve(int batch, int tokens);
     int ensure_enc_ws(int P, int L);
     int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st, bool do_prompts = true);

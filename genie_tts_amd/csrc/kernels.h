@@ -17,6 +17,7 @@ enum EpiMode {
     EPI_VQDIST = 4,      // C = (rowsq[m] - v) + colsq[n]   (VQ distance, encoder #30-34)
     EPI_MISH = 5,        // C = v * tanh(softplus(v))        (MelStyleEncoder spectral)
     EPI_SLAB = 6,        // split-K: C + z*slab_stride = raw partial of K slice z (no bias)
+    EPI_GELU = 7,        // C = 0.5 v (1 + erf(v / sqrt 2))  (exact GELU, CN-HuBERT)
 };
 
 struct KVScatter {

@@ -28,6 +28,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, int row0, int c
         switch (a.mode) {
             case EPI_STORE: a.C[(long)row * a.ldc + col] = v; break;
             case EPI_RELU: a.C[(long)row * a.ldc + col] = fmaxf(v, 0.f); break;
+            case EPI_GELU: a.C[(long)row * a.ldc + col] = 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); break;
             case EPI_RESID: a.C[(long)row * a.ldc + col] = a.res[(long)row * a.ldr + col] + v; break;
             case EPI_MISH: {
                 const float sp = v > 0.f ? v + log1pf(expf(-v)) : log1pf(expf(v));

@@ -110,6 +110,8 @@ def lib():
         L.gsv_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int]
         L.gsv_debug_ptrace.argtypes = [vp, vp, ctypes.c_int]
         L.gsv_get_counter.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
+        L.gsv_hubert_frames.argtypes = [ctypes.c_int32]
+        L.gsv_hubert.argtypes = [vp, vp, ctypes.c_int32, vp, vp]
         _lib = L
     return _lib
 
@@ -121,7 +123,7 @@ EXPORTED = (
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
-    "gsv_get_counter",
+    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames",
 )
 
 
@@ -393,6 +395,17 @@ class Engine:
         _check(lib().gsv_prompt_encode(self.h, _ptr(ra), ra.numel(), _ptr(sv), _ptr(ge), _ptr(ga),
                                        _stream()), "gsv_prompt_encode")
         return ge, ga
+
+    def hubert(self, audio_16k):
+        """CN-HuBERT (gsv_hubert): raw 16 kHz audio [N] -> ssl_content [768, T] on the device."""
+        t = self.torch
+        a = self._dev(audio_16k, t.float32).reshape(-1)
+        T = lib().gsv_hubert_frames(a.numel())
+        if T < 1:
+            raise EngineError(f"audio of {a.numel()} samples is too short for CN-HuBERT")
+        out = t.empty((768, T), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_hubert(self.h, _ptr(a), a.numel(), _ptr(out), _stream()), "gsv_hubert")
+        return out
 
     def debug_copy(self, name: str, n: int):
         t = self.torch

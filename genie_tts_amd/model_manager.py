@@ -15,7 +15,7 @@ import logging
 import os
 from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Dict, Optional, Union
 
 import numpy as np
 
@@ -70,6 +70,7 @@ class ModelManager:
         self.character_to_language: Dict[str, str] = {}
         self.character_model_paths: Dict[str, str] = {}
         self.sampler: Optional[Sampler] = None
+        self.cn_hubert = None            # HubertSession (ModelManager.py:127,172-195)
 
     def _put(self, name: str, model: GSVModel) -> None:
         self.character_to_model[name] = model
@@ -99,6 +100,27 @@ class ModelManager:
         self._put(name, build_model(weights, version, language, self.device, self.sampler))
         self.character_to_language[name] = language
         return True
+
+    def load_cn_hubert(self, model: Union[str, Dict[str, np.ndarray], None] = None) -> bool:
+        """CN-HuBERT on its own engine (`g/ModelManager.py:172-195`): `model` is the
+        GenieData/chinese-hubert-base directory or in-memory weights (hubert_spec
+        names); default: $HUBERT_MODEL_DIR."""
+        if self.cn_hubert is not None:
+            return True
+        from .sessions import HubertSession
+        if model is None:
+            model = os.getenv("HUBERT_MODEL_DIR")
+            if not model:
+                raise FileNotFoundError("CN-HuBERT: pass a directory or weights, or set HUBERT_MODEL_DIR")
+        w = W.load_hubert_weights(model) if isinstance(model, (str, os.PathLike)) else model
+        self.cn_hubert = HubertSession(Engine({"hubert": w}, "v2", device=self.device))
+        logger.info("CN-HuBERT loaded")
+        return True
+
+    def unload_cn_hubert(self) -> None:
+        if self.cn_hubert is not None:
+            self.cn_hubert.engine.close()
+            self.cn_hubert = None
 
     def get(self, character_name: str) -> Optional[GSVModel]:
         name = character_name.lower()

@@ -224,3 +224,15 @@ class PromptEncoderSession(_Session):
         ge, ga = self.engine.prompt_encode(input_feed["ref_audio"], input_feed["sv_emb"])
         return self._select(output_names, {"ge": _np(ge).reshape(1, 1024, 1),
                                            "ge_advanced": _np(ga).reshape(1, 512, 1)})
+
+
+class HubertSession(_Session):
+    """chinese-hubert-base.onnx, CN-HuBERT (reference call: ReferenceAudio.py:50-52):
+    raw 16 kHz audio -> ssl_content [1, 768, T]."""
+    INPUTS = (NodeArg("input_values", (1, "N"), "tensor(float)"),)
+    OUTPUTS = (NodeArg("ssl_content", (1, 768, "T"), "tensor(float)"),)
+
+    def run(self, output_names, input_feed):
+        self._need(input_feed, "input_values")
+        ssl = self.engine.hubert(input_feed["input_values"])
+        return self._select(output_names, {"ssl_content": _np(ssl)[None]})

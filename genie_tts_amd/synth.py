@@ -62,7 +62,7 @@ def _role_scale(name: str, shape: Tuple[int, ...]) -> Tuple[float, float]:
         return 0.25, 0.05
     if "emb_rel" in leaf:
         return 0.0, 0.3
-    if "embed" in name or "embedding" in name:
+    if ("embed" in name or "embedding" in name) and "pos_conv_embed" not in name:
         return 0.0, 1.0
     if len(shape) >= 2:
         fan_in = int(np.prod(shape[1:]))

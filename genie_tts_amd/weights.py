@@ -234,6 +234,51 @@ def prompt_encoder_spec() -> Spec:
     return s
 
 
+def hubert_spec() -> Spec:
+    """CN-HuBERT (chinese-hubert-base, GenieData/chinese-hubert-base; loaded at
+    `g/ModelManager.py:172-195`).  Names and shapes of transformers' HubertModel
+    (conv_bias=False, feat_extract_norm="group"), the model GPT-SoVITS exports;
+    the positional conv is stored weight-normed (g v / ||v||), as an exported
+    graph folds it.  The graph file itself is absent here: this layout is not
+    pinned to the real chinese-hubert-base.onnx initializer table."""
+    s: Spec = OrderedDict()
+    s["feature_extractor.conv_layers.0.conv.weight"] = (512, 1, 10)
+    s["feature_extractor.conv_layers.0.layer_norm.weight"] = (512,)
+    s["feature_extractor.conv_layers.0.layer_norm.bias"] = (512,)
+    for i, k in enumerate((3, 3, 3, 3, 2, 2), start=1):
+        s[f"feature_extractor.conv_layers.{i}.conv.weight"] = (512, 512, k)
+    s["feature_projection.layer_norm.weight"] = (512,)
+    s["feature_projection.layer_norm.bias"] = (512,)
+    s["feature_projection.projection.weight"] = (768, 512)
+    s["feature_projection.projection.bias"] = (768,)
+    s["encoder.pos_conv_embed.conv.weight"] = (768, 48, 128)
+    s["encoder.pos_conv_embed.conv.bias"] = (768,)
+    s["encoder.layer_norm.weight"] = (768,)
+    s["encoder.layer_norm.bias"] = (768,)
+    for l in range(12):
+        p = f"encoder.layers.{l}."
+        for m in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            s[p + f"attention.{m}.weight"] = (768, 768)
+            s[p + f"attention.{m}.bias"] = (768,)
+        s[p + "layer_norm.weight"] = (768,)
+        s[p + "layer_norm.bias"] = (768,)
+        s[p + "feed_forward.intermediate_dense.weight"] = (3072, 768)
+        s[p + "feed_forward.intermediate_dense.bias"] = (3072,)
+        s[p + "feed_forward.output_dense.weight"] = (768, 3072)
+        s[p + "feed_forward.output_dense.bias"] = (768,)
+        s[p + "final_layer_norm.weight"] = (768,)
+        s[p + "final_layer_norm.bias"] = (768,)
+    return s
+
+
+def load_hubert_weights(model_dir: str) -> Dict[str, np.ndarray]:
+    """GenieData/chinese-hubert-base: chinese-hubert-base.onnx + *_weights_fp16.bin
+    (`g/ModelManager.py:41-42,177-182`), read through the initializer table like
+    a character's bins.  Unverified against a real file (none offline)."""
+    return load_fp16_bin(os.path.join(model_dir, "chinese-hubert-base.onnx"),
+                         os.path.join(model_dir, "chinese-hubert-base_weights_fp16.bin"), hubert_spec())
+
+
 def spec_numel(spec: Spec) -> int:
     return int(sum(int(np.prod(v)) for v in spec.values()))
 

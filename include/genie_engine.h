@@ -16,6 +16,7 @@
  *   the 500-step loop + trim (Inference.py:95-109)   gsv_t2s_generate (on device, hipGraph)
  *   vocoder.run            (Inference.py:47-60)      gsv_vits_decode
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
+ *   cn_hubert.run          (ReferenceAudio.py:50-52) gsv_hubert
  *
  * Conventions
  *   - All functions return 0 on success, a negative GSV_E* code on failure;
@@ -163,6 +164,15 @@ int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_item* items
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */
 int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
                       const float* sv_emb, float* ge, float* ge_adv, void* stream);
+
+/* chinese-hubert-base.onnx (CN-HuBERT, ReferenceAudio.py:48-52; session loaded at
+ * ModelManager.py:172-195): input_values = raw 16 kHz audio (device [n_samples])
+ * -> ssl_content (device [768][T], the graph's [1, 768, T] output), T =
+ * gsv_hubert_frames(n_samples) (the conv stack's output length).  Needs an
+ * engine whose weights include the HuBERT tensors (transformers HubertModel
+ * names, encoder.pos_conv_embed.conv.weight already weight-normed). */
+int gsv_hubert_frames(int32_t n_samples);
+int gsv_hubert(gsv_engine* eng, const float* audio_16k, int32_t n_samples, float* ssl_content, void* stream);
 
 /* Debug hooks (tests only): copy a named VITS workspace buffer after
  * gsv_vits_decode ("ge","stats","z","y","q","te","g0","g1","spec","a");
