@@ -12,7 +12,8 @@ Same names, argument meaning and defaults as the reference:
   unload_character, clear_reference_audio_cache, stop, wait_for_playback_done
 
 What the engine does not contain (outside the hot path) is pluggable:
-  set_g2p(fn(text, language) -> (phones i64 [1,S], bert f32 [S,1024]))   -- G2P + RoBERTa
+  set_g2p(fn(text, language) -> (phones i64 [1,S], bert f32 [S,1024]))   -- G2P (+ BERT), or
+          -> (phones, None, input_ids, word2ph): RoBERTa then runs on the engine (load_roberta)
   set_ssl_extractor(fn(audio_16k [1,N]) -> ssl_content [1,768,H])       -- CN-HuBERT override
   set_sv_extractor(fn(audio_16k [1,N]) -> sv_emb [1,20480])             -- V2ProPlus SV model
 CN-HuBERT itself runs on the engine (gsv_hubert) once load_cn_hubert(dir | weights) has
@@ -77,6 +78,12 @@ def load_cn_hubert(model=None) -> None:
     model_manager.load_cn_hubert(model)
 
 
+def load_roberta(model=None) -> None:
+    """RoBERTa (chinese-roberta-wwm-ext-large) weights: the GenieData RoBERTa directory
+    or a dict of arrays (weights.roberta_spec names); `g/ModelManager.py:132-150`."""
+    model_manager.load_roberta_model(model)
+
+
 def set_sv_extractor(fn: Optional[Callable]) -> None:
     """fn(audio_16k f32 [1,N]) -> sv_emb f32 [1,20480] (the reference's speaker-verification session)."""
     global _sv_extractor
@@ -104,7 +111,14 @@ def _text_features(text: str, language: str, phonemes_seq=None, text_bert=None):
     if phonemes_seq is None:
         if _g2p is None:
             raise ValueError("no G2P: pass phonemes_seq (and text_bert) or call set_g2p()")
-        phonemes_seq, text_bert = _g2p(text, language)
+        g = _g2p(text, language)
+        phonemes_seq, text_bert = g[0], g[1]
+        if len(g) == 4 and text_bert is None and model_manager.roberta is not None:
+            # (phones, None, input_ids, word2ph): Chinese BERT features on the engine
+            # (GetPhonesAndBert.py:64-74; tokenizing text_clean stays with the G2P)
+            ids = np.asarray(g[2], np.int64).reshape(1, -1)
+            text_bert = model_manager.roberta.run(None, {"input_ids": ids, "attention_mask": np.ones_like(ids),
+                                                         "repeats": np.asarray(g[3], np.int64)})[0]
     ps = np.asarray(phonemes_seq, np.int64).reshape(1, -1)
     tb = np.zeros((ps.shape[1], 1024), np.float32) if text_bert is None else np.asarray(text_bert, np.float32)
     return ps, tb

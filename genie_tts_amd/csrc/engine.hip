@@ -63,6 +63,7 @@ gsv_engine::~gsv_engine() {
     if (ptrace) hipFree(ptrace);
     if (pws) hipFree(pws);
     if (hubert.ws) hipFree(hubert.ws);
+    if (bert.ws) hipFree(bert.ws);
     if (perr_host) hipHostFree(perr_host);
     if (vovf_host) hipHostFree(vovf_host);
     if (vovf) hipFree(vovf);
@@ -958,11 +959,15 @@ extern "C" int gsv_finalize_weights(gsv_engine* eng) {
     hipSetDevice(eng->device);
     if (eng->finalized) return set_error(GSV_E_STATE, "already finalized");
     const bool has_hubert = eng->find("feature_extractor.conv_layers.0.conv.weight") != nullptr;
-    if (!has_hubert || eng->find("ar_audio_embedding.word_embeddings.weight")) {
+    const bool has_roberta = eng->find("embeddings.word_embeddings.weight") != nullptr;
+    if (!(has_hubert || has_roberta) || eng->find("ar_audio_embedding.word_embeddings.weight")) {
         if (int e = eng->finalize_t2s()) return e;
     }
     if (has_hubert) {   // CN-HuBERT (a GenieData model, usually an engine of its own)
         if (int e = eng->finalize_hubert()) return e;
+    }
+    if (has_roberta) {  // RoBERTa (GenieData, Chinese BERT features)
+        if (int e = eng->finalize_roberta()) return e;
     }
     if (eng->find("vq_model.dec.conv_pre.weight")) {
         if (int e = eng->finalize_vits()) return e;

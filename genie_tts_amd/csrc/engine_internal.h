@@ -46,6 +46,16 @@ struct HubertWeights {
     size_t ws_floats = 0;
 };
 int hubert_frames(int n_samples);
+// RoBERTa (bert.hip): chinese-roberta-wwm-ext-large, transformers BertModel layout
+using BertLayerW = HubertLayerW;
+struct BertWeights {
+    bool ready = false;
+    float *word = nullptr, *pos = nullptr, *type = nullptr, *ln_w = nullptr, *ln_b = nullptr;
+    int vocab = 0, max_pos = 0, n_layers = 0;
+    std::vector<BertLayerW> L;        // layers 0 .. n_layers - 3 (hidden_states[-3])
+    float* ws = nullptr;
+    size_t ws_floats = 0;
+};
 }  // namespace gsv
 
 struct gsv_engine {
@@ -97,6 +107,7 @@ struct gsv_engine {
     gsv::VitsWorkspace vws;
     gsv::PromptEncWeights penc;
     gsv::HubertWeights hubert;
+    gsv::BertWeights bert;
 
     std::map<std::string, hipGraphExec_t> graphs;
     bool timing = false;
@@ -145,6 +156,8 @@ struct gsv_engine {
     int finalize_hubert();
     float* hubert_ws(size_t floats);
     int hubert_forward(const float* audio, int n, float* out, hipStream_t st);
+    int finalize_roberta();
+    int roberta_forward(const int64_t* ids, int N, const int* rows, int n_out, float* out, hipStream_t st);
     int reserve(int batch, int tokens);
     int ensure_enc_ws(int P, int L);
     int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st, bool do_prompts = true);

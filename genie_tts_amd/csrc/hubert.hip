@@ -71,35 +71,6 @@ __global__ __launch_bounds__(512) void k_hb_gn_gelu(float* x, int C, const float
     *p = gelu_erf((*p - mean[c]) * rstd[c] * g[c] + b[c]);
 }
 
-// LayerNorm over rows of D (<= 1024) values, eps 1e-5, two-pass (mean, then mean
-// of squared deviations), one block per row.
-__global__ __launch_bounds__(256) void k_hb_ln(const float* in, float* out, int D, const float* g, const float* b) {
-    __shared__ float red[16];
-    const long r = blockIdx.x;
-    const float* x = in + r * D;
-    float v[4];
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int d = threadIdx.x + 256 * i;
-        v[i] = d < D ? x[d] : 0.f;
-        s += v[i];
-    }
-    const float mean = block_sum(s, red) / (float)D;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int d = threadIdx.x + 256 * i;
-        if (d < D) q += (v[i] - mean) * (v[i] - mean);
-    }
-    const float den = sqrtf(block_sum(q, red) / (float)D + 1e-5f);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int d = threadIdx.x + 256 * i;
-        if (d < D) out[r * D + d] = (v[i] - mean) / den * g[d] + b[d];
-    }
-}
-
 // im2col of the positional conv, all groups: A[g][t][j * 48 + i] = h[t - 64 + j][48 g + i]
 __global__ __launch_bounds__(256) void k_hb_pos_im2col(const float* h, int T, float* A) {
     const int t = blockIdx.x, g = blockIdx.y;
@@ -137,8 +108,40 @@ __global__ __launch_bounds__(256) void k_hb_transpose(const float* h, int T, flo
 constexpr int HB_KS[7] = {10, 3, 3, 3, 3, 2, 2};
 constexpr int HB_SS[7] = {5, 2, 2, 2, 2, 2, 2};
 
-GemmArgs hb_gemm(int M, int N, int K, const float* A, long lda, const __half* W, const float* bias, float* C,
-                 long ldc, int mode, const float* res = nullptr, long ldr = 0) {
+}  // namespace
+
+// LayerNorm over rows of D (<= 1024) values, two-pass (mean, then mean of squared
+// deviations), one block per row (CN-HuBERT eps 1e-5, RoBERTa eps 1e-12).
+__global__ __launch_bounds__(256) void k_ln_rows_d(const float* in, float* out, int D, const float* g, const float* b,
+                                                    float eps) {
+    __shared__ float red[16];
+    const long r = blockIdx.x;
+    const float* x = in + r * D;
+    float v[4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int d = threadIdx.x + 256 * i;
+        v[i] = d < D ? x[d] : 0.f;
+        s += v[i];
+    }
+    const float mean = block_sum(s, red) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int d = threadIdx.x + 256 * i;
+        if (d < D) q += (v[i] - mean) * (v[i] - mean);
+    }
+    const float den = sqrtf(block_sum(q, red) / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int d = threadIdx.x + 256 * i;
+        if (d < D) out[r * D + d] = (v[i] - mean) / den * g[d] + b[d];
+    }
+}
+
+GemmArgs gemm_f16(int M, int N, int K, const float* A, long lda, const void* W, const float* bias, float* C,
+                  long ldc, int mode, const float* res, long ldr) {
     GemmArgs a{};
     a.M = M; a.N = N; a.K = K;
     a.A = A; a.lda = lda;
@@ -150,7 +153,10 @@ GemmArgs hb_gemm(int M, int N, int K, const float* A, long lda, const __half* W,
     return a;
 }
 
-}  // namespace
+void layernorm_rows_d(const float* in, float* out, int rows, int D, const float* g, const float* b, float eps,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(k_ln_rows_d, dim3(rows), dim3(256), 0, s, in, out, D, g, b, eps);
+}
 
 int hubert_frames(int n) {
     int T = n;
@@ -284,18 +290,18 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
     hipLaunchKernelGGL(k_hb_gn_gelu, dim3(T0), dim3(512), 0, st, cA, 512, gmean, grstd, H.gn_w, H.gn_b);
     float *src = cA, *dst = cB;
     for (int i = 1; i < 7; ++i) {
-        gemm_nt(hb_gemm(Ts[i + 1], 512, HB_KS[i] * 512, src, (long)HB_SS[i] * 512, H.conv_w[i], nullptr, dst, 512,
+        gemm_nt(gemm_f16(Ts[i + 1], 512, HB_KS[i] * 512, src, (long)HB_SS[i] * 512, H.conv_w[i], nullptr, dst, 512,
                         EPI_GELU),
                 st);
         std::swap(src, dst);
     }
     // ---- feature projection: LayerNorm(512) -> Linear(512 -> 768)
-    hipLaunchKernelGGL(k_hb_ln, dim3(T), dim3(256), 0, st, src, dst, 512, H.fp_ln_w, H.fp_ln_b);
-    gemm_nt(hb_gemm(T, 768, 512, dst, 512, H.fp_w, H.fp_b, xproj, 768, EPI_STORE), st);
+    layernorm_rows_d(src, dst, T, 512, H.fp_ln_w, H.fp_ln_b, 1e-5f, st);
+    gemm_nt(gemm_f16(T, 768, 512, dst, 512, H.fp_w, H.fp_b, xproj, 768, EPI_STORE), st);
     // ---- positional conv embedding: h = x + GELU(conv(x)), then LayerNorm(768)
     hipLaunchKernelGGL(k_hb_pos_im2col, dim3(T, 16), dim3(256), 0, st, xproj, T, im);
     for (int g = 0; g < 16; ++g) {
-        GemmArgs a = hb_gemm(T, 48, 6144, im + (size_t)g * T * 6144, 6144, H.pos_w + (size_t)g * 48 * 6144,
+        GemmArgs a = gemm_f16(T, 48, 6144, im + (size_t)g * T * 6144, 6144, H.pos_w + (size_t)g * 48 * 6144,
                              nullptr, slabs + 48 * g, 768, EPI_SLAB);
         a.ksplit = NZ_POS;
         a.slab_stride = (long)T * 768;
@@ -304,11 +310,11 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
     hipMemcpyAsync(tmp, xproj, (size_t)T * 768 * 4, hipMemcpyDeviceToDevice, st);
     hipLaunchKernelGGL(k_hb_pos_reduce, dim3((T * 768 + 255) / 256), dim3(256), 0, st, slabs, NZ_POS,
                        (long)T * 768, H.pos_b, tmp, T * 768);
-    hipLaunchKernelGGL(k_hb_ln, dim3(T), dim3(256), 0, st, tmp, h, 768, H.enc_ln_w, H.enc_ln_b);
+    layernorm_rows_d(tmp, h, T, 768, H.enc_ln_w, H.enc_ln_b, 1e-5f, st);
     // ---- 12 post-norm encoder layers
     for (int l = 0; l < 12; ++l) {
         const HubertLayerW& L = H.L[l];
-        gemm_nt(hb_gemm(T, 2304, 768, h, 768, L.wqkv, L.bqkv, qkv, 2304, EPI_STORE), st);
+        gemm_nt(gemm_f16(T, 2304, 768, h, 768, L.wqkv, L.bqkv, qkv, 2304, EPI_STORE), st);
         MhaArgs m{};
         m.q = qkv; m.q_ts = 2304; m.q_cs = 1;
         m.k = qkv + 768; m.k_ts = 2304; m.k_cs = 1;
@@ -317,11 +323,11 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
         m.nq = T; m.nk = T; m.heads = 12; m.dk = 64;
         m.postdiv = 0; m.scale = 8.f;   // q * 64^-0.5 (exact: a power of two)
         mha(m, st);
-        gemm_nt(hb_gemm(T, 768, 768, att, 768, L.wo, L.bo, tmp, 768, EPI_RESID, h, 768), st);
-        hipLaunchKernelGGL(k_hb_ln, dim3(T), dim3(256), 0, st, tmp, h, 768, L.ln1w, L.ln1b);
-        gemm_nt(hb_gemm(T, 3072, 768, h, 768, L.w1, L.b1, f, 3072, EPI_GELU), st);
-        gemm_nt(hb_gemm(T, 768, 3072, f, 3072, L.w2, L.b2, tmp, 768, EPI_RESID, h, 768), st);
-        hipLaunchKernelGGL(k_hb_ln, dim3(T), dim3(256), 0, st, tmp, h, 768, L.ln2w, L.ln2b);
+        gemm_nt(gemm_f16(T, 768, 768, att, 768, L.wo, L.bo, tmp, 768, EPI_RESID, h, 768), st);
+        layernorm_rows_d(tmp, h, T, 768, L.ln1w, L.ln1b, 1e-5f, st);
+        gemm_nt(gemm_f16(T, 3072, 768, h, 768, L.w1, L.b1, f, 3072, EPI_GELU), st);
+        gemm_nt(gemm_f16(T, 768, 3072, f, 3072, L.w2, L.b2, tmp, 768, EPI_RESID, h, 768), st);
+        layernorm_rows_d(tmp, h, T, 768, L.ln2w, L.ln2b, 1e-5f, st);
     }
     hipLaunchKernelGGL(k_hb_transpose, dim3((T + 31) / 32, 24), dim3(256), 0, st, h, T, out);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "hubert launch");

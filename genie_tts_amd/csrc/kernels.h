@@ -46,6 +46,9 @@ struct GemmArgs {
     int a_nslab; long a_slab_stride; const float* a_bias; int a_relu;
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
+// Args of a GEMM with fp16 weights W[N][K] (ldw = K): C = epi(A W^T + bias)
+GemmArgs gemm_f16(int M, int N, int K, const float* A, long lda, const void* W, const float* bias, float* C,
+                  long ldc, int mode, const float* res = nullptr, long ldr = 0);
 // EPI_SLAB (split-K into slabs) is available for fp16 weights with these shapes
 bool gemm_slabs_supported(int K, long lda, long ldw);
 
@@ -56,6 +59,9 @@ void layernorm_rows(const float* in, float* out, int rows, const float* g, const
 void layernorm_rows_slabs(const float* slabs, int nsplit, long slab_stride, const float* bias,
                           const float* res, float* out, int rows, const float* g, const float* b,
                           hipStream_t s);
+// LayerNorm over rows of D <= 1024 values with the given eps (CN-HuBERT, RoBERTa)
+void layernorm_rows_d(const float* in, float* out, int rows, int D, const float* g, const float* b, float eps,
+                      hipStream_t s);
 void sumsq_rows(const float* in, long ld, int rows, int cols, float* out, hipStream_t s);
 void argmin_dist_rows(const float* dist, int rows, int cols, int64_t* out, hipStream_t s);
 

@@ -112,6 +112,7 @@ def lib():
         L.gsv_get_counter.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
         L.gsv_hubert_frames.argtypes = [ctypes.c_int32]
         L.gsv_hubert.argtypes = [vp, vp, ctypes.c_int32, vp, vp]
+        L.gsv_roberta.argtypes = [vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
         _lib = L
     return _lib
 
@@ -123,7 +124,7 @@ EXPORTED = (
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
-    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames",
+    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta",
 )
 
 
@@ -405,6 +406,20 @@ class Engine:
             raise EngineError(f"audio of {a.numel()} samples is too short for CN-HuBERT")
         out = t.empty((768, T), dtype=t.float32, device=self.dev)
         _check(lib().gsv_hubert(self.h, _ptr(a), a.numel(), _ptr(out), _stream()), "gsv_hubert")
+        return out
+
+    def roberta(self, input_ids, repeats, attention_mask=None):
+        """RoBERTa (gsv_roberta): token ids [N] (CLS .. SEP), word2ph [n_chars] ->
+        text_bert [sum(word2ph), 1024] on the device."""
+        t = self.torch
+        ids = self._dev(np.asarray(input_ids).reshape(-1) if not isinstance(input_ids, t.Tensor)
+                        else input_ids.reshape(-1), t.int64)
+        rep = np.ascontiguousarray(np.asarray(repeats, np.int64).reshape(-1))
+        mask = None if attention_mask is None else np.ascontiguousarray(np.asarray(attention_mask, np.int64).reshape(-1))
+        out = t.empty((int(rep.sum()), 1024), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_roberta(self.h, _ptr(ids), None if mask is None else mask.ctypes.data_as(ctypes.c_void_p),
+                                 ids.numel(), rep.ctypes.data_as(ctypes.c_void_p), rep.size, _ptr(out), _stream()),
+               "gsv_roberta")
         return out
 
     def debug_copy(self, name: str, n: int):

@@ -71,6 +71,7 @@ class ModelManager:
         self.character_model_paths: Dict[str, str] = {}
         self.sampler: Optional[Sampler] = None
         self.cn_hubert = None            # HubertSession (ModelManager.py:127,172-195)
+        self.roberta = None              # RobertaSession (ModelManager.py:129,132-150)
 
     def _put(self, name: str, model: GSVModel) -> None:
         self.character_to_model[name] = model
@@ -115,6 +116,22 @@ class ModelManager:
         w = W.load_hubert_weights(model) if isinstance(model, (str, os.PathLike)) else model
         self.cn_hubert = HubertSession(Engine({"hubert": w}, "v2", device=self.device))
         logger.info("CN-HuBERT loaded")
+        return True
+
+    def load_roberta_model(self, model: Union[str, Dict[str, np.ndarray], None] = None) -> bool:
+        """RoBERTa on its own engine (`g/ModelManager.py:132-150`): `model` is the
+        GenieData RoBERTa directory or in-memory weights (roberta_spec names);
+        default: $ROBERTA_MODEL_DIR."""
+        if self.roberta is not None:
+            return True
+        from .sessions import RobertaSession
+        if model is None:
+            model = os.getenv("ROBERTA_MODEL_DIR")
+            if not model:
+                raise FileNotFoundError("RoBERTa: pass a directory or weights, or set ROBERTA_MODEL_DIR")
+        w = W.load_roberta_weights(model) if isinstance(model, (str, os.PathLike)) else model
+        self.roberta = RobertaSession(Engine({"roberta": w}, "v2", device=self.device))
+        logger.info("RoBERTa loaded")
         return True
 
     def unload_cn_hubert(self) -> None:

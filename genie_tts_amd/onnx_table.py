@@ -83,3 +83,49 @@ def read_initializer_table(path: str) -> Dict[str, Tuple[List[int], Optional[int
                 name, dims, off, ln = _tensor_entry(v2)
                 table[name] = (dims, off, ln)
     return table
+
+
+def read_initializer_values(path: str, spec) -> Dict[str, "object"]:
+    """Inline initializers (TensorProto data_type=2 field, raw_data=9) of a graph
+    whose weights are stored in the file itself (RoBERTa.onnx is loaded without an
+    fp16 bin, `g/ModelManager.py:139`): FLOAT (1) or FLOAT16 (10) raw data, checked
+    against `spec` (name -> shape)."""
+    import numpy as np
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    found = {}
+    for f, _, v in _walk(buf):
+        if f != 7:
+            continue
+        for f2, _, v2 in _walk(v):
+            if f2 != 5:
+                continue
+            name, dims, dtype, raw = "", [], 0, b""
+            for f3, wt, v3 in _walk(v2):
+                if f3 == 1:
+                    if wt == 0:
+                        dims.append(v3)
+                    else:
+                        q = 0
+                        while q < len(v3):
+                            d, q = _varint(v3, q)
+                            dims.append(d)
+                elif f3 == 2:
+                    dtype = v3
+                elif f3 == 8:
+                    name = bytes(v3).decode()
+                elif f3 == 9:
+                    raw = bytes(v3)
+            if name in spec:
+                dt = {1: np.float32, 10: np.float16}.get(dtype)
+                if dt is None or not raw:
+                    raise ValueError(f"{path}: {name} has no inline FLOAT/FLOAT16 raw data")
+                found[name] = np.frombuffer(raw, dtype=dt).reshape(dims)
+    out = {}
+    for name, shape in spec.items():
+        if name not in found:
+            raise KeyError(f"{path}: initializer {name} not found")
+        if tuple(found[name].shape) != tuple(shape):
+            raise ValueError(f"{name}: shape {found[name].shape} in graph, expected {shape}")
+        out[name] = found[name]
+    return out

@@ -236,3 +236,18 @@ class HubertSession(_Session):
         self._need(input_feed, "input_values")
         ssl = self.engine.hubert(input_feed["input_values"])
         return self._select(output_names, {"ssl_content": _np(ssl)[None]})
+
+
+class RobertaSession(_Session):
+    """RoBERTa.onnx, Chinese BERT features (reference call: GetPhonesAndBert.py:64-74):
+    input_ids [1, N], attention_mask [1, N], repeats = word2ph [n_chars] ->
+    text_bert [sum(repeats), 1024]."""
+    INPUTS = (NodeArg("input_ids", (1, "N"), "tensor(int64)"), NodeArg("attention_mask", (1, "N"), "tensor(int64)"),
+              NodeArg("repeats", ("C",), "tensor(int64)"))
+    OUTPUTS = (NodeArg("text_bert", ("P", 1024), "tensor(float)"),)
+
+    def run(self, output_names, input_feed):
+        self._need(input_feed, "input_ids", "attention_mask", "repeats")
+        f = input_feed
+        out = self.engine.roberta(f["input_ids"], f["repeats"], f["attention_mask"])
+        return self._select(output_names, {"text_bert": _np(out)})

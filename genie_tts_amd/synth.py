@@ -50,9 +50,9 @@ def _role_scale(name: str, shape: Tuple[int, ...]) -> Tuple[float, float]:
     leaf = name.rsplit(".", 1)[-1]
     if leaf == "alpha":
         return 1.0, 0.2
-    if leaf in ("gamma",) or re.search(r"norm\d?\.weight$", name):
+    if leaf in ("gamma",) or re.search(r"(norm\d?|LayerNorm)\.weight$", name):
         return 1.0, 0.1
-    if leaf in ("beta",) or re.search(r"norm\d?\.bias$", name):
+    if leaf in ("beta",) or re.search(r"(norm\d?|LayerNorm)\.bias$", name):
         return 0.0, 0.05
     if leaf == "weight_g":
         return 1.0, 0.25

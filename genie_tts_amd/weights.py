@@ -279,6 +279,43 @@ def load_hubert_weights(model_dir: str) -> Dict[str, np.ndarray]:
                          os.path.join(model_dir, "chinese-hubert-base_weights_fp16.bin"), hubert_spec())
 
 
+def roberta_spec(n_layers: int = 24, vocab: int = 21128, max_pos: int = 512) -> Spec:
+    """RoBERTa for Chinese BERT features (chinese-roberta-wwm-ext-large, GenieData
+    RoBERTa.onnx, `g/ModelManager.py:44,132-150`): transformers BertModel names
+    (hidden 1024, 16 heads, FFN 4096); the graph reads hidden_states[-3], so the
+    last two layers are never run.  Not pinned to the real RoBERTa.onnx table."""
+    s: Spec = OrderedDict()
+    s["embeddings.word_embeddings.weight"] = (vocab, 1024)
+    s["embeddings.position_embeddings.weight"] = (max_pos, 1024)
+    s["embeddings.token_type_embeddings.weight"] = (2, 1024)
+    s["embeddings.LayerNorm.weight"] = (1024,)
+    s["embeddings.LayerNorm.bias"] = (1024,)
+    for l in range(n_layers):
+        p = f"encoder.layer.{l}."
+        for m in ("query", "key", "value"):
+            s[p + f"attention.self.{m}.weight"] = (1024, 1024)
+            s[p + f"attention.self.{m}.bias"] = (1024,)
+        s[p + "attention.output.dense.weight"] = (1024, 1024)
+        s[p + "attention.output.dense.bias"] = (1024,)
+        s[p + "attention.output.LayerNorm.weight"] = (1024,)
+        s[p + "attention.output.LayerNorm.bias"] = (1024,)
+        s[p + "intermediate.dense.weight"] = (4096, 1024)
+        s[p + "intermediate.dense.bias"] = (4096,)
+        s[p + "output.dense.weight"] = (1024, 4096)
+        s[p + "output.dense.bias"] = (1024,)
+        s[p + "output.LayerNorm.weight"] = (1024,)
+        s[p + "output.LayerNorm.bias"] = (1024,)
+    return s
+
+
+def load_roberta_weights(model_dir: str) -> Dict[str, np.ndarray]:
+    """GenieData RoBERTa/RoBERTa.onnx weights (`g/ModelManager.py:44,139`) through the
+    initializer table; the reference loads that graph without an fp16 bin, so its
+    initializers are read in place (fp32).  Unverified against a real file."""
+    from .onnx_table import read_initializer_values
+    return read_initializer_values(os.path.join(model_dir, "RoBERTa.onnx"), roberta_spec())
+
+
 def spec_numel(spec: Spec) -> int:
     return int(sum(int(np.prod(v)) for v in spec.values()))
 

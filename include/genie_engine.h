@@ -17,6 +17,7 @@
  *   vocoder.run            (Inference.py:47-60)      gsv_vits_decode
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
  *   cn_hubert.run          (ReferenceAudio.py:50-52) gsv_hubert
+ *   roberta_model.run      (GetPhonesAndBert.py:73)  gsv_roberta
  *
  * Conventions
  *   - All functions return 0 on success, a negative GSV_E* code on failure;
@@ -173,6 +174,16 @@ int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
  * names, encoder.pos_conv_embed.conv.weight already weight-normed). */
 int gsv_hubert_frames(int32_t n_samples);
 int gsv_hubert(gsv_engine* eng, const float* audio_16k, int32_t n_samples, float* ssl_content, void* stream);
+
+/* RoBERTa.onnx (chinese-roberta-wwm-ext-large BERT features for Chinese text,
+ * GetPhonesAndBert.py:64-74; session ModelManager.py:132-150): input_ids (device
+ * i64 [n_tokens], CLS .. SEP), attention_mask (host i64 [n_tokens], all ones, or
+ * NULL), repeats = word2ph (host i64 [n_chars], n_chars <= n_tokens - 2) ->
+ * text_bert (device [sum(repeats)][1024]) = hidden_states[-3] of the character
+ * rows 1 .. n_chars, row i repeated repeats[i - 1] times.  Needs an engine whose
+ * weights include the BertModel tensors (transformers names). */
+int gsv_roberta(gsv_engine* eng, const int64_t* input_ids, const int64_t* attention_mask, int32_t n_tokens,
+                const int64_t* repeats, int32_t n_chars, float* text_bert, void* stream);
 
 /* Debug hooks (tests only): copy a named VITS workspace buffer after
  * gsv_vits_decode ("ge","stats","z","y","q","te","g0","g1","spec","a");

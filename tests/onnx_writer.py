@@ -41,3 +41,21 @@ def model(inits: List[Tuple[str, List[int], int, int]], location: str) -> bytes:
     for name, dims, off, ln in inits:
         graph += _field(5, 2, tensor_external(name, dims, off, ln, location))
     return _field(1, 0, _varint(9)) + _field(7, 2, graph)
+
+
+def tensor_inline(name: str, arr) -> bytes:
+    """An initializer with its data in the file (raw_data), FLOAT or FLOAT16."""
+    import numpy as np
+    a = np.ascontiguousarray(arr)
+    body = _field(1, 2, b"".join(_varint(d) for d in a.shape))
+    body += _field(2, 0, _varint(10 if a.dtype == np.float16 else 1))
+    body += _str(8, name)
+    body += _field(9, 2, a.astype(a.dtype.newbyteorder("<")).tobytes())
+    return body
+
+
+def model_inline(arrays) -> bytes:
+    graph = _str(2, "g")
+    for name, a in arrays.items():
+        graph += _field(5, 2, tensor_inline(name, a))
+    return _field(1, 0, _varint(9)) + _field(7, 2, graph)
