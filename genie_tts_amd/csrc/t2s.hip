@@ -717,8 +717,125 @@ __global__ __launch_bounds__(1024) void k_attn_tile(AttnArgs a) {
     if ((lane & 1) == 0) a.out[(long)r * a.ldo + h * 32 + d] = tot;
 }
 
+// Prefill attention of one sequence, online softmax over 64-key chunks: a block
+// = one head x 16 query rows (4 waves x 4 rows).  The head's K/V chunk is staged
+// once per block in LDS (rows padded to 36 floats: conflict-free 16-B reads by
+// 16 lanes).  Scores: lane = key (its K row in registers, scaled by s), the 4
+// query rows (scaled by s) read as LDS broadcasts -> s_rj = (q s).(k s) as
+// stage#91-94; per row a wave-wide running max / sum (exp(x - max) #95).  P.V:
+// lane = (row, 2 dims), P rows through wave-private LDS.  The same arithmetic as
+// k_attn_rows except the summation order and the running rescale.  One K/V pass
+// per 16 rows instead of one per row (k_attn_rows re-reads the head's K/V from L2
+// for every query row).
+#define AF_ROWS 16
+#define AF_KC 64
+#define AF_KS 36
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_attn_flash(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) float Ks[AF_KC * AF_KS];
+    __shared__ __attribute__((aligned(16))) float Vs[AF_KC * AF_KS];
+    __shared__ __attribute__((aligned(16))) float Qs[AF_ROWS][32];
+    __shared__ __attribute__((aligned(16))) float Ps[4][4][AF_KC];
+    __shared__ int rl[AF_ROWS];
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r0 = blockIdx.y * AF_ROWS, nr = min(AF_ROWS, a.rows - r0);
+    const float sc = a.scale;
+    if (tid < AF_ROWS) rl[tid] = tid < nr ? a.row_len[r0 + tid] : 0;
+    for (int e = tid; e < AF_ROWS * 8; e += 256) {   // q rows (scaled), 16-B pieces
+        const int r = e >> 3, c = e & 7;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < nr) v = *reinterpret_cast<const float4*>(a.q + (long)(r0 + r) * a.ldq + h * 32 + 4 * c);
+        *reinterpret_cast<float4*>(&Qs[r][4 * c]) = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+    }
+    __syncthreads();
+    int kmax = 0;
+#pragma unroll
+    for (int i = 0; i < AF_ROWS; ++i) kmax = max(kmax, rl[i]);
+    const float* K = a.k + (long)h * a.tmax * 32;
+    const float* V = a.v + (long)h * a.tmax * 32;
+    int len[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) len[r] = rl[4 * w + r];
+    float m[4], l[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { m[r] = -INFINITY; l[r] = 0.f; }
+    const int pr = lane >> 4, pd = 2 * (lane & 15);   // P.V: this lane's row (of the wave's 4) and dims
+    f32x2v o = {0.f, 0.f};
+    for (int k0 = 0; k0 < kmax; k0 += AF_KC) {
+        const int nk = min(AF_KC, kmax - k0);
+        for (int e = tid; e < AF_KC * 8; e += 256) {   // K/V chunk -> LDS (rows past the cache: zeros)
+            const int t = e >> 3, c = e & 7;
+            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+            if (t < nk) {
+                kv = *reinterpret_cast<const float4*>(K + (long)(k0 + t) * 32 + 4 * c);
+                vv = *reinterpret_cast<const float4*>(V + (long)(k0 + t) * 32 + 4 * c);
+            }
+            *reinterpret_cast<float4*>(Ks + t * AF_KS + 4 * c) = kv;
+            *reinterpret_cast<float4*>(Vs + t * AF_KS + 4 * c) = vv;
+        }
+        __syncthreads();
+        // ---- scores: lane = key k0 + lane
+        f32x2v kr[16];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float4 k4 = *reinterpret_cast<const float4*>(Ks + lane * AF_KS + 4 * c);
+            kr[2 * c] = f32x2v{k4.x * sc, k4.y * sc};
+            kr[2 * c + 1] = f32x2v{k4.z * sc, k4.w * sc};
+        }
+        float corr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float* qr = Qs[4 * w + r];
+            f32x2v acc = {0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float4 q4 = *reinterpret_cast<const float4*>(qr + 4 * c);
+                acc += f32x2v{q4.x, q4.y} * kr[2 * c];
+                acc += f32x2v{q4.z, q4.w} * kr[2 * c + 1];
+            }
+            const float s = k0 + lane < len[r] ? acc.x + acc.y : -INFINITY;
+            const float mc = wave_max(s);
+            const float mn = fmaxf(m[r], mc);
+            corr[r] = mn == -INFINITY ? 1.f : __expf(m[r] - mn);
+            const float p = s == -INFINITY ? 0.f : __expf(s - mn);
+            l[r] = l[r] * corr[r] + wave_sum(p);
+            m[r] = mn;
+            Ps[w][r][lane] = p;
+        }
+        __builtin_amdgcn_wave_barrier();   // Ps of this wave written before its lanes read it
+        // ---- P.V: lane = (row pr, dims pd, pd + 1)
+        const float cr = pr == 0 ? corr[0] : pr == 1 ? corr[1] : pr == 2 ? corr[2] : corr[3];
+        o *= cr;
+        const float* prow = Ps[w][pr];
+#pragma unroll 4
+        for (int j = 0; j < AF_KC; j += 4) {
+            const float4 p4 = *reinterpret_cast<const float4*>(prow + j);
+            o += p4.x * *reinterpret_cast<const f32x2v*>(Vs + (j + 0) * AF_KS + pd);
+            o += p4.y * *reinterpret_cast<const f32x2v*>(Vs + (j + 1) * AF_KS + pd);
+            o += p4.z * *reinterpret_cast<const f32x2v*>(Vs + (j + 2) * AF_KS + pd);
+            o += p4.w * *reinterpret_cast<const f32x2v*>(Vs + (j + 3) * AF_KS + pd);
+        }
+        __syncthreads();   // K/V/P consumed before the next chunk lands
+    }
+    const float lr = pr == 0 ? l[0] : pr == 1 ? l[1] : pr == 2 ? l[2] : l[3];
+    const int row = 4 * w + pr;
+    if (row < nr) {
+        float* dst = a.out + (long)(r0 + row) * a.ldo + h * 32 + pd;
+        dst[0] = o.x / lr;
+        dst[1] = o.y / lr;
+    }
+}
+
 void attn_rows(const AttnArgs& a, hipStream_t s) {
     if (a.rows <= 0) return;
+    static const bool flash = [] {
+        const char* e = std::getenv("GENIE_ATTN_FLASH");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (flash && !a.row_seq && !a.row_skip) {
+        hipLaunchKernelGGL(k_attn_flash, dim3(16, (a.rows + AF_ROWS - 1) / AF_ROWS), dim3(256), 0, s, a);
+        return;
+    }
     // prefill of one sequence (row r sees keys [0, row_len[r]) <= rows).  Off by
     // default: measured slower than k_attn_rows at N0 = 225 (prefill 2.14 vs 1.83 ms)
     static const bool tile = [] {

@@ -324,11 +324,13 @@ void ln_channels(const float* x, const float* y, float* out, int C, int T, const
 // window 4; (v2)#308-...) and MelStyleEncoder's ScaledDotProductAttention.
 #define MHA_MAXK 2048
 #define MHA_MAXD 128
+#define MHA_MAXW 8      // largest rel-pos window
 __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
     __shared__ float qs[MHA_MAXD];
     __shared__ float p[MHA_MAXK];
     __shared__ float red[16];
     __shared__ float part[2][MHA_MAXD];
+    __shared__ float qe[2 * MHA_MAXW + 1];
     const int hd = blockIdx.x, i = blockIdx.y, tid = threadIdx.x;
     const int dk = a.dk, c0 = hd * dk;
     for (int d = tid; d < dk; d += 256) {
@@ -336,19 +338,34 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
         qs[d] = a.postdiv ? qv : qv / a.scale;
     }
     __syncthreads();
+    if (a.ek) {   // rel-pos key terms q . ek[r] of the window, one wave per r, lanes over d
+        const int lane = tid & 63, w = tid >> 6;
+        for (int r = w; r <= 2 * a.window; r += 4) {
+            float sl = 0.f;
+            for (int d = lane; d < dk; d += 64) sl += qs[d] * a.ek[(long)r * dk + d];
+            sl = wave_sum(sl);
+            if (lane == 0) qe[r] = sl;
+        }
+        __syncthreads();
+    }
     float lmax = -INFINITY;
     for (int j = tid; j < a.nk; j += 256) {
+        // 32 key loads in flight per step (the d order of the single sum is kept)
+        const float* kp = a.k + (long)j * a.k_ts + (long)c0 * a.k_cs;
         float s = 0.f;
-        for (int d = 0; d < dk; ++d) s += qs[d] * a.k[(long)j * a.k_ts + (long)(c0 + d) * a.k_cs];
+        int d = 0;
+        for (; d + 32 <= dk; d += 32) {
+            float kv[32];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) kv[u] = kp[(long)(d + u) * a.k_cs];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) s += qs[d + u] * kv[u];
+        }
+        for (; d < dk; ++d) s += qs[d] * kp[(long)d * a.k_cs];
         if (a.postdiv) s = s / a.scale;
         if (a.ek) {
             const int r = j - i;
-            if (r >= -a.window && r <= a.window) {
-                const float* e = a.ek + (long)(r + a.window) * dk;
-                float sl = 0.f;
-                for (int d = 0; d < dk; ++d) sl += qs[d] * e[d];
-                s = s + sl;
-            }
+            if (r >= -a.window && r <= a.window) s = s + qe[r + a.window];
         }
         p[j] = s;
         lmax = fmaxf(lmax, s);
@@ -366,8 +383,17 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
     // out[d] = sum_j p_j v[j][d]  (+ sum_{|j-i|<=W} p_j ev[j-i+W][d])
     const int half = tid >> 7, dd = tid & 127;
     for (int d = dd; d < dk; d += 128) {
+        const float* vp = a.v + (long)(c0 + d) * a.v_cs;
         float o = 0.f;
-        for (int j = half; j < a.nk; j += 2) o += p[j] * a.v[(long)j * a.v_ts + (long)(c0 + d) * a.v_cs];
+        int j = half;
+        for (; j + 30 < a.nk; j += 32) {   // 16 value loads in flight per step, j order kept
+            float vv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) vv[u] = vp[(long)(j + 2 * u) * a.v_ts];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) o += p[j + 2 * u] * vv[u];
+        }
+        for (; j < a.nk; j += 2) o += p[j] * vp[(long)j * a.v_ts];
         part[half][d] = o;
     }
     __syncthreads();
@@ -499,16 +525,31 @@ void stft_mag(const float* reim, int frames, int bins, float* spec, hipStream_t 
     hipLaunchKernelGGL(k_stft_mag, dim3((n + 255) / 256), dim3(256), 0, s, reim, frames, bins, spec);
 }
 
-// temporal_avg_pool: sum over time / T (the mask is all ones at batch 1)
-__global__ void k_time_mean(const float* x, int T, int C, float* out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// temporal_avg_pool: sum over time / T (the mask is all ones at batch 1).  Block =
+// 64 channels x 4 time phases (t = phase mod 4, 8 loads in flight per thread),
+// the 4 phase sums added in phase order.
+__global__ __launch_bounds__(256) void k_time_mean(const float* x, int T, int C, float* out) {
+    __shared__ float part[4][64];
+    const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) s += x[(long)t * C + c];
-    out[c] = s / (float)T;
+    if (c < C) {
+        int t = ph;
+        for (; t + 28 < T; t += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = x[(long)(t + 4 * u) * C + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; t < T; t += 4) s += x[(long)t * C + c];
+    }
+    part[ph][cl] = s;
+    __syncthreads();
+    if (ph == 0 && c < C) out[c] = (((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl]) / (float)T;
 }
 void time_mean(const float* x, int T, int C, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_time_mean, dim3((C + 63) / 64), dim3(64), 0, s, x, T, C, out);
+    hipLaunchKernelGGL(k_time_mean, dim3((C + 63) / 64), dim3(256), 0, s, x, T, C, out);
 }
 
 __global__ void k_prelu(const float* x, const float* a, float* out, int n) {
