@@ -399,11 +399,15 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
     __syncthreads();
     for (int d = tid; d < dk; d += 256) {
         float o = part[0][d] + part[1][d];
-        if (a.ev) {
+        if (a.ev) {   // every ev load of the window in flight at once, summed in r order
+            float evv[2 * MHA_MAXW + 1];
+#pragma unroll
+            for (int r = 0; r <= 2 * MHA_MAXW; ++r) evv[r] = r <= 2 * a.window ? a.ev[(long)r * dk + d] : 0.f;
             float ol = 0.f;
-            for (int r = -a.window; r <= a.window; ++r) {
-                const int j = i + r;
-                if (j >= 0 && j < a.nk) ol += p[j] * a.ev[(long)(r + a.window) * dk + d];
+#pragma unroll
+            for (int r = 0; r <= 2 * MHA_MAXW; ++r) {
+                const int j = i + r - a.window;
+                if (r <= 2 * a.window && j >= 0 && j < a.nk) ol += p[j] * evv[r];
             }
             o = o + ol;
         }
@@ -412,6 +416,7 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
 }
 
 void mha(const MhaArgs& a, hipStream_t s) {
+    if ((a.ek || a.ev) && a.window > MHA_MAXW) return;   // window 4 in every graph; the host never asks more
     hipLaunchKernelGGL(k_mha, dim3(a.heads, a.nq), dim3(256), 0, s, a);
 }
 
