@@ -126,9 +126,10 @@ __device__ __forceinline__ bool block_ok1(bool ok, Shared1& sh) {
 // workgroup), in ONE interleaved DPP reduction of the shifted sum and sum of
 // squares: with c = row[0], mean = c + E[v - c] and var = E[(v - c)^2] -
 // E[v - c]^2 (the shift keeps the difference well conditioned when |mean| >> std;
-// ORT's own LayerNorm kernel is one-pass too).  One barrier (the caller's, after
-// the row is written) per LayerNorm.
-__device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, float& den) {
+// ORT's own LayerNorm kernel is one-pass too); the scale is returned as
+// rden = 1 / sqrt(var + eps) (v_rsq_f32, so the normalisation is a multiply).
+// One barrier (the caller's, after the row is written) per LayerNorm.
+__device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, float& rden) {
     const int lane = threadIdx.x & 63;
     const float4 a = *reinterpret_cast<const float4*>(buf + 8 * lane);
     const float4 b = *reinterpret_cast<const float4*>(buf + 8 * lane + 4);
@@ -143,7 +144,7 @@ __device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, floa
     const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[0]), 63)) * (1.0f / 512.0f);
     const float q = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[1]), 63)) * (1.0f / 512.0f);
     mean = c + d;
-    den = sqrtf(fmaxf(q - d * d, 0.f) + 1e-5f);
+    rden = __builtin_amdgcn_rsqf(fmaxf(q - d * d, 0.f) + 1e-5f);   // 1 / sqrt(var + eps), v_rsq_f32
 }
 
 // Batch-1 GEMV on the 16x16x32 f16 MFMA (v_mfma_f32_16x16x32_f16).  The weights
@@ -241,7 +242,7 @@ __device__ __forceinline__ void merge_waves1(Shared1& sh, int w, int lane) {
     M = fmaxf(M, dpp_f<0xB1, 0xF>(M));
     M = fmaxf(M, dpp_f<0x4E, 0xF>(M));
     M = fmaxf(M, dpp_f<0x141, 0xF>(M));
-    const float e = mj == -INFINITY ? 0.f : expf(mj - M);
+    const float e = mj == -INFINITY ? 0.f : __expf(mj - M);
     float L = e * sh.wred[1][j];
     L += dpp_f<0xB1, 0xF>(L);
     L += dpp_f<0x4E, 0xF>(L);
@@ -262,15 +263,18 @@ __device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, floa
 #pragma unroll
     for (int u = 0; u < NU; ++u)
         kr[u] = *reinterpret_cast<const float4*>(sh.at.k + min(64 * u + g, KVL1 - 1) * 32 + 4 * c8);
+    // (q s) . (k s) as (q s s) . k: the key's scale folded into the query once per
+    // lane instead of once per key element (rounding differs at the ulp level)
+    const float p0 = q0 * sc, p1 = q1 * sc, p2 = q2 * sc, p3 = q3 * sc;
     float sv[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         float4 k4 = kr[u];
         if (64 * u + g == kv) k4 = knew;
-        float x = q0 * (k4.x * sc);
-        x += q1 * (k4.y * sc);
-        x += q2 * (k4.z * sc);
-        x += q3 * (k4.w * sc);
+        float x = p0 * k4.x;
+        x += p1 * k4.y;
+        x += p2 * k4.z;
+        x += p3 * k4.w;
         sv[u] = x;
     }
 #pragma unroll
@@ -444,9 +448,9 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
     const float v = g[16] + (lp2[tid] + f);
     sh.lnb[0][tid] = v;
     if (!block_ok1(ok, sh)) return false;
-    float mean, den;
-    ln_row_stats(sh.lnb[0], mean, den);
-    xv = (v - mean) / den * lp2[512 + tid] + lp2[1024 + tid];
+    float mean, rden;
+    ln_row_stats(sh.lnb[0], mean, rden);
+    xv = (v - mean) * rden * lp2[512 + tid] + lp2[1024 + tid];
     return true;
 }
 
@@ -691,9 +695,9 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 if (tid < 128) sh.b1[tid] = b1v;
                 if (!block_ok1(ok, sh)) return;
                 STAMP1(2);
-                float mean, den;
-                ln_row_stats(sh.lnb[1], mean, den);
-                const float h1 = (v - mean) / den * n1w + n1b;
+                float mean, rden;
+                ln_row_stats(sh.lnb[1], mean, rden);
+                const float h1 = (v - mean) * rden * n1w + n1b;
                 h1_pub = h1;   // published with the FFN2 partials: no store in flight during FFN1/FFN2
                 split_h(h1, sh.xh[tid], sh.xl[tid]);   // LayerNorm output: always in fp16 range
             }
