@@ -10,7 +10,12 @@ so every utterance runs a forced number of loop steps):
            whole path -- T2S encoder, prefill, greedy decode (81 loop steps ->
            80 semantic tokens), VITS (ref STFT + MelStyleEncoder, TextEncoder,
            flow, HiFi-GAN) -> 102,400 samples = 3.2 s of 32 kHz audio.  R=48,
-           S=45, H=264 (P=132 prompts), 5.3 s reference.  A step = one utterance.
+           S=45, H=264 (P=132 prompts), 5.3 s reference.  A step = one utterance
+           of a stream of them (a paragraph split into sentences): each one's
+           vocoder runs on --vocoder-cus CUs of its own (default 64) beside the
+           next one's T2S on the other CUs (gsv_vits_decode_async); the line's
+           "sequential" object times one utterance alone on every CU
+           (--vocoder-cus 0 makes that the headline mode).
   batch64  configs[2]: 64 mixed-length JP sentences (S~U[30,60], G~U[50,110]),
            top-k 5 sampled, ONE ragged batched decode + the vocoder per
            utterance.  A step = the 64-sentence batch.
@@ -23,7 +28,7 @@ GPU (torchrun), independent replicas, no collective on the data path; the
 barrier and the max-over-ranks time use a gloo (host) group -- no RCCL.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload single|batch64|mixed100]
-                       [--no-cpu-baseline]
+                       [--vocoder-cus K] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -89,6 +94,29 @@ class Runner:
         self.eng.set_option("persist", 1)
         self.phase = {"t2s": 0.0, "vits": 0.0, "encode+prefill": 0.0, "decode": 0.0}
 
+    def step_overlap(self):
+        """One utterance with its vocoder overlapped on its own CUs: the T2S of this
+        utterance runs while the previous utterance's vocoder finishes beside it."""
+        t0 = time.perf_counter()
+        utts = [(self.d_ref, self.d_txt[0], self.d_ref_bert, self.d_bert[0], self.d_ssl, self.items[0].force_steps)]
+        sems = self.eng.t2s_generate(utts, self.sp)
+        t1 = time.perf_counter()
+        tm = self.eng.timing()
+        self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
+        self.phase["decode"] += tm[2] * 1e-3
+        self.finish()                                       # the previous utterance's vocoder
+        cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
+        self.pending = self.eng.vits_decode_async(dict(text_seq=self.d_txt[0], pred_semantic=sems[0],
+                                                       noise_seed=self.seed, **cond))
+        self.phase["t2s"] += t1 - t0
+        self.phase["vits"] += time.perf_counter() - t1
+        return sems, 1280 * int(sems[0].size)
+
+    def finish(self):
+        if getattr(self, "pending", None) is not None:
+            self.eng.vits_wait()
+            self.pending = None
+
     def step(self):
         torch = self.torch
         t0 = time.perf_counter()
@@ -117,10 +145,12 @@ class Runner:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("single", "batch64", "mixed100"), default="single")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--vocoder-cus", type=int, default=64,
+                    help="single workload: CUs reserved for the overlapped vocoder (0 = sequential)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,6 +165,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
+    # a non-default stream: work on the legacy null stream would serialise with every
+    # blocking stream (the CU-masked engine streams are blocking)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     from genie_tts_amd import workloads, replicas
     from genie_tts_amd.probe import persist_roofline, composite_roofline
@@ -150,9 +183,14 @@ def main():
     run = Runner(wl, items, dev, local if world > 1 else 0)
     timed_single = args.workload == "single"
     run.eng.set_timing(True)                      # phase events (+ live dominant-kernel events at B = 1)
+    overlap = timed_single and args.vocoder_cus > 0
+    if overlap:
+        run.eng.set_vocoder_cus(args.vocoder_cus)
+    do_step = run.step_overlap if overlap else run.step
 
     for _ in range(args.warmup):
-        sems, n_samples = run.step()
+        sems, n_samples = do_step()
+    run.finish()
     torch.cuda.synchronize()
     run.phase = {k: 0.0 for k in run.phase}
     if timed_single:
@@ -164,9 +202,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sems, n_samples = run.step()
+        sems, n_samples = do_step()
         if timed_single:
             phase_ms.append(run.eng.timing())
+    run.finish()                                  # the last utterance's vocoder is inside the timed region
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -175,13 +214,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    R_, H_ = wl.reference.ref_seq.shape[1], wl.reference.ssl.shape[2]
+    n0s = [R_ + it.text_seq.shape[1] + H_ // 2 for it in items]
+    roof = persist_roofline(run.eng, n0=n0s[0], steps=items[0].force_steps, B=1) if timed_single else None
+    seq = None
+    if overlap and rank == 0 and world == 1:
+        # one utterance alone (no overlap, every CU): the single-request latency
+        run.eng.set_vocoder_cus(0)
+        run.step()
+        torch.cuda.synchronize()
+        ns = min(args.steps, 10)
+        ts = time.perf_counter()
+        for _ in range(ns):
+            run.step()
+        torch.cuda.synchronize()
+        seq = (time.perf_counter() - ts) / ns
+
     ms_per_step = dt / args.steps * 1e3
     utt_s = units_per_step * args.steps / dt
     audio_s = n_samples / SR                                  # this rank's audio per step
     rtf = (dt / args.steps) / audio_s
     tokens = [int(s.size) for s in sems]
-    R_, H_ = wl.reference.ref_seq.shape[1], wl.reference.ssl.shape[2]
-    n0s = [R_ + it.text_seq.shape[1] + H_ // 2 for it in items]
 
     out = {
         "metric": METRIC,
@@ -203,11 +256,19 @@ def main():
     }
     if args.workload == "single":
         it = items[0]
-        out["config"] = {"workload": "configs[1]: V2 speaker, single utterance, greedy, 1 utt per replica",
+        out["config"] = {"workload": "configs[1]: V2 speaker, single utterance, greedy, 1 utt per replica" +
+                                     (f"; a stream of such utterances, each one's vocoder on {args.vocoder_cus} CUs "
+                                      "beside the next one's T2S" if overlap else ""),
                          "ref_phones": R_, "text_phones": it.text_seq.shape[1], "ssl_frames": H_,
                          "loop_steps": it.force_steps, "semantic_tokens": tokens[0],
-                         "samples": n_samples, "parallelism": f"replicas x{world}"}
-        out["roofline"] = persist_roofline(run.eng, n0=n0s[0], steps=it.force_steps, B=1)
+                         "samples": n_samples, "parallelism": f"replicas x{world}",
+                         "vocoder_cus": args.vocoder_cus,
+                         "persist_timeouts": run.eng.counter("persist_timeouts"),
+                         "vits_f32_reruns": run.eng.counter("vits_f32_reruns")}
+        out["roofline"] = roof
+        if seq is not None:
+            out["sequential"] = {"utt_s": 1.0 / seq, "ms_per_utt": seq * 1e3, "x_realtime": audio_s / seq,
+                                 "note": "one utterance at a time on every CU (single-request latency)"}
         if phase_ms:
             pm = np.mean(np.asarray(phase_ms), axis=0)
             out["phase_ms"] = {"encode": float(pm[0]), "prefill": float(pm[1]), "decode": float(pm[2]),

@@ -43,6 +43,8 @@ from .text_splitter import TextSplitter
 logger = logging.getLogger(__name__)
 
 SAMPLE_RATE = 32000
+# CUs reserved for the overlapped vocoder of multi-sentence synthesis (0: sequential)
+VOCODER_CUS = int(os.environ.get("GENIE_VOCODER_CUS", "64"))
 SUPPORTED_AUDIO_EXTS = A.SUPPORTED_AUDIO_EXTS
 _reference_audios: Dict[str, ReferenceAudio] = {}
 _clip_cache: "OrderedDict[str, ReferenceAudio]" = OrderedDict()   # ReferenceAudio._prompt_cache (LRU 10)
@@ -213,6 +215,23 @@ def _synthesize(character_name: str, sentence, text_bert=None, sampler=None) -> 
                           m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p, sampler=sampler)
 
 
+def _synthesize_all(character_name: str, sentences: List, text_bert=None, sampler=None):
+    """Every sentence, in order; on the engine the vocoder of one sentence overlaps the
+    T2S of the next (GENIE.tts_stream)."""
+    if len(sentences) < 2:
+        return [_synthesize(character_name, s, text_bert, sampler) for s in sentences]
+    m = model_manager.get(character_name)
+    if m is None:
+        raise ValueError(f"character '{character_name}' is not loaded")
+    ref = _reference_audios[character_name]
+    if m.PROMPT_ENCODER is not None and ref.sv_emb is None and getattr(ref, "sv_fn", None) is not None:
+        ref.sv_emb = np.asarray(ref.sv_fn(ref.audio_16k), np.float32).reshape(1, -1)
+    tts_client.stop_event.clear()
+    return list(tts_client.tts_stream(sentences, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER,
+                                      m.VITS, m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p,
+                                      sampler=sampler, vocoder_cus=VOCODER_CUS))
+
+
 def _play(audio: np.ndarray) -> None:
     try:
         import sounddevice as sd   # noqa: F401  (absent here, as on most servers)
@@ -230,8 +249,8 @@ def tts(character_name: str, text: Union[str, Sequence[int], np.ndarray], play: 
     if character_name not in _reference_audios:
         logger.error("Please call 'set_reference_audio' first to set the reference audio.")
         return None
-    chunks = [_synthesize(character_name, s, text_bert, sampler) for s in _sentences(text, split_sentence)]
-    chunks = [c for c in chunks if c is not None]
+    chunks = [c for c in _synthesize_all(character_name, _sentences(text, split_sentence), text_bert, sampler)
+              if c is not None]
     audio = np.concatenate(chunks) if chunks else np.zeros(0, np.float32)
     if save_path:
         A.write_wav(os.fspath(save_path), audio, SAMPLE_RATE)

@@ -57,6 +57,9 @@ gsv_engine::~gsv_engine() {
     pk_allocs.clear();
     if (pk_tiles) hipFree(pk_tiles);
     if (own_stream && stream) hipStreamDestroy(stream);
+    if (vstream) hipStreamDestroy(vstream);
+    for (hipEvent_t e : {vev_in, vev_done})
+        if (e) hipEventDestroy(e);
     if (done_host) hipHostFree(done_host);
     for (auto& e : kev) if (e) hipEventDestroy(e);
     if (ktrace) hipFree(ktrace);
@@ -745,7 +748,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (allow_persist && use_persist && B <= 8 && persist_groups(B, n_cu) > 0) return decode_persistent(B, sp, st);
+    if (allow_persist && use_persist && B <= 8 && persist_groups(B, decode_cus()) > 0) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -808,7 +811,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
 }
 
 int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) {
-    return decode_persistent_as(B, sp, st, B == 1 && use_persist1 && n_cu >= persist1_grid());
+    return decode_persistent_as(B, sp, st, B == 1 && use_persist1 && decode_cus() >= persist1_grid(3));
 }
 
 // one: the single-sequence kernel (t2s_persist1.hip) instead of the general one.
@@ -841,8 +844,10 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
         return set_error(GSV_E_HIP, "pinned alloc");
     PersistArgs a{};
     a.B = B;
-    a.groups = persist_groups(B, n_cu);
-    if (const char* e = std::getenv("GENIE_PERSIST_GROUPS")) a.groups = std::max(1, std::min(a.groups, std::atoi(e)));
+    // layer groups: as many as the engine stream's CUs hold (all of them unless the
+    // vocoder is overlapped on its own CUs)
+    a.groups = one ? std::min(persist1_max_groups(), decode_cus() / persist1_grid(1)) : persist_groups(B, decode_cus());
+    if (const char* e = std::getenv("GENIE_PERSIST_GROUPS")) a.groups = std::max(one ? 3 : 1, std::min(a.groups, std::atoi(e)));
     for (int l = 0; l < 24; ++l) {
         const T2SLayerW& W = layers[l];
         a.L[l] = PLayer{W.w_in, W.w_out, W.w1, W.w2, W.b_in, W.b_out, W.b1, W.b2, W.n1w, W.n1b, W.n2w, W.n2b};
@@ -871,6 +876,8 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
+    // a queued overlapped vocoder call: enqueue it now, while the GPU decodes
+    if (int r = vits_launch_queued()) return r;
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
     // code 2: the single-sequence kernel met an activation beyond the fp16 range of
     // its split-operand MFMA GEMVs.  It stopped before writing the sequence state
@@ -1209,6 +1216,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->persist1_pf_delay = std::max(0, value);
     } else if (n.size() == 5 && n.compare(0, 4, "knob") == 0 && n[4] >= '0' && n[4] <= '3') {
         eng->persist1_knob[n[4] - '0'] = value;   // single-sequence decode tuning variant (0 = default)
+    } else if (n == "vocoder_cus") {   // overlapped vocoder: CUs reserved for gsv_vits_decode_async
+        return eng->set_vocoder_cus(value);
     } else if (n == "convh") {
         eng->use_convh = value != 0;
     } else if (n == "ptrace") {

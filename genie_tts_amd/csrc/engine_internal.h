@@ -208,6 +208,20 @@ struct gsv_engine {
     int* vflags_host = nullptr;
     int vflag_cap = 0;
     int vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s);
+    int vits_read_ms();
+    // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
+    int vocoder_cus = 0;
+    hipStream_t vstream = nullptr;     // vocoder: K CUs (the engine stream: the other n_cu - K)
+    hipEvent_t vev_in = nullptr, vev_done = nullptr;
+    bool vpending = false;             // launched, not yet finished
+    bool vqueued = false;              // accepted, launched by the next decode (or vits_wait)
+    gsv_vits_item vcall{};
+    float vcall_scale = 0.f;
+    int set_vocoder_cus(int K);
+    int vits_async(const gsv_vits_item& u, float noise_scale, hipStream_t caller);
+    int vits_wait(hipStream_t caller);
+    int vits_launch_queued();
+    int decode_cus() const { return n_cu - vocoder_cus; }   // CUs of the engine (T2S) stream
     int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                       float* ge_adv, hipStream_t st);
 };

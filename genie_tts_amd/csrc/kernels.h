@@ -261,9 +261,11 @@ int persist_grid(int B, int groups);
 size_t persist_ring_bytes(int B);
 int persist_max_tokens();
 hipError_t decode_persist(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
-// Single-sequence persistent decode (t2s_persist1.hip): 8 layer groups x 32
-// workgroups, two hand-offs per layer.  Needs persist1_grid() resident CUs; B must be 1.
-int persist1_grid();
+// Single-sequence persistent decode (t2s_persist1.hip): a.groups (3..8) layer
+// groups x 32 workgroups, two hand-offs per layer.  Needs persist1_grid(groups)
+// resident CUs; B must be 1.
+int persist1_grid(int groups);
+int persist1_max_groups();
 size_t persist1_ring_bytes();
 hipError_t decode_persist1(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 

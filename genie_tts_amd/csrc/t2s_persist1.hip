@@ -18,11 +18,12 @@
 // (the general kernel, t2s_persist.hip, needs 3 per layer because every
 // workgroup tracks the residual stream).  Everything else is local.
 //
-// Grid: 8 layer groups x 32 workgroups = 256 (one per CU; LDS forces it).  Group
-// g owns layers g, g+8, g+16 and keeps its weights of the owned layer it works on
-// next in registers (q/k/v rows 48, out-proj column 16; W1 rows 64, W2 column 64
-// VGPRs) with the head's K/V rows in LDS, all loaded during the 7 layers it
-// waits; a waiting workgroup sleeps on one wake-up granule (the output of the
+// Grid: G layer groups x 32 workgroups (one per CU; LDS forces it): G = 8 fills
+// the chip (256); with the vocoder overlapped on its own CUs (engine option
+// "vocoder_cus") G = 6 or 7.  Group g owns layers g, g+G, g+2G, ... and keeps its
+// weights of the owned layer it works on next in registers (q/k/v rows 48,
+// out-proj column 16; W1 rows 64, W2 column 64 VGPRs) with the head's K/V rows in
+// LDS, all loaded during the G-1 layers it waits; a waiting workgroup sleeps on one wake-up granule (the output of the
 // layer two before its own) and polls its real inputs only then.  Group 1's FFN
 // workgroups also hold the logits rows (ar_predict_layer, 64 + 1 per workgroup)
 // in LDS for the whole launch and compute the logits after layer 23; group 2's
@@ -45,7 +46,7 @@ namespace {
 using namespace pk;
 constexpr int PT = 512;            // threads per workgroup (8 waves)
 constexpr int PWV = PT / 64;
-constexpr int NG = 8;              // layer groups: layer l -> group l % NG
+constexpr int NG_MAX = 8;          // layer groups (a.groups, 3..8): layer l -> group l % a.groups
 constexpr int GW = 32;             // workgroups per group: 16 attention + 16 FFN
 constexpr int NF = 16;             // FFN slices per layer (128 hidden units each)
 constexpr int KVL1 = 448;          // K/V rows of a head staged in LDS
@@ -458,7 +459,7 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
 // Attention workgroup: head h of layers grp, grp + 8, grp + 16.
 // --------------------------------------------------------------------------
 __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int grp, int h) {
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, ng = a.groups;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool sampler = grp == SAMPLER_GRP && h == 0;
     const int ny0 = a.ny[0], kv0 = a.kvlen[0], st0 = a.steps[0];
@@ -504,7 +505,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         if (!step_start(a, ws, s, grp == 0, sh)) break;
         const unsigned tag = ws.tag(s);
         const int kv = kv0 + s;
-        for (int l = grp; l < 24; l += NG) {
+        for (int l = grp; l < 24; l += ng) {
             const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
             float xv;
@@ -578,9 +579,9 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             STAMP1(5);
             __syncthreads();   // LDS operands consumed before the next layer's LDS-DMA lands
             // ---- next owned layer (this step) or the first one of the next step
-            const int ln = l + NG < 24 ? l + NG : grp;
+            const int ln = l + ng < 24 ? l + ng : grp;
             pf_wait(a.pf_delay);   // let the hand-off leave before this CU streams again
-            prefetch(ln, l + NG < 24 ? kv : kv + 1);
+            prefetch(ln, l + ng < 24 ? kv : kv + 1);
             if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         }
         // ---- sampler: logits granules of this step -> token -> TK(s + 1)
@@ -628,7 +629,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
 // [64 j, 64 j + 64) in group LOGIT_GRP).
 // --------------------------------------------------------------------------
 __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int grp, int j) {
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, ng = a.groups;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool logits = grp == LOGIT_GRP;
     const int ny0 = a.ny[0];
@@ -675,7 +676,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
     for (int s = 0; s < a.smax; ++s) {
         if (!step_start(a, ws, s, grp == 0, sh)) break;
         const unsigned tag = ws.tag(s);
-        for (int l = grp; l < 24; l += NG) {
+        for (int l = grp; l < 24; l += ng) {
             const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
             float xv;
@@ -755,7 +756,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             STAMP1(4);
             __syncthreads();   // fs / b1 consumed before the next prefetch lands
             pf_wait(a.pf_delay);
-            prefetch(l + NG < 24 ? l + NG : grp);
+            prefetch(l + ng < 24 ? l + ng : grp);
             if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         }
         if (logits) {
@@ -795,12 +796,14 @@ __global__ __launch_bounds__(PT) void k_decode_persist1(PersistArgs a) {
 
 }  // namespace
 
-int persist1_grid() { return NG * GW; }
+int persist1_grid(int groups) { return groups * GW; }
+int persist1_max_groups() { return NG_MAX; }
 
 size_t persist1_ring_bytes() { return (size_t)Ws1::SLOT * RING1 * 8; }
 
 hipError_t decode_persist1(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(k_decode_persist1, dim3(NG * GW), dim3(PT), 0, s, start, stop, 0, a);
+    if (a.groups < 3 || a.groups > NG_MAX) return hipErrorInvalidValue;   // groups 1, 2 own the logits, sampler
+    hipExtLaunchKernelGGL(k_decode_persist1, dim3(a.groups * GW), dim3(PT), 0, s, start, stop, 0, a);
     return hipGetLastError();
 }
 

@@ -415,19 +415,131 @@ int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* 
             return set_error(GSV_E_HIP, "overflow flag alloc");
         hipMemset(vovf, 0, 64);
     }
-    if (!use_convh)
-        return vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
-                                noise_scale, audio, s, nullptr, timing);
+    if (vpending || vqueued)   // the overlapped vocoder call shares the workspace: finish it first
+        if (int r = vits_wait(nullptr)) return r;
+    if (!use_convh) {
+        if (int r = vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps,
+                                     noise_seed, noise_scale, audio, s, nullptr, timing))
+            return r;
+        return vits_read_ms();
+    }
     if (int r = vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
                                  noise_scale, audio, s, vovf, timing))
         return r;
     hipMemcpyAsync(vovf_host, vovf, 4, hipMemcpyDeviceToHost, s);
     if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vits sync");
-    if (*vovf_host == 0) return 0;
+    if (*vovf_host == 0) return vits_read_ms();
     hipMemsetAsync(vovf, 0, 4, s);
     ++vits_f32_reruns;
-    return vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed, noise_scale,
-                            audio, s, nullptr, timing);
+    if (int r = vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
+                                 noise_scale, audio, s, nullptr, timing))
+        return r;
+    return vits_read_ms();
+}
+
+// Phase time of the last timed vocoder pass (events ev[4], ev[5] around it).
+int gsv_engine::vits_read_ms() {
+    if (!timing) return 0;
+    if (hipEventSynchronize(ev[5]) != hipSuccess) return set_error(GSV_E_HIP, "vits timing");
+    hipEventElapsedTime(&ms[3], ev[4], ev[5]);
+    return 0;
+}
+
+// ---------------------------------------------------------------- overlapped vocoder
+// Option "vocoder_cus" = K splits the CUs: the engine stream (T2S: encoder,
+// prefill, the persistent decode with (n_cu - K) / 32 layer groups) is masked to
+// n_cu - K of them and the vocoder stream to the other K, so the vocoder of
+// utterance i runs beside the T2S of utterance i + 1 -- the persistent decode
+// needs all its workgroups resident, and disjoint masks guarantee it.  (An
+// unmasked engine stream with only the decode kernel on a masked one measured
+// slower: its prefill ran at the speed of 64-192 CUs, the HW queues -- 4 per
+// process -- being shared with the masked streams.)  The mask bits number the CUs
+// XCD-interleaved (bit i: XCD i % 8; measured -- a mask balanced under the
+// XCD-major reading left XCDs short and the decode timed out for K = 32, 96), so
+// bits [0, K) give the vocoder K / 8 CUs of every XCD and every XCD keeps the
+// (n_cu - K) / 8 CUs its share of the decode grid needs (workgroups go to the
+// XCDs round robin).
+int gsv_engine::set_vocoder_cus(int K) {
+    if (K != 0 && (K % 8 != 0 || K < 8 || n_cu - K < 3 * persist1_grid(1) || n_cu % 32 != 0))
+        return set_error(GSV_E_ARG, "vocoder_cus: a multiple of 8 leaving >= 96 CUs for the decode");
+    if (int r = vits_wait(nullptr)) return r;
+    hipDeviceSynchronize();
+    hipStream_t ns = nullptr, nv = nullptr;
+    if (K == 0) {
+        if (hipStreamCreateWithFlags(&ns, hipStreamNonBlocking) != hipSuccess) return set_error(GSV_E_HIP, "stream");
+    } else {
+        const int words = (n_cu + 31) / 32;
+        std::vector<uint32_t> mt(words, 0u), mv(words, 0u);
+        for (int i = 0; i < n_cu; ++i) (i < K ? mv : mt)[i / 32] |= 1u << (i % 32);
+        if (hipExtStreamCreateWithCUMask(&ns, (uint32_t)words, mt.data()) != hipSuccess ||
+            hipExtStreamCreateWithCUMask(&nv, (uint32_t)words, mv.data()) != hipSuccess)
+            return set_error(GSV_E_HIP, "CU-masked stream");
+        for (hipEvent_t* e : {&vev_in, &vev_done})
+            if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
+                return set_error(GSV_E_HIP, "vocoder events");
+    }
+    if (own_stream && stream) hipStreamDestroy(stream);
+    if (vstream) hipStreamDestroy(vstream);
+    stream = ns;
+    own_stream = true;
+    vstream = nv;
+    vocoder_cus = K;
+    return 0;
+}
+
+// The call is queued, not launched: its ~400 launches are issued by the next
+// T2S generate right after the persistent decode kernel (vits_launch_queued), so
+// the host enqueues them while the GPU decodes instead of delaying that T2S.
+int gsv_engine::vits_async(const gsv_vits_item& u, float noise_scale, hipStream_t caller) {
+    if (!vstream) return set_error(GSV_E_STATE, "overlapped vocoder: set option vocoder_cus first");
+    if (int r = vits_wait(nullptr)) return r;
+    if (use_convh && !vovf) {
+        if (hipMalloc(&vovf, 64) != hipSuccess || hipHostMalloc((void**)&vovf_host, 64, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "overflow flag alloc");
+        hipMemset(vovf, 0, 64);
+    }
+    hipEventRecord(vev_in, caller);   // the inputs are ready in the caller's stream order here
+    vcall = u;
+    vcall_scale = noise_scale;
+    vqueued = true;
+    return 0;
+}
+
+int gsv_engine::vits_launch_queued() {
+    if (!vqueued) return 0;
+    vqueued = false;
+    const gsv_vits_item& u = vcall;
+    hipStreamWaitEvent(vstream, vev_in, 0);
+    if (int r = vits_decode_pass(vws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge, u.ge_adv,
+                                 u.noise_mode == 1 ? u.eps : nullptr, u.noise_mode == 2 ? u.noise_seed : 0,
+                                 vcall_scale, u.audio, vstream, use_convh ? vovf : nullptr, timing))
+        return r;
+    if (use_convh) hipMemcpyAsync(vovf_host, vovf, 4, hipMemcpyDeviceToHost, vstream);
+    hipEventRecord(vev_done, vstream);
+    vpending = true;
+    return 0;
+}
+
+int gsv_engine::vits_wait(hipStream_t caller) {
+    if (int r = vits_launch_queued()) return r;
+    if (!vpending) return 0;
+    vpending = false;
+    if (hipEventSynchronize(vev_done) != hipSuccess) return set_error(GSV_E_HIP, "overlapped vocoder");
+    if (use_convh && *vovf_host) {   // fp16-range overflow: the same utterance again on the f32 path
+        const gsv_vits_item& u = vcall;
+        hipMemsetAsync(vovf, 0, 4, vstream);
+        ++vits_f32_reruns;
+        if (int r = vits_decode_pass(vws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
+                                     u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
+                                     u.noise_mode == 2 ? u.noise_seed : 0, vcall_scale, u.audio, vstream, nullptr,
+                                     timing))
+            return r;
+        hipEventRecord(vev_done, vstream);
+        if (hipEventSynchronize(vev_done) != hipSuccess) return set_error(GSV_E_HIP, "overlapped vocoder re-run");
+    }
+    if (int r = vits_read_ms()) return r;
+    if (caller) hipStreamWaitEvent(caller, vev_done, 0);
+    return 0;
 }
 
 // One utterance on stream s with workspace W.  ovf != NULL: the MRF convs run on
@@ -579,11 +691,7 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
         cp.in_act = 1; cp.in_slope = 0.01f;
         conv1d(cp, s);
     }
-    if (timed) {
-        hipEventRecord(ev[5], s);
-        hipEventSynchronize(ev[5]);
-        hipEventElapsedTime(&ms[3], ev[4], ev[5]);
-    }
+    if (timed) hipEventRecord(ev[5], s);   // read by vits_read_ms once the pass is known to be final
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vits launch");
 }
 
@@ -593,6 +701,8 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
 // flag; after the join, flagged utterances are decoded again on the f32 path.
 int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s) {
     if (n <= 0) return 0;
+    if (n > 1 && (vpending || vqueued))
+        if (int r = vits_wait(nullptr)) return r;
     if (n == 1) {   // one utterance: the engine stream itself, no lane fork/join
         const gsv_vits_item& u = it[0];
         return vits_decode(u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge, u.ge_adv,
@@ -709,11 +819,27 @@ extern "C" int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_
     return eng->vits_decode_batch(n, items, noise_scale, sc.st());
 }
 
+extern "C" int gsv_vits_decode_async(gsv_engine* eng, const gsv_vits_item* item, float noise_scale, void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    if (!item || item->noise_mode < 0 || item->noise_mode > 2 || (item->noise_mode == 1 && !item->eps) || !item->audio)
+        return set_error(GSV_E_ARG, "bad vocoder item");
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    return eng->vits_async(*item, noise_scale, (hipStream_t)stream);
+}
+
+extern "C" int gsv_vits_wait(gsv_engine* eng, void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    hipSetDevice(eng->device);
+    return eng->vits_wait((hipStream_t)stream);
+}
+
 extern "C" int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
                                  const float* sv_emb, float* ge, float* ge_adv, void* stream) {
     if (!eng) return set_error(GSV_E_ARG, "null engine");
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    if (int r = eng->vits_wait(nullptr)) return r;   // shares the vocoder workspace
     StreamScope sc(eng, stream);
     return eng->prompt_encode(ref_audio, n_audio, sv_emb, ge, ge_adv, sc.st());
 }

@@ -92,6 +92,8 @@ def lib():
                                       ctypes.POINTER(ctypes.c_int32), vp]
         L.gsv_vits_decode.argtypes = [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp, ctypes.c_float, vp, vp]
         L.gsv_vits_decode_batch.argtypes = [vp, i32, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
+        L.gsv_vits_decode_async.argtypes = [vp, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
+        L.gsv_vits_wait.argtypes = [vp, vp]
         L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
@@ -124,7 +126,8 @@ EXPORTED = (
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
-    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta",
+    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
+    "gsv_vits_wait",
 )
 
 
@@ -356,36 +359,62 @@ class Engine:
                "gsv_vits_decode")
         return audio
 
+    def _vits_item(self, it: dict):
+        """(VitsItem, tensors it points at, audio tensor) of one vocoder call."""
+        t = self.torch
+        ts, sem = self._ids(it["text_seq"]), self._ids(it["pred_semantic"])
+        G = sem.numel()
+        ra = it.get("ref_audio")
+        ra = None if ra is None else self._dev(ra, t.float32).reshape(-1)
+        g = it.get("ge")
+        g = None if g is None else self._dev(g, t.float32).reshape(-1)
+        ga = it.get("ge_advanced")
+        ga = None if ga is None else self._dev(ga, t.float32).reshape(-1)
+        e = it.get("eps")
+        e = None if e is None else self._dev(e, t.float32).reshape(192, 2 * G)
+        seed = it.get("noise_seed")
+        mode = 1 if e is not None else (2 if seed is not None else 0)
+        audio = t.empty((1280 * G,), dtype=t.float32, device=self.dev)
+        item = VitsItem(ts.data_ptr(), ts.numel(), sem.data_ptr(), G, 0 if ra is None else ra.data_ptr(),
+                        0 if ra is None else ra.numel(), 0 if g is None else g.data_ptr(),
+                        0 if ga is None else ga.data_ptr(), 0 if e is None else e.data_ptr(),
+                        int(seed or 0) & 0xFFFFFFFFFFFFFFFF, mode, audio.data_ptr())
+        return item, [ts, sem, ra, g, ga, e], audio
+
     def vits_decode_batch(self, items: Sequence[dict], noise_scale: float = 0.5):
         """Several vocoder calls at once (concurrent engine lanes).  Each item: text_seq,
         pred_semantic, and ref_audio (V2) or ge + ge_advanced (V2ProPlus); optional eps or
         noise_seed.  Returns one audio tensor [1280 G] per item."""
-        t = self.torch
         arr = (VitsItem * len(items))()
         keep, outs = [], []
         for i, it in enumerate(items):
-            ts, sem = self._ids(it["text_seq"]), self._ids(it["pred_semantic"])
-            G = sem.numel()
-            ra = it.get("ref_audio")
-            ra = None if ra is None else self._dev(ra, t.float32).reshape(-1)
-            g = it.get("ge")
-            g = None if g is None else self._dev(g, t.float32).reshape(-1)
-            ga = it.get("ge_advanced")
-            ga = None if ga is None else self._dev(ga, t.float32).reshape(-1)
-            e = it.get("eps")
-            e = None if e is None else self._dev(e, t.float32).reshape(192, 2 * G)
-            seed = it.get("noise_seed")
-            mode = 1 if e is not None else (2 if seed is not None else 0)
-            audio = t.empty((1280 * G,), dtype=t.float32, device=self.dev)
-            arr[i] = VitsItem(ts.data_ptr(), ts.numel(), sem.data_ptr(), G, 0 if ra is None else ra.data_ptr(),
-                              0 if ra is None else ra.numel(), 0 if g is None else g.data_ptr(),
-                              0 if ga is None else ga.data_ptr(), 0 if e is None else e.data_ptr(),
-                              int(seed or 0) & 0xFFFFFFFFFFFFFFFF, mode, audio.data_ptr())
-            keep += [ts, sem, ra, g, ga, e]
+            arr[i], k, audio = self._vits_item(it)
+            keep += k
             outs.append(audio)
         _check(lib().gsv_vits_decode_batch(self.h, len(items), arr, ctypes.c_float(noise_scale), _stream()),
                "gsv_vits_decode_batch")
         return outs
+
+    vocoder_cus = 0
+
+    def set_vocoder_cus(self, k: int):
+        """Reserve k CUs for the overlapped vocoder (0: off; see gsv_vits_decode_async)."""
+        self.set_option("vocoder_cus", k)
+        self.vocoder_cus = int(k)
+
+    def vits_decode_async(self, item: dict, noise_scale: float = 0.5):
+        """Start one vocoder call on the vocoder CUs (gsv_vits_decode_async) and return its
+        audio tensor [1280 G], valid after vits_wait().  item as for vits_decode_batch."""
+        it, keep, audio = self._vits_item(item)
+        _check(lib().gsv_vits_decode_async(self.h, ctypes.byref(it), ctypes.c_float(noise_scale), _stream()),
+               "gsv_vits_decode_async")
+        self._vits_keep = keep   # device inputs stay alive until the call is finished
+        return audio
+
+    def vits_wait(self):
+        """Finish the pending vits_decode_async call; orders the current stream after it."""
+        _check(lib().gsv_vits_wait(self.h, _stream()), "gsv_vits_wait")
+        self._vits_keep = None
 
     def prompt_encode(self, ref_audio, sv_emb):
         t = self.torch

@@ -109,6 +109,59 @@ class GENIE:
         return vocoder.run(None, {"text_seq": text_seq, "pred_semantic": sem, "ge": prompt_audio.global_emb,
                                   "ge_advanced": prompt_audio.global_emb_advanced})[0]
 
+    def tts_stream(self, texts: Sequence[Union[str, np.ndarray]], prompt_audio: ReferenceAudio, encoder,
+                   first_stage_decoder, stage_decoder, vocoder, prompt_encoder=None, language: str = "japanese",
+                   text_bert: Optional[np.ndarray] = None, g2p: Optional[Callable] = None,
+                   sampler: Optional[Sampler] = None, vocoder_cus: int = 64):
+        """tts over a list of sentences, yielding each sentence's audio in order (the
+        reference runs them one after the other: TTSPlayer._tts_worker_loop,
+        Core/TTSPlayer.py:56-107).  Engine-backed sessions pipeline them: sentence i's
+        vocoder runs on `vocoder_cus` CUs of its own while sentence i+1's T2S runs on
+        the rest (gsv_vits_decode_async), so sentence i is yielded once sentence i+1's
+        T2S is done.  Same tokens and audio as calling tts per sentence."""
+        eng = _engine_of(encoder, first_stage_decoder, stage_decoder, vocoder)
+        if eng is None or vocoder_cus <= 0 or len(texts) < 2:
+            for t in texts:
+                yield self.tts(t, prompt_audio, encoder, first_stage_decoder, stage_decoder, vocoder, prompt_encoder,
+                               language, text_bert, g2p, sampler)
+            return
+        if eng.vocoder_cus != vocoder_cus:
+            eng.set_vocoder_cus(vocoder_cus)
+        if prompt_encoder is None:
+            cond = {"ref_audio": prompt_audio.audio_32k}
+        else:
+            prompt_audio.update_global_emb(prompt_encoder)
+            cond = {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced}
+        pending = None
+        for t in texts:
+            if self.stop_event.is_set():
+                break
+            if isinstance(t, str):
+                if g2p is None:
+                    raise ValueError("text input needs a g2p(text, language) callable (G2P is outside this engine)")
+                text_seq, tb = g2p("。" + t, language)
+            else:
+                text_seq = np.asarray(t, np.int64).reshape(1, -1)
+                tb = text_bert if text_bert is not None else np.zeros((text_seq.shape[1], 1024), np.float32)
+            sem = self.t2s(prompt_audio.phonemes_seq, prompt_audio.text_bert, text_seq, tb,
+                           prompt_audio.ssl_content, eng, sampler or first_stage_decoder.sampler)
+            if pending is not None:
+                eng.vits_wait()
+                yield pending.cpu().numpy()
+            G = sem.size
+            eps = vocoder.eps_fn(G) if vocoder.eps_fn else None
+            item = dict(text_seq=text_seq, pred_semantic=sem, **cond)
+            if eps is not None:
+                item["eps"] = eps
+            else:
+                seed = vocoder.next_seed()
+                if seed is not None:
+                    item["noise_seed"] = seed
+            pending = eng.vits_decode_async(item, vocoder.noise_scale)
+        if pending is not None:
+            eng.vits_wait()
+            yield pending.cpu().numpy()
+
     def t2s(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, engine, sampler: Sampler) -> np.ndarray:
         """Whole T2S on the device; returns the trimmed, EOS-filtered [1,1,G] tokens."""
         tok = engine.t2s_generate([(ref_seq, text_seq, ref_bert, text_bert,

@@ -161,6 +161,19 @@ typedef struct {
 int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_item* items, float noise_scale,
                           void* stream);
 
+/* Overlapped vocoder for a stream of sentences (the reference synthesises them one
+ * after the other: TTSPlayer._tts_worker_loop, Core/TTSPlayer.py:56-107, each
+ * sentence a full Inference.tts, Core/Inference.py:16).  After
+ * gsv_set_option(eng, "vocoder_cus", K) the engine stream runs on n_cu - K CUs and
+ * the vocoder on the other K, so sentence i's vocoder overlaps sentence i+1's T2S.
+ * gsv_vits_decode_async starts one vocoder call (ordered after `stream`) and returns
+ * without waiting; the item's buffers must stay valid until gsv_vits_wait, which
+ * finishes it (fp16-range overflow -> the f32 re-run, as gsv_vits_decode) and orders
+ * `stream` (may be NULL) after it.  One call in flight: a second async call, any
+ * other vocoder call or gsv_prompt_encode finishes the pending one first. */
+int gsv_vits_decode_async(gsv_engine* eng, const gsv_vits_item* item, float noise_scale, void* stream);
+int gsv_vits_wait(gsv_engine* eng, void* stream);
+
 /* prompt_encoder_fp32.onnx (V2ProPlus): ref_audio (device [n_audio]),
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */
 int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,

@@ -132,3 +132,26 @@ def test_tts_batch_equals_single(model):
                          sampler=sp)
         assert single.shape == b.shape
         np.testing.assert_allclose(single, b, atol=1e-6)
+
+
+def test_tts_stream_equals_single(model):
+    """GENIE.tts_stream (vocoder of sentence i overlapped with the T2S of sentence
+    i+1 on split CUs) yields what tts gives sentence by sentence."""
+    from genie_tts_amd.inference import GENIE, ReferenceAudio
+    m, _ = model
+    ref = ReferenceAudio(phonemes_seq=synth.synth_phones(12, "s-r"), text_bert=np.zeros((12, 1024), np.float32),
+                         audio_32k=synth.synth_ref_audio(32000 * 2, "s-a").reshape(1, -1),
+                         ssl_content=synth.synth_ssl(41, "s-s").reshape(1, 768, -1))
+    texts = [synth.synth_phones(n, f"s-t{n}") for n in (10, 17, 25, 12)]
+    gen = GENIE()
+    sp = m.T2S_FIRST_STAGE_DECODER.sampler
+    args = (ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER, m.VITS, None)
+    try:
+        streamed = list(gen.tts_stream(texts, *args, sampler=sp, vocoder_cus=64))
+    finally:
+        m.ENGINE.set_vocoder_cus(0)
+    assert len(streamed) == len(texts)
+    for t, a in zip(texts, streamed):
+        single = gen.tts(t, *args, sampler=sp)
+        assert single.shape == a.shape
+        np.testing.assert_allclose(single, a, atol=1e-6)

@@ -1,0 +1,93 @@
+"""GPU: the overlapped vocoder (option "vocoder_cus", gsv_vits_decode_async /
+gsv_vits_wait) -- a stream of sentences where sentence i's vocoder runs on its
+own CUs beside sentence i+1's T2S (the reference runs them one after the other,
+TTSPlayer._tts_worker_loop, Core/TTSPlayer.py:56-107).
+
+Bars: with the decode on (256 - K) / 32 layer groups, every token bit-exact
+against the reference-graph fixtures; every waveform RMS <= 1e-4 against them
+(north_star) and identical to the engine's own sequential vocoder output; no
+persistent-decode timeout (the CU split keeps the decode grid resident)."""
+import os
+
+import numpy as np
+import pytest
+
+from genie_tts_amd import synth
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gold(name):
+    return dict(np.load(os.path.join(GOLD, name), allow_pickle=False))
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from genie_tts_amd.engine import Engine
+    w = synth.synthetic_character("v2")
+    e = Engine({k: w[k] for k in w}, "v2", pe_div_term=np.load(os.path.join(GOLD, "pe_div_term.npy")))
+    e.set_option("persist", 1)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("K", [64, 96, 32])
+def test_overlapped_stream_matches_reference_graphs(eng, K):
+    import torch
+    from genie_tts_amd.engine import make_sampler
+    t, nom, v = gold("t2s_nominal81.npz"), gold("t2s_nominal.npz"), gold("vits_v2_g80.npz")
+    n = len(t["step_tokens"])
+    smp = make_sampler(force_steps=n)
+    utt = (nom["ref_seq"], nom["text_seq"], None, None, nom["ssl"])
+    eng.set_vocoder_cus(0)
+    seq_audio = eng.vits_decode(v["text_seq"], v["pred_semantic"], ref_audio=v["ref_audio"],
+                                noise_seed=int(v["noise_seed"])).cpu()
+    t0 = eng.counter("persist_timeouts")
+    eng.set_vocoder_cus(K)
+    try:
+        audios = []
+        for i in range(3):   # T2S of sentence i beside the vocoder of sentence i-1
+            out = eng.t2s_generate([utt], smp)
+            np.testing.assert_array_equal(out[0], t["pred_semantic"].reshape(-1))
+            if i:
+                eng.vits_wait()
+            audios.append(eng.vits_decode_async(dict(text_seq=v["text_seq"], pred_semantic=v["pred_semantic"],
+                                                     ref_audio=v["ref_audio"], noise_seed=int(v["noise_seed"]))))
+        eng.vits_wait()
+        for a in audios:
+            a = a.cpu()
+            assert torch.equal(a, seq_audio)
+            rms = float(np.sqrt(np.mean((a.numpy() - v["audio_philox"]) ** 2)))
+            assert rms <= 1e-4, rms
+        assert eng.counter("persist_timeouts") == t0
+    finally:
+        eng.set_vocoder_cus(0)
+
+
+def test_overlapped_vocoder_needs_the_split(eng):
+    from genie_tts_amd.engine import EngineError
+    v = gold("vits_v2_g80.npz")
+    eng.set_vocoder_cus(0)
+    with pytest.raises(EngineError, match="vocoder_cus"):
+        eng.vits_decode_async(dict(text_seq=v["text_seq"], pred_semantic=v["pred_semantic"], ref_audio=v["ref_audio"]))
+    for bad in (12, 4, 256, 200):
+        with pytest.raises(EngineError, match="vocoder_cus"):
+            eng.set_vocoder_cus(bad)
+    eng.vits_wait()   # nothing pending: a no-op
+
+
+def test_sync_vocoder_finishes_a_pending_call(eng):
+    """A synchronous vocoder call after an async one: the pending call is finished
+    first (they share the workspace), and both outputs are correct."""
+    v = gold("vits_v2_g80.npz")
+    kw = dict(ref_audio=v["ref_audio"])
+    eng.set_vocoder_cus(64)
+    try:
+        a = eng.vits_decode_async(dict(text_seq=v["text_seq"], pred_semantic=v["pred_semantic"], **kw))
+        b = eng.vits_decode(v["text_seq"], v["pred_semantic"], **kw)
+        for x in (a, b):
+            rms = float(np.sqrt(np.mean((x.cpu().numpy() - v["audio_zero"]) ** 2)))
+            assert rms <= 1e-4, rms
+    finally:
+        eng.set_vocoder_cus(0)
