@@ -98,8 +98,13 @@ class Runner:
         """One utterance with its vocoder overlapped on its own CUs: the T2S of this
         utterance runs while the previous utterance's vocoder finishes beside it."""
         t0 = time.perf_counter()
-        utts = [(self.d_ref, self.d_txt[0], self.d_ref_bert, self.d_bert[0], self.d_ssl, self.items[0].force_steps)]
-        sems = self.eng.t2s_generate(utts, self.sp)
+        if getattr(self, "utt", None) is None:
+            self.utt = (self.d_ref, self.d_txt[0], self.d_ref_bert, self.d_bert[0], self.d_ssl,
+                        self.items[0].force_steps)
+        # the next utterance of the stream (here the same one again): encoded and
+        # prefilled on the vocoder CUs while this one decodes
+        self.eng.t2s_prefetch(self.utt, self.sp)
+        sems = self.eng.t2s_generate([self.utt], self.sp)
         t1 = time.perf_counter()
         tm = self.eng.timing()
         self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3

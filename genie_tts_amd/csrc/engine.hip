@@ -58,7 +58,7 @@ gsv_engine::~gsv_engine() {
     if (pk_tiles) hipFree(pk_tiles);
     if (own_stream && stream) hipStreamDestroy(stream);
     if (vstream) hipStreamDestroy(vstream);
-    for (hipEvent_t e : {vev_in, vev_done})
+    for (hipEvent_t e : {vev_in, vev_done, pf_in, pf_done, pf_copied, pf_fork, pf_ev[0], pf_ev[1], pf_ev[2]})
         if (e) hipEventDestroy(e);
     if (done_host) hipHostFree(done_host);
     for (auto& e : kev) if (e) hipEventDestroy(e);
@@ -335,7 +335,7 @@ int gsv_engine::encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t
 
 // ------------------------------------------------------------ prefill
 int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, int P,
-                             const gsv_sampler* sp, float* logits_out, hipStream_t st) {
+                             const gsv_sampler* sp, float* logits_out, hipStream_t st, int noise_b) {
     const int N0 = L + P;
     if (N0 + 1 > tmax) return set_error(GSV_E_CAPACITY, "prefill exceeds reserved tokens");
     if (x != pH) hipMemcpyAsync(pH, x, (size_t)L * 512 * 4, hipMemcpyDeviceToDevice, st);
@@ -401,7 +401,8 @@ int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, in
     sa.y = y + (size_t)b * tmax; sa.ny = ny + b; sa.seen = seen + (size_t)b * 33;
     sa.done = done + b; sa.stop_out = nullptr; sa.steps = steps + b; sa.kvlen = kvlen + b;
     sa.prefill = 1; sa.logits_out = logits_out; sa.ldlo = 1025;
-    sa.b0 = b;   // Philox counter: the slot's own noise for its first-stage token
+    sa.b0 = noise_b >= 0 ? noise_b : b;   // Philox counter: the slot's own noise for its first-stage token
+                                          // (a prefetch into slot 1 draws slot 0's: it is decoded there)
     sample_tokens(sa, st);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "prefill launch");
 }
@@ -871,13 +872,17 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     hipMemsetAsync(perr, 0, 4, st);
     const bool probe = timing && kev[0] != nullptr;
+    // a queued prefetch starts once this stream's prefill (same workspaces) is done
+    if (pf_queued && !pf_pending) hipEventRecord(pf_fork, st);
     const hipError_t le = one ? decode_persist1(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr)
                               : decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr);
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
-    // a queued overlapped vocoder call: enqueue it now, while the GPU decodes
+    // a queued overlapped vocoder call and T2S prefetch: enqueue them now (vocoder
+    // CUs, in that order), while the GPU decodes
     if (int r = vits_launch_queued()) return r;
+    if (int r = pf_launch_queued()) return r;
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
     // code 2: the single-sequence kernel met an activation beyond the fp16 range of
     // its split-operand MFMA GEMVs.  It stopped before writing the sequence state
@@ -909,6 +914,103 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
         }
     }
     return 0;
+}
+
+// ============================================================ T2S prefetch
+// The next utterance of a stream is encoded and prefilled ahead, on the vocoder
+// CUs (after the overlapped vocoder call queued before it), into slot 1 while
+// slot 0 decodes; the generate it was made for copies slot 1 into slot 0 (KV rows
+// [0, N0) of every layer and head + the sequence state, one launch) and decodes
+// there, so every decode path keeps working on slot 0 and the tokens are the
+// ones the plain path gives (the prefill samples with slot 0's Philox counter).
+namespace {
+struct SlotCopyArgs {
+    float* kc[24];
+    float* vc[24];
+    long sstride;
+    int tmax, n0;
+    int64_t* y;
+    int *ny, *kvlen, *steps;
+    uint8_t* done;
+    uint32_t* seen;
+};
+// block (head h, layer l, k|v): rows [0, n0) of the head, contiguous n0 x 32 floats
+__global__ __launch_bounds__(256) void k_slot_copy(SlotCopyArgs a) {
+    const int h = blockIdx.x, l = blockIdx.y;
+    float* base = (blockIdx.z ? a.vc[l] : a.kc[l]) + (long)h * a.tmax * 32;
+    const float4* src = reinterpret_cast<const float4*>(base + a.sstride);
+    float4* dst = reinterpret_cast<float4*>(base);
+    for (int i = threadIdx.x; i < a.n0 * 8; i += 256) dst[i] = src[i];
+    if (h == 0 && l == 0 && blockIdx.z == 0) {
+        for (int i = threadIdx.x; i < a.tmax; i += 256) a.y[i] = a.y[a.tmax + i];
+        if (threadIdx.x < 33) a.seen[threadIdx.x] = a.seen[33 + threadIdx.x];
+        if (threadIdx.x == 0) {
+            a.ny[0] = a.ny[1];
+            a.kvlen[0] = a.kvlen[1];
+            a.steps[0] = a.steps[1];
+            a.done[0] = a.done[1];
+        }
+    }
+}
+
+bool same_utt(const gsv_utt& a, const gsv_utt& b) {
+    return a.ref_seq == b.ref_seq && a.n_ref == b.n_ref && a.text_seq == b.text_seq && a.n_text == b.n_text &&
+           a.ref_bert == b.ref_bert && a.text_bert == b.text_bert && a.ssl == b.ssl && a.n_ssl == b.n_ssl &&
+           a.force_steps == b.force_steps;
+}
+bool same_sampler(const gsv_sampler& a, const gsv_sampler& b) {
+    return a.top_k == b.top_k && a.temperature == b.temperature && a.repetition_penalty == b.repetition_penalty &&
+           a.greedy == b.greedy && a.seed == b.seed && a.max_steps == b.max_steps && a.force_steps == b.force_steps;
+}
+// the sampler generate runs with (defaults of the reference graphs)
+int norm_sampler(const gsv_sampler* s, gsv_sampler& sp) {
+    sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
+    if (sp.top_k < 1 || sp.top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
+    if (sp.max_steps <= 0) sp.max_steps = 500;
+    return 0;
+}
+}  // namespace
+
+// Launch the queued prefetch into slot 1 (vocoder stream) unless slot 1 still
+// holds a launched one that no generate has taken yet.
+int gsv_engine::pf_launch_queued() {
+    if (!pf_queued || pf_pending) return 0;
+    pf_queued = false;
+    pf_p = pf_q;
+    const gsv_utt& u = pf_p.u;
+    const int L = u.n_ref + u.n_text, P = u.n_ssl / 2;
+    hipStreamWaitEvent(vstream, pf_in, 0);
+    hipStreamWaitEvent(vstream, pf_fork, 0);   // the engine stream's encoder / prefill work (same workspaces)
+    if (pf_copied_valid) hipStreamWaitEvent(vstream, pf_copied, 0);   // slot 1 taken by the last generate
+    if (timing) hipEventRecord(pf_ev[0], vstream);
+    if (int e = encode(&u, pH, prompts_buf, vstream)) return e;
+    if (timing) hipEventRecord(pf_ev[1], vstream);
+    if (int e = prefill_slot(1, pH, L, prompts_buf, P, &pf_p.sp, nullptr, vstream, 0)) return e;
+    if (timing) hipEventRecord(pf_ev[2], vstream);
+    hipEventRecord(pf_done, vstream);
+    pf_pending = true;
+    return 0;
+}
+
+// Finish a launched prefetch (it writes the T2S workspaces) and forget a queued
+// one (unless keep_queued).
+int gsv_engine::pf_drop(bool keep_queued) {
+    if (!keep_queued) pf_queued = false;
+    if (!pf_pending) return 0;
+    pf_pending = false;
+    return hipEventSynchronize(pf_done) == hipSuccess ? 0 : set_error(GSV_E_HIP, "T2S prefetch");
+}
+
+void gsv_engine::pf_take(hipStream_t st) {
+    hipStreamWaitEvent(st, pf_done, 0);
+    SlotCopyArgs a{};
+    for (int l = 0; l < 24; ++l) { a.kc[l] = kcache[l]; a.vc[l] = vcache[l]; }
+    a.sstride = (long)16 * tmax * 32; a.tmax = tmax; a.n0 = pf_p.n0;
+    a.y = y; a.ny = ny; a.kvlen = kvlen; a.steps = steps; a.done = done; a.seen = seen;
+    hipLaunchKernelGGL(k_slot_copy, dim3(16, 24, 2), dim3(256), 0, st, a);
+    hipEventRecord(pf_copied, st);
+    pf_copied_valid = true;
+    pf_pending = false;
 }
 
 // ============================================================ C ABI
@@ -990,6 +1092,7 @@ extern "C" int gsv_finalize_weights(gsv_engine* eng) {
 extern "C" int gsv_reserve(gsv_engine* eng, int max_batch, int max_tokens) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     return eng->reserve(max_batch, max_tokens);
 }
@@ -1001,6 +1104,7 @@ extern "C" int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64
     if (!u || !x || !prompts) return set_error(GSV_E_ARG, "null arg");
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     hipSetDevice(eng->device);
+    if (int e = eng->pf_drop()) return e;
     StreamScope sc(eng, stream);
     return eng->encode(u, x, prompts, sc.st());
 }
@@ -1010,6 +1114,7 @@ extern "C" int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t
                                int64_t* yout, float* logits_out, void* stream) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_CAPACITY, "slot out of range");
     if (s && (s->top_k < 1 || s->top_k > 64)) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
@@ -1027,6 +1132,7 @@ extern "C" int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int nsteps, const 
                                     int64_t* yout, uint8_t* stop, float* logits_out, void* stream) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (seq != 0) return set_error(GSV_E_ARG, "decode_steps supports slot 0");
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
@@ -1052,6 +1158,7 @@ extern "C" int gsv_t2s_read_kv(gsv_engine* eng, int seq, int layer, float* k, fl
                                void* stream) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (layer < 0 || layer >= 24 || seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_ARG, "range");
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
@@ -1076,9 +1183,15 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (batch <= 0 || !utts || !out_tokens || !out_len) return set_error(GSV_E_ARG, "bad args");
-    gsv_sampler sp = s ? *s : gsv_sampler{15, 1.0f, 1.35f, 1, 0, 500, 0};
-    if (sp.top_k < 1 || sp.top_k > 64) return set_error(GSV_E_ARG, "top_k must be in [1, 64]");
-    if (sp.max_steps <= 0) sp.max_steps = 500;
+    gsv_sampler sp;
+    if (int e = norm_sampler(s, sp)) return e;
+    // prefetched (gsv_t2s_prefetch, launched into slot 1 during the last decode)?  A
+    // queued prefetch is for a later call: it stays queued (launched during this
+    // decode) unless this is a batch, whose prefill uses slot 1 itself.
+    const bool hit = batch == 1 && eng->pf_pending && same_utt(utts[0], eng->pf_p.u) &&
+                     same_sampler(sp, eng->pf_p.sp);
+    if (!hit)
+        if (int e = eng->pf_drop(batch == 1)) return e;
     const int steps_cap = sp.force_steps > 0 ? sp.force_steps : sp.max_steps;
     int need = 0, limit = 0;
     std::vector<int> hforce(batch);
@@ -1095,6 +1208,9 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     hipStream_t st = sc.st();
     hipMemcpyAsync(eng->forceb, hforce.data(), batch * 4, hipMemcpyHostToDevice, st);
     eng->loop_limit = limit;
+    if (hit) {   // encoded and prefilled ahead (gsv_t2s_prefetch): slot 1 -> slot 0
+        eng->pf_take(st);
+    } else {
     if (eng->timing) hipEventRecord(eng->ev[0], st);
     hipMemsetAsync(eng->done, 1, eng->max_batch, st);
     if (batch > 1 && eng->use_packed) {
@@ -1108,6 +1224,7 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
             if (int e = eng->prefill_slot(b, eng->pH, L, eng->prompts_buf, P, &sp, nullptr, st)) return e;
         }
     }
+    }
     if (eng->timing) hipEventRecord(eng->ev[2], st);
     const int rc = eng->decode_loop(batch, &sp, st);
     eng->loop_limit = 0;
@@ -1120,9 +1237,9 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     std::vector<int64_t> hy((size_t)batch * eng->tmax);
     hipMemcpyAsync(hy.data(), eng->y, hy.size() * 8, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "generate sync");
-    if (eng->timing) {
-        hipEventElapsedTime(&eng->ms[0], eng->ev[0], eng->ev[1]);
-        hipEventElapsedTime(&eng->ms[1], eng->ev[1], eng->ev[2]);
+    if (eng->timing) {   // a prefetched utterance: its encode / prefill phases ran on the vocoder CUs
+        hipEventElapsedTime(&eng->ms[0], hit ? eng->pf_ev[0] : eng->ev[0], hit ? eng->pf_ev[1] : eng->ev[1]);
+        hipEventElapsedTime(&eng->ms[1], hit ? eng->pf_ev[1] : eng->ev[1], hit ? eng->pf_ev[2] : eng->ev[2]);
         hipEventElapsedTime(&eng->ms[2], eng->ev[2], eng->ev[3]);
     }
     for (int b = 0; b < batch; ++b) {
@@ -1138,6 +1255,34 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
         std::memcpy(out_tokens + (size_t)b * out_stride, yy + start, (size_t)cnt * 8);
         out_len[b] = cnt;
     }
+    return 0;
+}
+
+extern "C" int gsv_t2s_prefetch(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* s, void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    if (!utt) return set_error(GSV_E_ARG, "null utterance");
+    if (!eng->vstream) return set_error(GSV_E_STATE, "T2S prefetch: set option vocoder_cus first");
+    if (utt->force_steps < 0) return set_error(GSV_E_ARG, "negative force_steps");
+    const int L = utt->n_ref + utt->n_text, P = utt->n_ssl / 2;
+    if (L <= 0 || P <= 0) return set_error(GSV_E_ARG, "empty utterance");
+    gsv_sampler sp;
+    if (int e = norm_sampler(s, sp)) return e;
+    const int cap = utt->force_steps > 0 ? utt->force_steps : sp.force_steps > 0 ? sp.force_steps : sp.max_steps;
+    const int need = L + P + cap + 16;
+    if (eng->max_batch < 2 || need > eng->tmax)   // the KV cache is re-allocated: nothing may be in flight
+        if (int e = eng->pf_drop()) return e;
+    if (int e = eng->reserve(2, need)) return e;
+    if (!eng->pf_in) {
+        for (hipEvent_t* e : {&eng->pf_in, &eng->pf_done, &eng->pf_copied, &eng->pf_fork})
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return set_error(GSV_E_HIP, "prefetch events");
+        for (hipEvent_t& e : eng->pf_ev)
+            if (hipEventCreate(&e) != hipSuccess) return set_error(GSV_E_HIP, "prefetch events");
+    }
+    hipEventRecord(eng->pf_in, (hipStream_t)stream);   // the inputs are ready in the caller's order here
+    eng->pf_q = gsv_engine::Prefetch{*utt, sp, L + P};   // replaces a queued one; a launched one stays
+    eng->pf_queued = true;
     return 0;
 }
 

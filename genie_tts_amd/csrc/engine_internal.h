@@ -175,7 +175,7 @@ struct gsv_engine {
     int ensure_packed(int rows, int B);
     int prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp, hipStream_t st);
     int prefill_slot(int b, const float* x, int L, const int64_t* pr, int P, const gsv_sampler* sp,
-                     float* logits_out, hipStream_t st);
+                     float* logits_out, hipStream_t st, int noise_b = -1);
     gsv::SampleArgs sampler_args(const gsv_sampler* sp, int B);
     void decode_step(int B, const gsv_sampler* sp, float* logits_out, hipStream_t st);
     hipGraphExec_t step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st);
@@ -222,6 +222,23 @@ struct gsv_engine {
     int vits_wait(hipStream_t caller);
     int vits_launch_queued();
     int decode_cus() const { return n_cu - vocoder_cus; }   // CUs of the engine (T2S) stream
+    // T2S prefetch (gsv_t2s_prefetch): encode + prefill of the next utterance into
+    // slot 1 on the vocoder CUs while slot 0 decodes; taken into slot 0 by the
+    // generate it was made for
+    struct Prefetch {
+        gsv_utt u;
+        gsv_sampler sp;
+        int n0;
+    };
+    Prefetch pf_q{}, pf_p{};           // queued (launched by the next decode) / launched into slot 1
+    bool pf_queued = false, pf_pending = false;
+    bool pf_copied_valid = false;      // pf_copied recorded (slot 1 read by the last take)
+    hipEvent_t pf_in = nullptr, pf_done = nullptr, pf_copied = nullptr;
+    hipEvent_t pf_fork = nullptr;      // engine stream before the decode kernel the prefetch runs beside
+    hipEvent_t pf_ev[3] = {};          // timing: encode, prefill, end (vocoder stream)
+    int pf_launch_queued();
+    int pf_drop(bool keep_queued = false);
+    void pf_take(hipStream_t st);
     int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                       float* ge_adv, hipStream_t st);
 };

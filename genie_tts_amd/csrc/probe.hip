@@ -24,6 +24,7 @@ extern "C" int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (eng->max_batch < B) return set_error(GSV_E_CAPACITY, "probe: reserve first");
+    if (int e = eng->pf_drop()) return e;
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
     const long sstride = (long)16 * eng->tmax * 32;

@@ -463,6 +463,7 @@ int gsv_engine::set_vocoder_cus(int K) {
     if (K != 0 && (K % 8 != 0 || K < 8 || n_cu - K < 3 * persist1_grid(1) || n_cu % 32 != 0))
         return set_error(GSV_E_ARG, "vocoder_cus: a multiple of 8 leaving >= 96 CUs for the decode");
     if (int r = vits_wait(nullptr)) return r;
+    if (int r = pf_drop()) return r;   // a launched prefetch runs on the vocoder stream
     hipDeviceSynchronize();
     hipStream_t ns = nullptr, nv = nullptr;
     if (K == 0) {

@@ -94,6 +94,7 @@ def lib():
         L.gsv_vits_decode_batch.argtypes = [vp, i32, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
         L.gsv_vits_decode_async.argtypes = [vp, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
         L.gsv_vits_wait.argtypes = [vp, vp]
+        L.gsv_t2s_prefetch.argtypes = [vp, ctypes.POINTER(Utt), ctypes.POINTER(Sampler), vp]
         L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
@@ -127,7 +128,7 @@ EXPORTED = (
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
     "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
-    "gsv_vits_wait",
+    "gsv_vits_wait", "gsv_t2s_prefetch",
 )
 
 
@@ -286,8 +287,16 @@ class Engine:
             return out
         arr = (Utt * len(utts))()
         keep = []
+        pf = getattr(self, "_pf", [])
+        hit = next((j for j, p in enumerate(pf) if len(utts) == 1 and p[0] is utts[0]), None)
+        # consumed entries go; on a single-utterance miss the engine keeps a queued
+        # prefetch (the latest), whose buffers must stay alive; a batch drops all
+        self._pf = pf[hit + 1:] if hit is not None else pf[-1:] if len(utts) == 1 else []
         for i, u in enumerate(utts):
-            arr[i], k = self.make_utt(*u)
+            if hit is not None:
+                arr[i], k = pf[hit][1], pf[hit][2]   # the prefetched utterance: the same device buffers
+            else:
+                arr[i], k = self.make_utt(*u)
             keep.append(k)
         sp = sampler or make_sampler()
         out = np.zeros((len(utts), out_stride), dtype=np.int64)
@@ -297,6 +306,16 @@ class Engine:
                                       lens.ctypes.data_as(ctypes.c_void_p), _stream()),
                "gsv_t2s_generate")
         return [out[i, :lens[i]].copy() for i in range(len(utts))]
+
+    def t2s_prefetch(self, utt: Tuple, sampler: Optional[Sampler] = None):
+        """Encode + prefill `utt` (a t2s_generate tuple) ahead on the vocoder CUs while the
+        current decode runs (gsv_t2s_prefetch); the next t2s_generate([utt], sampler)
+        with this same tuple object decodes from it."""
+        u, keep = self.make_utt(*utt)
+        sp = sampler or make_sampler()
+        _check(lib().gsv_t2s_prefetch(self.h, ctypes.byref(u), ctypes.byref(sp), _stream()), "gsv_t2s_prefetch")
+        # the engine holds a launched prefetch (for the next generate) and a queued one
+        self._pf = (getattr(self, "_pf", []) + [(utt, u, keep)])[-2:]
 
     def t2s_prefill(self, x, prompts, sampler: Optional[Sampler] = None, seq: int = 0):
         t = self.torch

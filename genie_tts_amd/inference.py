@@ -117,8 +117,10 @@ class GENIE:
         reference runs them one after the other: TTSPlayer._tts_worker_loop,
         Core/TTSPlayer.py:56-107).  Engine-backed sessions pipeline them: sentence i's
         vocoder runs on `vocoder_cus` CUs of its own while sentence i+1's T2S runs on
-        the rest (gsv_vits_decode_async), so sentence i is yielded once sentence i+1's
-        T2S is done.  Same tokens and audio as calling tts per sentence."""
+        the rest (gsv_vits_decode_async), and sentence i+1's encoder + prefill run on
+        those CUs during sentence i's decode (gsv_t2s_prefetch), so sentence i is
+        yielded once sentence i+1's T2S is done.  Same tokens and audio as calling
+        tts per sentence."""
         eng = _engine_of(encoder, first_stage_decoder, stage_decoder, vocoder)
         if eng is None or vocoder_cus <= 0 or len(texts) < 2:
             for t in texts:
@@ -132,19 +134,27 @@ class GENIE:
         else:
             prompt_audio.update_global_emb(prompt_encoder)
             cond = {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced}
-        pending = None
+        # every sentence's inputs up front: sentence i+1 is prefetched (encoded and
+        # prefilled on the vocoder CUs) while sentence i decodes
+        seqs = []
         for t in texts:
-            if self.stop_event.is_set():
-                break
             if isinstance(t, str):
                 if g2p is None:
                     raise ValueError("text input needs a g2p(text, language) callable (G2P is outside this engine)")
-                text_seq, tb = g2p("。" + t, language)
+                seqs.append(g2p("。" + t, language))
             else:
-                text_seq = np.asarray(t, np.int64).reshape(1, -1)
-                tb = text_bert if text_bert is not None else np.zeros((text_seq.shape[1], 1024), np.float32)
-            sem = self.t2s(prompt_audio.phonemes_seq, prompt_audio.text_bert, text_seq, tb,
-                           prompt_audio.ssl_content, eng, sampler or first_stage_decoder.sampler)
+                ts = np.asarray(t, np.int64).reshape(1, -1)
+                seqs.append((ts, text_bert if text_bert is not None else np.zeros((ts.shape[1], 1024), np.float32)))
+        ssl = np.asarray(prompt_audio.ssl_content, np.float32).reshape(768, -1)
+        utts = [(prompt_audio.phonemes_seq, ts, prompt_audio.text_bert, tb, ssl) for ts, tb in seqs]
+        sp = sampler or first_stage_decoder.sampler
+        pending = None
+        for i, (text_seq, _) in enumerate(seqs):
+            if self.stop_event.is_set():
+                break
+            if i + 1 < len(utts):
+                eng.t2s_prefetch(utts[i + 1], sp)
+            sem = eng.t2s_generate([utts[i]], sp)[0].reshape(1, 1, -1)
             if pending is not None:
                 eng.vits_wait()
                 yield pending.cpu().numpy()

@@ -18,6 +18,8 @@
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
  *   cn_hubert.run          (ReferenceAudio.py:50-52) gsv_hubert
  *   roberta_model.run      (GetPhonesAndBert.py:73)  gsv_roberta
+ *   per-sentence tts loop  (TTSPlayer.py:56-107)     gsv_t2s_prefetch + gsv_vits_decode_async
+ *                                                    / gsv_vits_wait (option "vocoder_cus")
  *
  * Conventions
  *   - All functions return 0 on success, a negative GSV_E* code on failure;
@@ -173,6 +175,18 @@ int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_item* items
  * other vocoder call or gsv_prompt_encode finishes the pending one first. */
 int gsv_vits_decode_async(gsv_engine* eng, const gsv_vits_item* item, float noise_scale, void* stream);
 int gsv_vits_wait(gsv_engine* eng, void* stream);
+
+/* The T2S side of the same pipeline: encode + prefill the NEXT sentence ahead, on
+ * the vocoder CUs while the current sentence decodes (the reference's per-sentence
+ * encoder + first-stage decoder, Inference.py:63-72, moved off the critical path).
+ * Needs option "vocoder_cus".  Call it for sentence i+1 before gsv_t2s_generate of
+ * sentence i: it is queued and launched (into a spare KV slot, behind a queued
+ * gsv_vits_decode_async call) right after that generate's decode kernel; the next
+ * gsv_t2s_generate with batch 1 and a field-wise equal utt / sampler then decodes
+ * from it (identical tokens).  A batch-1 generate of another utterance keeps a
+ * queued prefetch; a batch generate or any other T2S call discards it.  The utt's
+ * buffers must stay valid until the generate that uses it. */
+int gsv_t2s_prefetch(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* sampler, void* stream);
 
 /* prompt_encoder_fp32.onnx (V2ProPlus): ref_audio (device [n_audio]),
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */

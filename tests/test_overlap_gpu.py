@@ -91,3 +91,49 @@ def test_sync_vocoder_finishes_a_pending_call(eng):
             assert rms <= 1e-4, rms
     finally:
         eng.set_vocoder_cus(0)
+
+
+@pytest.mark.parametrize("greedy", [True, False])
+def test_prefetch_stream_matches_plain_generate(eng, greedy):
+    """gsv_t2s_prefetch: sentence i+1 encoded and prefilled into slot 1 on the
+    vocoder CUs while sentence i decodes, then taken into slot 0 -- every token
+    identical to a plain generate of the same sentence, greedy and top-k sampled
+    (the prefill draws slot 0's Philox noise), with BERT features and ragged
+    lengths (the slot copy moves exactly the prefilled rows)."""
+    from tests.common import t2s_inputs
+    from genie_tts_amd.engine import make_sampler
+    sp = make_sampler(top_k=15, greedy=greedy, seed=77, force_steps=24)
+    utts = [t2s_inputs(R=10 + 3 * i, S=8 + 5 * i, H=30 + 12 * i, tag=f"pf{i}", bert=i % 2 == 1) for i in range(4)]
+    eng.set_vocoder_cus(0)
+    plain = [eng.t2s_generate([u], sp)[0] for u in utts]
+    plain_batch = eng.t2s_generate(utts[:2], sp)
+    t0 = eng.counter("persist_timeouts")
+    eng.set_vocoder_cus(64)
+    try:
+        dev = [tuple(eng._dev(a, None) if a is not None else None for a in u) for u in utts]
+        got = []
+        for i in range(len(dev)):
+            if i + 1 < len(dev):
+                eng.t2s_prefetch(dev[i + 1], sp)
+            got.append(eng.t2s_generate([dev[i]], sp)[0])
+        for i, (a, b) in enumerate(zip(got, plain)):
+            assert a.tolist() == b.tolist(), f"utterance {i}"
+        assert eng.counter("persist_timeouts") == t0
+        # a different utterance than the one prefetched: the plain path, still exact
+        eng.t2s_prefetch(dev[1], sp)
+        assert eng.t2s_generate([dev[2]], sp)[0].tolist() == plain[2].tolist()
+        assert eng.t2s_generate([dev[3]], sp)[0].tolist() == plain[3].tolist()
+        # a batch after a queued prefetch discards it
+        eng.t2s_prefetch(dev[0], sp)
+        out = eng.t2s_generate([dev[0], dev[1]], sp)
+        assert [o.tolist() for o in out] == [o.tolist() for o in plain_batch]
+    finally:
+        eng.set_vocoder_cus(0)
+
+
+def test_prefetch_needs_the_split(eng):
+    from tests.common import t2s_inputs
+    from genie_tts_amd.engine import EngineError
+    eng.set_vocoder_cus(0)
+    with pytest.raises(EngineError, match="vocoder_cus"):
+        eng.t2s_prefetch(t2s_inputs(tag="pfx"))
