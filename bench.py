@@ -150,7 +150,7 @@ class Runner:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("single", "batch64", "mixed100"), default="single")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -68,6 +68,7 @@ gsv_engine::~gsv_engine() {
     if (hubert.ws) hipFree(hubert.ws);
     if (bert.ws) hipFree(bert.ws);
     if (perr_host) hipHostFree(perr_host);
+    if (res_pin) hipHostFree(res_pin);
     if (vovf_host) hipHostFree(vovf_host);
     if (vovf) hipFree(vovf);
     for (auto& L : vlanes) {
@@ -879,6 +880,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
+    if (res_batch) enqueue_results(res_batch, st);   // valid if this launch succeeds (checked below)
     // a queued overlapped vocoder call and T2S prefetch: enqueue them now (vocoder
     // CUs, in that order), while the GPU decodes
     if (int r = vits_launch_queued()) return r;
@@ -902,6 +904,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     }
     if (*perr_host != 0)
         return set_error(GSV_E_HIP, "persistent decode failed (code " + std::to_string(*perr_host) + ")");
+    res_ready = res_batch > 0;
     if (probe) {
         float ms = 0.f;
         const hipError_t e = hipEventElapsedTime(&ms, kev[0], kev[1]);
@@ -1011,6 +1014,27 @@ void gsv_engine::pf_take(hipStream_t st) {
     hipEventRecord(pf_copied, st);
     pf_copied_valid = true;
     pf_pending = false;
+}
+
+// ============================================================ generate results
+int gsv_engine::ensure_res_pin(int batch) {
+    const size_t need = (size_t)batch * 8 + (size_t)batch * tmax * 8;
+    if (need <= res_pin_bytes) return 0;
+    if (res_pin) hipHostFree(res_pin);
+    res_pin = nullptr;
+    res_pin_bytes = 0;
+    if (hipHostMalloc((void**)&res_pin, need, hipHostMallocDefault) != hipSuccess)
+        return set_error(GSV_E_HIP, "pinned result buffer");
+    res_pin_bytes = need;
+    return 0;
+}
+
+// [ny: batch int][steps: batch int][y: batch x tmax int64] -> res_pin
+void gsv_engine::enqueue_results(int batch, hipStream_t st) {
+    int* h = reinterpret_cast<int*>(res_pin);
+    hipMemcpyAsync(h, ny, (size_t)batch * 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(h + batch, steps, (size_t)batch * 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(res_pin + (size_t)batch * 8, y, (size_t)batch * tmax * 8, hipMemcpyDeviceToHost, st);
 }
 
 // ============================================================ C ABI
@@ -1226,17 +1250,24 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     }
     }
     if (eng->timing) hipEventRecord(eng->ev[2], st);
+    if (int e = eng->ensure_res_pin(batch)) return e;
+    eng->res_batch = batch;
+    eng->res_ready = false;
     const int rc = eng->decode_loop(batch, &sp, st);
+    eng->res_batch = 0;
     eng->loop_limit = 0;
     if (rc) return rc;
     if (eng->timing) hipEventRecord(eng->ev[3], st);
     // trim on host (Inference.py:108-109, then :41-44)
-    std::vector<int> hny(batch), hsteps(batch);
-    hipMemcpyAsync(hny.data(), eng->ny, batch * 4, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(hsteps.data(), eng->steps, batch * 4, hipMemcpyDeviceToHost, st);
-    std::vector<int64_t> hy((size_t)batch * eng->tmax);
-    hipMemcpyAsync(hy.data(), eng->y, hy.size() * 8, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "generate sync");
+    if (!eng->res_ready) {   // not already copied behind a successful persistent launch
+        eng->enqueue_results(batch, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "generate sync");
+    } else if (eng->timing && hipEventSynchronize(eng->ev[3]) != hipSuccess) {
+        return set_error(GSV_E_HIP, "generate sync");
+    }
+    const int* hny = reinterpret_cast<const int*>(eng->res_pin);
+    const int* hsteps = hny + batch;
+    int64_t* hy = reinterpret_cast<int64_t*>(eng->res_pin + (size_t)batch * 8);
     if (eng->timing) {   // a prefetched utterance: its encode / prefill phases ran on the vocoder CUs
         hipEventElapsedTime(&eng->ms[0], hit ? eng->pf_ev[0] : eng->ev[0], hit ? eng->pf_ev[1] : eng->ev[1]);
         hipEventElapsedTime(&eng->ms[1], hit ? eng->pf_ev[1] : eng->ev[1], hit ? eng->pf_ev[2] : eng->ev[2]);
@@ -1244,7 +1275,7 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     }
     for (int b = 0; b < batch; ++b) {
         const int n = hny[b];
-        int64_t* yy = hy.data() + (size_t)b * eng->tmax;
+        int64_t* yy = hy + (size_t)b * eng->tmax;
         yy[n - 1] = 0;
         const int idx = hsteps[b] - 1;
         int start = idx > 0 ? n - idx : 0;      // y[:, -idx:] ; idx == 0 -> whole y

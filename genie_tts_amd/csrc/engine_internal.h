@@ -184,6 +184,14 @@ struct gsv_engine {
     unsigned long long persist_spin_ticks = 300000000ull;   // option "persist_spin_ticks" (test hook)
     int decode_persistent(int B, const gsv_sampler* sp, hipStream_t st);
     int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one);
+    // generate's results (ny, steps, y rows) -> pinned host memory, enqueued by the
+    // persistent decode before its own sync (one host round trip per generate)
+    char* res_pin = nullptr;
+    size_t res_pin_bytes = 0;
+    int res_batch = 0;                 // > 0: decode_persistent_as enqueues the copies
+    bool res_ready = false;            // they were enqueued behind the final decode and synced
+    int ensure_res_pin(int batch);
+    void enqueue_results(int batch, hipStream_t st);
     long persist1_f16_reruns = 0;      // single-sequence launches re-run on the general kernel (fp16 range)
     int persist1_f16_limit = 0;
     int persist1_pf_delay = 0;         // GENIE_PF_DELAY: s_sleep(32) ticks before the next-layer prefetch
