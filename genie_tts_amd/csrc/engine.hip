@@ -187,6 +187,47 @@ int gsv_engine::finalize_t2s() {
         L.n2b = up_f32(p + "norm2.bias", &err);
     }
     if (err) return err;
+    // LayerNorm affine folded through the GEMV that consumes it (PersistArgs::fold), in
+    // double from the staged fp16-valued weights
+    {
+        constexpr size_t FL = 2 * 1536 + 2 * 2048;
+        std::vector<float> fold(24 * FL, 0.f);
+        auto fw = [&](const std::string& n) { return find(n); };
+        for (int l = 0; l < 24; ++l) {
+            const std::string p = "transformer_encoder.layers." + std::to_string(l) + ".";
+            const std::string q = "transformer_encoder.layers." + std::to_string(l - 1) + ".";
+            const Staged *win = fw(p + "self_attn.in_proj_weight"), *bin = fw(p + "self_attn.in_proj_bias");
+            const Staged *w1 = fw(p + "linear1.weight"), *b1 = fw(p + "linear1.bias");
+            const Staged *n1w = fw(p + "norm1.weight"), *n1b = fw(p + "norm1.bias");
+            const Staged* n2w = l > 0 ? fw(q + "norm2.weight") : nullptr;
+            const Staged* n2b = l > 0 ? fw(q + "norm2.bias") : nullptr;
+            float* F = fold.data() + l * FL;
+            for (int r = 0; r < 1536; ++r) {
+                double sb = 0.0, sc = 0.0;
+                if (l > 0)
+                    for (int k = 0; k < 512; ++k) {
+                        const double wv = win->data[(size_t)r * 512 + k];
+                        sb += wv * n2w->data[k];
+                        sc += wv * n2b->data[k];
+                    }
+                F[r] = (float)sb;
+                F[1536 + r] = (float)(sc + bin->data[r]);
+            }
+            for (int r = 0; r < 2048; ++r) {
+                double sb = 0.0, sc = 0.0;
+                for (int k = 0; k < 512; ++k) {
+                    const double wv = w1->data[(size_t)r * 512 + k];
+                    sb += wv * n1w->data[k];
+                    sc += wv * n1b->data[k];
+                }
+                F[3072 + r] = (float)sb;
+                F[5120 + r] = (float)(sc + b1->data[r]);
+            }
+        }
+        ln_fold = (float*)dalloc(fold.size() * 4);
+        if (!ln_fold) return set_error(GSV_E_HIP, "LayerNorm fold");
+        hipMemcpy(ln_fold, fold.data(), fold.size() * 4, hipMemcpyHostToDevice);
+    }
     hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
     text_emb = up_f32("encoder.ar_text_embedding.word_embeddings.weight", &err);
     bert_w = up_f32("encoder.bert_proj.weight", &err);
@@ -869,6 +910,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.trace = ptrace;
     a.pf_delay = persist1_pf_delay;
     for (int i = 0; i < 4; ++i) a.knob[i] = persist1_knob[i];
+    a.fold = ln_fold;
     a.spin_ticks = persist_spin_ticks;
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     hipMemsetAsync(perr, 0, 4, st);

@@ -75,6 +75,7 @@ struct gsv_engine {
     float *text_emb = nullptr, *bert_w = nullptr, *bert_b = nullptr, *alpha_text = nullptr;
     float *ssl_w = nullptr, *ssl_b = nullptr, *codebook = nullptr, *cb_sumsq = nullptr;
     float* pe_tab = nullptr;
+    float* ln_fold = nullptr;         // PersistArgs::fold (the LayerNorm affine folded through W_in / W1)
     int pe_max = 0;
     float qk_scale = 0.f;
 

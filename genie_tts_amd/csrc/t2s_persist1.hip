@@ -55,6 +55,7 @@ constexpr int RING1 = 4;           // granule ring depth (steps)
 constexpr int LOGIT_GRP = 1;       // FFN workgroups of this group compute the logits
 constexpr int SAMPLER_GRP = 2;     // head-0 attention workgroup of this group samples
 constexpr int LROWS = 64;          // logits rows per FFN workgroup (16 x 64 = 1024, + EOS row)
+constexpr long FOLD_LAYER = 2 * 1536 + 2 * 2048;   // PersistArgs::fold floats per layer
 
 // Granule ring.  Per step slot: PA [24][16][512], PFH [24][17][512] (rows 0..15 FFN2
 // partials, row 16 = h1), LG [PERSIST_LGS], TK [16].
@@ -81,7 +82,6 @@ struct Shared1 {
     float qkv[96];
     _Float16 osh[PWV][32], osl[PWV][32];   // MFMA row operand: head output split hi + lo (out-projection),
                                            // one copy per wave (each wave merges the head itself)
-    float b1[128];                  // FFN1 bias of the slice
     float lnb[2][512];              // LayerNorm inputs: [0] x_l (form_x), [1] LN1 (FFN)
     _Float16 xh[512], xl[512];      // MFMA row operand: h1 split hi + lo (FFN1)
     _Float16 fh[128], fl[128];      // MFMA row operand: FFN1 output split hi + lo (FFN2)
@@ -455,8 +455,44 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
     return true;
 }
 
+// The attention role's x_l without waiting for its LayerNorm statistics: u = the
+// LN2_{l-1} INPUT (l = 0: x_0 itself) -> sh.lnb[0], and the MFMA operand split of
+// u * n2w (l = 0: u) -> sh.xh / sh.xl, then the block barrier.  The q/k/v GEMV
+// runs on that operand while the statistics are formed: with x = (u - mean) rden
+// n2w + n2b,  W x + b = rden (W (u n2w) - mean W n2w) + (W n2b + b), the two
+// constant vectors folded per layer at load time (PersistArgs::fold).
+__device__ __forceinline__ bool form_u(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, const float* lp2,
+                                       Shared1& sh) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    float u, un;
+    if (l == 0) {
+        u = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
+        un = u;
+    } else {
+        const unsigned tag = ws.tag(s);
+        if (l >= 2) {
+            if (tid == 0) wait_tag_slow(ws.PFH(s, l - 2, 0), tag, a.err, ok, a.spin_ticks);
+            if (!block_ok1(ok, sh)) return false;
+        }
+        float g[17];
+        wait_gran_n<17>(ws.PFH(s, l - 1, 0) + tid, 512, tag, g, a.err, ok, a.spin_ticks);
+        float f = g[0];
+#pragma unroll
+        for (int j = 1; j < NF; ++j) f += g[j];
+        u = g[16] + (lp2[tid] + f);
+        un = u * lp2[512 + tid];
+    }
+    sh.lnb[0][tid] = u;
+    if (!split_h(un, sh.xh[tid], sh.xl[tid]) || !(fabsf(un) < a.f16_limit)) {
+        atomicCAS(a.err, 0, ERR_F16_RANGE);
+        ok = false;
+    }
+    return block_ok1(ok, sh);
+}
+
 // --------------------------------------------------------------------------
-// Attention workgroup: head h of layers grp, grp + 8, grp + 16.
+// Attention workgroup: head h of layers grp, grp + G, grp + 2G, ...
 // --------------------------------------------------------------------------
 __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int grp, int h) {
     const int tid = threadIdx.x, lane = tid & 63, ng = a.groups;
@@ -471,7 +507,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
     if (sampler && tid < 33) sh.seen[tid] = a.seen[tid];
     const long kvoff = (long)h * a.tmax * 32;
     uint4 wq[16], wo[4];
-    float bqv = 0.f;
+    float qfB = 0.f, qfC = 0.f;   // folded LN2 vectors of this lane's q/k/v row
     auto prefetch = [&](int l, int kv) {
         const PLayer& P = a.L[l];
         // MFMA B fragments (lane: column lane & 15, k 8 (lane >> 4) .. + 8 of each 32-chunk).
@@ -481,7 +517,8 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             const int row = (w >> 1) * 512 + h * 32 + 16 * (w & 1) + n16;
 #pragma unroll
             for (int c = 0; c < 16; ++c) wq[c] = ldg16(P.w_in + (long)row * 512 + 32 * c + k8, 0);
-            bqv = ldg(P.b_in, row);
+            qfB = ldg(a.fold, (long)l * FOLD_LAYER + row);
+            qfC = ldg(a.fold, (long)l * FOLD_LAYER + 1536 + row);
         }
         // out-projection: wave w -> output columns 64 w + 16 t + (lane & 15), K = the head's 32 dims
 #pragma unroll
@@ -508,12 +545,10 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         for (int l = grp; l < 24; l += ng) {
             const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
             STAMP1(0);
-            float xv;
-            if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
-            split_h(xv, sh.xh[tid], sh.xl[tid]);   // LayerNorm output: always in fp16 range
-            __syncthreads();
+            if (!form_u(a, ws, s, l, ny0 + s, &sh.p2[0][0], sh)) return;
             STAMP1(1);
-            // ---- q, k, v of head h on the MFMA: wave w < 6 -> 16 rows (C row 0 + row 1)
+            // ---- q, k, v of head h on the MFMA: wave w < 6 -> 16 rows (C row 0 + row 1),
+            // the LN2 statistics formed while the MFMAs run
             if (w < 6) {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
@@ -528,7 +563,11 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                         c1 = mfma16(af[i + 1], bfrag(wq[cb + i + 1]), c1);
                     }
                 }
-                if (lane < 16) sh.qkv[16 * w + lane] = bqv + ((c0[0] + c1[0]) + (c0[1] + c1[1]));
+                float mean, rden;
+                ln_row_stats(sh.lnb[0], mean, rden);
+                mean = l > 0 ? mean : 0.f;   // layer 0: x_0 is not a LayerNorm output
+                rden = l > 0 ? rden : 1.f;
+                if (lane < 16) sh.qkv[16 * w + lane] = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * qfB) + qfC;
             }
             STAMP1(6);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
@@ -652,7 +691,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
     }
     uint4 w1r[16], w2r[16];
     float bo = 0.f, n1w = 0.f, n1b = 0.f;    // out-proj bias and LN1 of layer l
-    float b1v = 0.f;                         // FFN1 bias of hidden unit 128 j + tid (tid < 128)
+    float ffB = 0.f, ffC = 0.f;              // folded LN1 vectors of this lane's FFN1 row
     auto prefetch = [&](int l) {
         const PLayer& P = a.L[l];
         // MFMA B fragments (lane: column lane & 15, k 8 (lane >> 4) .. + 8 of each 32-chunk)
@@ -666,7 +705,8 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + n16) * 2048 + j * 128 + 32 * c + k8, 0);
-        b1v = tid < 128 ? ldg(P.b1, j * 128 + tid) : 0.f;
+        ffB = ldg(a.fold, (long)l * FOLD_LAYER + 3072 + j * 128 + w * 16 + n16);
+        ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + j * 128 + w * 16 + n16);
         bo = ldg(P.b_out, tid); n1w = ldg(P.n1w, tid); n1b = ldg(P.n1b, tid);
         if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
     };
@@ -683,7 +723,11 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
             STAMP1(1);
             float h1_pub = 0.f;
-            // ---- h1_l = LN1(x_l + (bo + sum_h PA[l][h])), heads summed in order
+            // ---- v = x_l + (bo + sum_h PA[l][h]) (heads summed in order) -> lnb[1], and the
+            // MFMA operand split of v * n1w: FFN1 runs on it while the LN1 statistics are
+            // formed (W1 h1 + b1 = rden (W1 (v n1w) - mean W1 n1w) + (W1 n1b + b1), the
+            // constant vectors folded at load time, as form_u)
+            float v;
             {
                 bool ok = true;
                 float pa[16];
@@ -691,19 +735,16 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 float sum = pa[0];
 #pragma unroll
                 for (int hh = 1; hh < 16; ++hh) sum += pa[hh];
-                const float v = xv + (bo + sum);
+                v = xv + (bo + sum);
                 sh.lnb[1][tid] = v;
-                if (tid < 128) sh.b1[tid] = b1v;
+                const float un = v * n1w;
+                if (!split_h(un, sh.xh[tid], sh.xl[tid]) || !(fabsf(un) < a.f16_limit)) {
+                    atomicCAS(a.err, 0, ERR_F16_RANGE);
+                    ok = false;
+                }
                 if (!block_ok1(ok, sh)) return;
-                STAMP1(2);
-                float mean, rden;
-                ln_row_stats(sh.lnb[1], mean, rden);
-                const float h1 = (v - mean) * rden * n1w + n1b;
-                h1_pub = h1;   // published with the FFN2 partials: no store in flight during FFN1/FFN2
-                split_h(h1, sh.xh[tid], sh.xl[tid]);   // LayerNorm output: always in fp16 range
             }
-            __syncthreads();
-            STAMP1(6);
+            STAMP1(2);
             // ---- FFN1 rows of this slice on the MFMA (16 per wave), ReLU -> fh/fl
             {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
@@ -719,8 +760,11 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                         c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
                     }
                 }
+                float mean, rden;
+                ln_row_stats(sh.lnb[1], mean, rden);
+                h1_pub = (v - mean) * rden * n1w + n1b;   // h1_l, published with the FFN2 partials
                 if (lane < 16) {
-                    const float f = fmaxf(sh.b1[w * 16 + lane] + ((c0[0] + c1[0]) + (c0[1] + c1[1])), 0.f);
+                    const float f = fmaxf(rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * ffB) + ffC, 0.f);
                     split_h(f, sh.fh[w * 16 + lane], sh.fl[w * 16 + lane]);
                     if (!(fabsf(f) < a.f16_limit)) {
                         atomicCAS(a.err, 0, ERR_F16_RANGE);
@@ -728,6 +772,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                     }
                 }
             }
+            STAMP1(6);
             __syncthreads();
             if (sh.fail) return;
             STAMP1(3);
