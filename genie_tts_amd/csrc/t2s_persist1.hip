@@ -179,6 +179,7 @@ __device__ __forceinline__ bool split_h(float v, _Float16& hi, _Float16& lo) {
 }
 constexpr int ERR_F16_RANGE = 2;   // error word: an activation left the fp16 range (host re-runs)
 
+
 // Scores of the general case (more than 512 keys or rows beyond the LDS stage),
 // out of line so the common path keeps its registers.  Returns the lane's max.
 __device__ __noinline__ float scores_general1(Shared1& sh, const float* Kw, int kv, int T, float q0, float q1,
@@ -551,6 +552,8 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             // the LN2 statistics formed while the MFMAs run
             if (w < 6) {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                float mean, rden;
+                ln_row_stats(sh.lnb[0], mean, rden);   // first: interleaved with the MFMAs below
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
@@ -563,8 +566,6 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                         c1 = mfma16(af[i + 1], bfrag(wq[cb + i + 1]), c1);
                     }
                 }
-                float mean, rden;
-                ln_row_stats(sh.lnb[0], mean, rden);
                 mean = l > 0 ? mean : 0.f;   // layer 0: x_0 is not a LayerNorm output
                 rden = l > 0 ? rden : 1.f;
                 if (lane < 16) sh.qkv[16 * w + lane] = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * qfB) + qfC;
@@ -745,9 +746,14 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 if (!block_ok1(ok, sh)) return;
             }
             STAMP1(2);
-            // ---- FFN1 rows of this slice on the MFMA (16 per wave), ReLU -> fh/fl
+            // ---- FFN1 rows of this slice on the MFMA (16 per wave), ReLU -> fh/fl.  The LN1
+            // statistics come first in program order so the scheduler interleaves their
+            // VALU work with the MFMAs (two waves per SIMD share its matrix pipe: the
+            // MFMAs set the pace, the VALU slots are free)
             {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                float mean, rden;
+                ln_row_stats(sh.lnb[1], mean, rden);
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
@@ -760,8 +766,6 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                         c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
                     }
                 }
-                float mean, rden;
-                ln_row_stats(sh.lnb[1], mean, rden);
                 h1_pub = (v - mean) * rden * n1w + n1b;   // h1_l, published with the FFN2 partials
                 if (lane < 16) {
                     const float f = fmaxf(rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * ffB) + ffC, 0.f);
