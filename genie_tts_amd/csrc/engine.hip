@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <map>
 #include <memory>
 #include <string>
@@ -913,7 +914,8 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.fold = ln_fold;
     a.spin_ticks = persist_spin_ticks;
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
-    hipMemsetAsync(perr, 0, 4, st);
+    if (!perr_zeroed) hipMemsetAsync(perr, 0, 4, st);   // (a prefetched slot's copy launch zeroes it)
+    perr_zeroed = false;
     const bool probe = timing && kev[0] != nullptr;
     // a queued prefetch starts once this stream's prefill (same workspaces) is done
     if (pf_queued && !pf_pending) hipEventRecord(pf_fork, st);
@@ -927,7 +929,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     // CUs, in that order), while the GPU decodes
     if (int r = vits_launch_queued()) return r;
     if (int r = pf_launch_queued()) return r;
-    if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
+    if (host_wait(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
     // code 2: the single-sequence kernel met an activation beyond the fp16 range of
     // its split-operand MFMA GEMVs.  It stopped before writing the sequence state
     // back (KV rows and tokens of the partial run are rewritten), so the same
@@ -978,6 +980,9 @@ struct SlotCopyArgs {
     int *ny, *kvlen, *steps;
     uint8_t* done;
     uint32_t* seen;
+    int* forceb;
+    int force0;
+    int* err;
 };
 // block (head h, layer l, k|v): rows [0, n0) of the head, contiguous n0 x 32 floats
 __global__ __launch_bounds__(256) void k_slot_copy(SlotCopyArgs a) {
@@ -994,6 +999,8 @@ __global__ __launch_bounds__(256) void k_slot_copy(SlotCopyArgs a) {
             a.kvlen[0] = a.kvlen[1];
             a.steps[0] = a.steps[1];
             a.done[0] = a.done[1];
+            a.forceb[0] = a.force0;
+            if (a.err) a.err[0] = 0;
         }
     }
 }
@@ -1046,16 +1053,35 @@ int gsv_engine::pf_drop(bool keep_queued) {
     return hipEventSynchronize(pf_done) == hipSuccess ? 0 : set_error(GSV_E_HIP, "T2S prefetch");
 }
 
-void gsv_engine::pf_take(hipStream_t st) {
+// Also sets slot 0's forced step count and zeroes the decode error word (two
+// stream operations fewer before the decode launch).
+void gsv_engine::pf_take(hipStream_t st, int force0) {
     hipStreamWaitEvent(st, pf_done, 0);
+    if (!perr && hipMalloc((void**)&perr, 64) != hipSuccess) perr = nullptr;
     SlotCopyArgs a{};
     for (int l = 0; l < 24; ++l) { a.kc[l] = kcache[l]; a.vc[l] = vcache[l]; }
     a.sstride = (long)16 * tmax * 32; a.tmax = tmax; a.n0 = pf_p.n0;
     a.y = y; a.ny = ny; a.kvlen = kvlen; a.steps = steps; a.done = done; a.seen = seen;
+    a.forceb = forceb; a.force0 = force0; a.err = perr;
+    perr_zeroed = perr != nullptr;
     hipLaunchKernelGGL(k_slot_copy, dim3(16, 24, 2), dim3(256), 0, st, a);
     hipEventRecord(pf_copied, st);
     pf_copied_valid = true;
     pf_pending = false;
+}
+
+// ============================================================ host wait
+// The host thread waits for a decode by polling the stream (and yielding) rather
+// than sleeping in hipStreamSynchronize: the wake-up after a blocking sync costs
+// tens of microseconds per utterance (option "spin_wait", default on).
+hipError_t gsv_engine::host_wait(hipStream_t st) {
+    if (!spin_wait) return hipStreamSynchronize(st);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return hipSuccess;
+        if (e != hipErrorNotReady) return e;
+        std::this_thread::yield();
+    }
 }
 
 // ============================================================ generate results
@@ -1272,10 +1298,10 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (int e = eng->reserve(batch, need)) return e;
     StreamScope sc(eng, stream);
     hipStream_t st = sc.st();
-    hipMemcpyAsync(eng->forceb, hforce.data(), batch * 4, hipMemcpyHostToDevice, st);
+    if (!hit) hipMemcpyAsync(eng->forceb, hforce.data(), batch * 4, hipMemcpyHostToDevice, st);
     eng->loop_limit = limit;
     if (hit) {   // encoded and prefilled ahead (gsv_t2s_prefetch): slot 1 -> slot 0
-        eng->pf_take(st);
+        eng->pf_take(st, hforce[0]);
     } else {
     if (eng->timing) hipEventRecord(eng->ev[0], st);
     hipMemsetAsync(eng->done, 1, eng->max_batch, st);
@@ -1297,6 +1323,7 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     eng->res_ready = false;
     const int rc = eng->decode_loop(batch, &sp, st);
     eng->res_batch = 0;
+    eng->perr_zeroed = false;
     eng->loop_limit = 0;
     if (rc) return rc;
     if (eng->timing) hipEventRecord(eng->ev[3], st);
@@ -1434,6 +1461,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->persist1_pf_delay = std::max(0, value);
     } else if (n.size() == 5 && n.compare(0, 4, "knob") == 0 && n[4] >= '0' && n[4] <= '3') {
         eng->persist1_knob[n[4] - '0'] = value;   // single-sequence decode tuning variant (0 = default)
+    } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)
+        eng->spin_wait = value != 0;
     } else if (n == "vocoder_cus") {   // overlapped vocoder: CUs reserved for gsv_vits_decode_async
         return eng->set_vocoder_cus(value);
     } else if (n == "convh") {

@@ -247,7 +247,10 @@ struct gsv_engine {
     hipEvent_t pf_ev[3] = {};          // timing: encode, prefill, end (vocoder stream)
     int pf_launch_queued();
     int pf_drop(bool keep_queued = false);
-    void pf_take(hipStream_t st);
+    void pf_take(hipStream_t st, int force0);
+    bool perr_zeroed = false;          // the next persistent launch's error word was zeroed by pf_take
+    bool spin_wait = true;             // option "spin_wait"
+    hipError_t host_wait(hipStream_t st);
     int prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                       float* ge_adv, hipStream_t st);
 };
