@@ -94,27 +94,31 @@ class Runner:
         self.eng.set_option("persist", 1)
         self.phase = {"t2s": 0.0, "vits": 0.0, "encode+prefill": 0.0, "decode": 0.0}
 
-    def step_overlap(self):
-        """One utterance with its vocoder overlapped on its own CUs: the T2S of this
-        utterance runs while the previous utterance's vocoder finishes beside it."""
-        t0 = time.perf_counter()
+    def stream(self, n, phase_ms=None):
+        """n utterances as a pipelined stream: utterance i+1's T2S is queued behind
+        utterance i's (gsv_t2s_generate_start / _finish, so the decode CUs never wait
+        for the host), its encoder + prefill run on the vocoder CUs beside utterance
+        i's decode (gsv_t2s_prefetch), and utterance i's vocoder runs there beside
+        utterance i+1's decode (gsv_vits_decode_async)."""
+        eng = self.eng
         if getattr(self, "utt", None) is None:
             self.utt = (self.d_ref, self.d_txt[0], self.d_ref_bert, self.d_bert[0], self.d_ssl,
                         self.items[0].force_steps)
-        # the next utterance of the stream (here the same one again): encoded and
-        # prefilled on the vocoder CUs while this one decodes
-        self.eng.t2s_prefetch(self.utt, self.sp)
-        sems = self.eng.t2s_generate([self.utt], self.sp)
-        t1 = time.perf_counter()
-        tm = self.eng.timing()
-        self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
-        self.phase["decode"] += tm[2] * 1e-3
-        self.finish()                                       # the previous utterance's vocoder
         cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
-        self.pending = self.eng.vits_decode_async(dict(text_seq=self.d_txt[0], pred_semantic=sems[0],
-                                                       noise_seed=self.seed, **cond))
-        self.phase["t2s"] += t1 - t0
-        self.phase["vits"] += time.perf_counter() - t1
+        eng.t2s_prefetch(self.utt, self.sp)   # (the stream's utterances are all the same one here)
+        eng.t2s_generate_start(self.utt, self.sp)
+        sems = None
+        for i in range(n):
+            if i + 1 < n:
+                eng.t2s_prefetch(self.utt, self.sp)
+                eng.t2s_generate_start(self.utt, self.sp)
+            sems = [eng.t2s_generate_finish()]
+            if phase_ms is not None:
+                phase_ms.append(eng.timing())
+            self.finish()                                   # the previous utterance's vocoder
+            self.pending = eng.vits_decode_async(dict(text_seq=self.d_txt[0], pred_semantic=sems[0],
+                                                      noise_seed=self.seed, **cond))
+        self.finish()
         return sems, 1280 * int(sems[0].size)
 
     def finish(self):
@@ -191,11 +195,10 @@ def main():
     overlap = timed_single and args.vocoder_cus > 0
     if overlap:
         run.eng.set_vocoder_cus(args.vocoder_cus)
-    do_step = run.step_overlap if overlap else run.step
-
-    for _ in range(args.warmup):
-        sems, n_samples = do_step()
-    run.finish()
+        sems, n_samples = run.stream(max(1, args.warmup))
+    else:
+        for _ in range(args.warmup):
+            sems, n_samples = run.step()
     torch.cuda.synchronize()
     run.phase = {k: 0.0 for k in run.phase}
     if timed_single:
@@ -206,11 +209,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sems, n_samples = do_step()
-        if timed_single:
-            phase_ms.append(run.eng.timing())
-    run.finish()                                  # the last utterance's vocoder is inside the timed region
+    if overlap:   # the whole stream, fill and drain included (the last vocoder too)
+        sems, n_samples = run.stream(args.steps, phase_ms)
+    else:
+        for _ in range(args.steps):
+            sems, n_samples = run.step()
+            if timed_single:
+                phase_ms.append(run.eng.timing())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:

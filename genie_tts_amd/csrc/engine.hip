@@ -70,6 +70,12 @@ gsv_engine::~gsv_engine() {
     if (bert.ws) hipFree(bert.ws);
     if (perr_host) hipHostFree(perr_host);
     if (res_pin) hipHostFree(res_pin);
+    for (GenSlot& g : gq) {
+        if (g.res) hipHostFree(g.res);
+        if (g.perr_h) hipHostFree(g.perr_h);
+        for (hipEvent_t e : {g.d0, g.done, g.k0, g.k1})
+            if (e) hipEventDestroy(e);
+    }
     if (vovf_host) hipHostFree(vovf_host);
     if (vovf) hipFree(vovf);
     for (auto& L : vlanes) {
@@ -192,7 +198,7 @@ int gsv_engine::finalize_t2s() {
     // double from the staged fp16-valued weights
     {
         constexpr size_t FL = 2 * 1536 + 2 * 2048;
-        std::vector<float> fold(24 * FL, 0.f);
+        std::vector<float> fold(24 * FL + 2 * 1025, 0.f);
         auto fw = [&](const std::string& n) { return find(n); };
         for (int l = 0; l < 24; ++l) {
             const std::string p = "transformer_encoder.layers." + std::to_string(l) + ".";
@@ -223,6 +229,22 @@ int gsv_engine::finalize_t2s() {
                 }
                 F[3072 + r] = (float)sb;
                 F[5120 + r] = (float)(sc + b1->data[r]);
+            }
+        }
+        {   // logits head: LN2 of layer 23 folded through ar_predict_layer (no bias)
+            const Staged* wp = fw("ar_predict_layer.weight");
+            const Staged* n2w = fw("transformer_encoder.layers.23.norm2.weight");
+            const Staged* n2b = fw("transformer_encoder.layers.23.norm2.bias");
+            float* F = fold.data() + 24 * FL;
+            for (int r = 0; r < 1025; ++r) {
+                double sb = 0.0, sc = 0.0;
+                for (int k = 0; k < 512; ++k) {
+                    const double wv = wp->data[(size_t)r * 512 + k];
+                    sb += wv * n2w->data[k];
+                    sc += wv * n2b->data[k];
+                }
+                F[r] = (float)sb;
+                F[1025 + r] = (float)sc;
             }
         }
         ln_fold = (float*)dalloc(fold.size() * 4);
@@ -858,8 +880,13 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
     return decode_persistent_as(B, sp, st, B == 1 && use_persist1 && decode_cus() >= persist1_grid(3));
 }
 
-// one: the single-sequence kernel (t2s_persist1.hip) instead of the general one.
-int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one) {
+// Enqueue one persistent decode launch on st (no host wait): the error word is
+// copied to perr_dst and, when res_dst is given, the results of res_b sequences
+// (enqueue_results layout) behind it; queued vocoder / prefetch work is launched
+// on the vocoder CUs right after the kernel.  one: the single-sequence kernel
+// (t2s_persist1.hip) instead of the general one.
+int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bool one, int* perr_dst,
+                                hipEvent_t k0, hipEvent_t k1, char* res_dst, int res_b) {
     // One launch runs every loop step (t2s_persist.hip).  Hand-offs are tagged
     // granules in a ring; the launch epoch in the tag makes the ring reusable
     // without zeroing (re-zeroed when the epoch wraps or the layout changes).
@@ -884,8 +911,6 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
         pepoch = 1;
     }
     if (!perr && hipMalloc((void**)&perr, 64) != hipSuccess) return set_error(GSV_E_HIP, "error word");
-    if (!perr_host && hipHostMalloc((void**)&perr_host, 64, hipHostMallocDefault) != hipSuccess)
-        return set_error(GSV_E_HIP, "pinned alloc");
     PersistArgs a{};
     a.B = B;
     // layer groups: as many as the engine stream's CUs hold (all of them unless the
@@ -916,19 +941,39 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     a.f16_limit = persist1_f16_limit > 0 ? (float)persist1_f16_limit : 65504.f;
     if (!perr_zeroed) hipMemsetAsync(perr, 0, 4, st);   // (a prefetched slot's copy launch zeroes it)
     perr_zeroed = false;
-    const bool probe = timing && kev[0] != nullptr;
     // a queued prefetch starts once this stream's prefill (same workspaces) is done
     if (pf_queued && !pf_pending) hipEventRecord(pf_fork, st);
-    const hipError_t le = one ? decode_persist1(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr)
-                              : decode_persist(a, st, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr);
+    const hipError_t le = one ? decode_persist1(a, st, k0, k1) : decode_persist(a, st, k0, k1);
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
-    hipMemcpyAsync(perr_host, perr, 4, hipMemcpyDeviceToHost, st);
-    if (res_batch) enqueue_results(res_batch, st);   // valid if this launch succeeds (checked below)
+    hipMemcpyAsync(perr_dst, perr, 4, hipMemcpyDeviceToHost, st);
+    if (res_dst) enqueue_results(res_b, st, res_dst);   // valid if this launch succeeds
     // a queued overlapped vocoder call and T2S prefetch: enqueue them now (vocoder
     // CUs, in that order), while the GPU decodes
     if (int r = vits_launch_queued()) return r;
     if (int r = pf_launch_queued()) return r;
+    return 0;
+}
+
+void gsv_engine::probe_sample(hipEvent_t k0, hipEvent_t k1) {
+    float ms = 0.f;
+    const hipError_t e = hipEventElapsedTime(&ms, k0, k1);
+    if (e == hipSuccess && ms > 0.f) {
+        kern_us_sum += ms * 1000.0;
+        ++kern_n;
+    } else {
+        kern_err = e == hipSuccess ? -1 : (int)e;
+        (void)hipGetLastError();
+    }
+}
+
+int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one) {
+    if (!perr_host && hipHostMalloc((void**)&perr_host, 64, hipHostMallocDefault) != hipSuccess)
+        return set_error(GSV_E_HIP, "pinned alloc");
+    const bool probe = timing && kev[0] != nullptr;
+    if (int r = persist_enqueue(B, sp, st, one, perr_host, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr,
+                                res_batch ? res_pin : nullptr, res_batch))
+        return r;
     if (host_wait(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
     // code 2: the single-sequence kernel met an activation beyond the fp16 range of
     // its split-operand MFMA GEMVs.  It stopped before writing the sequence state
@@ -949,17 +994,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     if (*perr_host != 0)
         return set_error(GSV_E_HIP, "persistent decode failed (code " + std::to_string(*perr_host) + ")");
     res_ready = res_batch > 0;
-    if (probe) {
-        float ms = 0.f;
-        const hipError_t e = hipEventElapsedTime(&ms, kev[0], kev[1]);
-        if (e == hipSuccess && ms > 0.f) {
-            kern_us_sum += ms * 1000.0;
-            ++kern_n;
-        } else {
-            kern_err = e == hipSuccess ? -1 : (int)e;
-            (void)hipGetLastError();
-        }
-    }
+    if (probe) probe_sample(kev[0], kev[1]);
     return 0;
 }
 
@@ -1089,6 +1124,12 @@ int gsv_engine::ensure_res_pin(int batch) {
     const size_t need = (size_t)batch * 8 + (size_t)batch * tmax * 8;
     if (need <= res_pin_bytes) return 0;
     if (res_pin) hipHostFree(res_pin);
+    for (GenSlot& g : gq) {
+        if (g.res) hipHostFree(g.res);
+        if (g.perr_h) hipHostFree(g.perr_h);
+        for (hipEvent_t e : {g.d0, g.done, g.k0, g.k1})
+            if (e) hipEventDestroy(e);
+    }
     res_pin = nullptr;
     res_pin_bytes = 0;
     if (hipHostMalloc((void**)&res_pin, need, hipHostMallocDefault) != hipSuccess)
@@ -1097,12 +1138,34 @@ int gsv_engine::ensure_res_pin(int batch) {
     return 0;
 }
 
-// [ny: batch int][steps: batch int][y: batch x tmax int64] -> res_pin
-void gsv_engine::enqueue_results(int batch, hipStream_t st) {
-    int* h = reinterpret_cast<int*>(res_pin);
+// [ny: batch int][steps: batch int][y: batch x tmax int64] -> dst (pinned)
+void gsv_engine::enqueue_results(int batch, hipStream_t st, char* dst) {
+    int* h = reinterpret_cast<int*>(dst);
     hipMemcpyAsync(h, ny, (size_t)batch * 4, hipMemcpyDeviceToHost, st);
     hipMemcpyAsync(h + batch, steps, (size_t)batch * 4, hipMemcpyDeviceToHost, st);
-    hipMemcpyAsync(res_pin + (size_t)batch * 8, y, (size_t)batch * tmax * 8, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(dst + (size_t)batch * 8, y, (size_t)batch * tmax * 8, hipMemcpyDeviceToHost, st);
+}
+
+// Inference.py:108-109 then :41-44 on the copied results: y[:, -idx:] with the last
+// token zeroed, cut at the first id >= 1024.
+int gsv_engine::trim_results(const char* res, int batch, int64_t* out_tokens, int out_stride, int32_t* out_len) {
+    const int* hny = reinterpret_cast<const int*>(res);
+    const int* hsteps = hny + batch;
+    const int64_t* hy = reinterpret_cast<const int64_t*>(res + (size_t)batch * 8);
+    for (int b = 0; b < batch; ++b) {
+        const int n = hny[b];
+        const int64_t* yy = hy + (size_t)b * tmax;
+        const int idx = hsteps[b] - 1;
+        const int start = idx > 0 ? n - idx : 0;      // y[:, -idx:] ; idx == 0 -> whole y
+        int cnt = n - start;
+        for (int i = 0; i < cnt; ++i)
+            if ((start + i == n - 1 ? 0 : yy[start + i]) >= 1024) { cnt = i; break; }
+        if (cnt > out_stride) return set_error(GSV_E_CAPACITY, "out_stride too small");
+        std::memcpy(out_tokens + (size_t)b * out_stride, yy + start, (size_t)cnt * 8);
+        if (cnt > 0 && start + cnt == n) out_tokens[(size_t)b * out_stride + cnt - 1] = 0;   // y[0, -1] = 0
+        out_len[b] = cnt;
+    }
+    return 0;
 }
 
 // ============================================================ C ABI
@@ -1184,6 +1247,7 @@ extern "C" int gsv_finalize_weights(gsv_engine* eng) {
 extern "C" int gsv_reserve(gsv_engine* eng, int max_batch, int max_tokens) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->gen_drain()) return e;   // started generates finish first (results stay queued)
     if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     return eng->reserve(max_batch, max_tokens);
@@ -1196,6 +1260,7 @@ extern "C" int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64
     if (!u || !x || !prompts) return set_error(GSV_E_ARG, "null arg");
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     hipSetDevice(eng->device);
+    if (int e = eng->gen_drain()) return e;
     if (int e = eng->pf_drop()) return e;
     StreamScope sc(eng, stream);
     return eng->encode(u, x, prompts, sc.st());
@@ -1206,6 +1271,7 @@ extern "C" int gsv_t2s_prefill(gsv_engine* eng, int seq, const float* x, int32_t
                                int64_t* yout, float* logits_out, void* stream) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->gen_drain()) return e;   // started generates finish first (results stay queued)
     if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_CAPACITY, "slot out of range");
@@ -1224,6 +1290,7 @@ extern "C" int gsv_t2s_decode_steps(gsv_engine* eng, int seq, int nsteps, const 
                                     int64_t* yout, uint8_t* stop, float* logits_out, void* stream) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->gen_drain()) return e;   // started generates finish first (results stay queued)
     if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (seq != 0) return set_error(GSV_E_ARG, "decode_steps supports slot 0");
     StreamScope sc(eng, stream);
@@ -1250,6 +1317,7 @@ extern "C" int gsv_t2s_read_kv(gsv_engine* eng, int seq, int layer, float* k, fl
                                void* stream) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    if (int e = eng->gen_drain()) return e;   // started generates finish first (results stay queued)
     if (int e = eng->pf_drop()) return e;   // a prefetch writes the T2S workspaces and slot 1
     if (layer < 0 || layer >= 24 || seq < 0 || seq >= eng->max_batch) return set_error(GSV_E_ARG, "range");
     StreamScope sc(eng, stream);
@@ -1277,6 +1345,7 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (batch <= 0 || !utts || !out_tokens || !out_len) return set_error(GSV_E_ARG, "bad args");
     gsv_sampler sp;
     if (int e = norm_sampler(s, sp)) return e;
+    if (int e = eng->gen_drain()) return e;   // started generates finish first (results stay queued)
     // prefetched (gsv_t2s_prefetch, launched into slot 1 during the last decode)?  A
     // queued prefetch is for a later call: it stays queued (launched during this
     // decode) unless this is a batch, whose prefill uses slot 1 itself.
@@ -1329,33 +1398,153 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (eng->timing) hipEventRecord(eng->ev[3], st);
     // trim on host (Inference.py:108-109, then :41-44)
     if (!eng->res_ready) {   // not already copied behind a successful persistent launch
-        eng->enqueue_results(batch, st);
+        eng->enqueue_results(batch, st, eng->res_pin);
         if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "generate sync");
     } else if (eng->timing && hipEventSynchronize(eng->ev[3]) != hipSuccess) {
         return set_error(GSV_E_HIP, "generate sync");
     }
-    const int* hny = reinterpret_cast<const int*>(eng->res_pin);
-    const int* hsteps = hny + batch;
-    int64_t* hy = reinterpret_cast<int64_t*>(eng->res_pin + (size_t)batch * 8);
     if (eng->timing) {   // a prefetched utterance: its encode / prefill phases ran on the vocoder CUs
         hipEventElapsedTime(&eng->ms[0], hit ? eng->pf_ev[0] : eng->ev[0], hit ? eng->pf_ev[1] : eng->ev[1]);
         hipEventElapsedTime(&eng->ms[1], hit ? eng->pf_ev[1] : eng->ev[1], hit ? eng->pf_ev[2] : eng->ev[2]);
         hipEventElapsedTime(&eng->ms[2], eng->ev[2], eng->ev[3]);
     }
-    for (int b = 0; b < batch; ++b) {
-        const int n = hny[b];
-        int64_t* yy = hy + (size_t)b * eng->tmax;
-        yy[n - 1] = 0;
-        const int idx = hsteps[b] - 1;
-        int start = idx > 0 ? n - idx : 0;      // y[:, -idx:] ; idx == 0 -> whole y
-        int cnt = n - start;
-        for (int i = 0; i < cnt; ++i)
-            if (yy[start + i] >= 1024) { cnt = i; break; }
-        if (cnt > out_stride) return set_error(GSV_E_CAPACITY, "out_stride too small");
-        std::memcpy(out_tokens + (size_t)b * out_stride, yy + start, (size_t)cnt * 8);
-        out_len[b] = cnt;
+    return eng->trim_results(eng->res_pin, batch, out_tokens, out_stride, out_len);
+}
+
+// ============================================================ asynchronous generate
+int gsv_engine::gen_drain() {
+    if (gq_n == 0) return 0;
+    return hipStreamSynchronize(stream) == hipSuccess ? 0 : set_error(GSV_E_HIP, "generate drain");
+}
+
+int gsv_engine::gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t caller) {
+    if (gq_n == 2) return set_error(GSV_E_STATE, "two generates in flight: finish one first");
+    if (u.force_steps < 0) return set_error(GSV_E_ARG, "negative force_steps");
+    const int L = u.n_ref + u.n_text, P = u.n_ssl / 2;
+    if (L <= 0 || P <= 0) return set_error(GSV_E_ARG, "empty utterance");
+    const int cap = u.force_steps > 0 ? u.force_steps : sp.force_steps > 0 ? sp.force_steps : sp.max_steps;
+    const int need = L + P + cap + 16;
+    const bool hit = pf_pending && same_utt(u, pf_p.u) && same_sampler(sp, pf_p.sp);
+    if (!hit)
+        if (int e = pf_drop(true)) return e;
+    if (need > tmax || max_batch < 1) {   // the KV cache is re-allocated: nothing may be in flight
+        if (int e = gen_drain()) return e;
+        if (int e = pf_drop()) return e;
     }
+    if (int e = reserve(1, need)) return e;
+    GenSlot& g = gq[(gq_head + gq_n) % 2];
+    const size_t rb = 8 + (size_t)tmax * 8;
+    if (g.res_bytes < rb) {
+        if (g.res) hipHostFree(g.res);
+        g.res = nullptr;
+        g.res_bytes = 0;
+        if (hipHostMalloc((void**)&g.res, rb, hipHostMallocDefault) != hipSuccess) return set_error(GSV_E_HIP, "pinned results");
+        g.res_bytes = rb;
+    }
+    if (!g.perr_h) {
+        if (hipHostMalloc((void**)&g.perr_h, 64, hipHostMallocDefault) != hipSuccess) return set_error(GSV_E_HIP, "pinned alloc");
+        for (hipEvent_t* e : {&g.d0, &g.done, &g.k0, &g.k1})
+            if (hipEventCreate(e) != hipSuccess) return set_error(GSV_E_HIP, "generate events");
+    }
+    g.u = u;
+    g.sp = sp;
+    g.hit = hit;
+    g.sync = false;
+    g.sync_rc = 0;
+    hipStream_t st = stream;
+    hipEventRecord(ev_in, caller);   // the caller's inputs are ready here; its stream is NOT made to
+    hipStreamWaitEvent(st, ev_in, 0);   // wait for the engine (gen_finish orders it)
+    loop_limit = cap;
+    if (hit) {
+        pf_take(st, u.force_steps);
+    } else {
+        hipMemsetD32Async(forceb, u.force_steps, 1, st);
+        hipMemsetAsync(done, 1, max_batch, st);
+        if (timing) hipEventRecord(ev[0], st);
+        if (int e = encode(&u, pH, prompts_buf, st)) return e;
+        if (timing) hipEventRecord(ev[1], st);
+        if (int e = prefill_slot(0, pH, L, prompts_buf, P, &sp, nullptr, st)) return e;
+    }
+    hipEventRecord(g.d0, st);
+    const bool persist_ok = use_persist && use_persist1 && decode_cus() >= persist1_grid(3);
+    int rc = 0;
+    if (persist_ok) {
+        rc = persist_enqueue(1, &sp, st, true, g.perr_h, timing ? g.k0 : nullptr, timing ? g.k1 : nullptr, g.res, 1);
+    } else {   // no persistent path: this one runs to completion now
+        res_batch = 1;
+        res_ready = false;
+        rc = decode_loop(1, &sp, st);
+        res_batch = 0;
+        perr_zeroed = false;
+        if (rc == 0) enqueue_results(1, st, g.res);
+        *g.perr_h = 0;
+        g.sync = true;
+        g.sync_rc = rc;
+    }
+    loop_limit = 0;
+    if (rc && !g.sync) return rc;
+    hipEventRecord(g.done, st);
+    ++gq_n;
     return 0;
+}
+
+int gsv_engine::gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len, hipStream_t caller) {
+    if (gq_n == 0) return set_error(GSV_E_STATE, "no generate in flight");
+    GenSlot& g = gq[gq_head];
+    gq_head = (gq_head + 1) % 2;
+    --gq_n;
+    if (g.sync && g.sync_rc) return g.sync_rc;
+    for (;;) {   // poll, as host_wait
+        const hipError_t e = hipEventQuery(g.done);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return set_error(GSV_E_HIP, "generate");
+        if (spin_wait) std::this_thread::yield();
+        else if (hipEventSynchronize(g.done) != hipSuccess) return set_error(GSV_E_HIP, "generate");
+    }
+    if (*g.perr_h != 0) {
+        // the launch met an fp16-range activation (2) or a hand-off timeout (1): the
+        // sequence state was not written back; drain and run this utterance again on
+        // the synchronous path, which handles both (its own prefill, slot 0)
+        if (*g.perr_h == 2) ++persist1_f16_reruns;
+        else if (*g.perr_h == 1) ++persist_timeouts;
+        if (int e = gen_drain()) return e;
+        const int saved_n = gq_n;
+        gq_n = 0;   // the synchronous path must not see the queue
+        const int r = gsv_t2s_generate(this, 1, &g.u, &g.sp, out_tokens, out_stride, out_len, caller);
+        gq_n = saved_n;
+        return r;
+    }
+    if (timing) {
+        if (g.hit) {
+            hipEventElapsedTime(&ms[0], pf_ev[0], pf_ev[1]);
+            hipEventElapsedTime(&ms[1], pf_ev[1], pf_ev[2]);
+        } else {
+            hipEventElapsedTime(&ms[0], ev[0], ev[1]);
+            hipEventElapsedTime(&ms[1], ev[1], g.d0);
+        }
+        hipEventElapsedTime(&ms[2], g.d0, g.done);
+        if (!g.sync) probe_sample(g.k0, g.k1);
+    }
+    if (caller) hipStreamWaitEvent(caller, g.done, 0);
+    return trim_results(g.res, 1, out_tokens, out_stride, out_len);
+}
+
+extern "C" int gsv_t2s_generate_start(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* s, void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    if (!utt) return set_error(GSV_E_ARG, "null utterance");
+    gsv_sampler sp;
+    if (int e = norm_sampler(s, sp)) return e;
+    return eng->gen_start(*utt, sp, (hipStream_t)stream);
+}
+
+extern "C" int gsv_t2s_generate_finish(gsv_engine* eng, int64_t* out_tokens, int32_t out_stride, int32_t* out_len,
+                                       void* stream) {
+    ENG_CHECK(eng);
+    hipSetDevice(eng->device);
+    if (!out_tokens || !out_len) return set_error(GSV_E_ARG, "null output");
+    return eng->gen_finish(out_tokens, out_stride, out_len, (hipStream_t)stream);
 }
 
 extern "C" int gsv_t2s_prefetch(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* s, void* stream) {

@@ -192,7 +192,29 @@ struct gsv_engine {
     int res_batch = 0;                 // > 0: decode_persistent_as enqueues the copies
     bool res_ready = false;            // they were enqueued behind the final decode and synced
     int ensure_res_pin(int batch);
-    void enqueue_results(int batch, hipStream_t st);
+    void enqueue_results(int batch, hipStream_t st, char* dst);
+    int trim_results(const char* res, int batch, int64_t* out_tokens, int out_stride, int32_t* out_len);
+    int persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bool one, int* perr_dst, hipEvent_t k0,
+                        hipEvent_t k1, char* res_dst, int res_b);
+    void probe_sample(hipEvent_t k0, hipEvent_t k1);
+    // asynchronous single-utterance generate (gsv_t2s_generate_start / _finish): up to
+    // two in flight on the engine stream, so the next decode is queued behind the
+    // running one and the GPU never waits for the host between utterances
+    struct GenSlot {
+        gsv_utt u{};
+        gsv_sampler sp{};
+        int* perr_h = nullptr;        // pinned error word of this launch
+        char* res = nullptr;          // pinned results (enqueue_results layout, batch 1)
+        size_t res_bytes = 0;
+        hipEvent_t d0 = nullptr, done = nullptr, k0 = nullptr, k1 = nullptr;
+        bool hit = false, sync = false;
+        int sync_rc = 0;
+    };
+    GenSlot gq[2];
+    int gq_head = 0, gq_n = 0;
+    int gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t caller);
+    int gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len, hipStream_t caller);
+    int gen_drain();                   // wait for every started generate (their results stay queued)
     long persist1_f16_reruns = 0;      // single-sequence launches re-run on the general kernel (fp16 range)
     int persist1_f16_limit = 0;
     int persist1_pf_delay = 0;         // GENIE_PF_DELAY: s_sleep(32) ticks before the next-layer prefetch

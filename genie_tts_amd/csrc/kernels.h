@@ -257,7 +257,8 @@ struct PersistArgs {
                                                   // 0 = the default path)
     const float* fold;                            // single-sequence kernel: per layer [W_in n2w_{l-1} | W_in n2b_{l-1}
                                                   // + b_in | W1 n1w | W1 n1b + b1] (1536, 1536, 2048, 2048 floats;
-                                                  // layer 0: 0 | b_in), so a GEMV can run beside its LayerNorm stats
+                                                  // layer 0: 0 | b_in), so a GEMV can run beside its LayerNorm stats;
+                                                  // then [W_pred n2w_23 | W_pred n2b_23] (1025 each, the logits)
 };
 int persist_groups(int B, int n_cu);   // 0: the grid does not fit
 int persist_grid(int B, int groups);

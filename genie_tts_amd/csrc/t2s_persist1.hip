@@ -56,6 +56,7 @@ constexpr int LOGIT_GRP = 1;       // FFN workgroups of this group compute the l
 constexpr int SAMPLER_GRP = 2;     // head-0 attention workgroup of this group samples
 constexpr int LROWS = 64;          // logits rows per FFN workgroup (16 x 64 = 1024, + EOS row)
 constexpr long FOLD_LAYER = 2 * 1536 + 2 * 2048;   // PersistArgs::fold floats per layer
+constexpr long LOGIT_FOLD = 24 * FOLD_LAYER;        // then [W_pred n2w_23 | W_pred n2b_23] (1025 each)
 
 // Granule ring.  Per step slot: PA [24][16][512], PFH [24][17][512] (rows 0..15 FFN2
 // partials, row 16 = h1), LG [PERSIST_LGS], TK [16].
@@ -94,8 +95,10 @@ struct Shared1 {
     SampleLds<PT> samp;
     union {
         struct {                    // FFN role
-            uint4 wp[LROWS + 1][64];   // logits rows (group LOGIT_GRP), resident for the launch
+            uint4 wp[LROWS + 1][65];   // logits rows (group LOGIT_GRP), resident for the launch (rows
+                                       // padded by 16 B: the MFMA B reads of 16 rows are conflict-free)
             float lp23[3][512];        // LN2 of layer 23 (b2, scale, shift), logits group
+            float lfB[LROWS + 16], lfC[LROWS + 16];   // folded LN2_23 vectors of the rows (fold)
         } ff;
         struct {                    // attention role
             float k[KVL1 * 32];     // K/V rows [0, min(kv, KVL1)) of the head (LDS-DMA)
@@ -544,7 +547,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         const unsigned tag = ws.tag(s);
         const int kv = kv0 + s;
         for (int l = grp; l < 24; l += ng) {
-            const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
+            const bool probe = a.trace && ((s == 8 && (l == 12 || l == 13 || l == 23)) || (s == 9 && l == 0));
             STAMP1(0);
             if (!form_u(a, ws, s, l, ny0 + s, &sh.p2[0][0], sh)) return;
             STAMP1(1);
@@ -626,17 +629,60 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         }
         // ---- sampler: logits granules of this step -> token -> TK(s + 1)
         if (sampler) {
+            const bool probe = a.trace && s == 8;   // step-end trace (tools/knob_sweep.py)
             bool ok = true;
             if (tid == 0) wait_tag_slow(ws.PFH(s, 23, 0), tag, a.err, ok, a.spin_ticks);
             if (!block_ok1(ok, sh)) return;
+            STAMP1(0);
             const u64* lgg = ws.LG(s);
-            for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok, a.spin_ticks);
-            if (!block_ok1(ok, sh)) return;
             const int st = st0 + s;   // loop steps already executed
-            int raw = 0;
-            const int tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, 0, st + 1, a.top_k,
-                                             a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw,
-                                             sh.samp);
+            int raw = 0, tok = 0;
+            if (a.greedy) {
+                // greedy (RandomNormalLike := 1): the token is the first argmax of the penalised
+                // logits (sample_block's greedy branch), raw the first argmax of the raw ones.
+                // Logits polled straight into registers, both argmaxes reduced together: one
+                // barrier instead of sample_block's LDS staging and two block reductions.
+                float g[2];
+                wait_gran_n<2>(lgg + tid, PT, tag, g, a.err, ok, a.spin_ticks);
+                float rv = -INFINITY, gv = -INFINITY;
+                int ri = 0x7fffffff, gi = 0x7fffffff;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int i = tid + PT * j;
+                    float lj;
+                    if (j < 2) lj = g[j];
+                    else if (tid == 0) lj = wait_gran(lgg + 1024, tag, a.err, ok, a.spin_ticks);
+                    else continue;
+                    argmax_merge(rv, ri, lj, i);
+                    float pen = lj;
+                    if ((sh.seen[i >> 5] >> (i & 31)) & 1u) pen = lj < 0.f ? lj * a.rep_penalty : lj / a.rep_penalty;
+                    argmax_merge(gv, gi, pen / a.temperature, i);
+                }
+                const float rm = wave_max_dpp(rv), gm = wave_max_dpp(gv);
+                const int rmi = wave_min_dpp(rv == rm ? ri : 0x7fffffff);
+                const int gmi = wave_min_dpp(gv == gm ? gi : 0x7fffffff);
+                if (lane == 0) {   // (the previous readers of these slots passed many barriers ago)
+                    sh.samp.sv[w] = rm; sh.samp.si[w] = rmi;
+                    sh.samp.sv[8 + w] = gm; sh.samp.si[8 + w] = gmi;
+                }
+                if (!block_ok1(ok, sh)) return;
+                rv = sh.samp.sv[0]; ri = sh.samp.si[0];
+                gv = sh.samp.sv[8]; gi = sh.samp.si[8];
+#pragma unroll
+                for (int k = 1; k < PWV; ++k) {
+                    argmax_merge(rv, ri, sh.samp.sv[k], sh.samp.si[k]);
+                    argmax_merge(gv, gi, sh.samp.sv[8 + k], sh.samp.si[8 + k]);
+                }
+                raw = ri;
+                tok = gi;
+                STAMP1(1);
+            } else {
+                for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok, a.spin_ticks);
+                if (!block_ok1(ok, sh)) return;
+                STAMP1(1);
+                tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, sh.seen, 0, st + 1, a.top_k,
+                                       a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw, sh.samp);
+            }
             if (tid == 0) {
                 a.y[ny0 + s] = tok;
                 sh.seen[tok >> 5] |= 1u << (tok & 31);
@@ -647,6 +693,8 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 last_fin = fin ? 1 : 0;
                 st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
             }
+            STAMP1(2);
+            if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         }
         ++n_exec;
     }
@@ -686,6 +734,12 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             sh.ff.wp[r][c] = (r < LROWS || j == NF - 1) ? ldg16(a.w_pred, (long)row * 512 + 8 * c)
                                                         : make_uint4(0u, 0u, 0u, 0u);
         }
+        if (tid < LROWS + 16) {
+            const int row = tid < LROWS ? j * LROWS + tid : 1024;
+            const bool live = tid < LROWS || (tid == LROWS && j == NF - 1);
+            sh.ff.lfB[tid] = live ? ldg(a.fold, LOGIT_FOLD + row) : 0.f;
+            sh.ff.lfC[tid] = live ? ldg(a.fold, LOGIT_FOLD + 1025 + row) : 0.f;
+        }
         sh.ff.lp23[0][tid] = ldg(a.L[23].b2, tid);
         sh.ff.lp23[1][tid] = ldg(a.L[23].n2w, tid);
         sh.ff.lp23[2][tid] = ldg(a.L[23].n2b, tid);
@@ -718,7 +772,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
         if (!step_start(a, ws, s, grp == 0, sh)) break;
         const unsigned tag = ws.tag(s);
         for (int l = grp; l < 24; l += ng) {
-            const bool probe = a.trace && s == 8 && (l == 12 || l == 13);
+            const bool probe = a.trace && ((s == 8 && (l == 12 || l == 13 || l == 23)) || (s == 9 && l == 0));
             STAMP1(0);
             float xv;
             if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
@@ -809,28 +863,33 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
         }
         if (logits) {
-            // ---- x_24 = LN2_23(h1_23 + b2 + sum PF_23), logits rows (ar_predict_layer, no bias)
-            float xv;
-            if (!form_x(a, ws, s, 24, 0, &sh.ff.lp23[0][0], xv, sh)) return;
-            sh.x[tid] = xv;
-            __syncthreads();
-            const float4 x0 = *reinterpret_cast<const float4*>(&sh.x[lane * 8]);
-            const float4 x1 = *reinterpret_cast<const float4*>(&sh.x[lane * 8 + 4]);
-            float acc[8];
+            const bool probe = a.trace && s == 8;   // step-end trace (tools/knob_sweep.py)
+            STAMP1(0);
+            // ---- logits rows (ar_predict_layer, no bias) of x_24 = LN2_23(h1_23 + b2 + sum PF_23)
+            // on the MFMA, the LN2 folded through the rows as in form_u: wave w < 4 -> rows
+            // 16 w .. + 16 of this slice, wave 4 of the last slice -> the EOS row
+            if (!form_u(a, ws, s, 24, 0, &sh.ff.lp23[0][0], sh)) return;
+            STAMP1(1);
+            if (w < 4 || (w == 4 && j == NF - 1)) {
+                const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                float mean, rden;
+                ln_row_stats(sh.lnb[0], mean, rden);   // first: interleaved with the MFMAs below
+                const uint4* wb = &sh.ff.wp[min(16 * w + (lane & 15), LROWS)][lane >> 4];
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[q] = dot8(sh.ff.wp[w * 8 + q][lane], x0, x1);
-            wave_sum_n<8>(acc);
-            u64* lg = ws.LG(s);
-            if (lane == 63) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) st_gran(lg + j * LROWS + w * 8 + q, tag, acc[q]);
+                for (int cb = 0; cb < 16; cb += 2) {   // few operands live: the FFN weights stay in registers
+                    c0 = mfma16(afrag(ab, 32 * cb), bfrag(wb[4 * cb]), c0);
+                    c1 = mfma16(afrag(ab, 32 * (cb + 1)), bfrag(wb[4 * (cb + 1)]), c1);
+                }
+                if (lane < 16 && (w < 4 || lane == 0)) {
+                    const int rl = 16 * w + lane;   // LROWS: the EOS row
+                    const float v = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * sh.ff.lfB[rl]) + sh.ff.lfC[rl];
+                    st_gran(ws.LG(s) + (w < 4 ? j * LROWS + rl : 1024), tag, v);
+                }
             }
-            if (j == NF - 1 && w == 0) {
-                float e[1] = {dot8(sh.ff.wp[LROWS][lane], x0, x1)};
-                wave_sum_n<1>(e);
-                if (lane == 63) st_gran(lg + 1024, tag, e[0]);
-            }
-            __syncthreads();   // x consumed before the next step's writes
+            STAMP1(2);
+            if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
+            __syncthreads();   // operands consumed before the next step's writes
         }
     }
 }

@@ -462,6 +462,7 @@ int gsv_engine::vits_read_ms() {
 int gsv_engine::set_vocoder_cus(int K) {
     if (K != 0 && (K % 8 != 0 || K < 8 || n_cu - K < 3 * persist1_grid(1) || n_cu % 32 != 0))
         return set_error(GSV_E_ARG, "vocoder_cus: a multiple of 8 leaving >= 96 CUs for the decode");
+    if (gq_n) return set_error(GSV_E_STATE, "vocoder_cus: finish the started generates first");
     if (int r = vits_wait(nullptr)) return r;
     if (int r = pf_drop()) return r;   // a launched prefetch runs on the vocoder stream
     hipDeviceSynchronize();

@@ -95,6 +95,8 @@ def lib():
         L.gsv_vits_decode_async.argtypes = [vp, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
         L.gsv_vits_wait.argtypes = [vp, vp]
         L.gsv_t2s_prefetch.argtypes = [vp, ctypes.POINTER(Utt), ctypes.POINTER(Sampler), vp]
+        L.gsv_t2s_generate_start.argtypes = [vp, ctypes.POINTER(Utt), ctypes.POINTER(Sampler), vp]
+        L.gsv_t2s_generate_finish.argtypes = [vp, vp, i32, vp, vp]
         L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
         L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
@@ -128,7 +130,7 @@ EXPORTED = (
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
     "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
-    "gsv_vits_wait", "gsv_t2s_prefetch",
+    "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
 )
 
 
@@ -316,6 +318,38 @@ class Engine:
         _check(lib().gsv_t2s_prefetch(self.h, ctypes.byref(u), ctypes.byref(sp), _stream()), "gsv_t2s_prefetch")
         # the engine holds a launched prefetch (for the next generate) and a queued one
         self._pf = (getattr(self, "_pf", []) + [(utt, u, keep)])[-2:]
+
+    def t2s_generate_start(self, utt: Tuple, sampler: Optional[Sampler] = None):
+        """Queue the T2S of one utterance (gsv_t2s_generate_start) and return at once;
+        up to two in flight, so the next decode is queued behind the running one.
+        t2s_generate_finish() returns the oldest one's tokens."""
+        pf = getattr(self, "_pf", [])
+        hit = next((j for j, p in enumerate(pf) if p[0] is utt), None)
+        if hit is not None:
+            u, keep = pf[hit][1], pf[hit][2]
+            self._pf = pf[hit + 1:]
+        else:
+            u, keep = self.make_utt(*utt)
+            self._pf = pf[-1:]
+        sp = sampler or make_sampler()
+        _check(lib().gsv_t2s_generate_start(self.h, ctypes.byref(u), ctypes.byref(sp), _stream()),
+               "gsv_t2s_generate_start")
+        if not hasattr(self, "_gq"):
+            self._gq = []
+        self._gq.append((u, keep))
+
+    def t2s_generate_finish(self, out_stride: int = 1024) -> np.ndarray:
+        """Tokens of the oldest started generate (trimmed, EOS-filtered)."""
+        out = np.zeros((out_stride,), dtype=np.int64)
+        n = np.zeros(1, dtype=np.int32)
+        try:
+            _check(lib().gsv_t2s_generate_finish(self.h, out.ctypes.data_as(ctypes.c_void_p), out_stride,
+                                                 n.ctypes.data_as(ctypes.c_void_p), _stream()),
+                   "gsv_t2s_generate_finish")
+        finally:
+            if getattr(self, "_gq", None):
+                self._gq.pop(0)
+        return out[:n[0]].copy()
 
     def t2s_prefill(self, x, prompts, sampler: Optional[Sampler] = None, seq: int = 0):
         t = self.torch

@@ -134,8 +134,8 @@ class GENIE:
         else:
             prompt_audio.update_global_emb(prompt_encoder)
             cond = {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced}
-        # every sentence's inputs up front: sentence i+1 is prefetched (encoded and
-        # prefilled on the vocoder CUs) while sentence i decodes
+        # every sentence's inputs up front: sentence i+1's T2S is queued behind sentence
+        # i's, its encoder + prefill run on the vocoder CUs while sentence i decodes
         seqs = []
         for t in texts:
             if isinstance(t, str):
@@ -149,12 +149,19 @@ class GENIE:
         utts = [(prompt_audio.phonemes_seq, ts, prompt_audio.text_bert, tb, ssl) for ts, tb in seqs]
         sp = sampler or first_stage_decoder.sampler
         pending = None
+        n = len(utts)
+        eng.t2s_prefetch(utts[1], sp)          # launched beside sentence 0's decode
+        eng.t2s_generate_start(utts[0], sp)
         for i, (text_seq, _) in enumerate(seqs):
             if self.stop_event.is_set():
+                while getattr(eng, "_gq", None):   # started generates are collected, not used
+                    eng.t2s_generate_finish()
                 break
-            if i + 1 < len(utts):
-                eng.t2s_prefetch(utts[i + 1], sp)
-            sem = eng.t2s_generate([utts[i]], sp)[0].reshape(1, 1, -1)
+            if i + 1 < n:                      # queued behind sentence i's decode
+                if i + 2 < n:
+                    eng.t2s_prefetch(utts[i + 2], sp)
+                eng.t2s_generate_start(utts[i + 1], sp)
+            sem = eng.t2s_generate_finish().reshape(1, 1, -1)
             if pending is not None:
                 eng.vits_wait()
                 yield pending.cpu().numpy()

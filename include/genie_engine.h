@@ -18,8 +18,9 @@
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
  *   cn_hubert.run          (ReferenceAudio.py:50-52) gsv_hubert
  *   roberta_model.run      (GetPhonesAndBert.py:73)  gsv_roberta
- *   per-sentence tts loop  (TTSPlayer.py:56-107)     gsv_t2s_prefetch + gsv_vits_decode_async
- *                                                    / gsv_vits_wait (option "vocoder_cus")
+ *   per-sentence tts loop  (TTSPlayer.py:56-107)     gsv_t2s_prefetch, gsv_t2s_generate_start /
+ *                                                    _finish, gsv_vits_decode_async / gsv_vits_wait
+ *                                                    (option "vocoder_cus")
  *
  * Conventions
  *   - All functions return 0 on success, a negative GSV_E* code on failure;
@@ -187,6 +188,18 @@ int gsv_vits_wait(gsv_engine* eng, void* stream);
  * queued prefetch; a batch generate or any other T2S call discards it.  The utt's
  * buffers must stay valid until the generate that uses it. */
 int gsv_t2s_prefetch(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* sampler, void* stream);
+
+/* gsv_t2s_generate for one utterance, split so the GPU never waits for the host
+ * between the sentences of a stream: _start queues the utterance (taking its
+ * prefetch when one matches) and returns at once; up to two may be in flight, so
+ * the next decode is queued behind the running one.  _finish blocks for the oldest
+ * started one and returns its trimmed tokens (host [out_stride]) as
+ * gsv_t2s_generate would, ordering `stream` after it.  A launch that meets the
+ * fp16-range or hand-off-timeout condition is re-run synchronously inside _finish.
+ * Other T2S calls wait for the started ones first; their results stay queued. */
+int gsv_t2s_generate_start(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* sampler, void* stream);
+int gsv_t2s_generate_finish(gsv_engine* eng, int64_t* out_tokens, int32_t out_stride, int32_t* out_len,
+                            void* stream);
 
 /* prompt_encoder_fp32.onnx (V2ProPlus): ref_audio (device [n_audio]),
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */

@@ -137,3 +137,58 @@ def test_prefetch_needs_the_split(eng):
     eng.set_vocoder_cus(0)
     with pytest.raises(EngineError, match="vocoder_cus"):
         eng.t2s_prefetch(t2s_inputs(tag="pfx"))
+
+
+@pytest.mark.parametrize("greedy", [True, False])
+def test_async_generate_stream_matches_plain(eng, greedy):
+    """gsv_t2s_generate_start / _finish with two in flight (utterance i+1 queued behind
+    utterance i) and prefetches: every token identical to a plain generate."""
+    from tests.common import t2s_inputs
+    from genie_tts_amd.engine import make_sampler
+    sp = make_sampler(top_k=15, greedy=greedy, seed=91, force_steps=20)
+    utts = [t2s_inputs(R=11 + 2 * i, S=9 + 4 * i, H=33 + 10 * i, tag=f"as{i}", bert=i % 2 == 0) for i in range(5)]
+    eng.set_vocoder_cus(0)
+    plain = [eng.t2s_generate([u], sp)[0] for u in utts]
+    eng.set_vocoder_cus(64)
+    try:
+        dev = [tuple(eng._dev(a, None) if a is not None else None for a in u) for u in utts]
+        eng.t2s_prefetch(dev[1], sp)
+        eng.t2s_generate_start(dev[0], sp)
+        got = []
+        for i in range(len(dev)):
+            if i + 1 < len(dev):
+                if i + 2 < len(dev):
+                    eng.t2s_prefetch(dev[i + 2], sp)
+                eng.t2s_generate_start(dev[i + 1], sp)
+            got.append(eng.t2s_generate_finish())
+        for i, (a, b) in enumerate(zip(got, plain)):
+            assert a.tolist() == b.tolist(), f"utterance {i}"
+        # no prefetch at all: the starts prefill themselves, still exact
+        eng.t2s_generate_start(dev[3], sp)
+        eng.t2s_generate_start(dev[4], sp)
+        assert eng.t2s_generate_finish().tolist() == plain[3].tolist()
+        # a synchronous generate in between waits for the started one; its result stays queued
+        assert eng.t2s_generate([dev[2]], sp)[0].tolist() == plain[2].tolist()
+        assert eng.t2s_generate_finish().tolist() == plain[4].tolist()
+    finally:
+        eng.set_vocoder_cus(0)
+
+
+def test_async_generate_fp16_guard_reruns(eng):
+    """A started generate whose persistent launch meets the (test-lowered) fp16 limit is
+    re-run synchronously inside _finish: same tokens as the plain path."""
+    from tests.common import t2s_inputs
+    from genie_tts_amd.engine import make_sampler, EngineError
+    sp = make_sampler(force_steps=12)
+    u = t2s_inputs(R=12, S=10, H=41, tag="asf")
+    ref = eng.t2s_generate([u], sp)[0]
+    n0 = eng.counter("persist1_f16_reruns")
+    eng.set_option("persist1_f16_limit", 1)
+    try:
+        eng.t2s_generate_start(u, sp)
+        assert eng.t2s_generate_finish().tolist() == ref.tolist()
+    finally:
+        eng.set_option("persist1_f16_limit", 0)
+    assert eng.counter("persist1_f16_reruns") > n0
+    with pytest.raises(EngineError, match="no generate in flight"):
+        eng.t2s_generate_finish()

@@ -37,6 +37,17 @@ def phase_trace():
         t = (tr[b:b + 16, :8] - t0) * 10 / 1000.0
         print(f"{nm:6s} " + "  ".join(f"s{i} {t[:, i].min():6.2f}/{np.median(t[:, i]):6.2f}/{t[:, i].max():6.2f}"
                                     for i in range(8) if -1e5 < t[:, i].max() < 1e5), flush=True)
+    # step end (8 layer groups): layer 23 FFN (group 7, blocks 240..255) publish at s4, logits
+    # workgroups (group 1 FFN, blocks 48..63): s0 start, s1 x_24 formed, s2 logits published;
+    # sampler (block 64): s0 woken, s1 logits read, s2 token published; layer 0 of step 9
+    # (group 0 attention, blocks 0..15): s0 token known, s1 q/k/v operand ready, s5 published
+    def med(b0, b1, i):
+        v = (tr[b0:b1, i] - t0) * 10 / 1000.0
+        return float(np.median(v))
+    print("step end: L23 ffn publish %.2f | logits start %.2f x24 %.2f published %.2f | sampler woke %.2f "
+          "logits read %.2f token %.2f | L0(s9) start %.2f operand %.2f attn published %.2f | L1(s9)?" % (
+              med(240, 256, 4), med(48, 64, 0), med(48, 64, 1), med(48, 64, 2), med(64, 65, 0), med(64, 65, 1),
+              med(64, 65, 2), med(0, 16, 0), med(0, 16, 1), med(0, 16, 5)), flush=True)
     # shader clock: memtime ticks / realtime ticks (100 MHz) between the first and last stamp of a block
     for b in (128, 144):
         rt, st = tr[b, :8], tr[b, 8:16]
