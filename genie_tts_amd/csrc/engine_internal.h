@@ -251,7 +251,8 @@ struct gsv_engine {
     int set_vocoder_cus(int K);
     int vits_async(const gsv_vits_item& u, float noise_scale, hipStream_t caller);
     int vits_wait(hipStream_t caller);
-    int vits_launch_queued();
+    int vits_launch_queued(hipStream_t s = nullptr);
+    hipStream_t vlast = nullptr;       // stream the pending vocoder call was launched on
     int decode_cus() const { return n_cu - vocoder_cus; }   // CUs of the engine (T2S) stream
     // T2S prefetch (gsv_t2s_prefetch): encode + prefill of the next utterance into
     // slot 1 on the vocoder CUs while slot 0 decodes; taken into slot 0 by the

@@ -507,36 +507,42 @@ int gsv_engine::vits_async(const gsv_vits_item& u, float noise_scale, hipStream_
     return 0;
 }
 
-int gsv_engine::vits_launch_queued() {
+// s: the vocoder stream (beside a decode), or the engine stream when no T2S work is
+// queued behind (the last sentence of a stream: its n_cu - K CUs are idle then).
+int gsv_engine::vits_launch_queued(hipStream_t s) {
     if (!vqueued) return 0;
     vqueued = false;
+    if (!s) s = vstream;
     const gsv_vits_item& u = vcall;
-    hipStreamWaitEvent(vstream, vev_in, 0);
+    hipStreamWaitEvent(s, vev_in, 0);
     if (int r = vits_decode_pass(vws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge, u.ge_adv,
                                  u.noise_mode == 1 ? u.eps : nullptr, u.noise_mode == 2 ? u.noise_seed : 0,
-                                 vcall_scale, u.audio, vstream, use_convh ? vovf : nullptr, timing))
+                                 vcall_scale, u.audio, s, use_convh ? vovf : nullptr, timing))
         return r;
-    if (use_convh) hipMemcpyAsync(vovf_host, vovf, 4, hipMemcpyDeviceToHost, vstream);
-    hipEventRecord(vev_done, vstream);
+    if (use_convh) hipMemcpyAsync(vovf_host, vovf, 4, hipMemcpyDeviceToHost, s);
+    hipEventRecord(vev_done, s);
     vpending = true;
+    vlast = s;
     return 0;
 }
 
 int gsv_engine::vits_wait(hipStream_t caller) {
-    if (int r = vits_launch_queued()) return r;
+    // still queued (no decode launched since): nothing runs on the engine stream unless
+    // a started generate does, so the call takes the T2S CUs
+    if (int r = vits_launch_queued(gq_n == 0 ? stream : vstream)) return r;
     if (!vpending) return 0;
     vpending = false;
     if (hipEventSynchronize(vev_done) != hipSuccess) return set_error(GSV_E_HIP, "overlapped vocoder");
     if (use_convh && *vovf_host) {   // fp16-range overflow: the same utterance again on the f32 path
         const gsv_vits_item& u = vcall;
-        hipMemsetAsync(vovf, 0, 4, vstream);
+        hipMemsetAsync(vovf, 0, 4, vlast);
         ++vits_f32_reruns;
         if (int r = vits_decode_pass(vws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
                                      u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
-                                     u.noise_mode == 2 ? u.noise_seed : 0, vcall_scale, u.audio, vstream, nullptr,
+                                     u.noise_mode == 2 ? u.noise_seed : 0, vcall_scale, u.audio, vlast, nullptr,
                                      timing))
             return r;
-        hipEventRecord(vev_done, vstream);
+        hipEventRecord(vev_done, vlast);
         if (hipEventSynchronize(vev_done) != hipSuccess) return set_error(GSV_E_HIP, "overlapped vocoder re-run");
     }
     if (int r = vits_read_ms()) return r;
