@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <map>
 #include <memory>
@@ -41,6 +42,7 @@ void* gsv_engine::dalloc(size_t bytes) {
     void* p = nullptr;
     if (bytes == 0) bytes = 16;
     if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(alloc_mu);   // vocoder lane threads grow their workspaces
     allocs.push_back(p);
     return p;
 }
@@ -1650,6 +1652,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->persist1_pf_delay = std::max(0, value);
     } else if (n.size() == 5 && n.compare(0, 4, "knob") == 0 && n[4] >= '0' && n[4] <= '3') {
         eng->persist1_knob[n[4] - '0'] = value;   // single-sequence decode tuning variant (0 = default)
+    } else if (n == "vits_threads") {   // vocoder lanes issued by one host thread each (default 1)
+        eng->vits_threads = value != 0;
     } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)
         eng->spin_wait = value != 0;
     } else if (n == "vocoder_cus") {   // overlapped vocoder: CUs reserved for gsv_vits_decode_async

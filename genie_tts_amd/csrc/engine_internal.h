@@ -4,6 +4,7 @@
 #include <hip/hip_fp16.h>
 
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -65,6 +66,7 @@ struct gsv_engine {
     bool finalized = false;
     std::map<std::string, gsv::Staged> staged;
     std::vector<void*> allocs;        // weights + workspaces (engine lifetime)
+    std::mutex alloc_mu;              // guards allocs (vocoder lane threads)
     std::vector<void*> state_allocs;  // decode capacity (re-sized by reserve)
 
     // ---- T2S weights
@@ -239,6 +241,7 @@ struct gsv_engine {
     int* vflags_host = nullptr;
     int vflag_cap = 0;
     int vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s);
+    bool vits_threads = true;          // option "vits_threads": one host thread per vocoder lane
     int vits_read_ms();
     // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
     int vocoder_cus = 0;

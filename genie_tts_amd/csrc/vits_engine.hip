@@ -12,6 +12,8 @@
 
 #include "engine_internal.h"
 
+#include <thread>
+
 using namespace gsv;
 
 namespace {
@@ -742,15 +744,34 @@ int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_sc
     hipMemsetAsync(vflags, 0, (size_t)n * 4, s);
     hipEventRecord(vfork, s);
     for (int l = 0; l < K; ++l) hipStreamWaitEvent(vlanes[l].st, vfork, 0);
-    for (int i = 0; i < n; ++i) {
-        VitsLane& L = vlanes[i % K];
-        const gsv_vits_item& u = it[i];
-        if (int r = vits_decode_pass(L.ws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
-                                     u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
-                                     u.noise_mode == 2 ? u.noise_seed : 0, noise_scale, u.audio, L.st,
-                                     use_convh ? vflags + i : nullptr, false))
-            return r;
+    // each lane's launches are issued by a host thread of its own: a vocoder pass is a
+    // few hundred launches, and one thread issuing every lane's would pace the lanes
+    // (the per-pass host state -- split-K workspace, overflow flag -- is thread-local)
+    std::vector<int> rcs(K, 0);
+    auto lane_work = [&](int l) {
+        hipSetDevice(device);
+        VitsLane& L = vlanes[l];
+        for (int i = l; i < n; i += K) {
+            const gsv_vits_item& u = it[i];
+            if (int r = vits_decode_pass(L.ws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
+                                         u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
+                                         u.noise_mode == 2 ? u.noise_seed : 0, noise_scale, u.audio, L.st,
+                                         use_convh ? vflags + i : nullptr, false)) {
+                rcs[l] = r;
+                return;
+            }
+        }
+    };
+    if (K == 1 || !vits_threads) {
+        for (int l = 0; l < K; ++l) lane_work(l);
+    } else {
+        std::vector<std::thread> th;
+        for (int l = 1; l < K; ++l) th.emplace_back(lane_work, l);
+        lane_work(0);
+        for (auto& t : th) t.join();
     }
+    for (int l = 0; l < K; ++l)
+        if (rcs[l]) return set_error(rcs[l], "vocoder lane " + std::to_string(l) + " failed");
     for (int l = 0; l < K; ++l) {
         hipEventRecord(vlanes[l].join, vlanes[l].st);
         hipStreamWaitEvent(s, vlanes[l].join, 0);
