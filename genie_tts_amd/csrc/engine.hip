@@ -576,6 +576,9 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     // kept behind GENIE_PACKED_TILE for A/B
     static const bool tile_opt = [] { const char* e = std::getenv("GENIE_PACKED_TILE"); return e && std::atoi(e); }();
     const bool tiled = tile_opt && maxn0 <= ATTN_TILE_MAXK;
+    // the online-softmax kernel over the same tiles (GENIE_PACKED_FLASH=0: the per-row kernel)
+    static const bool flash_opt = [] { const char* e = std::getenv("GENIE_PACKED_FLASH"); return !(e && std::atoi(e) == 0); }();
+    const bool flash_tiles = flash_opt;
     const int* row_seq = pk_rowinfo;
     const int* row_pos = pk_rowinfo + R;
     const int* row_len = pk_rowinfo + 2 * R;
@@ -612,6 +615,10 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
             at.tiles = pk_tiles;
             at.ntiles = ntiles;
             attn_rows_tiled(at, st);
+        } else if (flash_tiles) {   // 16-row tiles of one sequence, K/V staged once per tile
+            at.tiles = pk_tiles;
+            at.ntiles = ntiles;
+            attn_rows_flash_tiled(at, st);
         } else {
             attn_rows(at, st);
         }

@@ -97,6 +97,8 @@ constexpr int ATTN_TILE_MAXK = 448;   // keys a k_attn_tile block stages in LDS
 void attn_rows(const AttnArgs& a, hipStream_t s);
 // Tiled prefill attention over a.tiles (all rows' keys <= ATTN_TILE_MAXK).
 void attn_rows_tiled(const AttnArgs& a, hipStream_t s);
+// Packed prefill attention over a.tiles on the online-softmax kernel (any key count).
+void attn_rows_flash_tiled(const AttnArgs& a, hipStream_t s);
 // Batched decode attention (one block per head x sequence) whose prologue reduces
 // the split-K QKV slabs of its head: q/k/v = b_in + sum_z slab[z][b][...] (fixed
 // order), appends the new K/V row at position kvlen[b], attends over [0, kvlen[b]].

@@ -738,7 +738,16 @@ __global__ __launch_bounds__(256) void k_attn_flash(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) float Ps[4][4][AF_KC];
     __shared__ int rl[AF_ROWS];
     const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r0 = blockIdx.y * AF_ROWS, nr = min(AF_ROWS, a.rows - r0);
+    // rows: 16 per block of one sequence, or (packed prefill) tile blockIdx.y of a.tiles:
+    // {sequence, first row, rows <= 16}, every row of a tile in the same sequence
+    int r0 = blockIdx.y * AF_ROWS, nr = min(AF_ROWS, a.rows - r0);
+    long kvbase = (long)h * a.tmax * 32;
+    if (a.tiles) {
+        const int* tl = a.tiles + 3 * blockIdx.y;
+        kvbase += (long)tl[0] * a.seq_stride;
+        r0 = tl[1];
+        nr = tl[2];
+    }
     const float sc = a.scale;
     if (tid < AF_ROWS) rl[tid] = tid < nr ? a.row_len[r0 + tid] : 0;
     for (int e = tid; e < AF_ROWS * 8; e += 256) {   // q rows (scaled), 16-B pieces
@@ -751,8 +760,8 @@ __global__ __launch_bounds__(256) void k_attn_flash(AttnArgs a) {
     int kmax = 0;
 #pragma unroll
     for (int i = 0; i < AF_ROWS; ++i) kmax = max(kmax, rl[i]);
-    const float* K = a.k + (long)h * a.tmax * 32;
-    const float* V = a.v + (long)h * a.tmax * 32;
+    const float* K = a.k + kvbase;
+    const float* V = a.v + kvbase;
     int len[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) len[r] = rl[4 * w + r];
@@ -853,6 +862,11 @@ void attn_rows_tiled(const AttnArgs& a, hipStream_t s) {
     if (a.ntiles <= 0) return;
     static_assert(AT_MAXK == ATTN_TILE_MAXK, "tile key capacity");
     hipLaunchKernelGGL(k_attn_tile, dim3(16, a.ntiles), dim3(1024), 0, s, a);
+}
+
+void attn_rows_flash_tiled(const AttnArgs& a, hipStream_t s) {
+    if (a.ntiles <= 0) return;
+    hipLaunchKernelGGL(k_attn_flash, dim3(16, a.ntiles), dim3(256), 0, s, a);
 }
 
 void attn_rows_plus(const AttnArgs& a, int len_add, hipStream_t s) {
