@@ -150,34 +150,43 @@ class GENIE:
         sp = sampler or first_stage_decoder.sampler
         pending = None
         n = len(utts)
-        eng.t2s_prefetch(utts[1], sp)          # launched beside sentence 0's decode
-        eng.t2s_generate_start(utts[0], sp)
-        for i, (text_seq, _) in enumerate(seqs):
-            if self.stop_event.is_set():
-                while getattr(eng, "_gq", None):   # started generates are collected, not used
-                    eng.t2s_generate_finish()
-                break
-            if i + 1 < n:                      # queued behind sentence i's decode
-                if i + 2 < n:
-                    eng.t2s_prefetch(utts[i + 2], sp)
-                eng.t2s_generate_start(utts[i + 1], sp)
-            sem = eng.t2s_generate_finish().reshape(1, 1, -1)
+        try:
+            eng.t2s_prefetch(utts[1], sp)          # launched beside sentence 0's decode
+            eng.t2s_generate_start(utts[0], sp)
+            for i, (text_seq, _) in enumerate(seqs):
+                if self.stop_event.is_set():
+                    break
+                if i + 1 < n:                      # queued behind sentence i's decode
+                    if i + 2 < n:
+                        eng.t2s_prefetch(utts[i + 2], sp)
+                    eng.t2s_generate_start(utts[i + 1], sp)
+                sem = eng.t2s_generate_finish().reshape(1, 1, -1)
+                if pending is not None:
+                    eng.vits_wait()
+                    done, pending = pending, None
+                    yield done.cpu().numpy()
+                G = sem.size
+                eps = vocoder.eps_fn(G) if vocoder.eps_fn else None
+                item = dict(text_seq=text_seq, pred_semantic=sem, **cond)
+                if eps is not None:
+                    item["eps"] = eps
+                else:
+                    seed = vocoder.next_seed()
+                    if seed is not None:
+                        item["noise_seed"] = seed
+                pending = eng.vits_decode_async(item, vocoder.noise_scale)
             if pending is not None:
                 eng.vits_wait()
-                yield pending.cpu().numpy()
-            G = sem.size
-            eps = vocoder.eps_fn(G) if vocoder.eps_fn else None
-            item = dict(text_seq=text_seq, pred_semantic=sem, **cond)
-            if eps is not None:
-                item["eps"] = eps
-            else:
-                seed = vocoder.next_seed()
-                if seed is not None:
-                    item["noise_seed"] = seed
-            pending = eng.vits_decode_async(item, vocoder.noise_scale)
-        if pending is not None:
-            eng.vits_wait()
-            yield pending.cpu().numpy()
+                done, pending = pending, None
+                yield done.cpu().numpy()
+        finally:   # stopped, failed or abandoned: started generates and the vocoder call complete
+            while getattr(eng, "_gq", None):
+                try:
+                    eng.t2s_generate_finish()
+                except Exception:
+                    break
+            if pending is not None:
+                eng.vits_wait()
 
     def t2s(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, engine, sampler: Sampler) -> np.ndarray:
         """Whole T2S on the device; returns the trimmed, EOS-filtered [1,1,G] tokens."""

@@ -155,3 +155,29 @@ def test_tts_stream_equals_single(model):
         single = gen.tts(t, *args, sampler=sp)
         assert single.shape == a.shape
         np.testing.assert_allclose(single, a, atol=1e-6)
+
+
+def test_tts_stream_abandoned_leaves_the_engine_clean(model):
+    """A stream closed after its first sentence (consumer gone): the started generates
+    and the vocoder call complete in the generator's cleanup, and the engine serves
+    the next stream exactly."""
+    from genie_tts_amd.inference import GENIE, ReferenceAudio
+    m, _ = model
+    ref = ReferenceAudio(phonemes_seq=synth.synth_phones(12, "c-r"), text_bert=np.zeros((12, 1024), np.float32),
+                         audio_32k=synth.synth_ref_audio(32000 * 2, "c-a").reshape(1, -1),
+                         ssl_content=synth.synth_ssl(41, "c-s").reshape(1, 768, -1))
+    texts = [synth.synth_phones(n, f"c-t{n}") for n in (11, 14, 9, 16)]
+    gen = GENIE()
+    sp = m.T2S_FIRST_STAGE_DECODER.sampler
+    args = (ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER, m.VITS, None)
+    try:
+        it = gen.tts_stream(texts, *args, sampler=sp, vocoder_cus=64)
+        first = next(it)
+        it.close()
+        assert not getattr(m.ENGINE, "_gq", None)
+        again = list(gen.tts_stream(texts, *args, sampler=sp, vocoder_cus=64))
+    finally:
+        m.ENGINE.set_vocoder_cus(0)
+    np.testing.assert_allclose(first, again[0], atol=1e-6)
+    for t, a in zip(texts, again):
+        np.testing.assert_allclose(gen.tts(t, *args, sampler=sp), a, atol=1e-6)
