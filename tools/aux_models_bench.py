@@ -1,0 +1,60 @@
+"""Measured time of the reference-side models on the engine (SURVEY §8 "next" rows):
+CN-HuBERT on a 5.3 s reference clip (ReferenceAudio.py:48-52, once per reference) and the
+24-layer Chinese RoBERTa on a 20-character sentence (GetPhonesAndBert.py:64-74, once per
+sentence), synthetic weights of the real shapes.  Prints one JSON line; the FLOP counts
+are the dense-matmul work of each model (T_min at the 157.3 TF/s f32 MFMA peak)."""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from genie_tts_amd import synth, weights as W  # noqa: E402
+from genie_tts_amd.engine import Engine, lib  # noqa: E402
+
+torch.cuda.set_device(0)
+out = {}
+# ---- CN-HuBERT: 5.3 s at 16 kHz
+eh = Engine({"hubert": synth.synth_weights(W.hubert_spec())}, "v2")
+audio = torch.as_tensor(synth.rng_for("hb").standard_normal(int(16000 * 5.3)).astype(np.float32) * 0.1, device="cuda")
+T = lib().gsv_hubert_frames(audio.numel())
+for _ in range(3):
+    eh.hubert(audio)
+torch.cuda.synchronize()
+n = 20
+t0 = time.perf_counter()
+for _ in range(n):
+    eh.hubert(audio)
+torch.cuda.synchronize()
+ms = (time.perf_counter() - t0) / n * 1e3
+# conv stack + 12 transformer layers (768, FFN 3072) + pos conv (768 x 48 x 128 per group x 16)
+conv = 2 * (T * 2 * 512 * 512 * 3 + T * 4 * 512 * 512 * 3 + T * 8 * 512 * 512 * 3 * 2 + T * 16 * 512 * 512 * 2)
+layers = 12 * 2 * T * (768 * 2304 + 768 * 768 + 2 * 768 * 3072) + 12 * 4 * T * T * 768
+pos = 2 * T * 768 * 48 * 128
+flops = conv + layers + pos + 2 * T * 512 * 768
+out["cn_hubert"] = {"audio_s": 5.3, "frames": int(T), "ms": ms, "gflop": flops / 1e9,
+                    "frac_f32_peak": flops / 157.3e12 / (ms * 1e-3)}
+eh.close()
+# ---- RoBERTa, 24 layers (hidden_states[-3]: 22 run), 20 characters
+er = Engine({"roberta": synth.synth_weights(W.roberta_spec(24))}, "v2")
+r = synth.rng_for("rbb")
+n_chars = 20
+ids = np.concatenate([[101], r.integers(672, 8000, size=n_chars), [102]]).astype(np.int64)
+w2p = r.integers(1, 4, size=n_chars).astype(np.int64)
+for _ in range(3):
+    er.roberta(ids, w2p)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(n):
+    er.roberta(ids, w2p)
+torch.cuda.synchronize()
+ms = (time.perf_counter() - t0) / n * 1e3
+N = ids.size
+flops = 22 * (2 * N * (1024 * 3072 + 1024 * 1024 + 2 * 1024 * 4096) + 4 * N * N * 1024)
+out["roberta"] = {"tokens": int(N), "layers_run": 22, "ms": ms, "gflop": flops / 1e9,
+                  "weights_mb": 22 * 12.6e6 * 2 / 1e6 / 2,
+                  "frac_hbm_weights": (22 * (1024 * 3072 + 1024 * 1024 + 2 * 1024 * 4096) * 2) / 8e12 / (ms * 1e-3)}
+er.close()
+print(json.dumps(out), flush=True)
