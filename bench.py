@@ -158,6 +158,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("single", "batch64", "mixed100"), default="single")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--vits-lanes", type=int, default=0,
+                    help="batched workloads: concurrent vocoder streams (0 = the engine default)")
     ap.add_argument("--vocoder-cus", type=int, default=64,
                     help="single workload: CUs reserved for the overlapped vocoder (0 = sequential)")
     args = ap.parse_args()
@@ -190,6 +192,8 @@ def main():
         items = wl.items
         units_per_step = world * len(items)       # every replica runs the workload (weak scaling)
     run = Runner(wl, items, dev, local if world > 1 else 0)
+    if args.vits_lanes:
+        run.eng.set_option("vits_lanes", args.vits_lanes)
     timed_single = args.workload == "single"
     run.eng.set_timing(True)                      # phase events (+ live dominant-kernel events at B = 1)
     overlap = timed_single and args.vocoder_cus > 0

@@ -1659,6 +1659,9 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->persist1_pf_delay = std::max(0, value);
     } else if (n.size() == 5 && n.compare(0, 4, "knob") == 0 && n[4] >= '0' && n[4] <= '3') {
         eng->persist1_knob[n[4] - '0'] = value;   // single-sequence decode tuning variant (0 = default)
+    } else if (n == "vits_lanes") {   // concurrent vocoder streams of gsv_vits_decode_batch
+        if (value < 1 || value > 16) return set_error(GSV_E_ARG, "vits_lanes: 1..16");
+        eng->vits_lanes = value;
     } else if (n == "vits_threads") {   // vocoder lanes issued by one host thread each (default 1)
         eng->vits_threads = value != 0;
     } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)

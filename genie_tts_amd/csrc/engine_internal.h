@@ -229,7 +229,8 @@ struct gsv_engine {
                          const float* eps, uint64_t noise_seed, float noise_scale, float* audio, hipStream_t st,
                          int* ovf, bool timed);
     // concurrent vocoder lanes (gsv_vits_decode_batch)
-    static constexpr int VITS_LANES = 4;   // = the box's hardware queues per process
+    int vits_lanes = 4;                    // option "vits_lanes" (1..16): concurrent vocoder streams;
+                                           // 4 = HIP's default hardware queues per process
     struct VitsLane {
         hipStream_t st = nullptr;
         hipEvent_t join = nullptr;

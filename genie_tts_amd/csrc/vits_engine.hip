@@ -719,7 +719,7 @@ int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_sc
                            u.noise_mode == 1 ? u.eps : nullptr, u.noise_mode == 2 ? u.noise_seed : 0, noise_scale,
                            u.audio, s);
     }
-    const int K = std::min(n, VITS_LANES);
+    const int K = std::min(n, vits_lanes);
     for (int l = (int)vlanes.size(); l < K; ++l) {
         VitsLane L;
         if (hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking) != hipSuccess ||
