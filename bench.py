@@ -150,6 +150,33 @@ class Runner:
         self.phase["vits"] += t2 - t1
         return sems, n
 
+    def step_pipelined(self):
+        """One batch with its vocoder overlapped: this batch's T2S runs beside the previous
+        batch's vocoder lanes (gsv_vits_decode_batch_async), then that vocoder is joined and
+        this batch's is started.  drain() joins the last one."""
+        t0 = time.perf_counter()
+        utts = [(self.d_ref, t, self.d_ref_bert, b, self.d_ssl, it.force_steps)
+                for t, b, it in zip(self.d_txt, self.d_bert, self.items)]
+        sems = self.eng.t2s_generate(utts, self.sp)
+        t1 = time.perf_counter()
+        tm = self.eng.timing()
+        self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
+        self.phase["decode"] += tm[2] * 1e-3
+        self.drain()
+        t2 = time.perf_counter()
+        cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
+        wavs = self.eng.vits_decode_batch_async([dict(text_seq=t, pred_semantic=sem, noise_seed=self.seed + i, **cond)
+                                                 for i, (t, sem) in enumerate(zip(self.d_txt, sems))])
+        self.batch_pending = True
+        self.phase["t2s"] += t1 - t0
+        self.phase["vits"] += t2 - t1      # the host's wait for the previous vocoder (not hidden)
+        return sems, sum(int(w.numel()) for w in wavs)
+
+    def drain(self):
+        if getattr(self, "batch_pending", False):
+            self.eng.vits_batch_wait()
+            self.batch_pending = False
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -162,6 +189,13 @@ def main():
                     help="batched workloads: concurrent vocoder streams (0 = the engine default)")
     ap.add_argument("--vocoder-cus", type=int, default=64,
                     help="single workload: CUs reserved for the overlapped vocoder (0 = sequential)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="batched workloads: 1 = each batch's vocoder beside the next batch's T2S, "
+                         "0 = one batch at a time")
+    ap.add_argument("--lane-priority", type=int, default=None,
+                    help="batched workloads: HIP stream priority of the vocoder lanes (lower = first)")
+    ap.add_argument("--t2s-priority", type=int, default=None,
+                    help="batched workloads: HIP stream priority of the engine (T2S) stream")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,15 +228,22 @@ def main():
     run = Runner(wl, items, dev, local if world > 1 else 0)
     if args.vits_lanes:
         run.eng.set_option("vits_lanes", args.vits_lanes)
+    if args.lane_priority is not None:
+        run.eng.set_option("lane_priority", args.lane_priority)
+    if args.t2s_priority is not None:
+        run.eng.set_option("t2s_priority", args.t2s_priority)
     timed_single = args.workload == "single"
     run.eng.set_timing(True)                      # phase events (+ live dominant-kernel events at B = 1)
     overlap = timed_single and args.vocoder_cus > 0
+    pipelined = not timed_single and args.pipeline > 0
+    step = run.step_pipelined if pipelined else run.step
     if overlap:
         run.eng.set_vocoder_cus(args.vocoder_cus)
         sems, n_samples = run.stream(max(1, args.warmup))
     else:
         for _ in range(args.warmup):
-            sems, n_samples = run.step()
+            sems, n_samples = step()
+        run.drain()
     torch.cuda.synchronize()
     run.phase = {k: 0.0 for k in run.phase}
     if timed_single:
@@ -215,11 +256,12 @@ def main():
     t0 = time.perf_counter()
     if overlap:   # the whole stream, fill and drain included (the last vocoder too)
         sems, n_samples = run.stream(args.steps, phase_ms)
-    else:
+    else:   # pipelined: the fill (first T2S alone) and the drain (last vocoder alone) are timed
         for _ in range(args.steps):
-            sems, n_samples = run.step()
+            sems, n_samples = step()
             if timed_single:
                 phase_ms.append(run.eng.timing())
+        run.drain()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -295,7 +337,9 @@ def main():
                          "version": wl.version, "sentences": len(wl.items), "sentences_this_rank": len(items),
                          "text_phones": [int(i.text_seq.shape[1]) for i in items][:8] + ["..."],
                          "semantic_tokens_this_rank": sum(tokens), "parallelism": f"replicas x{world}" +
-                         (" (LPT shards)" if args.workload == "mixed100" else "")}
+                         (" (LPT shards)" if args.workload == "mixed100" else ""),
+                         "pipelined": pipelined,
+                         "vits_f32_reruns": run.eng.counter("vits_f32_reruns")}
         ph = {k: v / args.steps * 1e3 for k, v in run.phase.items()}
         out["phase_ms"] = ph
         out["roofline_utterance"] = composite_roofline(ms_per_step, n0s, [it.force_steps for it in items], tokens,

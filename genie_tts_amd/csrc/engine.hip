@@ -55,6 +55,7 @@ void gsv_engine::release_all() {
 }
 
 gsv_engine::~gsv_engine() {
+    for (auto& t : vb_threads) t.join();
     release_all();
     for (void* p : pk_allocs) hipFree(p);
     pk_allocs.clear();
@@ -1202,6 +1203,8 @@ extern "C" int gsv_engine_create(int device, int version, gsv_engine** out) {
 extern "C" int gsv_engine_destroy(gsv_engine* eng) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
+    for (auto& t : eng->vb_threads) t.join();   // lane threads of an unfinished async batch
+    eng->vb_threads.clear();
     hipDeviceSynchronize();
     delete eng;
     return 0;
@@ -1662,6 +1665,35 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "vits_lanes") {   // concurrent vocoder streams of gsv_vits_decode_batch
         if (value < 1 || value > 16) return set_error(GSV_E_ARG, "vits_lanes: 1..16");
         eng->vits_lanes = value;
+    } else if (n == "lane_priority" || n == "t2s_priority") {
+        // HIP stream priorities (lower = served first): the overlapped batch vocoder's lanes
+        // beside the T2S of the next batch on the engine stream
+        int least = 0, greatest = 0;
+        hipDeviceGetStreamPriorityRange(&least, &greatest);
+        const int p = std::min(std::max(value, std::min(least, greatest)), std::max(least, greatest));
+        if (int r = eng->vits_batch_finish(nullptr)) return r;
+        if (int r = eng->vits_wait(nullptr)) return r;
+        hipDeviceSynchronize();
+        if (n == "lane_priority") {
+            eng->lane_priority = p;
+            for (auto& L : eng->vlanes) {   // the lanes' streams re-created at the new priority
+                hipStream_t ns = nullptr;
+                if (hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, p) != hipSuccess)
+                    return set_error(GSV_E_HIP, "lane stream");
+                hipStreamDestroy(L.st);
+                L.st = ns;
+            }
+        } else {
+            if (eng->vocoder_cus || eng->gq_n || !eng->own_stream)
+                return set_error(GSV_E_STATE, "t2s_priority: needs the engine's own unmasked stream, idle");
+            if (int r = eng->pf_drop()) return r;
+            hipStream_t ns = nullptr;
+            if (hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, p) != hipSuccess)
+                return set_error(GSV_E_HIP, "stream");
+            hipStreamDestroy(eng->stream);
+            eng->stream = ns;
+            eng->t2s_priority = p;
+        }
     } else if (n == "vits_threads") {   // vocoder lanes issued by one host thread each (default 1)
         eng->vits_threads = value != 0;
     } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)

@@ -5,6 +5,7 @@
 
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -242,7 +243,19 @@ struct gsv_engine {
     int* vflags_host = nullptr;
     int vflag_cap = 0;
     int vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s);
+    // overlapped batch (gsv_vits_decode_batch_async): issued by lane threads that may still
+    // run when the call returns; vits_batch_finish joins
+    std::vector<gsv_vits_item> vb_items;
+    std::vector<std::thread> vb_threads;
+    std::vector<int> vb_rcs;
+    int vb_k = 0;
+    float vb_scale = 0.f;
+    bool vb_active = false;
+    int vits_batch_launch(float noise_scale, hipStream_t s, bool join);
+    int vits_batch_finish(hipStream_t s);
     bool vits_threads = true;          // option "vits_threads": one host thread per vocoder lane
+    int lane_priority = 0;             // option "lane_priority": HIP stream priority of the lanes
+    int t2s_priority = 0;              // option "t2s_priority": of the engine stream (vocoder_cus 0)
     int vits_read_ms();
     // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
     int vocoder_cus = 0;

@@ -419,6 +419,8 @@ int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* 
     }
     if (vpending || vqueued)   // the overlapped vocoder call shares the workspace: finish it first
         if (int r = vits_wait(nullptr)) return r;
+    if (vb_active)
+        if (int r = vits_batch_finish(nullptr)) return r;
     if (!use_convh) {
         if (int r = vits_decode_pass(vws, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps,
                                      noise_seed, noise_scale, audio, s, nullptr, timing))
@@ -497,6 +499,8 @@ int gsv_engine::set_vocoder_cus(int K) {
 int gsv_engine::vits_async(const gsv_vits_item& u, float noise_scale, hipStream_t caller) {
     if (!vstream) return set_error(GSV_E_STATE, "overlapped vocoder: set option vocoder_cus first");
     if (int r = vits_wait(nullptr)) return r;
+    if (vb_active)
+        if (int r = vits_batch_finish(nullptr)) return r;
     if (use_convh && !vovf) {
         if (hipMalloc(&vovf, 64) != hipSuccess || hipHostMalloc((void**)&vovf_host, 64, hipHostMallocDefault) != hipSuccess)
             return set_error(GSV_E_HIP, "overflow flag alloc");
@@ -711,6 +715,8 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
 // flag; after the join, flagged utterances are decoded again on the f32 path.
 int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_scale, hipStream_t s) {
     if (n <= 0) return 0;
+    if (vb_active)   // an overlapped batch shares the lanes: finish it first
+        if (int r = vits_batch_finish(nullptr)) return r;
     if (n > 1 && (vpending || vqueued))
         if (int r = vits_wait(nullptr)) return r;
     if (n == 1) {   // one utterance: the engine stream itself, no lane fork/join
@@ -719,10 +725,22 @@ int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_sc
                            u.noise_mode == 1 ? u.eps : nullptr, u.noise_mode == 2 ? u.noise_seed : 0, noise_scale,
                            u.audio, s);
     }
+    vb_items.assign(it, it + n);
+    if (int r = vits_batch_launch(noise_scale, s, true)) return r;
+    return vits_batch_finish(s);
+}
+
+// Fork the batch in vb_items over the lanes (ordered after stream s) and issue it:
+// each lane's launches by a host thread of its own (a vocoder pass is a few hundred
+// launches, and one thread issuing every lane's would pace the lanes; the per-pass
+// host state -- split-K workspace, overflow flag -- is thread-local).  join: wait
+// for the issuing threads here; otherwise vits_batch_finish joins them.
+int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
+    const int n = (int)vb_items.size();
     const int K = std::min(n, vits_lanes);
     for (int l = (int)vlanes.size(); l < K; ++l) {
         VitsLane L;
-        if (hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking) != hipSuccess ||
+        if (hipStreamCreateWithPriority(&L.st, hipStreamNonBlocking, lane_priority) != hipSuccess ||
             hipEventCreateWithFlags(&L.join, hipEventDisableTiming) != hipSuccess)
             return set_error(GSV_E_HIP, "vocoder lane stream");
         vlanes.push_back(L);
@@ -744,48 +762,59 @@ int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_sc
     hipMemsetAsync(vflags, 0, (size_t)n * 4, s);
     hipEventRecord(vfork, s);
     for (int l = 0; l < K; ++l) hipStreamWaitEvent(vlanes[l].st, vfork, 0);
-    // each lane's launches are issued by a host thread of its own: a vocoder pass is a
-    // few hundred launches, and one thread issuing every lane's would pace the lanes
-    // (the per-pass host state -- split-K workspace, overflow flag -- is thread-local)
-    std::vector<int> rcs(K, 0);
-    auto lane_work = [&](int l) {
+    vb_k = K;
+    vb_scale = noise_scale;
+    vb_rcs.assign(K, 0);
+    auto lane_work = [this, K, n](int l) {
         hipSetDevice(device);
         VitsLane& L = vlanes[l];
         for (int i = l; i < n; i += K) {
-            const gsv_vits_item& u = it[i];
+            const gsv_vits_item& u = vb_items[i];
             if (int r = vits_decode_pass(L.ws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
                                          u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
-                                         u.noise_mode == 2 ? u.noise_seed : 0, noise_scale, u.audio, L.st,
+                                         u.noise_mode == 2 ? u.noise_seed : 0, vb_scale, u.audio, L.st,
                                          use_convh ? vflags + i : nullptr, false)) {
-                rcs[l] = r;
+                vb_rcs[l] = r;
                 return;
             }
         }
+        hipEventRecord(L.join, L.st);
     };
-    if (K == 1 || !vits_threads) {
+    vb_active = true;
+    if (!vits_threads) {
         for (int l = 0; l < K; ++l) lane_work(l);
     } else {
-        std::vector<std::thread> th;
-        for (int l = 1; l < K; ++l) th.emplace_back(lane_work, l);
-        lane_work(0);
-        for (auto& t : th) t.join();
+        for (int l = 0; l < K; ++l) vb_threads.emplace_back(lane_work, l);
+        if (join) {
+            for (auto& t : vb_threads) t.join();
+            vb_threads.clear();
+        }
     }
+    return 0;
+}
+
+// Join the batch: lanes -> stream s (NULL: the engine stream), f32 re-runs of the
+// utterances that met the fp16 range, phase time.
+int gsv_engine::vits_batch_finish(hipStream_t s) {
+    if (!vb_active) return 0;
+    vb_active = false;
+    for (auto& t : vb_threads) t.join();
+    vb_threads.clear();
+    if (!s) s = stream;
+    const int n = (int)vb_items.size(), K = vb_k;
     for (int l = 0; l < K; ++l)
-        if (rcs[l]) return set_error(rcs[l], "vocoder lane " + std::to_string(l) + " failed");
-    for (int l = 0; l < K; ++l) {
-        hipEventRecord(vlanes[l].join, vlanes[l].st);
-        hipStreamWaitEvent(s, vlanes[l].join, 0);
-    }
+        if (vb_rcs[l]) return set_error(vb_rcs[l], "vocoder lane " + std::to_string(l) + " failed");
+    for (int l = 0; l < K; ++l) hipStreamWaitEvent(s, vlanes[l].join, 0);
     if (use_convh) {
         hipMemcpyAsync(vflags_host, vflags, (size_t)n * 4, hipMemcpyDeviceToHost, s);
         if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vocoder batch sync");
         for (int i = 0; i < n; ++i) {
             if (!vflags_host[i]) continue;
             ++vits_f32_reruns;
-            const gsv_vits_item& u = it[i];
+            const gsv_vits_item& u = vb_items[i];
             if (int r = vits_decode_pass(vws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
                                          u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
-                                         u.noise_mode == 2 ? u.noise_seed : 0, noise_scale, u.audio, s, nullptr,
+                                         u.noise_mode == 2 ? u.noise_seed : 0, vb_scale, u.audio, s, nullptr,
                                          false))
                 return r;
         }
@@ -863,12 +892,37 @@ extern "C" int gsv_vits_wait(gsv_engine* eng, void* stream) {
     return eng->vits_wait((hipStream_t)stream);
 }
 
+extern "C" int gsv_vits_decode_batch_async(gsv_engine* eng, int32_t n, const gsv_vits_item* items,
+                                           float noise_scale, void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    if (n <= 0 || !items) return set_error(GSV_E_ARG, "bad args");
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    for (int i = 0; i < n; ++i)
+        if (items[i].noise_mode < 0 || items[i].noise_mode > 2 || (items[i].noise_mode == 1 && !items[i].eps) ||
+            !items[i].audio)
+            return set_error(GSV_E_ARG, "bad vocoder item " + std::to_string(i));
+    if (int r = eng->vits_batch_finish(nullptr)) return r;
+    if (int r = eng->vits_wait(nullptr)) return r;
+    eng->vb_items.assign(items, items + n);
+    // ordered after the caller's stream only: the engine stream stays free for the T2S
+    // of the next batch, which runs beside this one
+    return eng->vits_batch_launch(noise_scale, (hipStream_t)stream, false);
+}
+
+extern "C" int gsv_vits_batch_wait(gsv_engine* eng, void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    hipSetDevice(eng->device);
+    return eng->vits_batch_finish((hipStream_t)stream);
+}
+
 extern "C" int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
                                  const float* sv_emb, float* ge, float* ge_adv, void* stream) {
     if (!eng) return set_error(GSV_E_ARG, "null engine");
     hipSetDevice(eng->device);
     if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
     if (int r = eng->vits_wait(nullptr)) return r;   // shares the vocoder workspace
+    if (int r = eng->vits_batch_finish(nullptr)) return r;
     StreamScope sc(eng, stream);
     return eng->prompt_encode(ref_audio, n_audio, sv_emb, ge, ge_adv, sc.st());
 }

@@ -94,6 +94,8 @@ def lib():
         L.gsv_vits_decode_batch.argtypes = [vp, i32, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
         L.gsv_vits_decode_async.argtypes = [vp, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
         L.gsv_vits_wait.argtypes = [vp, vp]
+        L.gsv_vits_decode_batch_async.argtypes = [vp, i32, ctypes.POINTER(VitsItem), ctypes.c_float, vp]
+        L.gsv_vits_batch_wait.argtypes = [vp, vp]
         L.gsv_t2s_prefetch.argtypes = [vp, ctypes.POINTER(Utt), ctypes.POINTER(Sampler), vp]
         L.gsv_t2s_generate_start.argtypes = [vp, ctypes.POINTER(Utt), ctypes.POINTER(Sampler), vp]
         L.gsv_t2s_generate_finish.argtypes = [vp, vp, i32, vp, vp]
@@ -131,6 +133,7 @@ EXPORTED = (
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
     "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
     "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
+    "gsv_vits_decode_batch_async", "gsv_vits_batch_wait",
 )
 
 
@@ -447,6 +450,26 @@ class Engine:
         _check(lib().gsv_vits_decode_batch(self.h, len(items), arr, ctypes.c_float(noise_scale), _stream()),
                "gsv_vits_decode_batch")
         return outs
+
+    def vits_decode_batch_async(self, items: Sequence[dict], noise_scale: float = 0.5):
+        """vits_decode_batch without the join (gsv_vits_decode_batch_async): the lanes run
+        beside whatever T2S is issued next.  Returns the audio tensors, valid after
+        vits_batch_wait()."""
+        arr = (VitsItem * len(items))()
+        keep, outs = [], []
+        for i, it in enumerate(items):
+            arr[i], k, audio = self._vits_item(it)
+            keep += k
+            outs.append(audio)
+        _check(lib().gsv_vits_decode_batch_async(self.h, len(items), arr, ctypes.c_float(noise_scale),
+                                                 _stream()), "gsv_vits_decode_batch_async")
+        self._vits_batch_keep = (arr, keep, outs)   # items and device buffers live until the wait
+        return outs
+
+    def vits_batch_wait(self):
+        """Finish the pending vits_decode_batch_async; orders the current stream after it."""
+        _check(lib().gsv_vits_batch_wait(self.h, _stream()), "gsv_vits_batch_wait")
+        self._vits_batch_keep = None
 
     vocoder_cus = 0
 

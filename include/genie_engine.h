@@ -164,6 +164,19 @@ typedef struct {
 int gsv_vits_decode_batch(gsv_engine* eng, int32_t n, const gsv_vits_item* items, float noise_scale,
                           void* stream);
 
+/* The same batch, overlapped with the T2S of the next batch (a server batching the
+ * next sentence of every pending request; each sentence a full Inference.tts,
+ * Core/Inference.py:16-61).  gsv_vits_decode_batch_async forks the batch over the
+ * vocoder lanes (ordered after `stream`) and returns while lane threads may still be
+ * issuing; the engine stream stays free, so a gsv_t2s_generate issued next runs
+ * beside it.  Items and their buffers must stay valid until gsv_vits_batch_wait,
+ * which joins the lanes, re-runs fp16-range overflows on the f32 path and orders
+ * `stream` (may be NULL) after the batch.  Any other vocoder call finishes it first.
+ * Audio is identical to gsv_vits_decode_batch's. */
+int gsv_vits_decode_batch_async(gsv_engine* eng, int32_t n, const gsv_vits_item* items, float noise_scale,
+                                void* stream);
+int gsv_vits_batch_wait(gsv_engine* eng, void* stream);
+
 /* Overlapped vocoder for a stream of sentences (the reference synthesises them one
  * after the other: TTSPlayer._tts_worker_loop, Core/TTSPlayer.py:56-107, each
  * sentence a full Inference.tts, Core/Inference.py:16).  After

@@ -121,3 +121,37 @@ def test_vits_batch_lanes_match_single(setup):
     outs = e.vits_decode_batch(items)
     for i, (o, s1) in enumerate(zip(outs, singles)):
         np.testing.assert_array_equal(o.cpu().numpy(), s1, err_msg=f"item {i}")
+
+
+def test_vits_batch_async_beside_t2s(setup):
+    """gsv_vits_decode_batch_async: the lanes run while a batched T2S generate is issued
+    on the engine stream (the pipelined batch mode); audio equals the joined batch call
+    bit for bit and the T2S tokens equal those of the same generate run alone."""
+    from genie_tts_amd import workloads
+    from genie_tts_amd.engine import make_sampler
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    items = []
+    for i, (G, S) in enumerate([(20, 12), (33, 25), (8, 9), (47, 31), (26, 18), (40, 40), (12, 7)]):
+        txt = synth.synth_phones(S, f"va{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (5 + i) + 2 * i) % 1024).reshape(1, 1, G)
+        items.append(dict(text_seq=txt, pred_semantic=sem, noise_seed=2000 + i, **kw))
+    ref_audio = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+    wl = workloads.batch64(12, tag="vba")
+    r = wl.reference
+    utts = [(r.ref_seq, it.text_seq, None, None, r.ssl.reshape(768, -1), it.force_steps) for it in wl.items]
+    sp = make_sampler(top_k=5, greedy=False, seed=0xBA7C)
+    ref_tok = [t.tolist() for t in e.t2s_generate(utts, sp)]
+    for _ in range(2):
+        outs = e.vits_decode_batch_async(items)
+        tok = [t.tolist() for t in e.t2s_generate(utts, sp)]
+        e.vits_batch_wait()
+        assert tok == ref_tok
+        for i, (o, a) in enumerate(zip(outs, ref_audio)):
+            np.testing.assert_array_equal(o.cpu().numpy(), a, err_msg=f"item {i}")
+    # a synchronous vocoder call while a batch is pending finishes the batch first
+    outs = e.vits_decode_batch_async(items)
+    one = e.vits_decode(items[0]["text_seq"], items[0]["pred_semantic"], noise_seed=2000, **kw).cpu().numpy()
+    np.testing.assert_array_equal(one, ref_audio[0])
+    e.vits_batch_wait()
+    np.testing.assert_array_equal(outs[-1].cpu().numpy(), ref_audio[-1])
