@@ -192,6 +192,8 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="batched workloads: 1 = each batch's vocoder beside the next batch's T2S, "
                          "0 = one batch at a time")
+    ap.add_argument("--batch-vocoder-cus", type=int, default=0,
+                    help="batched workloads: CUs of the vocoder lanes (the T2S gets the rest; 0 = shared)")
     ap.add_argument("--lane-priority", type=int, default=None,
                     help="batched workloads: HIP stream priority of the vocoder lanes (lower = first)")
     ap.add_argument("--t2s-priority", type=int, default=None,
@@ -228,6 +230,8 @@ def main():
     run = Runner(wl, items, dev, local if world > 1 else 0)
     if args.vits_lanes:
         run.eng.set_option("vits_lanes", args.vits_lanes)
+    if args.batch_vocoder_cus and args.workload != "single":
+        run.eng.set_vocoder_cus(args.batch_vocoder_cus)
     if args.lane_priority is not None:
         run.eng.set_option("lane_priority", args.lane_priority)
     if args.t2s_priority is not None:

@@ -1676,13 +1676,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         hipDeviceSynchronize();
         if (n == "lane_priority") {
             eng->lane_priority = p;
-            for (auto& L : eng->vlanes) {   // the lanes' streams re-created at the new priority
-                hipStream_t ns = nullptr;
-                if (hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, p) != hipSuccess)
-                    return set_error(GSV_E_HIP, "lane stream");
-                hipStreamDestroy(L.st);
-                L.st = ns;
-            }
+            if (int r = eng->remake_lane_streams()) return r;
         } else {
             if (eng->vocoder_cus || eng->gq_n || !eng->own_stream)
                 return set_error(GSV_E_STATE, "t2s_priority: needs the engine's own unmasked stream, idle");

@@ -256,6 +256,8 @@ struct gsv_engine {
     bool vits_threads = true;          // option "vits_threads": one host thread per vocoder lane
     int lane_priority = 0;             // option "lane_priority": HIP stream priority of the lanes
     int t2s_priority = 0;              // option "t2s_priority": of the engine stream (vocoder_cus 0)
+    hipError_t make_lane_stream(hipStream_t* st);   // on the vocoder CUs under option vocoder_cus
+    int remake_lane_streams();
     int vits_read_ms();
     // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
     int vocoder_cus = 0;

@@ -463,11 +463,33 @@ int gsv_engine::vits_read_ms() {
 // bits [0, K) give the vocoder K / 8 CUs of every XCD and every XCD keeps the
 // (n_cu - K) / 8 CUs its share of the decode grid needs (workgroups go to the
 // XCDs round robin).
+// Lane streams re-created after a change of vocoder_cus / lane_priority (workspaces kept).
+int gsv_engine::remake_lane_streams() {
+    for (auto& L : vlanes) {
+        hipStream_t ns = nullptr;
+        if (make_lane_stream(&ns) != hipSuccess) return set_error(GSV_E_HIP, "lane stream");
+        hipStreamDestroy(L.st);
+        L.st = ns;
+    }
+    return 0;
+}
+
+// A vocoder lane's stream: on the vocoder CUs when option vocoder_cus splits the chip
+// (bits [0, vocoder_cus), as the overlapped single vocoder), else on every CU.
+hipError_t gsv_engine::make_lane_stream(hipStream_t* st) {
+    if (vocoder_cus == 0) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, lane_priority);
+    const int words = (n_cu + 31) / 32;
+    std::vector<uint32_t> mv(words, 0u);
+    for (int i = 0; i < vocoder_cus; ++i) mv[i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(st, (uint32_t)words, mv.data());
+}
+
 int gsv_engine::set_vocoder_cus(int K) {
     if (K != 0 && (K % 8 != 0 || K < 8 || n_cu - K < 3 * persist1_grid(1) || n_cu % 32 != 0))
         return set_error(GSV_E_ARG, "vocoder_cus: a multiple of 8 leaving >= 96 CUs for the decode");
     if (gq_n) return set_error(GSV_E_STATE, "vocoder_cus: finish the started generates first");
     if (int r = vits_wait(nullptr)) return r;
+    if (int r = vits_batch_finish(nullptr)) return r;
     if (int r = pf_drop()) return r;   // a launched prefetch runs on the vocoder stream
     hipDeviceSynchronize();
     hipStream_t ns = nullptr, nv = nullptr;
@@ -490,7 +512,7 @@ int gsv_engine::set_vocoder_cus(int K) {
     own_stream = true;
     vstream = nv;
     vocoder_cus = K;
-    return 0;
+    return remake_lane_streams();
 }
 
 // The call is queued, not launched: its ~400 launches are issued by the next
@@ -740,7 +762,7 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     const int K = std::min(n, vits_lanes);
     for (int l = (int)vlanes.size(); l < K; ++l) {
         VitsLane L;
-        if (hipStreamCreateWithPriority(&L.st, hipStreamNonBlocking, lane_priority) != hipSuccess ||
+        if (make_lane_stream(&L.st) != hipSuccess ||
             hipEventCreateWithFlags(&L.join, hipEventDisableTiming) != hipSuccess)
             return set_error(GSV_E_HIP, "vocoder lane stream");
         vlanes.push_back(L);

@@ -217,11 +217,24 @@ class GENIE:
         (text_seq, text_bert|None[, force_steps]).  All sequences decode together
         (one batched step per token, ragged: a finished sequence drops out); the
         vocoder runs per utterance."""
-        eng = model.ENGINE
+        toks = self.tts_batch_t2s(items, prompt_audio, model, sampler)
+        wavs = self.tts_batch_vocoder(items, toks, prompt_audio, model)
+        return [w if isinstance(w, np.ndarray) else w.cpu().numpy() for w in wavs]
+
+    def tts_batch_t2s(self, items: Sequence[tuple], prompt_audio: ReferenceAudio, model, sampler: Sampler):
+        """The T2S half of tts_batch: one ragged batched generate -> token arrays."""
         ssl = np.asarray(prompt_audio.ssl_content, np.float32).reshape(768, -1)
         utts = [(prompt_audio.phonemes_seq, it[0], prompt_audio.text_bert, it[1], ssl,
                  it[2] if len(it) > 2 else 0) for it in items]
-        toks = eng.t2s_generate(utts, sampler)
+        return model.ENGINE.t2s_generate(utts, sampler)
+
+    def tts_batch_vocoder(self, items: Sequence[tuple], toks, prompt_audio: ReferenceAudio, model,
+                          overlapped: bool = False):
+        """The vocoder half of tts_batch.  overlapped=True (engine-backed vocoder only) starts
+        the batch on the vocoder lanes and returns device tensors that are valid after
+        model.ENGINE.vits_batch_wait(); the T2S of the next batch runs beside it
+        (gsv_vits_decode_batch_async)."""
+        eng = model.ENGINE
         if model.PROMPT_ENCODER is not None:
             prompt_audio.update_global_emb(model.PROMPT_ENCODER)
         cond = ({"ref_audio": prompt_audio.audio_32k} if model.PROMPT_ENCODER is None else
@@ -230,10 +243,11 @@ class GENIE:
             return [model.VITS.run(None, {"text_seq": it[0], "pred_semantic": tok.reshape(1, 1, -1), **cond})[0]
                     for it, tok in zip(items, toks)]
         # engine-backed vocoder: all utterances on concurrent lanes (gsv_vits_decode_batch)
-        wavs = eng.vits_decode_batch([dict(text_seq=it[0], pred_semantic=tok, noise_seed=model.VITS.next_seed(),
-                                           **cond) for it, tok in zip(items, toks)],
-                                     model.VITS.noise_scale)
-        return [w.cpu().numpy() for w in wavs]
+        batch = [dict(text_seq=it[0], pred_semantic=tok, noise_seed=model.VITS.next_seed(), **cond)
+                 for it, tok in zip(items, toks)]
+        if overlapped:
+            return eng.vits_decode_batch_async(batch, model.VITS.noise_scale)
+        return eng.vits_decode_batch(batch, model.VITS.noise_scale)
 
 
 tts_client = GENIE()

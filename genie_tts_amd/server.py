@@ -61,6 +61,7 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
     if cfg.get("greedy"):
         model_manager.sampler = make_sampler(greedy=True)
     splitter = TextSplitter()
+    pipeline = bool(cfg.get("pipeline", True))
     pending: List[dict] = []        # tts requests: {"id", "character_name", "sentences", "next", "force_steps"}
 
     def reply(**kw):
@@ -68,6 +69,7 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
 
     def control(msg) -> None:
         cmd = msg["cmd"]
+        finish_inflight()            # control calls may replace what the overlapped vocoder uses
         try:
             if cmd == "load_character":
                 genie.load_character(msg["character_name"], msg["onnx_model_dir"], msg["language"])
@@ -104,10 +106,47 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
                         "force_steps": int(msg.get("force_steps") or 0), "save_path": msg.get("save_path"),
                         "chunks": []})
 
+    inflight: List[tuple] = []      # [(group, sentence indexes, wavs, engine)] of the overlapped vocoder
+
+    def finish_inflight() -> None:
+        """Join the overlapped vocoder of the previous round and stream its chunks."""
+        if not inflight:
+            return
+        group, idx, wavs, eng = inflight.pop()
+        try:
+            if eng is not None:
+                eng.vits_batch_wait()
+            wavs = [w if isinstance(w, np.ndarray) else w.cpu().numpy() for w in wavs]
+        except Exception as e:       # noqa: BLE001
+            for r in group:
+                reply(kind="error", id=r["id"], detail=f"{type(e).__name__}: {e}")
+                if r in pending:
+                    pending.remove(r)
+            return
+        for r, i, wav in zip(group, idx, wavs):
+            if r not in pending:      # failed or stopped meanwhile
+                continue
+            reply(kind="chunk", id=r["id"], data=A.to_pcm16(wav))
+            r["chunks"].append(np.asarray(wav, np.float32).reshape(-1))
+            r["done"] = i + 1
+            if r["done"] == len(r["sentences"]):
+                if r["save_path"]:
+                    A.write_wav(r["save_path"], np.concatenate(r["chunks"]))
+                reply(kind="end", id=r["id"])
+                pending.remove(r)
+
     def run_round() -> None:
-        """The next sentence of up to MAX_BATCH pending requests of one character."""
-        name = pending[0]["character_name"]
-        group = [r for r in pending if r["character_name"] == name][:MAX_BATCH]
+        """The next sentence of up to MAX_BATCH pending requests of one character.  With
+        cfg["pipeline"] (default) this round's T2S runs beside the previous round's vocoder
+        (gsv_vits_decode_batch_async), whose chunks are streamed once this T2S is done;
+        with nothing left to start, the vocoder is joined at once (no added latency)."""
+        ready = [r for r in pending if r["next"] < len(r["sentences"])]
+        if not ready:
+            finish_inflight()
+            return
+        name = ready[0]["character_name"]
+        group = [r for r in ready if r["character_name"] == name][:MAX_BATCH]
+        idx = [r["next"] for r in group]
         try:
             m = model_manager.get(name)
             ref = api._reference_audios.get(name)
@@ -118,26 +157,28 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
                 ts, tb = api._g2p("。" + r["sentences"][r["next"]], m.LANGUAGE)      # Inference.py:27-28
                 items.append((ts, tb, r["force_steps"]))
             tts_client.stop_event.clear()
-            wavs = tts_client.tts_batch(items, ref, m, m.T2S_FIRST_STAGE_DECODER.sampler)
+            toks = tts_client.tts_batch_t2s(items, ref, m, m.T2S_FIRST_STAGE_DECODER.sampler)
+            finish_inflight()
+            eng = m.ENGINE if getattr(m.VITS, "engine", None) is m.ENGINE else None
+            overlapped = pipeline and eng is not None
+            wavs = tts_client.tts_batch_vocoder(items, toks, ref, m, overlapped=overlapped)
         except Exception as e:       # noqa: BLE001
+            finish_inflight()
             for r in group:
                 reply(kind="error", id=r["id"], detail=f"{type(e).__name__}: {e}")
-                pending.remove(r)
+                if r in pending:
+                    pending.remove(r)
             return
-        for r, wav in zip(group, wavs):
-            reply(kind="chunk", id=r["id"], data=A.to_pcm16(wav))
-            r["chunks"].append(np.asarray(wav, np.float32).reshape(-1))
+        for r in group:
             r["next"] += 1
-            if r["next"] == len(r["sentences"]):
-                if r["save_path"]:
-                    A.write_wav(r["save_path"], np.concatenate(r["chunks"]))
-                reply(kind="end", id=r["id"])
-                pending.remove(r)
+        inflight.append((group, idx, wavs, eng if overlapped else None))
+        if not overlapped:
+            finish_inflight()
 
     reply(kind="ready", id=-1, index=index)
     while True:
         # block only when idle; otherwise drain what has arrived, then run one round
-        while not pending or conn.poll():
+        while (not pending and not inflight) or conn.poll():
             msg = conn.recv()
             if msg is None:
                 return
