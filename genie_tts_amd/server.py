@@ -61,7 +61,7 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
     if cfg.get("greedy"):
         model_manager.sampler = make_sampler(greedy=True)
     splitter = TextSplitter()
-    pipeline = bool(cfg.get("pipeline", True))
+    pipeline = bool(cfg.get("pipeline", False))
     pending: List[dict] = []        # tts requests: {"id", "character_name", "sentences", "next", "force_steps"}
 
     def reply(**kw):
@@ -137,9 +137,11 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
 
     def run_round() -> None:
         """The next sentence of up to MAX_BATCH pending requests of one character.  With
-        cfg["pipeline"] (default) this round's T2S runs beside the previous round's vocoder
-        (gsv_vits_decode_batch_async), whose chunks are streamed once this T2S is done;
-        with nothing left to start, the vocoder is joined at once (no added latency)."""
+        cfg["pipeline"] this round's T2S runs beside the previous round's vocoder
+        (gsv_vits_decode_batch_async), whose chunks are streamed once this T2S is done; with
+        nothing left to start, the vocoder is joined at once.  Off by default: measured on
+        one MI355X it raised p50 first audio (50 QPS: 47 -> 58 ms) without raising the
+        saturated rate (profiles/r02g_server_qps_pipeline.json)."""
         ready = [r for r in pending if r["next"] < len(r["sentences"])]
         if not ready:
             finish_inflight()
@@ -196,10 +198,10 @@ class Router:
     """Owns the worker processes; never touches the GPU itself."""
 
     def __init__(self, gpus: List[int], g2p: Optional[str] = None, ssl: Optional[str] = None,
-                 sv: Optional[str] = None, greedy: bool = False, worker=None):
+                 sv: Optional[str] = None, greedy: bool = False, worker=None, pipeline: bool = False):
         self.gpus = gpus
         self.worker = worker or _worker_main         # tests substitute a host-only worker
-        self.cfg = {"g2p": g2p, "ssl": ssl, "sv": sv, "greedy": greedy}
+        self.cfg = {"g2p": g2p, "ssl": ssl, "sv": sv, "greedy": greedy, "pipeline": pipeline}
         self.ids = itertools.count(1)
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.queues: Dict[int, asyncio.Queue] = {}

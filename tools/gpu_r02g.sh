@@ -1,7 +1,6 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_batch64_gpu.py tests/test_t2s_gpu.py > gpurun_out/r02g_t3.log 2>&1
-for a in "1" "0"; do
-timeout -k 10 200 python bench.py --workload batch64 --steps 8 --warmup 2 --pipeline $a --no-cpu-baseline > gpurun_out/o.json 2>> gpurun_out/r02g_b64.err
-echo "pipe $a $(cat gpurun_out/o.json)" >> gpurun_out/r02g_attn.txt
+bash tools/gpu_round.sh r02g pmc
+for p in 1 0; do
+timeout -k 10 400 python tools/qps_sweep.py --qps 5,20,50,100,200 --requests 120 --pipeline $p > gpurun_out/r02g_qps_p$p.json 2> gpurun_out/r02g_qps_p$p.err
 done

@@ -6,7 +6,7 @@ throughput.  Synthetic V2 character (seeded weights, no checkpoints offline), to
 G2P / SSL stand-ins (genie_tts_amd/stubs.py); every sentence is forced to 81 loop
 steps = 80 semantic tokens = 3.2 s of audio (random weights never emit EOS).
 
-Usage: python tools/qps_sweep.py [--gpus N] [--qps 5,10,20,40,80] [--requests 60]
+Usage: python tools/qps_sweep.py [--gpus N] [--qps 5,10,20,40,80] [--requests 60] [--pipeline 0|1]
 Prints one JSON line.
 """
 import argparse
@@ -37,10 +37,12 @@ async def main():
     ap.add_argument("--qps", default="5,10,20,40,80,160")
     ap.add_argument("--requests", type=int, default=60)
     ap.add_argument("--port", type=int, default=8765)
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="workers overlap each round's vocoder with the next round's T2S")
     a = ap.parse_args()
 
     router = Router(list(range(a.gpus)), g2p="genie_tts_amd.stubs:toy_g2p", ssl="genie_tts_amd.stubs:toy_ssl",
-                    greedy=True)
+                    greedy=True, pipeline=bool(a.pipeline))
     loop = asyncio.get_running_loop()
     t0 = time.time()
     router.start(loop)
