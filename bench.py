@@ -151,26 +151,36 @@ class Runner:
         return sems, n
 
     def step_pipelined(self):
-        """One batch with its vocoder overlapped: this batch's T2S runs beside the previous
-        batch's vocoder lanes (gsv_vits_decode_batch_async), then that vocoder is joined and
-        this batch's is started.  drain() joins the last one."""
-        t0 = time.perf_counter()
-        utts = [(self.d_ref, t, self.d_ref_bert, b, self.d_ssl, it.force_steps)
-                for t, b, it in zip(self.d_txt, self.d_bert, self.items)]
-        sems = self.eng.t2s_generate(utts, self.sp)
-        t1 = time.perf_counter()
-        tm = self.eng.timing()
-        self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
-        self.phase["decode"] += tm[2] * 1e-3
-        self.drain()
-        t2 = time.perf_counter()
+        """One pass over the workload with the vocoder overlapped: the items go in balanced
+        batches of <= 64 (the engine's decode batch); each batch's T2S runs beside the
+        previous batch's vocoder lanes (gsv_vits_decode_batch_async), then that vocoder is
+        joined and this batch's is started.  drain() joins the last one."""
+        n = len(self.items)
+        nb = -(-n // 64)
+        bounds = [n * j // nb for j in range(nb + 1)]
         cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
-        wavs = self.eng.vits_decode_batch_async([dict(text_seq=t, pred_semantic=sem, noise_seed=self.seed + i, **cond)
-                                                 for i, (t, sem) in enumerate(zip(self.d_txt, sems))])
-        self.batch_pending = True
-        self.phase["t2s"] += t1 - t0
-        self.phase["vits"] += t2 - t1      # the host's wait for the previous vocoder (not hidden)
-        return sems, sum(int(w.numel()) for w in wavs)
+        sems_all, n_samples = [], 0
+        for j in range(nb):
+            lo, hi = bounds[j], bounds[j + 1]
+            t0 = time.perf_counter()
+            utts = [(self.d_ref, self.d_txt[i], self.d_ref_bert, self.d_bert[i], self.d_ssl, self.items[i].force_steps)
+                    for i in range(lo, hi)]
+            sems = self.eng.t2s_generate(utts, self.sp)
+            t1 = time.perf_counter()
+            tm = self.eng.timing()
+            self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
+            self.phase["decode"] += tm[2] * 1e-3
+            self.drain()
+            t2 = time.perf_counter()
+            wavs = self.eng.vits_decode_batch_async(
+                [dict(text_seq=self.d_txt[lo + i], pred_semantic=sem, noise_seed=self.seed + lo + i, **cond)
+                 for i, sem in enumerate(sems)])
+            self.batch_pending = True
+            self.phase["t2s"] += t1 - t0
+            self.phase["vits"] += t2 - t1      # the host's wait for the previous vocoder (not hidden)
+            sems_all += sems
+            n_samples += sum(int(w.numel()) for w in wavs)
+        return sems_all, n_samples
 
     def drain(self):
         if getattr(self, "batch_pending", False):
