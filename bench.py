@@ -188,6 +188,38 @@ class Runner:
             self.batch_pending = False
 
 
+def concurrent_streams(args):
+    """The single-utterance workload as S concurrent sentence streams on this one GPU: S
+    child ranks (torch.distributed.run, gloo barrier + max time), each an engine whose
+    persistent decode runs on 96 CUs of its own and whose vocoder + next prefill share the
+    vocoder CUs.  Throughput of the GPU under concurrent single-utterance requests; the
+    headline stays the single stream (north_star: single-stream real time)."""
+    import socket
+    import subprocess
+    S = args.concurrent_streams
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={S}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__),
+           "--streams-per-gpu", str(S), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--vocoder-cus", "64", "--decode-cus", "96", "--no-cpu-baseline"]
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        d = json.loads(line)
+    except Exception as e:   # reported, never fatal to the headline line
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    return {"streams": S, "utt_s": d["value"], "x_realtime": d["value"] * d["audio_s_per_step"],
+            "ms_per_utt_per_stream": d["ms_per_step"], "decode_cus_per_stream": 96, "vocoder_cus_shared": 64,
+            "persist_timeouts": d["config"]["persist_timeouts"],
+            "note": f"{S} sentence streams on one GPU, one rank each, decode CUs disjoint (CU-masked "
+                    "persistent decode), vocoder + prefetch CUs shared"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,6 +231,16 @@ def main():
                     help="batched workloads: concurrent vocoder streams (0 = the engine default)")
     ap.add_argument("--vocoder-cus", type=int, default=64,
                     help="single workload: CUs reserved for the overlapped vocoder (0 = sequential)")
+    ap.add_argument("--decode-cus", type=int, default=0,
+                    help="single workload: CUs of the decode (0 = all but the vocoder's)")
+    ap.add_argument("--decode-cu-offset", type=int, default=0,
+                    help="single workload: first decode CU past the vocoder CUs")
+    ap.add_argument("--streams-per-gpu", type=int, default=1,
+                    help="single workload under torchrun: S ranks share one GPU, each decoding on "
+                         "--decode-cus CUs of its own (offset rank %% S x decode-cus) beside the shared vocoder CUs")
+    ap.add_argument("--concurrent-streams", type=int, default=2,
+                    help="single workload, N=1: also time this many sentence streams sharing the GPU "
+                         "(child ranks, --streams-per-gpu) and report them beside the headline (0/1 = off)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="batched workloads: 1 = each batch's vocoder beside the next batch's T2S, "
                          "0 = one batch at a time")
@@ -213,6 +255,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    sub = local % args.streams_per_gpu          # stream index on this GPU
+    local //= args.streams_per_gpu              # the GPU
     import torch
     dist = None
     if world > 1:
@@ -252,6 +296,8 @@ def main():
     pipelined = not timed_single and args.pipeline > 0
     step = run.step_pipelined if pipelined else run.step
     if overlap:
+        run.eng.set_option("decode_cus", args.decode_cus)
+        run.eng.set_option("decode_cu_offset", args.decode_cu_offset + sub * args.decode_cus)
         run.eng.set_vocoder_cus(args.vocoder_cus)
         sems, n_samples = run.stream(max(1, args.warmup))
     else:
@@ -310,7 +356,7 @@ def main():
         "metric": METRIC,
         "value": utt_s,
         "unit": "utt/s",
-        "n_gpus": world,
+        "n_gpus": world // args.streams_per_gpu,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -333,6 +379,8 @@ def main():
                          "loop_steps": it.force_steps, "semantic_tokens": tokens[0],
                          "samples": n_samples, "parallelism": f"replicas x{world}",
                          "vocoder_cus": args.vocoder_cus,
+                         "streams_per_gpu": args.streams_per_gpu,
+                         "decode_cus": args.decode_cus or None,
                          "persist_timeouts": run.eng.counter("persist_timeouts"),
                          "vits_f32_reruns": run.eng.counter("vits_f32_reruns")}
         out["roofline"] = roof
@@ -371,6 +419,8 @@ def main():
                                "sample": f"1 full utterance ({cs} samples) of the same workload, "
                                          f"oracle/restate.py torch-fp32 on {model}",
                                "rtf": cdt / (cs / SR)}
+    if (rank == 0 and world == 1 and overlap and args.concurrent_streams > 1 and args.streams_per_gpu == 1):
+        out["concurrent_streams"] = concurrent_streams(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

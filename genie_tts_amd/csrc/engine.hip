@@ -1692,6 +1692,16 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->vits_threads = value != 0;
     } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)
         eng->spin_wait = value != 0;
+    } else if (n == "decode_cus" || n == "decode_cu_offset") {   // see gsv_engine::decode_cus
+        if (value < 0) return set_error(GSV_E_ARG, n + ": >= 0");
+        const int save_d = eng->dec_cus_opt, save_o = eng->dec_cu_off;
+        (n == "decode_cus" ? eng->dec_cus_opt : eng->dec_cu_off) = value;
+        if (eng->vocoder_cus)
+            if (int r = eng->set_vocoder_cus(eng->vocoder_cus)) {
+                eng->dec_cus_opt = save_d;
+                eng->dec_cu_off = save_o;
+                return r;
+            }
     } else if (n == "vocoder_cus") {   // overlapped vocoder: CUs reserved for gsv_vits_decode_async
         return eng->set_vocoder_cus(value);
     } else if (n == "convh") {

@@ -272,7 +272,13 @@ struct gsv_engine {
     int vits_wait(hipStream_t caller);
     int vits_launch_queued(hipStream_t s = nullptr);
     hipStream_t vlast = nullptr;       // stream the pending vocoder call was launched on
-    int decode_cus() const { return n_cu - vocoder_cus; }   // CUs of the engine (T2S) stream
+    // CUs of the engine (T2S) stream: under vocoder_cus K the mask bits [K + dec_cu_off, +decode_cus())
+    // (options "decode_cus" / "decode_cu_offset": several engines, e.g. one per process, can
+    // share the vocoder CUs [0, K) while each decodes on CUs of its own)
+    int dec_cus_opt = 0, dec_cu_off = 0;
+    int decode_cus() const {
+        return vocoder_cus == 0 ? n_cu : dec_cus_opt > 0 ? dec_cus_opt : n_cu - vocoder_cus - dec_cu_off;
+    }
     // T2S prefetch (gsv_t2s_prefetch): encode + prefill of the next utterance into
     // slot 1 on the vocoder CUs while slot 0 decodes; taken into slot 0 by the
     // generate it was made for

@@ -487,6 +487,10 @@ hipError_t gsv_engine::make_lane_stream(hipStream_t* st) {
 int gsv_engine::set_vocoder_cus(int K) {
     if (K != 0 && (K % 8 != 0 || K < 8 || n_cu - K < 3 * persist1_grid(1) || n_cu % 32 != 0))
         return set_error(GSV_E_ARG, "vocoder_cus: a multiple of 8 leaving >= 96 CUs for the decode");
+    const int D = dec_cus_opt > 0 ? dec_cus_opt : n_cu - K - dec_cu_off;
+    if (K != 0 && (dec_cu_off % 8 != 0 || D % 32 != 0 || D < 3 * persist1_grid(1) || K + dec_cu_off + D > n_cu))
+        return set_error(GSV_E_ARG, "decode_cus / decode_cu_offset: a multiple of 32 (>= 96) CUs at a multiple "
+                                    "of 8 past the vocoder CUs, within the chip");
     if (gq_n) return set_error(GSV_E_STATE, "vocoder_cus: finish the started generates first");
     if (int r = vits_wait(nullptr)) return r;
     if (int r = vits_batch_finish(nullptr)) return r;
@@ -498,7 +502,10 @@ int gsv_engine::set_vocoder_cus(int K) {
     } else {
         const int words = (n_cu + 31) / 32;
         std::vector<uint32_t> mt(words, 0u), mv(words, 0u);
-        for (int i = 0; i < n_cu; ++i) (i < K ? mv : mt)[i / 32] |= 1u << (i % 32);
+        for (int i = 0; i < n_cu; ++i) {
+            if (i < K) mv[i / 32] |= 1u << (i % 32);
+            else if (i >= K + dec_cu_off && i < K + dec_cu_off + D) mt[i / 32] |= 1u << (i % 32);
+        }
         if (hipExtStreamCreateWithCUMask(&ns, (uint32_t)words, mt.data()) != hipSuccess ||
             hipExtStreamCreateWithCUMask(&nv, (uint32_t)words, mv.data()) != hipSuccess)
             return set_error(GSV_E_HIP, "CU-masked stream");

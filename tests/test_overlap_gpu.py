@@ -192,3 +192,36 @@ def test_async_generate_fp16_guard_reruns(eng):
     assert eng.counter("persist1_f16_reruns") > n0
     with pytest.raises(EngineError, match="no generate in flight"):
         eng.t2s_generate_finish()
+
+
+@pytest.mark.parametrize("D,off", [(96, 0), (96, 96), (128, 32)])
+def test_decode_cu_range(eng, D, off):
+    """Options decode_cus / decode_cu_offset (several sentence streams sharing one GPU,
+    bench.py --streams-per-gpu): the persistent decode on D CUs at an offset past the
+    vocoder CUs gives the golden tokens, with no residency timeout."""
+    from genie_tts_amd.engine import EngineError, make_sampler
+    t, nom, v = gold("t2s_nominal81.npz"), gold("t2s_nominal.npz"), gold("vits_v2_g80.npz")
+    smp = make_sampler(force_steps=len(t["step_tokens"]))
+    utt = (nom["ref_seq"], nom["text_seq"], None, None, nom["ssl"])
+    eng.set_vocoder_cus(0)
+    t0 = eng.counter("persist_timeouts")
+    try:
+        eng.set_option("decode_cus", D)
+        eng.set_option("decode_cu_offset", off)
+        eng.set_vocoder_cus(64)
+        for i in range(2):
+            out = eng.t2s_generate([utt], smp)
+            np.testing.assert_array_equal(out[0], t["pred_semantic"].reshape(-1))
+            if i:
+                eng.vits_wait()
+            eng.vits_decode_async(dict(text_seq=v["text_seq"], pred_semantic=v["pred_semantic"],
+                                       ref_audio=v["ref_audio"], noise_seed=int(v["noise_seed"])))
+        eng.vits_wait()
+        assert eng.counter("persist_timeouts") == t0
+        for bad in (("decode_cus", 80), ("decode_cus", 224), ("decode_cu_offset", 4), ("decode_cu_offset", 160)):
+            with pytest.raises(EngineError, match="decode_cu"):
+                eng.set_option(*bad)
+    finally:
+        eng.set_vocoder_cus(0)
+        eng.set_option("decode_cus", 0)
+        eng.set_option("decode_cu_offset", 0)

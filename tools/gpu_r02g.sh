@@ -1,6 +1,4 @@
 set -e
 mkdir -p gpurun_out
-bash tools/gpu_round.sh r02g pmc
-for p in 1 0; do
-timeout -k 10 400 python tools/qps_sweep.py --qps 5,20,50,100,200 --requests 120 --pipeline $p > gpurun_out/r02g_qps_p$p.json 2> gpurun_out/r02g_qps_p$p.err
-done
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_overlap_gpu.py > gpurun_out/r02g_t5.log 2>&1
+timeout -k 10 400 python bench.py > gpurun_out/r02g_bench2.json 2> gpurun_out/r02g_bench2.err
