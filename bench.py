@@ -91,6 +91,8 @@ class Runner:
         self.ge = self.ge_adv = None
         if wl.version != "v2":
             self.ge, self.ge_adv = self.eng.prompt_encode(self.d_audio, T(ref.sv_emb.reshape(-1)))
+        else:   # the vocoder's reference branch once per reference (gsv_ref_encode), as the API does
+            self.ge_v2 = self.eng.ref_encode(self.d_audio)
         self.eng.set_option("persist", 1)
         self.phase = {"t2s": 0.0, "vits": 0.0, "encode+prefill": 0.0, "decode": 0.0}
 
@@ -104,7 +106,7 @@ class Runner:
         if getattr(self, "utt", None) is None:
             self.utt = (self.d_ref, self.d_txt[0], self.d_ref_bert, self.d_bert[0], self.d_ssl,
                         self.items[0].force_steps)
-        cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
+        cond = dict(ge=self.ge_v2) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
         eng.t2s_prefetch(self.utt, self.sp)   # (the stream's utterances are all the same one here)
         eng.t2s_generate_start(self.utt, self.sp)
         sems = None
@@ -137,7 +139,7 @@ class Runner:
         self.phase["encode+prefill"] += (tm[0] + tm[1]) * 1e-3
         self.phase["decode"] += tm[2] * 1e-3
         # vocoder with the reference's z_p noise (RandomNormalLike x 0.5) from the device Philox stream
-        cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
+        cond = dict(ge=self.ge_v2) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
         if len(sems) == 1:
             wavs = [self.eng.vits_decode(self.d_txt[0], sems[0], noise_seed=self.seed, **cond)]
         else:   # concurrent vocoder lanes
@@ -158,7 +160,7 @@ class Runner:
         n = len(self.items)
         nb = -(-n // 64)
         bounds = [n * j // nb for j in range(nb + 1)]
-        cond = dict(ref_audio=self.d_audio) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
+        cond = dict(ge=self.ge_v2) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
         sems_all, n_samples = [], 0
         for j in range(nb):
             lo, hi = bounds[j], bounds[j + 1]

@@ -259,6 +259,7 @@ struct gsv_engine {
     hipError_t make_lane_stream(hipStream_t* st);   // on the vocoder CUs under option vocoder_cus
     int remake_lane_streams();
     int vits_read_ms();
+    int ref_encode(const float* ref_audio, int n_audio, float* ge, hipStream_t s);
     // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
     int vocoder_cus = 0;
     hipStream_t vstream = nullptr;     // vocoder: K CUs (the engine stream: the other n_cu - K)

@@ -597,7 +597,8 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     if (!V.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
     if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
     const bool pp = version == GSV_V2PP;
-    if (pp ? (!ge_in || !ge_adv_in) : !ref_audio) return set_error(GSV_E_ARG, "missing conditioning input");
+    if (pp ? (!ge_in || !ge_adv_in) : (!ref_audio && !ge_in))
+        return set_error(GSV_E_ARG, "missing conditioning input");
     const int T = 2 * G, S = n_text;
     if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, W, T, S, pp ? 0 : n_audio)) return r;
@@ -609,7 +610,10 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
     const float* ge;
     const float* ge_m;
-    if (!pp) {
+    if (!pp && ge_in) {   // V2 with the reference's ge from gsv_ref_encode (once per reference)
+        ge = ge_in;
+        ge_m = ge_in;
+    } else if (!pp) {
         run_ref_enc(W, V.ref, ref_audio, n_audio, W.ge, s);
         ge = W.ge;
         ge_m = W.ge;
@@ -856,6 +860,20 @@ int gsv_engine::vits_batch_finish(hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vocoder batch");
 }
 
+// V2: the reference encoder alone (vits(v2)#79-271: ref spectrogram -> MelStyleEncoder ->
+// ge [512]); it depends on the reference audio only, so a caller synthesising many
+// sentences against one reference computes it once and passes it as gsv_vits_item.ge.
+int gsv_engine::ref_encode(const float* ref_audio, int n_audio, float* ge, hipStream_t s) {
+    if (!vits.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
+    if (version == GSV_V2PP) return set_error(GSV_E_STATE, "V2ProPlus: use gsv_prompt_encode");
+    if (n_audio < 2048) return set_error(GSV_E_ARG, "reference audio too short");
+    if (int r = ensure_vits_ws(this, vws, 2, 2, n_audio)) return r;
+    SplitkScope sk(vws.splitk, vws.splitk_cap);
+    (void)hipGetLastError();
+    run_ref_enc(vws, vits.ref, ref_audio, n_audio, ge, s);
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "reference encoder launch");
+}
+
 int gsv_engine::prompt_encode(const float* ref_audio, int n_audio, const float* sv_emb, float* ge,
                               float* ge_adv, hipStream_t s) {
     if (!penc.ready) return set_error(GSV_E_STATE, "prompt encoder weights not loaded");
@@ -943,6 +961,17 @@ extern "C" int gsv_vits_batch_wait(gsv_engine* eng, void* stream) {
     if (!eng) return set_error(GSV_E_ARG, "null engine");
     hipSetDevice(eng->device);
     return eng->vits_batch_finish((hipStream_t)stream);
+}
+
+extern "C" int gsv_ref_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio, float* ge, void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    if (!ref_audio || !ge) return set_error(GSV_E_ARG, "bad args");
+    hipSetDevice(eng->device);
+    if (!eng->finalized) return set_error(GSV_E_STATE, "weights not finalized");
+    if (int r = eng->vits_wait(nullptr)) return r;   // shares the vocoder workspace
+    if (int r = eng->vits_batch_finish(nullptr)) return r;
+    StreamScope sc(eng, stream);
+    return eng->ref_encode(ref_audio, n_audio, ge, sc.st());
 }
 
 extern "C" int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,

@@ -100,6 +100,7 @@ def lib():
         L.gsv_t2s_generate_start.argtypes = [vp, ctypes.POINTER(Utt), ctypes.POINTER(Sampler), vp]
         L.gsv_t2s_generate_finish.argtypes = [vp, vp, i32, vp, vp]
         L.gsv_prompt_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.gsv_ref_encode.argtypes = [vp, vp, i32, vp, vp]
         L.gsv_debug_copy.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int64, vp]
         L.gsv_debug_conv1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
@@ -133,7 +134,7 @@ EXPORTED = (
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
     "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
     "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
-    "gsv_vits_decode_batch_async", "gsv_vits_batch_wait",
+    "gsv_vits_decode_batch_async", "gsv_vits_batch_wait", "gsv_ref_encode",
 )
 
 
@@ -491,6 +492,15 @@ class Engine:
         """Finish the pending vits_decode_async call; orders the current stream after it."""
         _check(lib().gsv_vits_wait(self.h, _stream()), "gsv_vits_wait")
         self._vits_keep = None
+
+    def ref_encode(self, ref_audio):
+        """V2: the vocoder's reference branch alone (gsv_ref_encode) -> ge [512] on the device;
+        pass it as ge= (without ref_audio) to every vocoder call against this reference."""
+        t = self.torch
+        ra = self._dev(ref_audio, t.float32).reshape(-1)
+        ge = t.empty((512,), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_ref_encode(self.h, _ptr(ra), ra.numel(), _ptr(ge), _stream()), "gsv_ref_encode")
+        return ge
 
     def prompt_encode(self, ref_audio, sv_emb):
         t = self.torch

@@ -130,7 +130,8 @@ class GENIE:
         if eng.vocoder_cus != vocoder_cus:
             eng.set_vocoder_cus(vocoder_cus)
         if prompt_encoder is None:
-            cond = {"ref_audio": prompt_audio.audio_32k}
+            cond = (vocoder.v2_cond(prompt_audio.audio_32k) if getattr(vocoder, "engine", None) is eng
+                    else {"ref_audio": prompt_audio.audio_32k})
         else:
             prompt_audio.update_global_emb(prompt_encoder)
             cond = {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced}
@@ -239,6 +240,8 @@ class GENIE:
             prompt_audio.update_global_emb(model.PROMPT_ENCODER)
         cond = ({"ref_audio": prompt_audio.audio_32k} if model.PROMPT_ENCODER is None else
                 {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced})
+        if model.PROMPT_ENCODER is None and getattr(model.VITS, "engine", None) is eng:
+            cond = model.VITS.v2_cond(prompt_audio.audio_32k)   # the reference branch once per reference
         if getattr(model.VITS, "engine", None) is not eng:
             return [model.VITS.run(None, {"text_seq": it[0], "pred_semantic": tok.reshape(1, 1, -1), **cond})[0]
                     for it, tok in zip(items, toks)]

@@ -16,6 +16,7 @@
  *   the 500-step loop + trim (Inference.py:95-109)   gsv_t2s_generate (on device, hipGraph)
  *   vocoder.run            (Inference.py:47-60)      gsv_vits_decode
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
+ *   vocoder.run's refer branch (Inference.py:50, V2)  gsv_ref_encode (once per reference)
  *   cn_hubert.run          (ReferenceAudio.py:50-52) gsv_hubert
  *   roberta_model.run      (GetPhonesAndBert.py:73)  gsv_roberta
  *   per-sentence tts loop  (TTSPlayer.py:56-107)     gsv_t2s_prefetch, gsv_t2s_generate_start /
@@ -136,7 +137,8 @@ int gsv_t2s_read_kv(gsv_engine* eng, int seq, int layer, float* k, float* v, int
 
 /* --------------------------------------------------------------- VITS ---- */
 /* vits_fp32.onnx.  text_seq (device i64 [n_text]), sem (device i64 [n_sem]).
- * V2: ref_audio (device f32 [n_audio] at 32 kHz), ge/ge_adv NULL.
+ * V2: ref_audio (device f32 [n_audio] at 32 kHz), ge/ge_adv NULL; or ref_audio NULL and
+ *     ge (device [512]) from gsv_ref_encode of that audio (identical output).
  * V2ProPlus: ge (device [1024]), ge_adv (device [512]), ref_audio NULL.
  * eps: (device [192, 2*n_sem]) noise for z_p, or NULL => zeros.
  * audio (device f32 [640*2*n_sem]). */
@@ -154,8 +156,9 @@ int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
 typedef struct {
     const int64_t* text_seq; int32_t n_text;   /* device */
     const int64_t* sem;      int32_t n_sem;    /* device */
-    const float* ref_audio;  int32_t n_audio;  /* V2: device 32 kHz audio, else NULL */
-    const float* ge;         const float* ge_adv;   /* V2ProPlus: device [1024], [512] */
+    const float* ref_audio;  int32_t n_audio;  /* V2: device 32 kHz audio (or NULL with ge), else NULL */
+    const float* ge;         const float* ge_adv;   /* V2ProPlus: device [1024], [512];
+                                                       V2: optional ge [512] of gsv_ref_encode */
     const float* eps;                          /* noise_mode 1 */
     uint64_t noise_seed;                       /* noise_mode 2 */
     int32_t noise_mode;
@@ -213,6 +216,13 @@ int gsv_t2s_prefetch(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* sam
 int gsv_t2s_generate_start(gsv_engine* eng, const gsv_utt* utt, const gsv_sampler* sampler, void* stream);
 int gsv_t2s_generate_finish(gsv_engine* eng, int64_t* out_tokens, int32_t out_stride, int32_t* out_len,
                             void* stream);
+
+/* V2: the vocoder graph's reference branch alone (vits_fp32.onnx(v2)#79-271: refer
+ * spectrogram -> MelStyleEncoder; ReferenceAudio.py:40-45 feeds it the 32 kHz audio on
+ * every vocoder.run) -> ge (device [512]).  It depends on the reference only: pass it as
+ * the ge of gsv_vits_decode or of a gsv_vits_item, with ref_audio NULL, for every sentence spoken
+ * against that reference; the audio is identical to passing ref_audio. */
+int gsv_ref_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio, float* ge, void* stream);
 
 /* prompt_encoder_fp32.onnx (V2ProPlus): ref_audio (device [n_audio]),
  * sv_emb (device [20480]) -> ge (device [1024]), ge_adv (device [512]). */

@@ -155,3 +155,32 @@ def test_vits_batch_async_beside_t2s(setup):
     np.testing.assert_array_equal(one, ref_audio[0])
     e.vits_batch_wait()
     np.testing.assert_array_equal(outs[-1].cpu().numpy(), ref_audio[-1])
+
+
+def test_v2_ref_encode_once(setup):
+    """gsv_ref_encode: the V2 vocoder's reference branch computed once and passed as ge
+    gives the same audio, bit for bit, as passing the reference audio to every call
+    (single, batched lanes and the overlapped batch); V2ProPlus rejects it."""
+    from genie_tts_amd.engine import EngineError
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    if ver != "v2":
+        with pytest.raises(EngineError, match="prompt_encode"):
+            e.ref_encode(synth.synth_ref_audio(32000 * 2 + 1234))
+        return
+    ge = e.ref_encode(kw["ref_audio"])
+    assert ge.shape == (512,)
+    items = []
+    for i, (G, S) in enumerate([(20, 12), (33, 25), (8, 9)]):
+        txt = synth.synth_phones(S, f"vr{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (3 + i) + i) % 1024).reshape(1, 1, G)
+        items.append(dict(text_seq=txt, pred_semantic=sem, noise_seed=77 + i))
+    ref = [o.cpu().numpy() for o in e.vits_decode_batch([dict(it, **kw) for it in items])]
+    got = [o.cpu().numpy() for o in e.vits_decode_batch([dict(it, ge=ge) for it in items])]
+    one = e.vits_decode(items[1]["text_seq"], items[1]["pred_semantic"], noise_seed=78, ge=ge).cpu().numpy()
+    outs = e.vits_decode_batch_async([dict(it, ge=ge) for it in items])
+    e.vits_batch_wait()
+    for i in range(3):
+        np.testing.assert_array_equal(got[i], ref[i])
+        np.testing.assert_array_equal(outs[i].cpu().numpy(), ref[i])
+    np.testing.assert_array_equal(one, ref[1])
