@@ -12,7 +12,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_server_concurrent_streams(tmp_path):
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_server_concurrent_streams(tmp_path, pipeline):
+    """pipeline=True: each round's vocoder beside the next round's T2S (the chunks of a
+    round are streamed after the next round's T2S; same sizes, same order)."""
     import httpx
     from genie_tts_amd.server import Router, create_app
     from genie_tts_amd.text_splitter import TextSplitter
@@ -25,7 +28,8 @@ def test_server_concurrent_streams(tmp_path):
     G = 24
 
     async def run():
-        router = Router([0], g2p="genie_tts_amd.stubs:toy_g2p", ssl="genie_tts_amd.stubs:toy_ssl", greedy=True)
+        router = Router([0], g2p="genie_tts_amd.stubs:toy_g2p", ssl="genie_tts_amd.stubs:toy_ssl", greedy=True,
+                        pipeline=pipeline)
         router.start(asyncio.get_running_loop(), timeout=300)
         try:
             res = await router.broadcast("load_synthetic", character_name="srv", version="v2")
