@@ -15,7 +15,7 @@ for s in $STEPS; do
     bench) timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
            cat gpurun_out/${TAG}_bench.json ;;
     prof)  rm -rf gpurun_out/prof_${TAG}
-           timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o bench -- python3 bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench_under_rocprof.log 2>&1 || { tail -30 gpurun_out/${TAG}_bench_under_rocprof.log; exit 1; }
+           timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o bench -- python3 bench.py --no-cpu-baseline --concurrent-streams 0 > gpurun_out/${TAG}_bench_under_rocprof.log 2>&1 || { tail -30 gpurun_out/${TAG}_bench_under_rocprof.log; exit 1; }
            python tools/prof_summary.py gpurun_out/prof_${TAG} > gpurun_out/${TAG}_kernel_stats.txt 2>&1; head -25 gpurun_out/${TAG}_kernel_stats.txt ;;
     batched) for w in batch64 mixed100; do
              timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > gpurun_out/${TAG}_$w.json 2> gpurun_out/${TAG}_$w.err || { tail -30 gpurun_out/${TAG}_$w.err; exit 1; }
@@ -23,7 +23,7 @@ for s in $STEPS; do
            done ;;
     pmc)   for c in FETCH_SIZE WRITE_SIZE; do
              rm -rf gpurun_out/pmc_${TAG}_$c
-             timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$c -o pmc -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/${TAG}_pmc_$c.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_$c.log; exit 1; }
+             timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$c -o pmc -- python3 bench.py --no-cpu-baseline --concurrent-streams 0 --steps 3 --warmup 1 > gpurun_out/${TAG}_pmc_$c.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_$c.log; exit 1; }
              python tools/pmc_summary.py gpurun_out/pmc_${TAG}_$c --gfx950-fetch-x2 --json gpurun_out/${TAG}_pmc_$c.json > gpurun_out/${TAG}_pmc_$c.txt 2>&1; grep -i "persist\|conv1d<11" gpurun_out/${TAG}_pmc_$c.txt | head -5 || true
            done ;;
   esac
