@@ -148,6 +148,12 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
             return
         name = ready[0]["character_name"]
         group = [r for r in ready if r["character_name"] == name][:MAX_BATCH]
+        if 5 <= len(group) <= 9:
+            # T2S time by batch (tools/batch_sweep.py, profiles/r02h_batch_sweep.json): B <= 4
+            # runs the two-group persistent decode (B=4: 36 ms), B = 5..8 only fits one layer
+            # group (70-96 ms), B >= 10 the batched graph path (~100 ms); so 4 now, the rest
+            # next round (4 + 4 = 72 ms < 96 ms for 8)
+            group = group[:4]
         idx = [r["next"] for r in group]
         try:
             m = model_manager.get(name)
