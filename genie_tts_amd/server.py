@@ -44,6 +44,17 @@ def _resolve(spec: Optional[str]):
     return getattr(importlib.import_module(mod), fn)
 
 
+def round_size(ready: int) -> int:
+    """Sentences a worker round takes out of `ready` of one character.  From the T2S time
+    per batch (tools/batch_sweep.py, profiles/r02h_batch_sweep.json): B <= 4 runs the
+    two-group persistent decode (B = 4: 36 ms), B = 5..8 fits only one layer group
+    (70-96 ms), B >= 10 the batched graph path (~100 ms, 150 ms at 64); so 5-9 ready
+    sentences go as 4 now and the rest next round (4 + 4 = 72 ms < 96 ms for 8)."""
+    if 5 <= ready <= 9:
+        return 4
+    return min(ready, MAX_BATCH)
+
+
 # --------------------------------------------------------------------- worker
 def _worker_main(index: int, conn, cfg: dict) -> None:
     """One GPU (HIP_VISIBLE_DEVICES was set by the router before spawning)."""
@@ -147,13 +158,8 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
             finish_inflight()
             return
         name = ready[0]["character_name"]
-        group = [r for r in ready if r["character_name"] == name][:MAX_BATCH]
-        if 5 <= len(group) <= 9:
-            # T2S time by batch (tools/batch_sweep.py, profiles/r02h_batch_sweep.json): B <= 4
-            # runs the two-group persistent decode (B=4: 36 ms), B = 5..8 only fits one layer
-            # group (70-96 ms), B >= 10 the batched graph path (~100 ms); so 4 now, the rest
-            # next round (4 + 4 = 72 ms < 96 ms for 8)
-            group = group[:4]
+        group = [r for r in ready if r["character_name"] == name]
+        group = group[:round_size(len(group))]
         idx = [r["next"] for r in group]
         try:
             m = model_manager.get(name)
