@@ -27,8 +27,15 @@ Inputs are resident in HBM before the timed region.  Multi-GPU: one process per
 GPU (torchrun), independent replicas, no collective on the data path; the
 barrier and the max-over-ranks time use a gloo (host) group -- no RCCL.
 
+The single workload's line also carries "concurrent_streams": the same stream run by two
+child ranks sharing the GPU (each decoding on 96 CUs of its own, the vocoder CUs shared;
+--streams-per-gpu), the GPU's rate under concurrent single-sentence requests.  The batched
+workloads pipeline each batch's vocoder beside the next batch's T2S (--pipeline 0: one batch
+at a time).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload single|batch64|mixed100]
-                       [--vocoder-cus K] [--no-cpu-baseline]
+                       [--vocoder-cus K] [--concurrent-streams S] [--pipeline 0|1]
+                       [--vits-lanes L] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
