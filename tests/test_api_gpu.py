@@ -117,13 +117,16 @@ def test_api_tts_end_to_end(model):
     api.clear_reference_audio_cache()
 
 
-def test_tts_batch_equals_single(model):
+@pytest.mark.parametrize("lens", [(10, 17, 25), (10, 17, 25, 8, 13, 21)])
+def test_tts_batch_equals_single(model, lens):
+    """3 sentences: one batched generate; 6: two chunks (4 + 2) on the two-group
+    persistent decode (GENIE.tts_batch_t2s)."""
     from genie_tts_amd.inference import GENIE, ReferenceAudio
     m, _ = model
     ref = ReferenceAudio(phonemes_seq=synth.synth_phones(12, "b-r"), text_bert=np.zeros((12, 1024), np.float32),
                          audio_32k=synth.synth_ref_audio(32000 * 2, "b-a").reshape(1, -1),
                          ssl_content=synth.synth_ssl(41, "b-s").reshape(1, 768, -1))
-    texts = [synth.synth_phones(n, f"b-t{n}") for n in (10, 17, 25)]
+    texts = [synth.synth_phones(n, f"b-t{n}") for n in lens]
     gen = GENIE()
     sp = m.T2S_FIRST_STAGE_DECODER.sampler
     batch = gen.tts_batch([(t, None) for t in texts], ref, m, sp)
