@@ -70,6 +70,31 @@ def test_vits_waveform_conv_paths(setup, convh):
     assert rms <= RMS_TOL, f"rms {rms:.3e}"
 
 
+def test_vits_fp16_range_guard_reruns_f32(setup):
+    """An MRF conv input beyond the fp16 range (|x| > 65504, `vits_convh.hip` range guard)
+    re-runs the utterance on the f32 path: the audio equals the convh=0 path's and the
+    `vits_f32_reruns` counter moves.  Huge noise (eps x 1e6) drives the activations there."""
+    ver, e, _, _ = setup
+    G, S = 24, 16
+    txt = synth.synth_phones(S, f"vt{S}")
+    sem = ((np.arange(G, dtype=np.int64) * 29 + 5) % 1024).reshape(1, 1, G)
+    eps = (synth.rng_for(f"big{G}").standard_normal((1, 192, 2 * G)) * 1e6).astype(np.float32)
+    kw = _cond(ver)
+    n0 = e.counter("vits_f32_reruns")
+    out = e.vits_decode(txt, sem, eps=eps, **kw).cpu().numpy()
+    assert e.counter("vits_f32_reruns") == n0 + 1
+    e.set_option("convh", 0)
+    try:
+        ref = e.vits_decode(txt, sem, eps=eps, **kw).cpu().numpy()
+    finally:
+        e.set_option("convh", 1)
+    assert np.isfinite(out).all()
+    assert np.array_equal(out, ref)
+    # normal inputs stay on the fp16-split path
+    e.vits_decode(txt, sem, eps=eps * 1e-6, **kw)
+    assert e.counter("vits_f32_reruns") == n0 + 1
+
+
 def test_prompt_encoder(setup):
     ver, e, _, w = setup
     if ver == "v2":
