@@ -95,6 +95,25 @@ def test_vits_fp16_range_guard_reruns_f32(setup):
     assert e.counter("vits_f32_reruns") == n0 + 1
 
 
+def test_vits_batch_range_guard_reruns_only_that_item(setup):
+    """Batched vocoder (`gsv_vits_decode_batch`): only the item whose MRF inputs left the fp16
+    range re-runs on the f32 path; every item's audio equals its single call's."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    items = []
+    for i, (G, S, big) in enumerate([(16, 12, False), (24, 16, True), (20, 14, False)]):
+        eps = synth.rng_for(f"bb{i}").standard_normal((1, 192, 2 * G)).astype(np.float32)
+        items.append(dict(text_seq=synth.synth_phones(S, f"bb{S}"),
+                          pred_semantic=((np.arange(G, dtype=np.int64) * 31 + i) % 1024).reshape(1, 1, G),
+                          eps=eps * (1e6 if big else 1.0), **kw))
+    n0 = e.counter("vits_f32_reruns")
+    outs = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+    assert e.counter("vits_f32_reruns") == n0 + 1
+    for it, o in zip(items, outs):
+        single = e.vits_decode(it["text_seq"], it["pred_semantic"], eps=it["eps"], **kw).cpu().numpy()
+        assert np.array_equal(o, single)
+
+
 def test_prompt_encoder(setup):
     ver, e, _, w = setup
     if ver == "v2":
