@@ -114,6 +114,28 @@ def test_vits_batch_range_guard_reruns_only_that_item(setup):
         assert np.array_equal(o, single)
 
 
+def test_vits_async_range_guard_reruns_f32(setup):
+    """Overlapped vocoder call (`gsv_vits_decode_async` on the vocoder CUs): past the fp16 range
+    it re-runs on the f32 path inside `gsv_vits_wait`; audio equals the single call's."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    G, S = 24, 16
+    it = dict(text_seq=synth.synth_phones(S, f"va{S}"),
+              pred_semantic=((np.arange(G, dtype=np.int64) * 13 + 3) % 1024).reshape(1, 1, G),
+              eps=(synth.rng_for("vabig").standard_normal((1, 192, 2 * G)) * 1e6).astype(np.float32), **kw)
+    single = e.vits_decode(it["text_seq"], it["pred_semantic"], eps=it["eps"], **kw).cpu().numpy()
+    n0 = e.counter("vits_f32_reruns")
+    e.set_vocoder_cus(64)
+    try:
+        audio = e.vits_decode_async(it)
+        e.vits_wait()
+        got = audio.cpu().numpy()
+    finally:
+        e.set_vocoder_cus(0)
+    assert e.counter("vits_f32_reruns") == n0 + 1
+    assert np.array_equal(got, single)
+
+
 def test_prompt_encoder(setup):
     ver, e, _, w = setup
     if ver == "v2":
