@@ -229,6 +229,90 @@ def concurrent_streams(args):
                     "persistent decode), vocoder + prefetch CUs shared"}
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`--gpus N` run without a launcher (WORLD_SIZE unset): one rank per GPU as child
+    processes of `torch.distributed.run`, started before this process touches the GPU
+    (nothing is exec'd in place).  Their output is relayed line by line (rank 0 prints the
+    JSON line); the exit code is theirs."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+              "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
+class StubRunner:
+    """CPU stand-in for Runner (tests of the multi-rank launcher and the max-over-ranks
+    timing): a step sleeps `stub_ms`; no GPU, no engine."""
+
+    def __init__(self, wl, items, stub_ms):
+        self.items, self.ms = items, stub_ms
+        self.phase = {}
+
+    def step(self):
+        time.sleep(self.ms * 1e-3)
+        return [np.zeros(it.tokens, np.int64) for it in self.items], 1280 * sum(it.tokens for it in self.items)
+
+    def drain(self):
+        pass
+
+
+def over_ranks(dist, dt: float, units: int):
+    """(max wall time over the ranks, per-rank units/s) over the gloo group; (dt, [units/dt])
+    without one.  The job's rate is every rank's units over the slowest rank's time."""
+    if dist is None:
+        return dt, [units / dt]
+    import torch
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = [None] * dist.get_world_size()
+    dist.all_gather_object(per, units / dt)
+    return float(t.item()), [float(x) for x in per]
+
+
+def stub_main(args):
+    """The multi-rank harness with StubRunner replicas (no GPU): gloo barrier, K timed
+    steps, max over ranks, rank 0's JSON line -- what a GPU run reports, minus the engine."""
+    from genie_tts_amd import workloads
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    wl = workloads.single()
+    run = StubRunner(wl, wl.items, args.stub_ms * (1 + 0.5 * rank))   # uneven ranks: the max must win
+    for _ in range(args.warmup):
+        run.step()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, n_samples = run.step()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    dt, per = over_ranks(dist, dt, args.steps * len(run.items))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": world * args.steps * len(run.items) / dt, "unit": "utt/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": dt / args.steps * 1e3, "per_rank_utt_s": per, "stub": True}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -259,7 +343,14 @@ def main():
                     help="batched workloads: HIP stream priority of the vocoder lanes (lower = first)")
     ap.add_argument("--t2s-priority", type=int, default=None,
                     help="batched workloads: HIP stream priority of the engine (T2S) stream")
+    ap.add_argument("--stub-ms", type=float, default=0.0,
+                    help=argparse.SUPPRESS)   # tests: a CPU stub replica whose step sleeps this long
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.stub_ms > 0:
+        return stub_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -335,9 +426,7 @@ def main():
     dt = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt, per_rank = over_ranks(dist, dt, args.steps * len(items))   # this rank's utterances
 
     R_, H_ = wl.reference.ref_seq.shape[1], wl.reference.ssl.shape[2]
     n0s = [R_ + it.text_seq.shape[1] + H_ // 2 for it in items]
@@ -378,6 +467,7 @@ def main():
         "x_realtime": 1.0 / rtf,
         "audio_s_per_step": audio_s,
         "tokens_per_step": sum(tokens),
+        "per_rank_utt_s": per_rank,
     }
     if args.workload == "single":
         it = items[0]
@@ -416,7 +506,9 @@ def main():
         out["roofline_utterance"] = composite_roofline(ms_per_step, n0s, [it.force_steps for it in items], tokens,
                                                        wl.version)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "single":
-        threads = min(16, len(os.sched_getaffinity(0)))
+        # every CPU this job is allotted: the GPU box gives one GPU's job 16 host CPUs
+        # (OMP_NUM_THREADS=16 there) although the machine shows more; here: all 8
+        threads = min(int(os.environ.get("OMP_NUM_THREADS") or 10 ** 6), len(os.sched_getaffinity(0)))
         cdt, cs = cpu_baseline(wl, threads)
         model = ""
         try:
@@ -425,6 +517,7 @@ def main():
         except Exception:
             pass
         out["cpu_baseline"] = {"value": 1.0 / cdt, "unit": "utt/s", "cores": threads, "kind": "port",
+                               "cores_note": "all host CPUs allotted to this one-GPU job (OMP_NUM_THREADS share)",
                                "sample": f"1 full utterance ({cs} samples) of the same workload, "
                                          f"oracle/restate.py torch-fp32 on {model}",
                                "rtf": cdt / (cs / SR)}

@@ -1704,7 +1704,9 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
             }
     } else if (n == "vocoder_cus") {   // overlapped vocoder: CUs reserved for gsv_vits_decode_async
         return eng->set_vocoder_cus(value);
-    } else if (n == "convh") {
+    } else if (n == "convh") {   // a queued or pending vocoder call finishes under the mode it began with
+        if (int r = eng->vits_wait(nullptr)) return r;
+        if (int r = eng->vits_batch_finish(nullptr)) return r;
         eng->use_convh = value != 0;
     } else if (n == "ptrace") {
         if (value && !eng->ptrace) {

@@ -248,6 +248,7 @@ struct gsv_engine {
     std::vector<gsv_vits_item> vb_items;
     std::vector<std::thread> vb_threads;
     std::vector<int> vb_rcs;
+    std::vector<std::string> vb_errs;   // each failed lane thread's error text
     int vb_k = 0;
     float vb_scale = 0.f;
     bool vb_active = false;

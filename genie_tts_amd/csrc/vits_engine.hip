@@ -163,6 +163,11 @@ static int load_attn_layers(gsv_engine* e, const std::string& pre, int n, std::v
         if (int r = load_conv(e, a + "conv_o", L.o, false)) return r;
         if (int r = load_conv(e, pre + ".ffn_layers." + std::to_string(i) + ".conv_1", L.ffn1, false)) return r;
         if (int r = load_conv(e, pre + ".ffn_layers." + std::to_string(i) + ".conv_2", L.ffn2, false)) return r;
+        for (const char* nm : {"emb_rel_k", "emb_rel_v"}) {   // k_mha's rel-pos terms: window 4 (<= MHA_MAXW)
+            const auto* st = e->find(a + nm);
+            if (st && st->data.size() != (size_t)(2 * 4 + 1) * 96)
+                return set_error(GSV_E_WEIGHT, a + nm + ": expected [1, 9, 96] (relative window 4)");
+        }
         L.ek = up_named(e, a + "emb_rel_k", &err);
         L.ev = up_named(e, a + "emb_rel_v", &err);
         L.g1 = up_named(e, pre + ".norm_layers_1." + std::to_string(i) + ".gamma", &err);
@@ -798,6 +803,7 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     vb_k = K;
     vb_scale = noise_scale;
     vb_rcs.assign(K, 0);
+    vb_errs.assign(K, std::string());
     auto lane_work = [this, K, n](int l) {
         hipSetDevice(device);
         VitsLane& L = vlanes[l];
@@ -808,6 +814,7 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
                                          u.noise_mode == 2 ? u.noise_seed : 0, vb_scale, u.audio, L.st,
                                          use_convh ? vflags + i : nullptr, false)) {
                 vb_rcs[l] = r;
+                vb_errs[l] = gsv_last_error();   // g_err is thread-local: keep the lane thread's text
                 return;
             }
         }
@@ -835,9 +842,13 @@ int gsv_engine::vits_batch_finish(hipStream_t s) {
     vb_threads.clear();
     if (!s) s = stream;
     const int n = (int)vb_items.size(), K = vb_k;
-    for (int l = 0; l < K; ++l)
-        if (vb_rcs[l]) return set_error(vb_rcs[l], "vocoder lane " + std::to_string(l) + " failed");
     for (int l = 0; l < K; ++l) hipStreamWaitEvent(s, vlanes[l].join, 0);
+    for (int l = 0; l < K; ++l)
+        if (vb_rcs[l]) {   // the other lanes may still write their audio: drain them before reporting
+            hipStreamSynchronize(s);
+            for (int k = 0; k < K; ++k) hipStreamSynchronize(vlanes[k].st);
+            return set_error(vb_rcs[l], "vocoder lane " + std::to_string(l) + ": " + vb_errs[l]);
+        }
     if (use_convh) {
         hipMemcpyAsync(vflags_host, vflags, (size_t)n * 4, hipMemcpyDeviceToHost, s);
         if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vocoder batch sync");

@@ -127,7 +127,8 @@ class GENIE:
                 yield self.tts(t, prompt_audio, encoder, first_stage_decoder, stage_decoder, vocoder, prompt_encoder,
                                language, text_bert, g2p, sampler)
             return
-        if eng.vocoder_cus != vocoder_cus:
+        prev_cus = eng.vocoder_cus     # restored when the stream ends: later single-sentence and
+        if prev_cus != vocoder_cus:    # batched calls keep every CU (decode groups, lanes)
             eng.set_vocoder_cus(vocoder_cus)
         if prompt_encoder is None:
             cond = (vocoder.v2_cond(prompt_audio.audio_32k) if getattr(vocoder, "engine", None) is eng
@@ -188,6 +189,8 @@ class GENIE:
                     break
             if pending is not None:
                 eng.vits_wait()
+            if eng.vocoder_cus != prev_cus:
+                eng.set_vocoder_cus(prev_cus)
 
     def t2s(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, engine, sampler: Sampler) -> np.ndarray:
         """Whole T2S on the device; returns the trimmed, EOS-filtered [1,1,G] tokens."""

@@ -141,10 +141,14 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
             r["chunks"].append(np.asarray(wav, np.float32).reshape(-1))
             r["done"] = i + 1
             if r["done"] == len(r["sentences"]):
-                if r["save_path"]:
-                    A.write_wav(r["save_path"], np.concatenate(r["chunks"]))
-                reply(kind="end", id=r["id"])
                 pending.remove(r)
+                if r["save_path"]:
+                    try:              # a client-supplied path: its failure ends this request only
+                        A.write_wav(r["save_path"], np.concatenate(r["chunks"]))
+                    except Exception as e:   # noqa: BLE001
+                        reply(kind="error", id=r["id"], detail=f"save_path: {type(e).__name__}: {e}")
+                        continue
+                reply(kind="end", id=r["id"])
 
     def run_round() -> None:
         """The next sentence of up to MAX_BATCH pending requests of one character.  With
@@ -189,6 +193,15 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
         if not overlapped:
             finish_inflight()
 
+    def fail_all(e: Exception) -> None:
+        """An unexpected error outside a request's own handler: every request in this
+        worker gets an error reply and the worker keeps serving."""
+        logger.exception("worker %d: round failed", index)
+        inflight.clear()
+        for r in pending:
+            reply(kind="error", id=r["id"], detail=f"worker error: {type(e).__name__}: {e}")
+        pending.clear()
+
     reply(kind="ready", id=-1, index=index)
     while True:
         # block only when idle; otherwise drain what has arrived, then run one round
@@ -196,13 +209,19 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
             msg = conn.recv()
             if msg is None:
                 return
-            if msg["cmd"] == "tts":
-                accept(msg)
-            else:
-                control(msg)
+            try:
+                if msg["cmd"] == "tts":
+                    accept(msg)
+                else:
+                    control(msg)
+            except Exception as e:   # noqa: BLE001
+                fail_all(e)
             if pending and not conn.poll():
                 break
-        run_round()
+        try:
+            run_round()
+        except Exception as e:   # noqa: BLE001
+            fail_all(e)
 
 
 # --------------------------------------------------------------------- router
@@ -220,6 +239,9 @@ class Router:
         self.load: List[int] = [0] * len(gpus)
         self.conns, self.procs, self.threads = [], [], []
         self.send_locks: List[threading.Lock] = []
+        self.dead: set = set()                        # workers whose pipe closed
+        self.sent_to: Dict[int, set] = {}             # request id -> workers that owe it replies
+        self.state_lock = threading.Lock()
 
     def start(self, loop: asyncio.AbstractEventLoop, timeout: float = 600.0) -> None:
         self.loop = loop
@@ -252,33 +274,61 @@ class Router:
             try:
                 msg = conn.recv()
             except (EOFError, OSError):
+                self._worker_died(i)
                 return
             q = self.queues.get(msg["id"])
             if q is not None:
                 self.loop.call_soon_threadsafe(q.put_nowait, (i, msg))
 
+    def _worker_died(self, i: int) -> None:
+        """Worker i's pipe closed: it gets no more requests, and every request still
+        waiting on it (a tts stream or a broadcast's reply) gets an error."""
+        with self.state_lock:
+            self.dead.add(i)
+            owed = [rid for rid, ws in self.sent_to.items() if i in ws]
+        logger.error("worker %d exited; %d request(s) failed", i, len(owed))
+        for rid in owed:
+            q = self.queues.get(rid)
+            if q is not None:
+                self.loop.call_soon_threadsafe(q.put_nowait, (i, dict(kind="error", id=rid,
+                                                                     detail=f"worker {i} exited")))
+
     def _send(self, i: int, msg: dict) -> None:
         with self.send_locks[i]:
             self.conns[i].send(msg)
+
+    def _live(self) -> List[int]:
+        with self.state_lock:
+            live = [i for i in range(len(self.conns)) if i not in self.dead]
+        if not live:
+            raise RuntimeError("no live engine worker")
+        return live
 
     async def broadcast(self, cmd: str, **kw) -> List[dict]:
         rid = next(self.ids)
         q: asyncio.Queue = asyncio.Queue()
         self.queues[rid] = q
         try:
-            for i in range(len(self.conns)):
+            live = self._live()
+            with self.state_lock:
+                self.sent_to[rid] = set(live)
+            for i in live:
                 self._send(i, dict(cmd=cmd, id=rid, **kw))
-            return [(await q.get())[1] for _ in self.conns]
+            return [(await q.get())[1] for _ in live]
         finally:
             self.queues.pop(rid, None)
+            with self.state_lock:
+                self.sent_to.pop(rid, None)
 
     async def tts(self, **kw):
-        """Async iterator of PCM chunks from the least-loaded worker."""
+        """Async iterator of PCM chunks from the least-loaded live worker."""
         rid = next(self.ids)
         q: asyncio.Queue = asyncio.Queue()
         self.queues[rid] = q
-        i = min(range(len(self.load)), key=lambda k: self.load[k])
+        i = min(self._live(), key=lambda k: self.load[k])
         self.load[i] += 1
+        with self.state_lock:
+            self.sent_to[rid] = {i}
         try:
             self._send(i, dict(cmd="tts", id=rid, **kw))
             while True:
@@ -292,6 +342,8 @@ class Router:
         finally:
             self.load[i] -= 1
             self.queues.pop(rid, None)
+            with self.state_lock:
+                self.sent_to.pop(rid, None)
 
     def close(self) -> None:
         for i, c in enumerate(self.conns):
