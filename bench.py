@@ -20,8 +20,11 @@ so every utterance runs a forced number of loop steps):
            top-k 5 sampled, ONE ragged batched decode + the vocoder per
            utterance.  A step = the 64-sentence batch.
   mixed100 configs[3]: V2ProPlus EN+ZH 100-sentence set, LPT-sharded over the
-           ranks (genie_tts_amd/replicas.py), each rank batching its shard.  A
-           step = the whole set (weak scaling does not apply: total work fixed).
+           ranks (genie_tts_amd/replicas.py), each rank batching its shard; the
+           Chinese sentences' BERT features come from RoBERTa (24-layer
+           chinese-roberta-wwm-ext-large shapes, synthetic weights) on the engine,
+           inside the timed region.  A step = the whole set (weak scaling does not
+           apply: total work fixed).
 
 Inputs are resident in HBM before the timed region.  Multi-GPU: one process per
 GPU (torchrun), independent replicas, no collective on the data path; the
@@ -84,7 +87,12 @@ class Runner:
         self.torch = torch
         self.wl = wl
         self.items = items
-        self.eng = Engine(synth.synthetic_character(wl.version), wl.version, device=device_index)
+        w = synth.synthetic_character(wl.version)
+        self.zh = any(it.bert_ids is not None for it in items)
+        if self.zh:   # Chinese sentences: RoBERTa on the same engine (GetPhonesAndBert.py:64-74)
+            from genie_tts_amd import workloads
+            w["roberta"] = workloads.roberta_weights()
+        self.eng = Engine(w, wl.version, device=device_index)
         ref = wl.reference
         T = lambda a, dt=None: torch.as_tensor(np.ascontiguousarray(a), device=dev)
         self.d_ref = T(ref.ref_seq.reshape(-1))
@@ -93,6 +101,7 @@ class Runner:
         self.d_ref_bert = None if not np.any(ref.ref_bert) else T(ref.ref_bert)
         self.d_txt = [T(it.text_seq.reshape(-1)) for it in items]
         self.d_bert = [None if it.text_bert is None else T(it.text_bert) for it in items]
+        self.d_bert_ids = [None if it.bert_ids is None else T(it.bert_ids) for it in items]
         self.sp = make_sampler(top_k=wl.top_k, greedy=wl.greedy)
         self.seed = 0x5EED
         self.ge = self.ge_adv = None
@@ -101,7 +110,7 @@ class Runner:
         else:   # the vocoder's reference branch once per reference (gsv_ref_encode), as the API does
             self.ge_v2 = self.eng.ref_encode(self.d_audio)
         self.eng.set_option("persist", 1)
-        self.phase = {"t2s": 0.0, "vits": 0.0, "encode+prefill": 0.0, "decode": 0.0}
+        self.phase = {"t2s": 0.0, "vits": 0.0, "encode+prefill": 0.0, "decode": 0.0, "roberta": 0.0}
 
     def stream(self, n, phase_ms=None):
         """n utterances as a pipelined stream: utterance i+1's T2S is queued behind
@@ -135,11 +144,25 @@ class Runner:
             self.eng.vits_wait()
             self.pending = None
 
+    def berts(self, lo, hi):
+        """BERT features of items [lo, hi): the Chinese ones from RoBERTa over their device
+        token ids in one packed pass (gsv_roberta_batch) -- inside the timed region, as the
+        reference runs RoBERTa per Chinese sentence on every tts call -- the rest as given."""
+        out = self.d_bert[lo:hi]
+        zh = [i for i in range(lo, hi) if self.d_bert_ids[i] is not None]
+        if zh:
+            t0 = time.perf_counter()
+            feats = self.eng.roberta_batch([(self.d_bert_ids[i], self.items[i].word2ph) for i in zh])
+            for i, f in zip(zh, feats):
+                out[i - lo] = f
+            self.phase["roberta"] = self.phase.get("roberta", 0.0) + time.perf_counter() - t0
+        return out
+
     def step(self):
         torch = self.torch
         t0 = time.perf_counter()
         utts = [(self.d_ref, t, self.d_ref_bert, b, self.d_ssl, it.force_steps)
-                for t, b, it in zip(self.d_txt, self.d_bert, self.items)]
+                for t, b, it in zip(self.d_txt, self.berts(0, len(self.items)), self.items)]
         sems = self.eng.t2s_generate(utts, self.sp)        # returns host tokens: synchronous
         t1 = time.perf_counter()
         tm = self.eng.timing()                              # device phases of this generate (ms)
@@ -172,7 +195,8 @@ class Runner:
         for j in range(nb):
             lo, hi = bounds[j], bounds[j + 1]
             t0 = time.perf_counter()
-            utts = [(self.d_ref, self.d_txt[i], self.d_ref_bert, self.d_bert[i], self.d_ssl, self.items[i].force_steps)
+            bert = self.berts(lo, hi)
+            utts = [(self.d_ref, self.d_txt[i], self.d_ref_bert, bert[i - lo], self.d_ssl, self.items[i].force_steps)
                     for i in range(lo, hi)]
             sems = self.eng.t2s_generate(utts, self.sp)
             t1 = time.perf_counter()
@@ -374,7 +398,8 @@ def main():
     from genie_tts_amd.probe import persist_roofline, composite_roofline
     wl = {"single": workloads.single, "batch64": workloads.batch64, "mixed100": workloads.mixed100}[args.workload]()
     if args.workload == "mixed100":
-        reqs = [replicas.Request(i, it.text_seq, it.text_bert, it.force_steps) for i, it in enumerate(wl.items)]
+        reqs = [replicas.Request(i, it.text_seq, it.text_bert, it.force_steps, it.bert_ids, it.word2ph)
+                for i, it in enumerate(wl.items)]
         shard = replicas.lpt_assign([replicas.predicted_cost(r) for r in reqs], world)[rank]
         items = [wl.items[i] for i in shard]
         units_per_step = len(wl.items)            # the whole set per step, over all ranks

@@ -19,19 +19,21 @@
 namespace gsv {
 namespace {
 
-// x[t] = LN(word[ids[t]] + pos[t] + type0), D = 1024, one block per token
+// x[t] = LN(word[ids[t]] + pos[p(t)] + type0), D = 1024, one block per token;
+// p(t) = row_pos[t] for packed sentences, else t
 __global__ __launch_bounds__(256) void k_bert_embed(const int64_t* ids, const float* word, const float* pos,
                                                      const float* type0, const float* g, const float* b, float eps,
-                                                     float* out) {
+                                                     const int* row_pos, float* out) {
     __shared__ float red[16];
     const int t = blockIdx.x;
     const long id = ids[t];
+    const long pt = row_pos ? row_pos[t] : t;
     float v[4];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int d = threadIdx.x + 256 * i;
-        v[i] = (word[id * 1024 + d] + type0[d]) + pos[(long)t * 1024 + d];
+        v[i] = (word[id * 1024 + d] + type0[d]) + pos[pt * 1024 + d];
         s += v[i];
     }
     const float mean = block_sum(s, red) / 1024.f;
@@ -108,9 +110,10 @@ int gsv_engine::finalize_roberta() {
     return 0;
 }
 
-int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int n_out, float* out, hipStream_t st) {
+int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int n_out, float* out, hipStream_t st,
+                                const int* row_pos, const int* row_seg) {
     const BertWeights& B = bert;
-    const size_t need = (size_t)N * (1024 * 4 + 3072 + 4096) + (size_t)n_out + 64;
+    const size_t need = (size_t)N * (1024 * 4 + 3072 + 4096) + (size_t)n_out + 3 * (size_t)N + 64;
     if (need > bert.ws_floats) {
         if (bert.ws) hipFree(bert.ws);
         bert.ws = nullptr;
@@ -122,9 +125,14 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
     float *tmp = h + (size_t)N * 1024, *att = tmp + (size_t)N * 1024, *qkv = att + (size_t)N * 1024;
     float* f = qkv + (size_t)N * 3072;
     int* drows = reinterpret_cast<int*>(f + (size_t)N * 4096);
+    int* dpos = drows + n_out;
+    int* dseg = dpos + N;
     hipMemcpyAsync(drows, rows, (size_t)n_out * 4, hipMemcpyHostToDevice, st);
+    if (row_pos) hipMemcpyAsync(dpos, row_pos, (size_t)N * 4, hipMemcpyHostToDevice, st);
+    if (row_seg) hipMemcpyAsync(dseg, row_seg, (size_t)N * 8, hipMemcpyHostToDevice, st);
     constexpr float EPS = 1e-12f;
-    hipLaunchKernelGGL(k_bert_embed, dim3(N), dim3(256), 0, st, ids, B.word, B.pos, B.type, B.ln_w, B.ln_b, EPS, h);
+    hipLaunchKernelGGL(k_bert_embed, dim3(N), dim3(256), 0, st, ids, B.word, B.pos, B.type, B.ln_w, B.ln_b, EPS,
+                       row_pos ? dpos : nullptr, h);
     for (const BertLayerW& L : B.L) {
         gemm_nt(gemm_f16(N, 3072, 1024, h, 1024, L.wqkv, L.bqkv, qkv, 3072, EPI_STORE), st);
         MhaArgs m{};
@@ -134,6 +142,7 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
         m.out = att; m.o_ts = 1024; m.o_cs = 1;
         m.nq = N; m.nk = N; m.heads = 16; m.dk = 64;
         m.postdiv = 0; m.scale = 8.f;   // scores / sqrt(64) (exact: a power of two)
+        m.row_seg = row_seg ? dseg : nullptr;   // packed: each sentence attends within itself
         mha(m, st);
         gemm_nt(gemm_f16(N, 1024, 1024, att, 1024, L.wo, L.bo, tmp, 1024, EPI_RESID, h, 1024), st);
         layernorm_rows_d(tmp, h, N, 1024, L.ln1w, L.ln1b, EPS, st);
@@ -142,7 +151,7 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
         layernorm_rows_d(tmp, h, N, 1024, L.ln2w, L.ln2b, EPS, st);
     }
     hipLaunchKernelGGL(k_bert_repeat, dim3(n_out), dim3(256), 0, st, h, drows, out);
-    // the row table is read by the kernel above; keep the pageable source alive until it ran
+    // the row tables are read by the kernels above; keep the pageable sources alive until they ran
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "RoBERTa");
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "RoBERTa launch");
 }
@@ -166,4 +175,36 @@ extern "C" int gsv_roberta(gsv_engine* eng, const int64_t* input_ids, const int6
     hipSetDevice(eng->device);
     StreamScope sc(eng, stream);
     return eng->roberta_forward(input_ids, n_tokens, rows.data(), (int)rows.size(), text_bert, sc.st());
+}
+
+extern "C" int gsv_roberta_batch(gsv_engine* eng, int32_t n_seq, const int64_t* input_ids, const int32_t* n_tokens,
+                                 const int64_t* repeats, const int32_t* n_chars, float* text_bert, void* stream) {
+    if (!eng) return set_error(GSV_E_ARG, "null engine");
+    if (n_seq < 1 || !input_ids || !n_tokens || !n_chars || !text_bert) return set_error(GSV_E_ARG, "null arg");
+    if (!eng->finalized || !eng->bert.ready) return set_error(GSV_E_STATE, "RoBERTa weights not loaded");
+    std::vector<int> rows, pos, seg;
+    int row0 = 0;
+    long rep0 = 0;
+    for (int s = 0; s < n_seq; ++s) {
+        const int nt = n_tokens[s], nc = n_chars[s];
+        if (nt < 2 || nt > eng->bert.max_pos) return set_error(GSV_E_ARG, "RoBERTa: bad token count");
+        if (nc < 0 || nc > nt - 2) return set_error(GSV_E_ARG, "RoBERTa: more characters than tokens");
+        if (nc > 0 && !repeats) return set_error(GSV_E_ARG, "null repeats");
+        for (int i = 0; i < nc; ++i) {
+            if (repeats[rep0 + i] < 0) return set_error(GSV_E_ARG, "RoBERTa: negative repeat");
+            for (int64_t r = 0; r < repeats[rep0 + i]; ++r) rows.push_back(row0 + 1 + i);   // CLS dropped
+        }
+        for (int t = 0; t < nt; ++t) {
+            pos.push_back(t);
+            seg.push_back(row0);
+            seg.push_back(nt);
+        }
+        row0 += nt;
+        rep0 += nc;
+    }
+    if (rows.empty()) return 0;
+    hipSetDevice(eng->device);
+    StreamScope sc(eng, stream);
+    return eng->roberta_forward(input_ids, row0, rows.data(), (int)rows.size(), text_bert, sc.st(), pos.data(),
+                                seg.data());
 }

@@ -161,7 +161,11 @@ struct gsv_engine {
     float* hubert_ws(size_t floats);
     int hubert_forward(const float* audio, int n, float* out, hipStream_t st);
     int finalize_roberta();
-    int roberta_forward(const int64_t* ids, int N, const int* rows, int n_out, float* out, hipStream_t st);
+    // RoBERTa over N token rows; rows[n_out]: the token row of each output row.  Packed
+    // sentences: row_pos (host [N], position within its sentence) and row_seg (host [N][2],
+    // {first row, rows} of its sentence), else one sentence.
+    int roberta_forward(const int64_t* ids, int N, const int* rows, int n_out, float* out, hipStream_t st,
+                        const int* row_pos = nullptr, const int* row_seg = nullptr);
     int reserve(int batch, int tokens);
     int ensure_enc_ws(int P, int L);
     int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st, bool do_prompts = true);

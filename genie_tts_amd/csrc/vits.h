@@ -75,6 +75,8 @@ struct MhaArgs {
     int nq, nk, heads, dk;
     int postdiv; float scale;          // prescale: divisor sqrt(dk); postdiv: temperature
     const float* ek; const float* ev; int window;   // rel-pos (or null)
+    const int* row_seg;   // optional (device) [nq][2] {first key, key count} per query row: packed
+                          // sequences attend within their own rows (no rel-pos); nk is then unused
 };
 void mha(const MhaArgs& a, hipStream_t s);
 

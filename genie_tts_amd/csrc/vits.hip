@@ -333,6 +333,15 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
     __shared__ float qe[2 * MHA_MAXW + 1];
     const int hd = blockIdx.x, i = blockIdx.y, tid = threadIdx.x;
     const int dk = a.dk, c0 = hd * dk;
+    int nk = a.nk;
+    const float* kb = a.k;
+    const float* vb = a.v;
+    if (a.row_seg) {   // packed sequences: this row's keys are rows [seg0, seg0 + nk)
+        const int seg0 = a.row_seg[2 * i];
+        nk = a.row_seg[2 * i + 1];
+        kb += (long)seg0 * a.k_ts;
+        vb += (long)seg0 * a.v_ts;
+    }
     for (int d = tid; d < dk; d += 256) {
         const float qv = a.q[(long)i * a.q_ts + (long)(c0 + d) * a.q_cs];
         qs[d] = a.postdiv ? qv : qv / a.scale;
@@ -349,9 +358,9 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
         __syncthreads();
     }
     float lmax = -INFINITY;
-    for (int j = tid; j < a.nk; j += 256) {
+    for (int j = tid; j < nk; j += 256) {
         // 32 key loads in flight per step (the d order of the single sum is kept)
-        const float* kp = a.k + (long)j * a.k_ts + (long)c0 * a.k_cs;
+        const float* kp = kb + (long)j * a.k_ts + (long)c0 * a.k_cs;
         float s = 0.f;
         int d = 0;
         for (; d + 32 <= dk; d += 32) {
@@ -372,28 +381,28 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
     }
     const float m = block_max(lmax, red);
     float lsum = 0.f;
-    for (int j = tid; j < a.nk; j += 256) {
+    for (int j = tid; j < nk; j += 256) {
         const float e = expf(p[j] - m);
         p[j] = e;
         lsum += e;
     }
     const float sum = block_sum(lsum, red);
-    for (int j = tid; j < a.nk; j += 256) p[j] = p[j] / sum;
+    for (int j = tid; j < nk; j += 256) p[j] = p[j] / sum;
     __syncthreads();
     // out[d] = sum_j p_j v[j][d]  (+ sum_{|j-i|<=W} p_j ev[j-i+W][d])
     const int half = tid >> 7, dd = tid & 127;
     for (int d = dd; d < dk; d += 128) {
-        const float* vp = a.v + (long)(c0 + d) * a.v_cs;
+        const float* vp = vb + (long)(c0 + d) * a.v_cs;
         float o = 0.f;
         int j = half;
-        for (; j + 30 < a.nk; j += 32) {   // 16 value loads in flight per step, j order kept
+        for (; j + 30 < nk; j += 32) {   // 16 value loads in flight per step, j order kept
             float vv[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) vv[u] = vp[(long)(j + 2 * u) * a.v_ts];
 #pragma unroll
             for (int u = 0; u < 16; ++u) o += p[j + 2 * u] * vv[u];
         }
-        for (; j < a.nk; j += 2) o += p[j] * vp[(long)j * a.v_ts];
+        for (; j < nk; j += 2) o += p[j] * vp[(long)j * a.v_ts];
         part[half][d] = o;
     }
     __syncthreads();
@@ -407,7 +416,7 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
 #pragma unroll
             for (int r = 0; r <= 2 * MHA_MAXW; ++r) {
                 const int j = i + r - a.window;
-                if (r <= 2 * a.window && j >= 0 && j < a.nk) ol += p[j] * evv[r];
+                if (r <= 2 * a.window && j >= 0 && j < nk) ol += p[j] * evv[r];
             }
             o = o + ol;
         }
@@ -416,7 +425,7 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
 }
 
 void mha(const MhaArgs& a, hipStream_t s) {
-    if ((a.ek || a.ev) && a.window > MHA_MAXW) return;   // window 4 in every graph; the host never asks more
+    if ((a.ek || a.ev) && a.window > MHA_MAXW) return;   // window 4, checked when the weights load
     hipLaunchKernelGGL(k_mha, dim3(a.heads, a.nq), dim3(256), 0, s, a);
 }
 

@@ -121,6 +121,7 @@ def lib():
         L.gsv_hubert_frames.argtypes = [ctypes.c_int32]
         L.gsv_hubert.argtypes = [vp, vp, ctypes.c_int32, vp, vp]
         L.gsv_roberta.argtypes = [vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
+        L.gsv_roberta_batch.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -134,7 +135,7 @@ EXPORTED = (
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
     "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
     "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
-    "gsv_vits_decode_batch_async", "gsv_vits_batch_wait", "gsv_ref_encode",
+    "gsv_vits_decode_batch_async", "gsv_vits_batch_wait", "gsv_ref_encode", "gsv_roberta_batch",
 )
 
 
@@ -536,6 +537,25 @@ class Engine:
                                  ids.numel(), rep.ctypes.data_as(ctypes.c_void_p), rep.size, _ptr(out), _stream()),
                "gsv_roberta")
         return out
+
+    def roberta_batch(self, sentences):
+        """Packed RoBERTa over several sentences (gsv_roberta_batch): sentences = [(input_ids
+        [N_i] CLS .. SEP, word2ph [C_i])] -> one text_bert tensor [sum(word2ph_i), 1024] per
+        sentence (views of one device buffer), identical to per-sentence roberta()."""
+        t = self.torch
+        ids = [np.asarray(i, np.int64).reshape(-1) for i, _ in sentences]
+        reps = [np.asarray(r, np.int64).reshape(-1) for _, r in sentences]
+        dids = self._dev(np.concatenate(ids), t.int64)
+        nt = np.asarray([i.size for i in ids], np.int32)
+        nc = np.asarray([r.size for r in reps], np.int32)
+        rep = np.ascontiguousarray(np.concatenate(reps)) if sum(r.size for r in reps) else np.zeros(1, np.int64)
+        rows = [int(r.sum()) for r in reps]
+        out = t.empty((max(1, sum(rows)), 1024), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_roberta_batch(self.h, len(sentences), _ptr(dids), nt.ctypes.data_as(ctypes.c_void_p),
+                                       rep.ctypes.data_as(ctypes.c_void_p), nc.ctypes.data_as(ctypes.c_void_p),
+                                       _ptr(out), _stream()), "gsv_roberta_batch")
+        offs = np.concatenate([[0], np.cumsum(rows)])
+        return [out[offs[i]:offs[i + 1]] for i in range(len(sentences))]
 
     def debug_copy(self, name: str, n: int):
         t = self.torch

@@ -43,7 +43,7 @@ class GSVModel:
 
 def build_model(weights: Dict[str, Dict[str, np.ndarray]], version: str, language: str = "Japanese",
                 device: int = 0, sampler: Optional[Sampler] = None, model_dir: Optional[str] = None,
-                pe_div_term: Optional[np.ndarray] = None) -> GSVModel:
+                pe_div_term: Optional[np.ndarray] = None, vits_noise: str = "philox") -> GSVModel:
     eng = Engine(weights, version, device=device, pe_div_term=pe_div_term)
     emb = np.asarray(weights["t2s"]["ar_audio_embedding.word_embeddings.weight"], np.float32)
     st = _T2SState()
@@ -54,7 +54,7 @@ def build_model(weights: Dict[str, Dict[str, np.ndarray]], version: str, languag
         T2S_ENCODER=EncoderSession(eng),
         T2S_FIRST_STAGE_DECODER=FirstStageDecoderSession(eng, emb, st, sp),
         T2S_STAGE_DECODER=StageDecoderSession(eng, emb, st, sp),
-        VITS=VitsSession(eng, version),
+        VITS=VitsSession(eng, version, noise=vits_noise),
         PROMPT_ENCODER=pe,
         PROMPT_ENCODER_PATH=os.path.join(model_dir, "prompt_encoder_fp32.onnx") if (model_dir and pe) else None,
         ENGINE=eng,
@@ -70,6 +70,7 @@ class ModelManager:
         self.character_to_language: Dict[str, str] = {}
         self.character_model_paths: Dict[str, str] = {}
         self.sampler: Optional[Sampler] = None
+        self.vits_noise = "philox"       # z_p noise of new characters' vocoders ("zero": deterministic tests)
         self.cn_hubert = None            # HubertSession (ModelManager.py:127,172-195)
         self.roberta = None              # RobertaSession (ModelManager.py:129,132-150)
 
@@ -88,7 +89,8 @@ class ModelManager:
             self.character_to_model.move_to_end(name)
             return True
         version, w = W.load_character_weights(model_dir)
-        self._put(name, build_model(w, version, language, self.device, self.sampler, model_dir))
+        self._put(name, build_model(w, version, language, self.device, self.sampler, model_dir,
+                                    vits_noise=self.vits_noise))
         self.character_to_language[name] = language
         self.character_model_paths[name] = model_dir
         logger.info("Character %s loaded (%s) from %s", name, "V2ProPlus" if version != "v2" else "V2", model_dir)
@@ -98,7 +100,8 @@ class ModelManager:
                      language: str = "Japanese") -> bool:
         """Register a character from in-memory weights (synthetic characters, tests, benchmarks)."""
         name = character_name.lower()
-        self._put(name, build_model(weights, version, language, self.device, self.sampler))
+        self._put(name, build_model(weights, version, language, self.device, self.sampler,
+                                    vits_noise=self.vits_noise))
         self.character_to_language[name] = language
         return True
 

@@ -23,8 +23,10 @@ from typing import Callable, List, Optional, Sequence
 class Request:
     idx: int                      # position in the caller's order
     text_seq: object              # i64 [S] (or [1,S]) phoneme ids
-    text_bert: object = None      # f32 [S,1024] or None (zeros)
+    text_bert: object = None      # f32 [S,1024] or None (zeros, or RoBERTa below)
     force_steps: int = 0          # >0: known decode length (benchmarks)
+    bert_ids: object = None       # Chinese: RoBERTa input_ids [C+2] (CLS .. SEP) ...
+    word2ph: object = None        # ... and phones per character [C]: text_bert from RoBERTa
 
     @property
     def n_phones(self) -> int:
@@ -83,13 +85,31 @@ def run_sharded(requests: Sequence[Request], synth: Callable[[List[Request]], Li
     return [o for _, o in merged]
 
 
-def engine_synth(model, reference, sampler_factory) -> Callable[[List[Request]], List[object]]:
-    """synth() over one engine-backed GSVModel: one batched T2S for the shard
-    (each request's own forced length, if any), then the vocoder per utterance
-    (inference.GENIE.tts_batch).  sampler_factory() -> engine.Sampler."""
+def text_berts(reqs: Sequence[Request], roberta=None) -> List[object]:
+    """Each request's BERT features: its text_bert, or -- a Chinese sentence given as
+    RoBERTa inputs (bert_ids, word2ph) -- RoBERTa's, all such sentences of the list in one
+    packed pass (`roberta.roberta_batch`, gsv_roberta_batch; the reference runs one
+    RoBERTa session call per Chinese sentence, GetPhonesAndBert.py:64-74); else None
+    (zeros: Japanese / English)."""
+    out = [r.text_bert for r in reqs]
+    zh = [i for i, r in enumerate(reqs) if r.text_bert is None and r.bert_ids is not None]
+    if zh:
+        if roberta is None:
+            raise ValueError("Chinese requests given as RoBERTa inputs need a RoBERTa engine")
+        feats = roberta.roberta_batch([(reqs[i].bert_ids, reqs[i].word2ph) for i in zh])
+        for i, f in zip(zh, feats):
+            out[i] = f
+    return out
+
+
+def engine_synth(model, reference, sampler_factory, roberta=None) -> Callable[[List[Request]], List[object]]:
+    """synth() over one engine-backed GSVModel: the shard's Chinese BERT features
+    (text_berts, on `roberta` -- an Engine holding RoBERTa weights, e.g. model.ENGINE),
+    one batched T2S for the shard (each request's own forced length, if any), then the
+    vocoder per utterance (inference.GENIE.tts_batch).  sampler_factory() -> engine.Sampler."""
     from .inference import tts_client
 
     def synth(reqs: List[Request]):
-        items = [(r.text_seq, r.text_bert, r.force_steps) for r in reqs]
+        items = [(r.text_seq, b, r.force_steps) for r, b in zip(reqs, text_berts(reqs, roberta))]
         return tts_client.tts_batch(items, reference, model, sampler_factory())
     return synth

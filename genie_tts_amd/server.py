@@ -71,6 +71,8 @@ def _worker_main(index: int, conn, cfg: dict) -> None:
     genie.set_sv_extractor(_resolve(cfg.get("sv")))
     if cfg.get("greedy"):
         model_manager.sampler = make_sampler(greedy=True)
+    if cfg.get("noise"):             # "zero": deterministic vocoder noise (tests pin the streamed audio)
+        model_manager.vits_noise = cfg["noise"]
     splitter = TextSplitter()
     pipeline = bool(cfg.get("pipeline", False))
     pending: List[dict] = []        # tts requests: {"id", "character_name", "sentences", "next", "force_steps"}
@@ -229,10 +231,11 @@ class Router:
     """Owns the worker processes; never touches the GPU itself."""
 
     def __init__(self, gpus: List[int], g2p: Optional[str] = None, ssl: Optional[str] = None,
-                 sv: Optional[str] = None, greedy: bool = False, worker=None, pipeline: bool = False):
+                 sv: Optional[str] = None, greedy: bool = False, worker=None, pipeline: bool = False,
+                 noise: Optional[str] = None):
         self.gpus = gpus
         self.worker = worker or _worker_main         # tests substitute a host-only worker
-        self.cfg = {"g2p": g2p, "ssl": ssl, "sv": sv, "greedy": greedy, "pipeline": pipeline}
+        self.cfg = {"g2p": g2p, "ssl": ssl, "sv": sv, "greedy": greedy, "pipeline": pipeline, "noise": noise}
         self.ids = itertools.count(1)
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.queues: Dict[int, asyncio.Queue] = {}

@@ -10,9 +10,12 @@ semantic tokens (the trim of Inference.py:108-109 drops the last one).
 
   configs[1] single()        one 20-char JP utterance, S=45, G=80
   configs[2] batch64()       64 mixed-length JP sentences, S~U[30,60], G~U[50,110]
-  configs[3] mixed100()      V2ProPlus EN+ZH 100-sentence set (ZH BERT ~ N(0,1)
-                             as a RoBERTa stand-in, EN BERT zeros), S~U[20,60],
-                             G~U[50,110]
+  configs[3] mixed100()      V2ProPlus EN+ZH 100-sentence set, S~U[20,60],
+                             G~U[50,110]; EN BERT zeros, ZH BERT from RoBERTa
+                             (GetPhonesAndBert.py:64-74) over each ZH sentence's
+                             synthetic token ids + word2ph (Item.bert_ids/word2ph),
+                             computed by the engine (gsv_roberta_batch) in the
+                             bench's timed region, by oracle/bert.py for fixtures
 """
 from __future__ import annotations
 
@@ -46,6 +49,8 @@ class Item:
     text_bert: Optional[np.ndarray]      # f32 [S, 1024] or None (zeros)
     force_steps: int                     # loop steps (G + 1)
     lang: str = "ja"
+    bert_ids: Optional[np.ndarray] = None   # ZH: RoBERTa input_ids [C + 2] (CLS .. SEP)
+    word2ph: Optional[np.ndarray] = None    # ZH: phones per character [C], sum = S
 
     @property
     def tokens(self) -> int:
@@ -97,8 +102,23 @@ def batch64(n: int = 64, tag: str = "b64") -> Workload:
     return Workload(f"configs[2] batch{n}", "v2", reference(tag), items, top_k=5, greedy=False)
 
 
+CLS_ID, SEP_ID = 101, 102
+
+
+def zh_tokens(S: int, tag: str):
+    """RoBERTa inputs of a synthetic Chinese sentence of S phones (the '。' prefix is one
+    character of one phone, every other character two phones -- initial + final, as
+    chinese_to_phones emits them; an odd count ends on a one-phone character):
+    input_ids [C + 2] = CLS, C vocabulary ids, SEP and word2ph [C], sum(word2ph) = S."""
+    w2p = [1] + [2] * ((S - 1) // 2) + ([1] if (S - 1) % 2 else [])
+    r = synth.rng_for("zh-ids:" + tag)
+    ids = np.concatenate([[CLS_ID], r.integers(672, 8000, size=len(w2p)), [SEP_ID]]).astype(np.int64)
+    return ids, np.asarray(w2p, np.int64)
+
+
 def mixed100(n: int = 100, tag: str = "m100") -> Workload:
-    """configs[3]: V2ProPlus EN+ZH sentences (alternating), ZH BERT ~ N(0,1), EN BERT zeros."""
+    """configs[3]: V2ProPlus EN+ZH sentences (alternating); EN BERT zeros, ZH BERT from
+    RoBERTa over the sentence's input_ids / word2ph (text_bert left None here)."""
     r = synth.rng_for("workload:" + tag)
     S = r.integers(20, 61, size=n)
     G = r.integers(50, 111, size=n)
@@ -106,7 +126,12 @@ def mixed100(n: int = 100, tag: str = "m100") -> Workload:
     for i in range(n):
         lang = "zh" if i % 2 == 0 else "en"
         ts = synth.synth_phones(int(S[i]), f"{tag}-t{i}", lang=lang)
-        tb = (synth.rng_for(f"{tag}-bert{i}").standard_normal((int(S[i]), 1024)).astype(np.float32)
-              if lang == "zh" else None)
-        items.append(Item(ts, tb, int(G[i]) + 1, lang))
+        ids, w2p = zh_tokens(int(S[i]), f"{tag}-{i}") if lang == "zh" else (None, None)
+        items.append(Item(ts, None, int(G[i]) + 1, lang, ids, w2p))
     return Workload(f"configs[3] mixed{n}", "v2ProPlus", reference(tag, sv=True), items)
+
+
+def roberta_weights(n_layers: int = 24):
+    """Synthetic RoBERTa (chinese-roberta-wwm-ext-large shapes) for the ZH sentences."""
+    from . import weights as W
+    return synth.synth_weights(W.roberta_spec(n_layers))

@@ -18,7 +18,7 @@
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
  *   vocoder.run's refer branch (Inference.py:50, V2)  gsv_ref_encode (once per reference)
  *   cn_hubert.run          (ReferenceAudio.py:50-52) gsv_hubert
- *   roberta_model.run      (GetPhonesAndBert.py:73)  gsv_roberta
+ *   roberta_model.run      (GetPhonesAndBert.py:73)  gsv_roberta (gsv_roberta_batch: many sentences)
  *   per-sentence tts loop  (TTSPlayer.py:56-107)     gsv_t2s_prefetch, gsv_t2s_generate_start /
  *                                                    _finish, gsv_vits_decode_async / gsv_vits_wait
  *                                                    (option "vocoder_cus")
@@ -247,6 +247,16 @@ int gsv_hubert(gsv_engine* eng, const float* audio_16k, int32_t n_samples, float
  * weights include the BertModel tensors (transformers names). */
 int gsv_roberta(gsv_engine* eng, const int64_t* input_ids, const int64_t* attention_mask, int32_t n_tokens,
                 const int64_t* repeats, int32_t n_chars, float* text_bert, void* stream);
+
+/* The same for n_seq sentences in one pass (the reference runs RoBERTa once per
+ * Chinese sentence; packed here: every GEMM over all sentences' token rows, attention
+ * within each sentence): input_ids (device i64, the sentences' CLS .. SEP ids
+ * concatenated), n_tokens (host [n_seq]), repeats (host i64, the sentences' word2ph
+ * concatenated), n_chars (host [n_seq]) -> text_bert (device, the sentences'
+ * [sum(word2ph_s)][1024] blocks concatenated in order).  Identical to n_seq gsv_roberta
+ * calls. */
+int gsv_roberta_batch(gsv_engine* eng, int32_t n_seq, const int64_t* input_ids, const int32_t* n_tokens,
+                      const int64_t* repeats, const int32_t* n_chars, float* text_bert, void* stream);
 
 /* Debug hooks (tests only): copy a named VITS workspace buffer after
  * gsv_vits_decode ("ge","stats","z","y","q","te","g0","g1","spec","a");

@@ -56,3 +56,21 @@ def test_roberta_session_feeds_chinese_text_features():
         model_manager.roberta = None
         genie.set_g2p(None)
         e.close()
+
+
+def test_roberta_batch_equals_single_calls():
+    """gsv_roberta_batch (packed rows, per-sentence attention) returns exactly what one
+    gsv_roberta call per sentence returns."""
+    from genie_tts_amd import workloads
+    e, B, m = _setup(4)
+    try:
+        sents = [workloads.zh_tokens(S, f"rbb-{S}") for S in (21, 37, 60, 8)]
+        got = e.roberta_batch(sents)
+        for (ids, w2p), g in zip(sents, got):
+            one = e.roberta(ids, w2p).cpu().numpy()
+            assert g.shape == one.shape == (int(w2p.sum()), 1024)
+            assert np.array_equal(g.cpu().numpy(), one)
+        ref = B.bert_features(m, sents[1][0], sents[1][1])
+        assert float(np.sqrt(np.mean((got[1].cpu().numpy() - ref) ** 2))) <= RMS_TOL
+    finally:
+        e.close()
