@@ -543,10 +543,10 @@ class Engine:
         [N_i] CLS .. SEP, word2ph [C_i])] -> one text_bert tensor [sum(word2ph_i), 1024] per
         sentence (views of one device buffer), identical to per-sentence roberta()."""
         t = self.torch
-        ids = [np.asarray(i, np.int64).reshape(-1) for i, _ in sentences]
+        ids = [self._ids(i) for i, _ in sentences]          # host arrays or device tensors
         reps = [np.asarray(r, np.int64).reshape(-1) for _, r in sentences]
-        dids = self._dev(np.concatenate(ids), t.int64)
-        nt = np.asarray([i.size for i in ids], np.int32)
+        dids = t.cat(ids) if len(ids) > 1 else ids[0]
+        nt = np.asarray([i.numel() for i in ids], np.int32)
         nc = np.asarray([r.size for r in reps], np.int32)
         rep = np.ascontiguousarray(np.concatenate(reps)) if sum(r.size for r in reps) else np.zeros(1, np.int64)
         rows = [int(r.sum()) for r in reps]
