@@ -26,9 +26,14 @@
 // LDS, all loaded during the G-1 layers it waits; a waiting workgroup sleeps on one wake-up granule (the output of the
 // layer two before its own) and polls its real inputs only then.  Group 1's FFN
 // workgroups also hold the logits rows (ar_predict_layer, 64 + 1 per workgroup)
-// in LDS for the whole launch and compute the logits after layer 23; group 2's
-// head-0 attention workgroup runs the sampler (sampler.h, K10) and publishes the
-// token granule TK that group 0 waits on.
+// in LDS for the whole launch and compute the logits after layer 23.  Greedy
+// decoding: each of them also reduces its rows to the first argmax of the
+// penalised and of the raw logits and publishes those 4 granules; every group-0
+// workgroup polls the 16 x 4 granules and resolves the token (and the stop rule)
+// itself -- one hop from the logits to layer 0 -- and group 0's head-0 attention
+// workgroup records it (y, seen, the token granule TK the other groups read).
+// Sampled decoding: the logits go to group 2's head-0 attention workgroup, which
+// runs the sampler (sampler.h, K10) and publishes TK, which group 0 waits on.
 //
 // Hand-offs: 8-byte {tag, value} granules (persist.h), tag = (epoch << 12) |
 // (step + 1) in a ring of RING1 step slots.  Every sum is formed in a fixed
@@ -383,8 +388,64 @@ __device__ __noinline__ void attn_general1(Shared1& sh, const float* Kw, const f
 // at once (its layer 0 starts from it) and sleeps on the layer-23 output of the
 // previous step first; the other groups only need the stop bit and poll slowly.
 // Returns false when the loop is over (or on error: sh.fail).
-__device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0, Shared1& sh) {
-    if (threadIdx.x == 0) {
+// Fused greedy step end (group 0, s >= 1): the token of step s - 1 from the logits
+// workgroups' local argmaxes (LG(s - 1): candidate q's {penalised max, its index, raw
+// max, its index} at 4 q .. 4 q + 3; q = 4 j + w covers rows 64 j + 16 w .. + 16, q =
+// 64 the EOS row): the first argmax over all 1025 logits, as sample_block's greedy
+// branch (value max, then the smallest index holding it); the stop rule
+// (stop_condition_tensor, t2s_stage_decoder_fp32.onnx#1807-1821) and the loop end
+// (Inference.py:95-106).  The publisher also appends y, marks seen and publishes TK(s).
+__device__ void resolve_greedy(const PersistArgs& a, const Ws1& ws, int s, int ny0, int st0, bool publisher,
+                               Shared1& sh, int& last_stop, int& last_fin) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    if (tid == 0) wait_tag_slow(ws.PFH(s - 1, 23, 0), ws.tag(s - 1), a.err, ok, a.spin_ticks);
+    if (!block_ok1(ok, sh)) return;
+    if (tid < 64) {
+        // lane q: candidate q's {penalised max, its index, raw max, its index} (16 rows of
+        // slice q / 4); lane 0 also the EOS row's (candidate 64, index 1024)
+        float f[4];
+        wait_gran_n<4>(ws.LG(s - 1) + 4 * tid, 1, ws.tag(s - 1), f, a.err, ok, a.spin_ticks);
+        float gv = f[0], rv = f[2];
+        int gi = __float_as_int(f[1]), ri = __float_as_int(f[3]);
+        if (tid == 0) {
+            float e[4];
+            wait_gran_n<4>(ws.LG(s - 1) + 256, 1, ws.tag(s - 1), e, a.err, ok, a.spin_ticks);
+            argmax_merge(gv, gi, e[0], __float_as_int(e[1]));
+            argmax_merge(rv, ri, e[2], __float_as_int(e[3]));
+        }
+        const float gm = wave_max_dpp(gv), rm = wave_max_dpp(rv);
+        const int tok = wave_min_dpp(gv == gm ? gi : 0x7fffffff);
+        const int raw = wave_min_dpp(rv == rm ? ri : 0x7fffffff);
+        if (tid == 0) {
+            const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
+            const bool fin = seq_finished(a.force_b, 0, a.force_steps, a.max_steps, st0 + s, stop);
+            sh.tok = tok;
+            sh.fin = fin ? 1 : 0;
+            if (publisher && ok) {
+                a.y[ny0 + s - 1] = tok;
+                sh.seen[tok >> 5] |= 1u << (tok & 31);
+                last_stop = stop;
+                last_fin = fin ? 1 : 0;
+                st_gran(ws.TK(s), ws.tag(s), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+            }
+        }
+    }
+    if (!ok) sh.fail = 1;
+}
+
+// Step start: thread 0 learns the token of step s (s >= 1: granule TK(s), whose
+// bit 16 says the previous step finished the sequence).  Group 0 needs the token
+// at once (its layer 0 starts from it): with fused greedy it resolves it itself
+// (resolve_greedy), else it sleeps on the layer-23 output of the previous step and
+// then polls TK; the other groups only need the stop bit and poll slowly (the
+// greedy logits workgroups also mark the token in their seen bitmap).
+// Returns false when the loop is over (or on error: sh.fail).
+__device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0, Shared1& sh, bool fused,
+                           bool mark_seen, bool publisher, int ny0, int st0, int& last_stop, int& last_fin) {
+    if (fused && grp0 && s > 0) {
+        resolve_greedy(a, ws, s, ny0, st0, publisher, sh, last_stop, last_fin);
+    } else if (threadIdx.x == 0) {
         bool ok = true;
         if (s > 0) {
             float v;
@@ -398,6 +459,7 @@ __device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0
             const unsigned u = __float_as_uint(v);
             sh.tok = (int)(u & 0xffff);
             sh.fin = ok ? (int)((u >> 16) & 1) : 1;
+            if (mark_seen && ok) sh.seen[sh.tok >> 5] |= 1u << (sh.tok & 31);
         }
         if (!ok) sh.fail = 1;
     }
@@ -501,14 +563,16 @@ __device__ __forceinline__ bool form_u(const PersistArgs& a, const Ws1& ws, int 
 __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int grp, int h) {
     const int tid = threadIdx.x, lane = tid & 63, ng = a.groups;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool sampler = grp == SAMPLER_GRP && h == 0;
+    const bool fused = a.greedy && a.knob[0] == 0;   // fused greedy step end (knob0 = 1: the sampler path)
+    const bool sampler = !fused && grp == SAMPLER_GRP && h == 0;
+    const bool publisher = fused ? (grp == 0 && h == 0) : sampler;   // records y / seen / sequence state
     const int ny0 = a.ny[0], kv0 = a.kvlen[0], st0 = a.steps[0];
     if (tid == 0) {
         sh.tok = (int)a.y[ny0 - 1];
         sh.fin = a.done[0] ? 1 : 0;
         sh.fail = 0;
     }
-    if (sampler && tid < 33) sh.seen[tid] = a.seen[tid];
+    if (publisher && tid < 33) sh.seen[tid] = a.seen[tid];
     const long kvoff = (long)h * a.tmax * 32;
     uint4 wq[16], wo[4];
     float qfB = 0.f, qfC = 0.f;   // folded LN2 vectors of this lane's q/k/v row
@@ -543,7 +607,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
     prefetch(grp, kv0);
     int n_exec = 0, last_stop = 0, last_fin = 0;
     for (int s = 0; s < a.smax; ++s) {
-        if (!step_start(a, ws, s, grp == 0, sh)) break;
+        if (!step_start(a, ws, s, grp == 0, sh, fused, false, publisher, ny0, st0, last_stop, last_fin)) break;
         const unsigned tag = ws.tag(s);
         const int kv = kv0 + s;
         for (int l = grp; l < 24; l += ng) {
@@ -698,8 +762,13 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         }
         ++n_exec;
     }
-    // ---- sequence state write-back (sampler workgroup)
-    if (sampler && n_exec > 0 && sh.fail == 0) {
+    // fused greedy at the launch's step cap: the last executed step's token is still unresolved
+    if (fused && grp == 0 && n_exec == a.smax && n_exec > 0 && sh.fail == 0 && sh.fin == 0) {
+        resolve_greedy(a, ws, n_exec, ny0, st0, publisher, sh, last_stop, last_fin);
+        __syncthreads();
+    }
+    // ---- sequence state write-back (the workgroup that recorded the tokens)
+    if (publisher && n_exec > 0 && sh.fail == 0) {
         __syncthreads();
         if (tid < 33) a.seen[tid] = sh.seen[tid];
         if (tid == 0) {
@@ -720,12 +789,15 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
     const int tid = threadIdx.x, lane = tid & 63, ng = a.groups;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool logits = grp == LOGIT_GRP;
-    const int ny0 = a.ny[0];
+    const bool fused = a.greedy && a.knob[0] == 0;
+    const int ny0 = a.ny[0], st0 = a.steps[0];
+    int last_stop = 0, last_fin = 0;   // (unused by FFN workgroups)
     if (tid == 0) {
         sh.tok = (int)a.y[ny0 - 1];
         sh.fin = a.done[0] ? 1 : 0;
         sh.fail = 0;
     }
+    if (logits && fused && tid < 33) sh.seen[tid] = a.seen[tid];   // the repetition penalty of its rows
     if (logits) {
         // rows 64 j + r (r < 64) and, on the last slice, the EOS row 1024 -- resident for the launch
         for (int e = tid; e < (LROWS + 1) * 64; e += PT) {
@@ -769,7 +841,8 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
     if (sh.fin) return;
     prefetch(grp);
     for (int s = 0; s < a.smax; ++s) {
-        if (!step_start(a, ws, s, grp == 0, sh)) break;
+        if (!step_start(a, ws, s, grp == 0, sh, fused, logits && fused, false, ny0, st0, last_stop, last_fin))
+            break;
         const unsigned tag = ws.tag(s);
         for (int l = grp; l < 24; l += ng) {
             const bool probe = a.trace && ((s == 8 && (l == 12 || l == 13 || l == 23)) || (s == 9 && l == 0));
@@ -881,10 +954,41 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                     c0 = mfma16(afrag(ab, 32 * cb), bfrag(wb[4 * cb]), c0);
                     c1 = mfma16(afrag(ab, 32 * (cb + 1)), bfrag(wb[4 * (cb + 1)]), c1);
                 }
-                if (lane < 16 && (w < 4 || lane == 0)) {
-                    const int rl = 16 * w + lane;   // LROWS: the EOS row
-                    const float v = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * sh.ff.lfB[rl]) + sh.ff.lfC[rl];
-                    st_gran(ws.LG(s) + (w < 4 ? j * LROWS + rl : 1024), tag, v);
+                const int rl = 16 * w + lane;   // LROWS: the EOS row
+                const float v = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * sh.ff.lfB[min(rl, LROWS)]) +
+                                sh.ff.lfC[min(rl, LROWS)];
+                if (!fused) {
+                    if (lane < 16 && (w < 4 || lane == 0)) st_gran(ws.LG(s) + (w < 4 ? j * LROWS + rl : 1024), tag, v);
+                } else {
+                    // greedy: this wave's 16 rows (wave 4: the EOS row alone) reduced to the first
+                    // argmax of the penalised logits (K10 penalty over the seen tokens,
+                    // / temperature) and of the raw ones: 4 granules of candidate q = 4 j + w
+                    // (q = 64: the EOS row), no barrier
+                    const int i = w < 4 ? j * LROWS + rl : 1024;
+                    const bool live = w < 4 ? lane < 16 : lane == 0;
+                    float pv = ((sh.seen[i >> 5] >> (i & 31)) & 1u) ? (v < 0.f ? v * a.rep_penalty : v / a.rep_penalty)
+                                                                   : v;
+                    pv = pv / a.temperature;
+                    float gv = live ? pv : -INFINITY, rv = live ? v : -INFINITY;
+                    int gi = live ? i : 0x7fffffff, ri = gi;
+                    // 16-lane row reductions (row 0 holds the live lanes): value max, then the
+                    // smallest index holding it
+                    gv = fmaxf(gv, dpp_f<0xB1, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0xB1, 0xF>(rv));
+                    gv = fmaxf(gv, dpp_f<0x4E, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x4E, 0xF>(rv));
+                    gv = fmaxf(gv, dpp_f<0x141, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x141, 0xF>(rv));
+                    gv = fmaxf(gv, dpp_f<0x140, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x140, 0xF>(rv));
+                    const float gm = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gv)));
+                    const float rm = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rv)));
+                    int gmi = (live && pv == gm) ? i : 0x7fffffff, rmi = (live && v == rm) ? i : 0x7fffffff;
+                    gmi = min(gmi, dpp_i<0xB1, 0xF>(gmi)); rmi = min(rmi, dpp_i<0xB1, 0xF>(rmi));
+                    gmi = min(gmi, dpp_i<0x4E, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x4E, 0xF>(rmi));
+                    gmi = min(gmi, dpp_i<0x141, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x141, 0xF>(rmi));
+                    gmi = min(gmi, dpp_i<0x140, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x140, 0xF>(rmi));
+                    if (lane < 4) {
+                        const float out = lane == 0 ? gm : lane == 1 ? __int_as_float(gmi)
+                                        : lane == 2 ? rm : __int_as_float(rmi);
+                        st_gran(ws.LG(s) + 4 * (w < 4 ? 4 * j + w : 64) + lane, tag, out);
+                    }
                 }
             }
             STAMP1(2);
