@@ -21,9 +21,10 @@ __device__ __forceinline__ int xcc_id() {
     return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf;   // HW_REG_XCC_ID bits [3:0]
 }
 
-__device__ bool sweep(const u64* base, unsigned tag) {   // thread t: granule t of 16 rows of 512
+__device__ bool sweep(const u64* base, unsigned tag, int G) {   // thread t < G: granule t of 16 rows
     u64 g[NP];
     const int t = threadIdx.x;
+    if (t >= G) return true;
 #pragma unroll
     for (int k = 0; k < NP; ++k) g[k] = ld_sc1(base + k * PT + t);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -41,7 +42,7 @@ __device__ bool sweep(const u64* base, unsigned tag) {   // thread t: granule t 
 }
 
 __global__ __launch_bounds__(PT) void k_hop(u64* A, u64* B, int iters, int config, unsigned long long* out, int* xcc,
-                                            int* fail) {
+                                            int* fail, int G) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (t == 0) xcc[b] = xcc_id();
     int member;
@@ -59,16 +60,65 @@ __global__ __launch_bounds__(PT) void k_hop(u64* A, u64* B, int iters, int confi
     for (int i = 1; i <= iters; ++i) {
         const u64 v = ((u64)(unsigned)i << 32) | (unsigned)(t + idx);
         if (prod) {
-            if (plain) st_plain(A + idx * PT + t, v); else st_sc1(A + idx * PT + t, v);
-            if (!sweep(B, i)) { *fail = 1; return; }
+            if (t < G) { if (plain) st_plain(A + idx * PT + t, v); else st_sc1(A + idx * PT + t, v); }
+            if (!sweep(B, i, G)) { *fail = 1; return; }
             __syncthreads();
         } else {
-            if (!sweep(A, i)) { *fail = 1; return; }
+            if (!sweep(A, i, G)) { *fail = 1; return; }
             __syncthreads();
-            if (plain) st_plain(B + idx * PT + t, v); else st_sc1(B + idx * PT + t, v);
+            if (t < G) { if (plain) st_plain(B + idx * PT + t, v); else st_sc1(B + idx * PT + t, v); }
         }
     }
     if (member == 0 && t == 0) out[config] = __builtin_amdgcn_s_memrealtime() - t0;
+}
+
+// 16-byte granules {tag, v0, v1, v2}: thread t < G polls granule t of every producer
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, int off) {   // buffer_load_dwordx4 ... sc1 (aux bit 4)
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off * 16, 0, 16));
+}
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ bool sweep16(const u32x4* base, unsigned tag, int G) {
+    const int t = threadIdx.x;
+    if (t >= G) return true;
+    u32x4 g[NP];
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) g[k] = ld16(r, k * PT + t);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) all &= g[k].x == tag;
+        if (all) return true;
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (g[k].x != tag) g[k] = ld16(r, k * PT + t);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;
+    }
+}
+__global__ __launch_bounds__(PT) void k_hop16(u32x4* A, u32x4* B, int iters, unsigned long long* out, int* fail, int G) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (b >= 32) return;
+    const bool prod = b < NP;
+    const int idx = b % NP;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 1; i <= iters; ++i) {
+        const u32x4 v = {(unsigned)i, (unsigned)t, (unsigned)idx, 7u};
+        if (prod) {
+            if (t < G) st16(A + idx * PT + t, v);
+            if (!sweep16(B, i, G)) { *fail = 1; return; }
+            __syncthreads();
+        } else {
+            if (!sweep16(A, i, G)) { *fail = 1; return; }
+            __syncthreads();
+            if (t < G) st16(B + idx * PT + t, v);
+        }
+    }
+    if (b == 0 && t == 0) out[3] = __builtin_amdgcn_s_memrealtime() - t0;
 }
 
 int main() {
@@ -82,12 +132,12 @@ int main() {
     hipMalloc(&fail, 4);
     const int iters = 2000;
     const char* names[3] = {"one XCD, sc1 stores  ", "one XCD, plain stores", "8 XCDs,  sc1 stores  "};
-    for (int rep = 0; rep < 2; ++rep)
+    for (int G : {512, 256})
         for (int c = 0; c < 3; ++c) {
             hipMemset(A, 0, NP * PT * 8 * 2);
             hipMemset(B, 0, NP * PT * 8 * 2);
             hipMemset(fail, 0, 4);
-            hipLaunchKernelGGL(k_hop, dim3(256), dim3(PT), 0, 0, A, B, iters, c, out, xcc, fail);
+            hipLaunchKernelGGL(k_hop, dim3(256), dim3(PT), 0, 0, A, B, iters, c, out, xcc, fail, G);
             if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
             unsigned long long h[4];
             int f, x[256];
@@ -96,9 +146,25 @@ int main() {
             hipMemcpy(x, xcc, 1024, hipMemcpyDeviceToHost);
             int same = 1;
             for (int m = 0; m < 32; ++m) same &= x[8 * m] == x[0];
-            printf("%s: %.3f us per hop%s  (blocks b%%8==0 on one XCC: %s, xcc[0..7] = %d %d %d %d %d %d %d %d)\n",
-                   names[c], h[c] * 10e-3 / (2.0 * iters), f ? "  TIMEOUT" : "", same ? "yes" : "no", x[0], x[1],
-                   x[2], x[3], x[4], x[5], x[6], x[7]);
+            printf("G=%3d granules/producer (%5.1f KB swept per consumer) %s: %.3f us per hop%s%s\n", G,
+                   G * 16 * 8 / 1024.0, names[c], h[c] * 10e-3 / (2.0 * iters), f ? "  TIMEOUT" : "",
+                   same ? "" : "  (placement not XCD-grouped)");
         }
+    u32x4 *A16, *B16;
+    hipMalloc(&A16, NP * PT * 16 * 2);
+    hipMalloc(&B16, NP * PT * 16 * 2);
+    for (int G : {171, 128, 64}) {
+        hipMemset(A16, 0, NP * PT * 16 * 2);
+        hipMemset(B16, 0, NP * PT * 16 * 2);
+        hipMemset(fail, 0, 4);
+        hipLaunchKernelGGL(k_hop16, dim3(256), dim3(PT), 0, 0, A16, B16, iters, out, fail, G);
+        if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
+        unsigned long long h[4];
+        int f;
+        hipMemcpy(h, out, 32, hipMemcpyDeviceToHost);
+        hipMemcpy(&f, fail, 4, hipMemcpyDeviceToHost);
+        printf("16-B granules G=%3d per producer (%5.1f KB swept per consumer) 8 XCDs sc1: %.3f us per hop%s\n", G,
+               G * 16 * 16 / 1024.0, h[3] * 10e-3 / (2.0 * iters), f ? "  TIMEOUT" : "");
+    }
     return 0;
 }
