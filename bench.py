@@ -119,22 +119,29 @@ class Runner:
         i's decode (gsv_t2s_prefetch), and utterance i's vocoder runs there beside
         utterance i+1's decode (gsv_vits_decode_async)."""
         eng = self.eng
-        if getattr(self, "utt", None) is None:
-            self.utt = (self.d_ref, self.d_txt[0], self.d_ref_bert, self.d_bert[0], self.d_ssl,
-                        self.items[0].force_steps)
+        if getattr(self, "utts", None) is None:
+            # the stream's sentences are all the workload's one utterance, but each sentence
+            # of a real stream has buffers of its own: alternate two copies, so sentence 0 is
+            # not taken for the prefetched sentence 1 (its prefill runs on the T2S CUs, as
+            # GENIE.tts_stream's first sentence does)
+            self.utts = [(self.d_ref, t, self.d_ref_bert, self.d_bert[0], self.d_ssl, self.items[0].force_steps)
+                         for t in (self.d_txt[0], self.d_txt[0].clone())]
+        utt = lambda i: self.utts[i % 2]
         cond = dict(ge=self.ge_v2) if self.ge is None else dict(ge=self.ge, ge_advanced=self.ge_adv)
-        eng.t2s_prefetch(self.utt, self.sp)   # (the stream's utterances are all the same one here)
-        eng.t2s_generate_start(self.utt, self.sp)
+        if n > 1:
+            eng.t2s_prefetch(utt(1), self.sp)   # launched beside sentence 0's decode
+        eng.t2s_generate_start(utt(0), self.sp)
         sems = None
         for i in range(n):
             if i + 1 < n:
-                eng.t2s_prefetch(self.utt, self.sp)
-                eng.t2s_generate_start(self.utt, self.sp)
+                if i + 2 < n:
+                    eng.t2s_prefetch(utt(i + 2), self.sp)
+                eng.t2s_generate_start(utt(i + 1), self.sp)
             sems = [eng.t2s_generate_finish()]
             if phase_ms is not None:
                 phase_ms.append(eng.timing())
             self.finish()                                   # the previous utterance's vocoder
-            self.pending = eng.vits_decode_async(dict(text_seq=self.d_txt[0], pred_semantic=sems[0],
+            self.pending = eng.vits_decode_async(dict(text_seq=utt(i)[1], pred_semantic=sems[0],
                                                       noise_seed=self.seed, **cond))
         self.finish()
         return sems, 1280 * int(sems[0].size)

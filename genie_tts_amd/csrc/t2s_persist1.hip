@@ -226,10 +226,12 @@ __device__ __noinline__ float scores_general1(Shared1& sh, const float* Kw, int 
     return lmax;
 }
 
-// One wave's share of the head's attention (the common case: T <= 512 keys, all
-// cached rows in LDS): keys t = 64 u + g (u < NU, g = 8 w + lane / 8), 8 lanes x 4
-// dims per key row (conflict-free 16-B LDS reads), every K and V read of the NU
-// rounds issued up front.  Online softmax within the wave: m_w = max s, p = exp(s -
+// One wave's share of the head's attention (the common case: T <= 512 keys, every
+// row [0, kv] in LDS -- the new row kv is written there with the q/k/v results):
+// keys t = 64 u + g (u < NU, g = 8 w + lane / 8), 8 lanes x 4 dims per key row
+// (conflict-free 16-B LDS reads), every K and V read of the NU rounds issued up
+// front.  Rows past kv are read as row kv (finite) and weighted by exp(-inf) = 0,
+// so the rounds carry no per-key selects beyond the score mask.  Online softmax within the wave: m_w = max s, p = exp(s -
 // m_w), l_w = sum p, o_w = sum p v (rows of 16 lanes summed by row_ror 8) -> LDS
 // sh.wred[0/1][w], sh.at.ov4[w][row]; the caller merges the 8 waves after a barrier.
 // x + (x of the other 16-lane row of the pair) / (of the other 32-lane half), every lane
@@ -267,20 +269,19 @@ __device__ __forceinline__ void merge_waves1(Shared1& sh, int w, int lane) {
 }
 
 template <int NU>
-__device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, float q2, float q3, float sc, float4 knew,
+__device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, float q2, float q3, float sc,
                                            int kv, int T, int c8, int g, int w, int lane) {
     float4 kr[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u)
-        kr[u] = *reinterpret_cast<const float4*>(sh.at.k + min(64 * u + g, KVL1 - 1) * 32 + 4 * c8);
+        kr[u] = *reinterpret_cast<const float4*>(sh.at.k + min(64 * u + g, kv) * 32 + 4 * c8);
     // (q s) . (k s) as (q s s) . k: the key's scale folded into the query once per
     // lane instead of once per key element (rounding differs at the ulp level)
     const float p0 = q0 * sc, p1 = q1 * sc, p2 = q2 * sc, p3 = q3 * sc;
     float sv[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-        float4 k4 = kr[u];
-        if (64 * u + g == kv) k4 = knew;
+        const float4 k4 = kr[u];
         float x = p0 * k4.x;
         x += p1 * k4.y;
         x += p2 * k4.z;
@@ -296,7 +297,7 @@ __device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, floa
     float4 vr[NU];   // V reads in flight during the max reduction
 #pragma unroll
     for (int u = 0; u < NU; ++u)
-        vr[u] = *reinterpret_cast<const float4*>(sh.at.v + min(64 * u + g, KVL1 - 1) * 32 + 4 * c8);
+        vr[u] = *reinterpret_cast<const float4*>(sh.at.v + min(64 * u + g, kv) * 32 + 4 * c8);
     float wm = -INFINITY;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
@@ -304,15 +305,12 @@ __device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, floa
         wm = fmaxf(wm, sv[u]);
     }
     const float m_w = wave_max_dpp(wm);
-    const float4 vnew = *reinterpret_cast<const float4*>(sh.qkv + 64 + 4 * c8);
+    const float mref = m_w == -INFINITY ? 0.f : m_w;   // (wave-uniform) every key of this wave masked
     float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f, lsum = 0.f;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-        const int t = 64 * u + g;
-        const float pu = sv[u] == -INFINITY ? 0.f : __expf(sv[u] - m_w);   // v_exp_f32 (ORT's MLAS exp is not libm's either)
-        float4 v4 = vr[u];
-        if (t == kv) v4 = vnew;
-        if (t > kv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);   // rows past the cache: unloaded LDS
+        const float pu = __expf(sv[u] - mref);   // v_exp_f32 (ORT's MLAS exp is not libm's either); masked: exp(-inf) = 0
+        const float4 v4 = vr[u];
         o0 += pu * v4.x;
         o1 += pu * v4.y;
         o2 += pu * v4.z;
@@ -592,14 +590,16 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
 #pragma unroll
         for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + h * 32 + k8, 0);
         if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
-        // K/V rows [0, min(kv, KVL1)) -> LDS, 8 rows (1 KB) per wave instruction.  Rows of
-        // the last chunk past kv are read (allocated: tmax >= kv + 16) and never used.
+        // K/V rows [0, min(kv, KVL1)) -> LDS, 8 rows (1 KB) per wave instruction; lanes of
+        // the last chunk past row kv - 1 stay idle (row kv is written by the q/k/v epilogue)
         const float* K = a.kc[l] + kvoff;
         const float* V = a.vc[l] + kvoff;
-        const int nch = (min(kv, KVL1) + 7) >> 3;
+        const int nr = min(kv, KVL1), nch = (nr + 7) >> 3;
         for (int i = w; i < nch; i += PWV) {
-            __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
+            if (8 * i + (lane >> 3) < nr) {
+                __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
+            }
         }
     };
     __syncthreads();
@@ -635,7 +635,14 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 }
                 mean = l > 0 ? mean : 0.f;   // layer 0: x_0 is not a LayerNorm output
                 rden = l > 0 ? rden : 1.f;
-                if (lane < 16) sh.qkv[16 * w + lane] = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * qfB) + qfC;
+                if (lane < 16) {
+                    const float val = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * qfB) + qfC;
+                    sh.qkv[16 * w + lane] = val;
+                    if (kv < KVL1 && w >= 2) {   // the new K / V row into the LDS stage (fast path reads it there)
+                        float* row = (w < 4 ? sh.at.k : sh.at.v) + kv * 32 + 16 * (w & 1);
+                        row[lane] = val;
+                    }
+                }
             }
             STAMP1(6);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
@@ -652,16 +659,16 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
             const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
             const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
-            if (T <= 512 && kv <= KVL1) {
+            if (T <= 512 && kv < KVL1) {
                 // common case: every cached row is in LDS (per-wave online softmax,
                 // wave_attn1); the round count is specialised so every LDS read of a
                 // round is issued up front.
                 const int nu = (T + 63) >> 6;
-                if (nu <= 2) wave_attn1<2>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
-                else if (nu <= 4) wave_attn1<4>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
-                else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
-                else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
-                else wave_attn1<8>(sh, q0, q1, q2, q3, sc, knew, kv, T, c8, g, w, lane);
+                if (nu <= 2) wave_attn1<2>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                else if (nu <= 4) wave_attn1<4>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                else wave_attn1<8>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
                 __syncthreads();
                 STAMP1(3);
                 merge_waves1(sh, w, lane);
