@@ -10,6 +10,17 @@ installed here, `hubert_version()`), configured as chinese-hubert-base
 GELU, post-norm encoder), loaded with the engine's synthetic weights
 (genie_tts_amd.weights.hubert_spec names).  ONNX-level parity: UNPINNED (no
 graph file, no fixtures in the reference).
+
+Input normalisation.  GPT-SoVITS's CNHubert module wraps HubertModel with a
+Wav2Vec2FeatureExtractor (zero-mean / unit-variance per clip when do_normalize),
+but its inference path calls the inner model directly on the raw 16 kHz clip
+(`ssl_model.model(wav16k.unsqueeze(0))["last_hidden_state"]` in GPT-SoVITS's
+inference_webui.get_tts_wav), and Genie feeds `cn_hubert.run({'input_values':
+audio_16k})` with the raw clip (ReferenceAudio.py:48-52).  So the graph's input is
+raw audio and the oracle's default is `normalize=False`; `normalize=True` is the
+CNHubert.forward variant, kept so tests can show the choice matters (the two differ
+far beyond the parity tolerance) -- whether the absent chinese-hubert-base.onnx bakes
+that step in stays unpinned.
 """
 from __future__ import annotations
 
@@ -54,8 +65,16 @@ def hubert_model(w: Dict[str, np.ndarray]):
     return m
 
 
+def feature_normalize(audio_16k: np.ndarray) -> np.ndarray:
+    """Wav2Vec2FeatureExtractor(do_normalize=True): (x - mean) / sqrt(var + 1e-7) per clip."""
+    x = np.asarray(audio_16k, np.float32).reshape(-1)
+    return ((x - x.mean()) / np.sqrt(x.var() + 1e-7)).astype(np.float32)
+
+
 @torch.no_grad()
-def ssl_content(model, audio_16k: np.ndarray) -> np.ndarray:
-    """[1, 768, T] = HubertModel(audio)["last_hidden_state"].transpose(1, 2)."""
-    x = torch.from_numpy(np.asarray(audio_16k, np.float32).reshape(1, -1))
+def ssl_content(model, audio_16k: np.ndarray, normalize: bool = False) -> np.ndarray:
+    """[1, 768, T] = HubertModel(audio)["last_hidden_state"].transpose(1, 2); normalize=True
+    first applies CNHubert.forward's feature-extractor normalisation (see the module doc)."""
+    a = feature_normalize(audio_16k) if normalize else np.asarray(audio_16k, np.float32)
+    x = torch.from_numpy(a.reshape(1, -1))
     return model(x).last_hidden_state.transpose(1, 2).numpy()

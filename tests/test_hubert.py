@@ -48,3 +48,20 @@ def test_oracle_reproduces_folded_pos_conv_weight():
     x = (0.1 * synth.rng_for("hb-cpu").standard_normal(8000)).astype(np.float32)
     out = H.ssl_content(m, x)
     assert out.shape == (1, 768, 24) and np.isfinite(out).all()
+
+
+def test_input_normalisation_variants_differ():
+    """The raw-clip input (GPT-SoVITS inference, Genie ReferenceAudio.py:48-52; the engine's
+    gsv_hubert) and CNHubert.forward's normalised input give different features: the
+    oracle keeps both, the engine implements the raw one (tests/test_hubert_gpu.py);
+    the two differ beyond the parity bar, so the choice is not cosmetic."""
+    H, m = _hf()
+    from genie_tts_amd import synth
+    x = (0.05 * synth.rng_for("hb-norm").standard_normal(8000) + 0.01).astype(np.float32)
+    raw, nrm = H.ssl_content(m, x), H.ssl_content(m, x, normalize=True)
+    n = H.feature_normalize(x)
+    assert abs(float(n.mean())) < 1e-5 and abs(float(n.std()) - 1.0) < 1e-3
+    assert raw.shape == nrm.shape
+    # the first conv layer's GroupNorm absorbs most of the rescaling, but not all:
+    # ~2e-3 RMS here, 20x the 1e-4 parity bar
+    assert float(np.sqrt(np.mean((raw - nrm) ** 2))) > 1e-3
