@@ -6,7 +6,7 @@ throughput.  Synthetic V2 character (seeded weights, no checkpoints offline), to
 G2P / SSL stand-ins (genie_tts_amd/stubs.py); every sentence is forced to 81 loop
 steps = 80 semantic tokens = 3.2 s of audio (random weights never emit EOS).
 
-Usage: python tools/qps_sweep.py [--gpus N] [--qps 5,10,20,40,80] [--requests 60] [--pipeline 0|1]
+Usage: python tools/qps_sweep.py [--gpus N] [--qps 5,10,20,40,80] [--requests 1000] [--pipeline 0|1]
 Prints one JSON line.
 """
 import argparse
@@ -35,7 +35,7 @@ async def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--qps", default="5,10,20,40,80,160")
-    ap.add_argument("--requests", type=int, default=60)
+    ap.add_argument("--requests", type=int, default=1000)
     ap.add_argument("--port", type=int, default=8765)
     ap.add_argument("--pipeline", type=int, default=0,
                     help="workers overlap each round's vocoder with the next round's T2S")
@@ -89,9 +89,13 @@ async def main():
             gaps = np.random.default_rng(int(qps)).exponential(1.0 / qps, size=len(texts))
             lat, done, tasks = [], [], []
             t_start = time.perf_counter()
-            for text, g in zip(texts, gaps):
+            t_note = time.perf_counter()
+            for k, (text, g) in enumerate(zip(texts, gaps)):
                 tasks.append(asyncio.create_task(one(text, lat, done)))
                 await asyncio.sleep(g)
+                if time.perf_counter() - t_note > 30:   # progress (long low-QPS points)
+                    print(f"qps {qps}: {k + 1}/{len(texts)} sent, {len(done)} done", file=sys.stderr, flush=True)
+                    t_note = time.perf_counter()
             await asyncio.gather(*tasks)
             wall = time.perf_counter() - t_start
             l = np.asarray(lat) * 1e3
