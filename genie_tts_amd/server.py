@@ -289,7 +289,8 @@ class Router:
         with self.state_lock:
             self.dead.add(i)
             owed = [rid for rid, ws in self.sent_to.items() if i in ws]
-        logger.error("worker %d exited; %d request(s) failed", i, len(owed))
+        if not getattr(self, "closing", False):
+            logger.error("worker %d exited; %d request(s) failed", i, len(owed))
         for rid in owed:
             q = self.queues.get(rid)
             if q is not None:
@@ -349,6 +350,7 @@ class Router:
                 self.sent_to.pop(rid, None)
 
     def close(self) -> None:
+        self.closing = True
         for i, c in enumerate(self.conns):
             try:
                 self._send(i, None)
