@@ -176,33 +176,6 @@ __device__ __forceinline__ const _Float16* abase(const _Float16* hi, const _Floa
 __device__ __forceinline__ h8v afrag(const _Float16* base, int k0) {
     return __builtin_bit_cast(h8v, *reinterpret_cast<const uint4*>(base + k0));
 }
-// 8 A fragments (chunks at kbase + 32 i halves, i < 8) read by the 8 lanes whose C rows
-// are used (rows 0 = hi and 1 = lo: lanes 0, 1, 16, 17, 32, 33, 48, 49) with the other
-// lanes masked off: 1/8 of the LDS bandwidth of full-wave reads (MI355X_MICROARCH.md:
-// the LDS array returns 256 B/clk/CU; a full-wave ds_read_b128 is 1 KB).  Rows 2..15
-// of C then hold garbage and are never read.  Waits for the reads before returning.
-__device__ __forceinline__ void afrag8_rows01(const _Float16* base, int kbase, h8v (&af)[8]) {
-    const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) _Float16*)(base + kbase));
-    const unsigned long long m = 0x0003000300030003ull;
-    unsigned long long sv;
-    asm volatile(
-        "s_mov_b64 %[sv], exec\n\t"
-        "s_and_b64 exec, exec, %[m]\n\t"
-        "ds_read_b128 %[f0], %[a]\n\t"
-        "ds_read_b128 %[f1], %[a] offset:64\n\t"
-        "ds_read_b128 %[f2], %[a] offset:128\n\t"
-        "ds_read_b128 %[f3], %[a] offset:192\n\t"
-        "ds_read_b128 %[f4], %[a] offset:256\n\t"
-        "ds_read_b128 %[f5], %[a] offset:320\n\t"
-        "ds_read_b128 %[f6], %[a] offset:384\n\t"
-        "ds_read_b128 %[f7], %[a] offset:448\n\t"
-        "s_mov_b64 exec, %[sv]\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : [f0] "=&v"(af[0]), [f1] "=&v"(af[1]), [f2] "=&v"(af[2]), [f3] "=&v"(af[3]), [f4] "=&v"(af[4]),
-          [f5] "=&v"(af[5]), [f6] "=&v"(af[6]), [f7] "=&v"(af[7]), [sv] "=&s"(sv)
-        : [a] "v"(a), [m] "s"(m)
-        : "memory");
-}
 __device__ __forceinline__ f32x4 mfma16(h8v a, h8v b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
@@ -652,7 +625,8 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
                     h8v af[8];
-                    afrag8_rows01(ab, 32 * cb, af);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
 #pragma unroll
                     for (int i = 0; i < 8; i += 2) {
                         c0 = mfma16(af[i], bfrag(wq[cb + i]), c0);
@@ -918,7 +892,8 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {   // 8 operand reads in flight, then 8 MFMAs
                     h8v af[8];
-                    afrag8_rows01(ab, 32 * cb, af);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
 #pragma unroll
                     for (int i = 0; i < 8; i += 2) {
                         c0 = mfma16(af[i], bfrag(w1r[cb + i]), c0);
