@@ -35,10 +35,17 @@
 // Sampled decoding: the logits go to group 2's head-0 attention workgroup, which
 // runs the sampler (sampler.h, K10) and publishes TK, which group 0 waits on.
 //
-// Hand-offs: 8-byte {tag, value} granules (persist.h), tag = (epoch << 12) |
-// (step + 1) in a ring of RING1 step slots.  Every sum is formed in a fixed
-// order, so results do not depend on arrival order.  Every spin is bounded; a
-// timeout sets the error word and every workgroup leaves.
+// Hand-offs: the two per-layer all-to-alls (PA, PFH) travel as 16-byte granules
+// {tag, v0, v1, v2} -- three consecutive columns and their tag in one write-through
+// store, swept by 16-byte loads (MI355X_MICROARCH.md: 8-byte accesses run at
+// 0.54-0.70x the 16-byte rate; tools/xcd_handoff.hip on this pattern: a 16-producer
+// row sweep 1.55 us vs 1.98 us with 8-byte {tag, value} granules).  Two threads poll
+// each column group (half of the rows each; the second continues the first's sum in
+// row order), so the poll registers stay small.  The logits candidates and the token
+// keep 8-byte granules (persist.h).  tag = (epoch << 12) | (step + 1) in a ring of
+// RING1 step slots.  Every sum is formed in a fixed order, so results do not depend
+// on arrival order.  Every spin is bounded; a timeout sets the error word and every
+// workgroup leaves.
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
@@ -63,28 +70,106 @@ constexpr int LROWS = 64;          // logits rows per FFN workgroup (16 x 64 = 1
 constexpr long FOLD_LAYER = 2 * 1536 + 2 * 2048;   // PersistArgs::fold floats per layer
 constexpr long LOGIT_FOLD = 24 * FOLD_LAYER;        // then [W_pred n2w_23 | W_pred n2b_23] (1025 each)
 
-// Granule ring.  Per step slot: PA [24][16][512], PFH [24][17][512] (rows 0..15 FFN2
-// partials, row 16 = h1), LG [PERSIST_LGS], TK [16].
+// A 512-column row as 16-byte granules: column c -> block b = c / 32, granule
+// 11 b + (c % 32) / 3, slot (c % 32) % 3 (11 granules per 32-column block, the last
+// holding 2 columns): GQ granules per row.
+constexpr int GQ = 176;
+__device__ __forceinline__ int gq_col(int q, int k) { return 32 * (q / 11) + 3 * (q % 11) + k; }
+__device__ __forceinline__ int gq_n(int q) { return q % 11 == 10 ? 2 : 3; }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Granule ring.  Per step slot: PA [24][16][GQ], PFH [24][17][GQ] (rows 0..15 FFN2
+// partials, row 16 = h1) of 16-byte granules, then LG [PERSIST_LGS], TK [16] of 8-byte
+// ones.  The 16-byte rows are addressed as a buffer (byte offsets).
 struct Ws1 {
     u64* ring;
     unsigned epoch;
-    static constexpr long oPFH = 24L * 16 * 512;
-    static constexpr long oLG = oPFH + 24L * 17 * 512;
+    __amdgpu_buffer_rsrc_t rs;                          // the ring as a buffer resource
+    static constexpr long ROW = 2L * GQ;                 // u64 units per 16-byte-granule row
+    static constexpr long oPFH = 24L * 16 * ROW;
+    static constexpr long oLG = oPFH + 24L * 17 * ROW;
     static constexpr long oTK = oLG + PERSIST_LGS;
     static constexpr long SLOT = oTK + 16;
     __device__ u64* slot(int s) const { return ring + (long)(s % RING1) * SLOT; }
     __device__ unsigned tag(int s) const { return (epoch << 12) | (unsigned)(s + 1); }
-    __device__ u64* PA(int s, int l, int h) const { return slot(s) + ((long)l * 16 + h) * 512; }
-    __device__ u64* PFH(int s, int l, int j) const { return slot(s) + oPFH + ((long)l * 17 + j) * 512; }
+    // byte offsets of the 16-byte rows (< 2^31: the ring is ~9 MB)
+    __device__ int PA(int s, int l, int h) const {
+        return (int)(((long)(s % RING1) * SLOT + ((long)l * 16 + h) * ROW) * 8);
+    }
+    __device__ int PFH(int s, int l, int j) const {
+        return (int)(((long)(s % RING1) * SLOT + oPFH + ((long)l * 17 + j) * ROW) * 8);
+    }
+    __device__ const u64* at(int byte_off) const { return ring + byte_off / 8; }
     __device__ u64* LG(int s) const { return slot(s) + oLG; }
     __device__ u64* TK(int s) const { return slot(s) + oTK; }
 };
+
+// One write-through 16-byte store {tag, v0, v1, v2} (buffer_store_dwordx4 ... sc1).
+__device__ __forceinline__ void st_g16(const Ws1& ws, int off, unsigned tag, float v0, float v1, float v2) {
+    const u32x4 v = {tag, __float_as_uint(v0), __float_as_uint(v1), __float_as_uint(v2)};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                           ws.rs, off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ u32x4 ld_g16(const Ws1& ws, int off) {   // buffer_load_dwordx4 ... sc1
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ws.rs, off, 0, 16 /* sc1 */));
+}
+
+// One lane waits for N 16-byte granules off + k * stride (k < N), all N loads in
+// flight; re-polls only the stale ones (persist.h wait_gran_n with 16-byte granules).
+template <int N>
+__device__ __forceinline__ void wait_g16_n(const Ws1& ws, int off, int stride, unsigned tag, u32x4 (&g)[N], int* err,
+                                           bool& ok, unsigned long long ticks) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) g[k] = ld_g16(ws, off + k * stride);
+    unsigned long long t0 = 0;
+    for (unsigned it = 0;; ++it) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < N; ++k) all &= g[k].x == tag;
+        if (all) break;
+        if (it == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");   // the loads below are re-issued every round
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (g[k].x != tag) g[k] = ld_g16(ws, off + k * stride);
+        if ((it & 63) == 63) {
+            if (ld_rlx(err) != 0) { ok = false; break; }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                atomicCAS(err, 0, 1);
+                ok = false;
+                break;
+            }
+        }
+    }
+}
+
+// A sleeping lane waits for the TAG of a 16-byte granule (dword 0) only.
+__device__ __forceinline__ void wait_tag16_slow(const u64* p, unsigned tag, int* err, bool& ok,
+                                                unsigned long long ticks) {
+    if ((unsigned)ld_rlxu64(p) == tag) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(8);
+        if ((unsigned)ld_rlxu64(p) == tag) return;
+        if ((it & 15) == 0) {
+            if (ld_rlx(err) != 0) { ok = false; return; }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                atomicCAS(err, 0, 1);
+                ok = false;
+                return;
+            }
+        }
+    }
+}
 
 // Small arrays first: their LDS offsets stay below 64 KB, so an access is the
 // lane's tid-based address plus an instruction offset (no extra address
 // registers live across the layer loop -- the kernel sits at the 256-VGPR limit).
 struct Shared1 {
-    float x[512];                   // x_l (attention), x_24 (logits)
+    float pk[PWV][64];              // per-wave staging of 64 published columns (16-byte granules)
+    float hs[3 * GQ];               // partial row sums of the first poll half (hop B / hop A)
+    float h1s[32];                  // h1 block j of an FFN workgroup, staged for its 11 granules
     float qkv[96];
     _Float16 osh[PWV][32], osl[PWV][32];   // MFMA row operand: head output split hi + lo (out-projection),
                                            // one copy per wave (each wave merges the head itself)
@@ -104,6 +189,8 @@ struct Shared1 {
                                        // padded by 16 B: the MFMA B reads of 16 rows are conflict-free)
             float lp23[3][512];        // LN2 of layer 23 (b2, scale, shift), logits group
             float lfB[LROWS + 16], lfC[LROWS + 16];   // folded LN2_23 vectors of the rows (fold)
+            float xr[512];             // x_l (form_x), read back by the hop-A column owners
+            float bo[512], n1w[512];   // out-projection bias and LN1 scale of the layer (LDS-DMA)
         } ff;
         struct {                    // attention role
             float k[KVL1 * 32];     // K/V rows [0, min(kv, KVL1)) of the head (LDS-DMA)
@@ -397,7 +484,7 @@ __device__ void resolve_greedy(const PersistArgs& a, const Ws1& ws, int s, int n
                                Shared1& sh, int& last_stop, int& last_fin) {
     const int tid = threadIdx.x;
     bool ok = true;
-    if (tid == 0) wait_tag_slow(ws.PFH(s - 1, 23, 0), ws.tag(s - 1), a.err, ok, a.spin_ticks);
+    if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s - 1, 23, 0)), ws.tag(s - 1), a.err, ok, a.spin_ticks);
     if (!block_ok1(ok, sh)) return;
     if (tid < 64) {
         // lane q: candidate q's {penalised max, its index, raw max, its index} (16 rows of
@@ -448,7 +535,7 @@ __device__ bool step_start(const PersistArgs& a, const Ws1& ws, int s, bool grp0
         if (s > 0) {
             float v;
             if (grp0) {
-                wait_tag_slow(ws.PFH(s - 1, 23, 0), ws.tag(s - 1), a.err, ok, a.spin_ticks);
+                wait_tag16_slow(ws.at(ws.PFH(s - 1, 23, 0)), ws.tag(s - 1), a.err, ok, a.spin_ticks);
                 v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks) : 0.f;
             } else {
                 wait_tag_slow(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks);
@@ -487,11 +574,64 @@ __device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int
     else if (w < 6) dma_half(Q.n2b, sh.p2[2], w & 1, lane);
 }
 
+// Hop B: u = h1_{l-1} + (b2 + sum_j PF[l-1][j]) (l >= 1; the partials summed in
+// slice order) -> sh.lnb[0], and with `split` the MFMA operand split of u * n2w ->
+// sh.xh / sh.xl; lp2 = LDS rows {b2, scale, shift} of LN2_{l-1}.  A sleeping lane
+// waits for the wake-up granule (layer l-2's output); then thread q < GQ polls rows
+// 0..7 of granule column q and thread 256 + q rows 8..16, continuing the first
+// thread's sums in row order (bit-identical to one thread summing rows 0..15).
+// Ends with a block barrier.
+__device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const Ws1& ws, int s, int l, const float* lp2,
+                                           Shared1& sh, bool split) {
+    const int tid = threadIdx.x, q = tid & 255;
+    const unsigned tag = ws.tag(s);
+    constexpr int RB = (int)Ws1::ROW * 8;   // bytes per row
+    bool ok = true;
+    if (l >= 2) {
+        if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s, l - 2, 0)), tag, a.err, ok, a.spin_ticks);
+        if (!block_ok1(ok, sh)) return false;
+    }
+    const int off = ws.PFH(s, l - 1, 0) + 16 * q;
+    u32x4 g[9];
+    if (tid < GQ) {
+        u32x4 h[8];
+        wait_g16_n<8>(ws, off, RB, tag, h, a.err, ok, a.spin_ticks);
+        float f0 = __uint_as_float(h[0].y), f1 = __uint_as_float(h[0].z), f2 = __uint_as_float(h[0].w);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) {
+            f0 += __uint_as_float(h[r].y);
+            f1 += __uint_as_float(h[r].z);
+            f2 += __uint_as_float(h[r].w);
+        }
+        sh.hs[3 * q] = f0; sh.hs[3 * q + 1] = f1; sh.hs[3 * q + 2] = f2;
+    } else if (tid >= 256 && q < GQ) {
+        wait_g16_n<9>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+    }
+    if (!block_ok1(ok, sh)) return false;
+    if (tid >= 256 && q < GQ) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k == 2 && gq_n(q) == 2) break;
+            float f = sh.hs[3 * q + k];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) f += __uint_as_float(g[r][1 + k]);
+            const int c = gq_col(q, k);
+            const float u = __uint_as_float(g[8][1 + k]) + (lp2[c] + f);
+            sh.lnb[0][c] = u;
+            if (split) {
+                const float un = u * lp2[512 + c];
+                if (!split_h(un, sh.xh[c], sh.xl[c]) || !(fabsf(un) < a.f16_limit)) {
+                    atomicCAS(a.err, 0, ERR_F16_RANGE);
+                    ok = false;
+                }
+            }
+        }
+    }
+    return block_ok1(ok, sh);
+}
+
 // x_l for column tid: layer 0 from the token (E_audio[tok] + alpha * pe[n]),
-// otherwise LN2_{l-1}(h1_{l-1} + (b2 + sum_j PF[l-1][j])), the partials summed in
-// slice order; lp2 = LDS rows {b2, scale, shift} of LN2_{l-1}.  A sleeping lane
-// waits for the wake-up granule (layer l-2's output) before every thread polls
-// its 17 granules.
+// otherwise LN2_{l-1}(u) with u from the hop-B gather.
 __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, const float* lp2,
                                        float& xv, Shared1& sh) {
     const int tid = threadIdx.x;
@@ -499,20 +639,8 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
         xv = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
         return true;
     }
-    const unsigned tag = ws.tag(s);
-    bool ok = true;
-    if (l >= 2) {
-        if (tid == 0) wait_tag_slow(ws.PFH(s, l - 2, 0), tag, a.err, ok, a.spin_ticks);
-        if (!block_ok1(ok, sh)) return false;
-    }
-    float g[17];
-    wait_gran_n<17>(ws.PFH(s, l - 1, 0) + tid, 512, tag, g, a.err, ok, a.spin_ticks);
-    float f = g[0];
-#pragma unroll
-    for (int j = 1; j < NF; ++j) f += g[j];
-    const float v = g[16] + (lp2[tid] + f);
-    sh.lnb[0][tid] = v;
-    if (!block_ok1(ok, sh)) return false;
+    if (!gather_pfh(a, ws, s, l, lp2, sh, false)) return false;
+    const float v = sh.lnb[0][tid];
     float mean, rden;
     ln_row_stats(sh.lnb[0], mean, rden);
     xv = (v - mean) * rden * lp2[512 + tid] + lp2[1024 + tid];
@@ -528,31 +656,29 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
 __device__ __forceinline__ bool form_u(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, const float* lp2,
                                        Shared1& sh) {
     const int tid = threadIdx.x;
+    if (l > 0) return gather_pfh(a, ws, s, l, lp2, sh, true);
     bool ok = true;
-    float u, un;
-    if (l == 0) {
-        u = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
-        un = u;
-    } else {
-        const unsigned tag = ws.tag(s);
-        if (l >= 2) {
-            if (tid == 0) wait_tag_slow(ws.PFH(s, l - 2, 0), tag, a.err, ok, a.spin_ticks);
-            if (!block_ok1(ok, sh)) return false;
-        }
-        float g[17];
-        wait_gran_n<17>(ws.PFH(s, l - 1, 0) + tid, 512, tag, g, a.err, ok, a.spin_ticks);
-        float f = g[0];
-#pragma unroll
-        for (int j = 1; j < NF; ++j) f += g[j];
-        u = g[16] + (lp2[tid] + f);
-        un = u * lp2[512 + tid];
-    }
+    const float u = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
     sh.lnb[0][tid] = u;
-    if (!split_h(un, sh.xh[tid], sh.xl[tid]) || !(fabsf(un) < a.f16_limit)) {
+    if (!split_h(u, sh.xh[tid], sh.xl[tid]) || !(fabsf(u) < a.f16_limit)) {
         atomicCAS(a.err, 0, ERR_F16_RANGE);
         ok = false;
     }
     return block_ok1(ok, sh);
+}
+
+// A wave's 64 published columns [64 w, 64 w + 64) (two 32-column blocks), staged by
+// lanes < 16 in sh.pk[w][16 t + lane], leave as the blocks' 22 granules of the row at
+// byte offset `row`.  In-wave LDS order needs no fence (LDS ops of a wave complete in
+// order; the asm statement keeps the compiler from moving the reads up).
+__device__ __forceinline__ void pub64(const Ws1& ws, Shared1& sh, int row, unsigned tag, int w, int lane) {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane < 22) {
+        const int b = lane >= 11 ? 1 : 0, r = lane - 11 * b;
+        const float* p = sh.pk[w] + 32 * b + 3 * r;
+        st_g16(ws, row + 16 * (11 * (2 * w + b) + r), tag, p[0], p[1], r == 10 ? 0.f : p[2]);
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -684,8 +810,9 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bfrag(wo[t]), f32x4{0.f, 0.f, 0.f, 0.f});
                 if (lane < 16) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) st_gran(ws.PA(s, l, h) + 64 * w + 16 * t + lane, tag, acc[t][0] + acc[t][1]);
+                    for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
                 }
+                pub64(ws, sh, ws.PA(s, l, h), tag, w, lane);
                 // the new K/V row (read by this workgroup only, next step)
                 if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
                 else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
@@ -702,7 +829,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         if (sampler) {
             const bool probe = a.trace && s == 8;   // step-end trace (tools/knob_sweep.py)
             bool ok = true;
-            if (tid == 0) wait_tag_slow(ws.PFH(s, 23, 0), tag, a.err, ok, a.spin_ticks);
+            if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s, 23, 0)), tag, a.err, ok, a.spin_ticks);
             if (!block_ok1(ok, sh)) return;
             STAMP1(0);
             const u64* lgg = ws.LG(s);
@@ -857,28 +984,54 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             float xv;
             if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
             STAMP1(1);
-            float h1_pub = 0.f;
             // ---- v = x_l + (bo + sum_h PA[l][h]) (heads summed in order) -> lnb[1], and the
             // MFMA operand split of v * n1w: FFN1 runs on it while the LN1 statistics are
             // formed (W1 h1 + b1 = rden (W1 (v n1w) - mean W1 n1w) + (W1 n1b + b1), the
             // constant vectors folded at load time, as form_u)
-            float v;
+            // (hop A: thread q < GQ sums heads 0..7 of granule column q, thread 256 + q
+            // continues with heads 8..15 and forms the column group's v / operand split)
             {
                 bool ok = true;
-                float pa[16];
-                wait_gran_n<16>(ws.PA(s, l, 0) + tid, 512, tag, pa, a.err, ok, a.spin_ticks);
-                float sum = pa[0];
+                constexpr int RB = (int)Ws1::ROW * 8;
+                const int q = tid & 255, off = ws.PA(s, l, 0) + 16 * q;
+                sh.ff.xr[tid] = xv;
+                sh.ff.bo[tid] = bo;
+                sh.ff.n1w[tid] = n1w;
+                u32x4 g[8];
+                if (tid < GQ) {
+                    wait_g16_n<8>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
+                    float f0 = __uint_as_float(g[0].y), f1 = __uint_as_float(g[0].z), f2 = __uint_as_float(g[0].w);
 #pragma unroll
-                for (int hh = 1; hh < 16; ++hh) sum += pa[hh];
-                v = xv + (bo + sum);
-                sh.lnb[1][tid] = v;
-                const float un = v * n1w;
-                if (!split_h(un, sh.xh[tid], sh.xl[tid]) || !(fabsf(un) < a.f16_limit)) {
-                    atomicCAS(a.err, 0, ERR_F16_RANGE);
-                    ok = false;
+                    for (int r = 1; r < 8; ++r) {
+                        f0 += __uint_as_float(g[r].y);
+                        f1 += __uint_as_float(g[r].z);
+                        f2 += __uint_as_float(g[r].w);
+                    }
+                    sh.hs[3 * q] = f0; sh.hs[3 * q + 1] = f1; sh.hs[3 * q + 2] = f2;
+                } else if (tid >= 256 && q < GQ) {
+                    wait_g16_n<8>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+                }
+                if (!block_ok1(ok, sh)) return;
+                if (tid >= 256 && q < GQ) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        if (k == 2 && gq_n(q) == 2) break;
+                        float sum = sh.hs[3 * q + k];
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) sum += __uint_as_float(g[r][1 + k]);
+                        const int c = gq_col(q, k);
+                        const float vc = sh.ff.xr[c] + (sh.ff.bo[c] + sum);
+                        sh.lnb[1][c] = vc;
+                        const float un = vc * sh.ff.n1w[c];
+                        if (!split_h(un, sh.xh[c], sh.xl[c]) || !(fabsf(un) < a.f16_limit)) {
+                            atomicCAS(a.err, 0, ERR_F16_RANGE);
+                            ok = false;
+                        }
+                    }
                 }
                 if (!block_ok1(ok, sh)) return;
             }
+            const float v = sh.lnb[1][tid];
             STAMP1(2);
             // ---- FFN1 rows of this slice on the MFMA (16 per wave), ReLU -> fh/fl.  The LN1
             // statistics come first in program order so the scheduler interleaves their
@@ -900,7 +1053,8 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                         c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
                     }
                 }
-                h1_pub = (v - mean) * rden * n1w + n1b;   // h1_l, published with the FFN2 partials
+                const float h1_pub = (v - mean) * rden * n1w + n1b;   // h1_l, published after the FFN2 partials
+                if ((tid >> 5) == j) sh.h1s[tid & 31] = h1_pub;
                 if (lane < 16) {
                     const float f = fmaxf(rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * ffB) + ffC, 0.f);
                     split_h(f, sh.fh[w * 16 + lane], sh.fl[w * 16 + lane]);
@@ -929,13 +1083,23 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                     for (int t = 0; t < 4; ++t) acc[t] = mfma16(af[c], bfrag(w2r[4 * t + c]), acc[t]);
                 if (lane < 16) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        st_gran(ws.PFH(s, l, j) + 64 * w + 16 * t + lane, tag, acc[t][0] + acc[t][1]);
+                    for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
+                }
+                pub64(ws, sh, ws.PFH(s, l, j), tag, w, lane);
+            }
+            // h1 block j of this workgroup (the next layer's residual input: 11 granules),
+            // after the partials: a store in flight stalls every later vmcnt(0)
+            // (staged before the FFN1 barrier; the lane index is re-formed here so no
+            // hoisted address waits in a spill slot: a reload's vmcnt(0) would wait for the
+            // partials' write-through stores)
+            if (w == 0) {
+                int ln = lane;
+                asm volatile("" : "+v"(ln));
+                if (ln < 11) {
+                    const float* p = sh.h1s + 3 * ln;
+                    st_g16(ws, ws.PFH(s, l, 16) + 16 * (11 * j + ln), tag, p[0], p[1], ln == 10 ? 0.f : p[2]);
                 }
             }
-            // h1 slice of this workgroup (the next layer's residual input), after the
-            // partials: a store in flight stalls every later vmcnt(0) (spill reloads)
-            if ((tid >> 5) == j) st_gran(ws.PFH(s, l, 16) + tid, tag, h1_pub);
             STAMP1(4);
             __syncthreads();   // fs / b1 consumed before the next prefetch lands
             pf_wait(a.pf_delay);
@@ -1007,7 +1171,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
 
 __global__ __launch_bounds__(PT) void k_decode_persist1(PersistArgs a) {
     __shared__ Shared1 sh;
-    const Ws1 ws{a.ring, a.epoch};
+    const Ws1 ws{a.ring, a.epoch, __builtin_amdgcn_make_buffer_rsrc(a.ring, 0, 0x7fffffff, 0x00020000)};
     const int grp = blockIdx.x / GW, r = blockIdx.x - grp * GW;
     if (r < 16) run_attn(a, ws, sh, grp, r);
     else run_ffn(a, ws, sh, grp, r - 16);

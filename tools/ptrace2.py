@@ -24,3 +24,8 @@ for nm, b in (("attn12", 128), ("ffn12", 144), ("attn13", 160), ("ffn13", 176)):
     t = (tr[b:b + 16, :8] - t0) * 10 / 1000.0
     print(f"{nm:6s} " + "  ".join(f"s{i} {t[:, i].min():6.2f}/{np.median(t[:, i]):6.2f}/{t[:, i].max():6.2f}"
                                 for i in range(8) if -1e5 < t[:, i].max() < 1e5))
+if "--wg" in sys.argv:   # per-workgroup stamps of the FFN groups (late-publisher hunt)
+    for nm, b in (("ffn12", 144), ("ffn13", 176)):
+        t = (tr[b:b + 16, :8] - t0) * 10 / 1000.0
+        for j in range(16):
+            print(f"{nm} wg{j:2d} " + " ".join(f"s{i} {t[j, i]:7.2f}" for i in (0, 1, 2, 6, 3, 4)))

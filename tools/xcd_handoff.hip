@@ -3,8 +3,9 @@
 // workgroups sweep them (thread t polls granule t of every producer, 16 loads), then
 // publish their own 512 granules, which the producers sweep: one iteration = 2 hops.
 //   config 0: the 32 workgroups on ONE XCD (blocks b % 8 == 0), sc1 stores + sc1 loads
-//   config 1: the same workgroups, PLAIN stores + sc1 loads (lines kept in the XCD L2)
+//   config 1: the same workgroups, volatile stores (which compile to sc0 sc1) + sc1 loads
 //   config 2: 32 workgroups spread over the 8 XCDs (blocks 0..31), sc1 stores (today's decode)
+//   config 3: the config-0 workgroups, stores with no cache bits + sc0 loads (the XCD's own L2)
 // Build: hipcc -O3 --offload-arch=gfx950 tools/xcd_handoff.hip -o tools/xcd_handoff
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -15,18 +16,27 @@ constexpr int NP = 16, PT = 512;
 
 __device__ __forceinline__ u64 ld_sc1(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_plain(u64* p, u64 v) { *(volatile u64*)p = v; }
+__device__ __forceinline__ void st_plain(u64* p, u64 v) { *(volatile u64*)p = v; }   // (emits sc0 sc1)
+__device__ __forceinline__ void st_l2(u64* p, u64 v) {   // buffer_store_dwordx2, no cache bits: stays in the XCD L2
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 8, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r, 0, 0, 0);
+}
 
 __device__ __forceinline__ int xcc_id() {
     return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf;   // HW_REG_XCC_ID bits [3:0]
 }
 
-__device__ bool sweep(const u64* base, unsigned tag, int G) {   // thread t < G: granule t of 16 rows
+__device__ __forceinline__ u64 ld_mode(const u64* p, bool l2) {
+    if (!l2) return ld_sc1(p);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 8, 0x00020000);
+    return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 1 /* sc0: bypass the CU's L1 */));
+}
+__device__ bool sweep(const u64* base, unsigned tag, int G, bool l2 = false) {   // thread t < G: granule t of 16 rows
     u64 g[NP];
     const int t = threadIdx.x;
     if (t >= G) return true;
 #pragma unroll
-    for (int k = 0; k < NP; ++k) g[k] = ld_sc1(base + k * PT + t);
+    for (int k = 0; k < NP; ++k) g[k] = ld_mode(base + k * PT + t, l2);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         bool all = true;
@@ -36,7 +46,7 @@ __device__ bool sweep(const u64* base, unsigned tag, int G) {   // thread t < G:
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            if ((unsigned)(g[k] >> 32) != tag) g[k] = ld_sc1(base + k * PT + t);
+            if ((unsigned)(g[k] >> 32) != tag) g[k] = ld_mode(base + k * PT + t, l2);
         if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;
     }
 }
@@ -46,7 +56,7 @@ __global__ __launch_bounds__(PT) void k_hop(u64* A, u64* B, int iters, int confi
     const int b = blockIdx.x, t = threadIdx.x;
     if (t == 0) xcc[b] = xcc_id();
     int member;
-    if (config < 2) {
+    if (config != 2) {
         if (b % 8 != 0) return;
         member = b / 8;            // 0..31
     } else {
@@ -55,18 +65,18 @@ __global__ __launch_bounds__(PT) void k_hop(u64* A, u64* B, int iters, int confi
     }
     const bool prod = member < NP;
     const int idx = member % NP;
-    const bool plain = config == 1;
+    const bool plain = config == 1, l2 = config == 3;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int i = 1; i <= iters; ++i) {
         const u64 v = ((u64)(unsigned)i << 32) | (unsigned)(t + idx);
         if (prod) {
-            if (t < G) { if (plain) st_plain(A + idx * PT + t, v); else st_sc1(A + idx * PT + t, v); }
-            if (!sweep(B, i, G)) { *fail = 1; return; }
+            if (t < G) { if (l2) st_l2(A + idx * PT + t, v); else if (plain) st_plain(A + idx * PT + t, v); else st_sc1(A + idx * PT + t, v); }
+            if (!sweep(B, i, G, l2)) { *fail = 1; return; }
             __syncthreads();
         } else {
-            if (!sweep(A, i, G)) { *fail = 1; return; }
+            if (!sweep(A, i, G, l2)) { *fail = 1; return; }
             __syncthreads();
-            if (t < G) { if (plain) st_plain(B + idx * PT + t, v); else st_sc1(B + idx * PT + t, v); }
+            if (t < G) { if (l2) st_l2(B + idx * PT + t, v); else if (plain) st_plain(B + idx * PT + t, v); else st_sc1(B + idx * PT + t, v); }
         }
     }
     if (member == 0 && t == 0) out[config] = __builtin_amdgcn_s_memrealtime() - t0;
@@ -131,17 +141,18 @@ int main() {
     hipMalloc(&xcc, 256 * 4);
     hipMalloc(&fail, 4);
     const int iters = 2000;
-    const char* names[3] = {"one XCD, sc1 stores  ", "one XCD, plain stores", "8 XCDs,  sc1 stores  "};
-    for (int G : {512, 256})
-        for (int c = 0; c < 3; ++c) {
+    const char* names[4] = {"one XCD, sc1 stores  ", "one XCD, volatile st ", "8 XCDs,  sc1 stores  ",
+                            "one XCD, plain st + sc0 ld"};
+    for (int G : {512, 256, 32, 1})
+        for (int c = 0; c < 4; ++c) {
             hipMemset(A, 0, NP * PT * 8 * 2);
             hipMemset(B, 0, NP * PT * 8 * 2);
             hipMemset(fail, 0, 4);
             hipLaunchKernelGGL(k_hop, dim3(256), dim3(PT), 0, 0, A, B, iters, c, out, xcc, fail, G);
             if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
-            unsigned long long h[4];
+            unsigned long long h[8];
             int f, x[256];
-            hipMemcpy(h, out, 32, hipMemcpyDeviceToHost);
+            hipMemcpy(h, out, 64, hipMemcpyDeviceToHost);
             hipMemcpy(&f, fail, 4, hipMemcpyDeviceToHost);
             hipMemcpy(x, xcc, 1024, hipMemcpyDeviceToHost);
             int same = 1;
