@@ -5,7 +5,11 @@
 //   config 0: the 32 workgroups on ONE XCD (blocks b % 8 == 0), sc1 stores + sc1 loads
 //   config 1: the same workgroups, volatile stores (which compile to sc0 sc1) + sc1 loads
 //   config 2: 32 workgroups spread over the 8 XCDs (blocks 0..31), sc1 stores (today's decode)
-//   config 3: the config-0 workgroups, stores with no cache bits + sc0 loads (the XCD's own L2)
+//   config 3: the config-0 workgroups, stores with no cache bits + sc0 loads (TIMES OUT: an sc0
+//             load is workgroup scope and keeps hitting the CU's stale L1 line)
+//   config 4: no-bit stores + "buffer_inv sc0" (drop the CU's L1) before every poll round + loads
+//             with no cache bits: served by the XCD's own L2
+//   config 5: no-bit stores + sc1 loads (does an agent-scope load see the XCD L2's dirty line?)
 // Build: hipcc -O3 --offload-arch=gfx950 tools/xcd_handoff.hip -o tools/xcd_handoff
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -26,12 +30,14 @@ __device__ __forceinline__ int xcc_id() {
     return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf;   // HW_REG_XCC_ID bits [3:0]
 }
 
-__device__ __forceinline__ u64 ld_mode(const u64* p, bool l2) {
-    if (!l2) return ld_sc1(p);
+// load mode: 0 sc1 (agent scope), 1 sc0, 2 no cache bits (after a buffer_inv sc0 of the poll round)
+__device__ __forceinline__ u64 ld_mode(const u64* p, int l2) {
+    if (l2 == 0) return ld_sc1(p);
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 8, 0x00020000);
-    return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 1 /* sc0: bypass the CU's L1 */));
+    if (l2 == 1) return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 1));
+    return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
 }
-__device__ bool sweep(const u64* base, unsigned tag, int G, bool l2 = false) {   // thread t < G: granule t of 16 rows
+__device__ bool sweep(const u64* base, unsigned tag, int G, int l2 = 0) {   // thread t < G: granule t of 16 rows
     u64 g[NP];
     const int t = threadIdx.x;
     if (t >= G) return true;
@@ -44,6 +50,7 @@ __device__ bool sweep(const u64* base, unsigned tag, int G, bool l2 = false) {  
         for (int k = 0; k < NP; ++k) all &= (unsigned)(g[k] >> 32) == tag;
         if (all) return true;
         __builtin_amdgcn_s_sleep(1);
+        if (l2 == 2) asm volatile("buffer_inv sc0" ::: "memory");
 #pragma unroll
         for (int k = 0; k < NP; ++k)
             if ((unsigned)(g[k] >> 32) != tag) g[k] = ld_mode(base + k * PT + t, l2);
@@ -65,18 +72,19 @@ __global__ __launch_bounds__(PT) void k_hop(u64* A, u64* B, int iters, int confi
     }
     const bool prod = member < NP;
     const int idx = member % NP;
-    const bool plain = config == 1, l2 = config == 3;
+    const bool plain = config == 1, nobit = config >= 3;
+    const int l2 = config == 3 ? 1 : config == 4 ? 2 : 0;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int i = 1; i <= iters; ++i) {
         const u64 v = ((u64)(unsigned)i << 32) | (unsigned)(t + idx);
         if (prod) {
-            if (t < G) { if (l2) st_l2(A + idx * PT + t, v); else if (plain) st_plain(A + idx * PT + t, v); else st_sc1(A + idx * PT + t, v); }
+            if (t < G) { if (nobit) st_l2(A + idx * PT + t, v); else if (plain) st_plain(A + idx * PT + t, v); else st_sc1(A + idx * PT + t, v); }
             if (!sweep(B, i, G, l2)) { *fail = 1; return; }
             __syncthreads();
         } else {
             if (!sweep(A, i, G, l2)) { *fail = 1; return; }
             __syncthreads();
-            if (t < G) { if (l2) st_l2(B + idx * PT + t, v); else if (plain) st_plain(B + idx * PT + t, v); else st_sc1(B + idx * PT + t, v); }
+            if (t < G) { if (nobit) st_l2(B + idx * PT + t, v); else if (plain) st_plain(B + idx * PT + t, v); else st_sc1(B + idx * PT + t, v); }
         }
     }
     if (member == 0 && t == 0) out[config] = __builtin_amdgcn_s_memrealtime() - t0;
@@ -141,10 +149,12 @@ int main() {
     hipMalloc(&xcc, 256 * 4);
     hipMalloc(&fail, 4);
     const int iters = 2000;
-    const char* names[4] = {"one XCD, sc1 stores  ", "one XCD, volatile st ", "8 XCDs,  sc1 stores  ",
-                            "one XCD, plain st + sc0 ld"};
+    const char* names[6] = {"one XCD, sc1 stores  ", "one XCD, volatile st ", "8 XCDs,  sc1 stores  ",
+                            "one XCD, no-bit st + sc0 ld", "one XCD, no-bit st + L1 inv + no-bit ld",
+                            "one XCD, no-bit st + sc1 ld"};
     for (int G : {512, 256, 32, 1})
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < 6; ++c) {
+            if (c == 3) continue;   // times out (see the header)
             hipMemset(A, 0, NP * PT * 8 * 2);
             hipMemset(B, 0, NP * PT * 8 * 2);
             hipMemset(fail, 0, 4);
