@@ -113,7 +113,12 @@ int gsv_engine::finalize_roberta() {
 int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int n_out, float* out, hipStream_t st,
                                 const int* row_pos, const int* row_seg) {
     const BertWeights& B = bert;
-    const size_t need = (size_t)N * (1024 * 4 + 3072 + 4096) + (size_t)n_out + 3 * (size_t)N + 64;
+    // out-projection / FFN2 of a few rows fill only N / 64 workgroups: K is split into
+    // slabs (4 / 8, reduced in slab order by the LayerNorm that follows).  The split does
+    // not depend on N, so a packed batch and one call per sentence give identical rows.
+    constexpr int zo = 4, z2 = 8, zmax = z2;
+    const size_t need = (size_t)N * (1024 * 4 + 3072 + 4096) + (size_t)n_out + 3 * (size_t)N + 64 +
+                        (size_t)zmax * N * 1024;
     if (need > bert.ws_floats) {
         if (bert.ws) hipFree(bert.ws);
         bert.ws = nullptr;
@@ -127,6 +132,7 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
     int* drows = reinterpret_cast<int*>(f + (size_t)N * 4096);
     int* dpos = drows + n_out;
     int* dseg = dpos + N;
+    float* slabs = reinterpret_cast<float*>(dseg + 2 * N + 16);   // zmax x [N][1024]
     hipMemcpyAsync(drows, rows, (size_t)n_out * 4, hipMemcpyHostToDevice, st);
     if (row_pos) hipMemcpyAsync(dpos, row_pos, (size_t)N * 4, hipMemcpyHostToDevice, st);
     if (row_seg) hipMemcpyAsync(dseg, row_seg, (size_t)N * 8, hipMemcpyHostToDevice, st);
@@ -144,11 +150,22 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
         m.postdiv = 0; m.scale = 8.f;   // scores / sqrt(64) (exact: a power of two)
         m.row_seg = row_seg ? dseg : nullptr;   // packed: each sentence attends within itself
         mha(m, st);
-        gemm_nt(gemm_f16(N, 1024, 1024, att, 1024, L.wo, L.bo, tmp, 1024, EPI_RESID, h, 1024), st);
-        layernorm_rows_d(tmp, h, N, 1024, L.ln1w, L.ln1b, EPS, st);
+        auto resid_ln = [&](const float* A, int K, const void* W, const float* bias, int z, const float* lw,
+                            const float* lb) {
+            if (z > 1) {
+                GemmArgs g = gemm_f16(N, 1024, K, A, K, W, nullptr, slabs, 1024, EPI_SLAB);
+                g.ksplit = z;
+                g.slab_stride = (long)N * 1024;
+                gemm_nt(g, st);
+                layernorm_rows_d_slabs(slabs, z, (long)N * 1024, bias, h, h, N, 1024, lw, lb, EPS, st);
+            } else {
+                gemm_nt(gemm_f16(N, 1024, K, A, K, W, bias, tmp, 1024, EPI_RESID, h, 1024), st);
+                layernorm_rows_d(tmp, h, N, 1024, lw, lb, EPS, st);
+            }
+        };
+        resid_ln(att, 1024, L.wo, L.bo, zo, L.ln1w, L.ln1b);
         gemm_nt(gemm_f16(N, 4096, 1024, h, 1024, L.w1, L.b1, f, 4096, EPI_GELU), st);
-        gemm_nt(gemm_f16(N, 1024, 4096, f, 4096, L.w2, L.b2, tmp, 1024, EPI_RESID, h, 1024), st);
-        layernorm_rows_d(tmp, h, N, 1024, L.ln2w, L.ln2b, EPS, st);
+        resid_ln(f, 4096, L.w2, L.b2, z2, L.ln2w, L.ln2b);
     }
     hipLaunchKernelGGL(k_bert_repeat, dim3(n_out), dim3(256), 0, st, h, drows, out);
     // the row tables are read by the kernels above; keep the pageable sources alive until they ran

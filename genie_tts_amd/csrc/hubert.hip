@@ -112,8 +112,11 @@ constexpr int HB_SS[7] = {5, 2, 2, 2, 2, 2, 2};
 
 // LayerNorm over rows of D (<= 1024) values, two-pass (mean, then mean of squared
 // deviations), one block per row (CN-HuBERT eps 1e-5, RoBERTa eps 1e-12).
+// With slabs: the input row is res + (bias + sum_z slab_z) (split-K GEMM partials
+// summed in slab order: EPI_RESID's res + (bias + acc) with acc formed in slices).
 __global__ __launch_bounds__(256) void k_ln_rows_d(const float* in, float* out, int D, const float* g, const float* b,
-                                                    float eps) {
+                                                    float eps, int nslab, long sstride, const float* bias,
+                                                    const float* res) {
     __shared__ float red[16];
     const long r = blockIdx.x;
     const float* x = in + r * D;
@@ -122,7 +125,15 @@ __global__ __launch_bounds__(256) void k_ln_rows_d(const float* in, float* out, 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int d = threadIdx.x + 256 * i;
-        v[i] = d < D ? x[d] : 0.f;
+        if (nslab == 0) {
+            v[i] = d < D ? x[d] : 0.f;
+        } else if (d < D) {
+            float acc = x[d];
+            for (int z = 1; z < nslab; ++z) acc += x[z * sstride + d];
+            v[i] = res[r * D + d] + (bias[d] + acc);
+        } else {
+            v[i] = 0.f;
+        }
         s += v[i];
     }
     const float mean = block_sum(s, red) / (float)D;
@@ -155,7 +166,13 @@ GemmArgs gemm_f16(int M, int N, int K, const float* A, long lda, const void* W, 
 
 void layernorm_rows_d(const float* in, float* out, int rows, int D, const float* g, const float* b, float eps,
                       hipStream_t s) {
-    hipLaunchKernelGGL(k_ln_rows_d, dim3(rows), dim3(256), 0, s, in, out, D, g, b, eps);
+    hipLaunchKernelGGL(k_ln_rows_d, dim3(rows), dim3(256), 0, s, in, out, D, g, b, eps, 0, 0L, nullptr, nullptr);
+}
+
+void layernorm_rows_d_slabs(const float* slabs, int nslab, long slab_stride, const float* bias, const float* res,
+                            float* out, int rows, int D, const float* g, const float* b, float eps, hipStream_t s) {
+    hipLaunchKernelGGL(k_ln_rows_d, dim3(rows), dim3(256), 0, s, slabs, out, D, g, b, eps, nslab, slab_stride, bias,
+                       res);
 }
 
 int hubert_frames(int n) {

@@ -62,6 +62,9 @@ void layernorm_rows_slabs(const float* slabs, int nsplit, long slab_stride, cons
 // LayerNorm over rows of D <= 1024 values with the given eps (CN-HuBERT, RoBERTa)
 void layernorm_rows_d(const float* in, float* out, int rows, int D, const float* g, const float* b, float eps,
                       hipStream_t s);
+// ... of res + (bias + sum_z slab[z]) (fixed order): the reduce of a split-K EPI_SLAB GEMM
+void layernorm_rows_d_slabs(const float* slabs, int nslab, long slab_stride, const float* bias, const float* res,
+                            float* out, int rows, int D, const float* g, const float* b, float eps, hipStream_t s);
 void sumsq_rows(const float* in, long ld, int rows, int cols, float* out, hipStream_t s);
 void argmin_dist_rows(const float* dist, int rows, int cols, int64_t* out, hipStream_t s);
 

@@ -242,6 +242,155 @@ __global__ __launch_bounds__(256) void k_gemm_x2(GemmArgs a) {
     gemm_epilogue(a, m0 + wm * 32, n0 + wn * 32 + r, lane, acc);
 }
 
+// =====================================================================
+// The same GEMM (identical MFMA sequence and split-K partition, so identical
+// results) with the operand tiles brought in by LDS-DMA (global_load_lds_dwordx4:
+// no VGPR staging) through a GX3_NS-deep ring of 64-k stages: GX3_NS - 1 stages
+// are in flight while one is consumed, so a block pays the HBM/L2 latency once
+// instead of once per K-step (k_gemm_x2 keeps two 128-k steps in registers and
+// waits on each).  One DMA instruction writes 1 KB of LDS (lane i -> bytes
+// [16 i, 16 i + 16)), so rows cannot be padded: the 16-byte chunks of a row are
+// XOR-swizzled instead (A: chunk c of row r in slot c ^ (r & 15); W: slot
+// c ^ ((n >> 1) & 7)), which keeps the MFMA fragment reads conflict-free.
+// Rows past M / N read row M - 1 / N - 1 (their results are never stored).
+// =====================================================================
+// vmcnt(later * D): the wave's DMA instructions of the `later` newest stages may stay in flight
+template <int D>
+__device__ __forceinline__ void gx3_wait(int later) {
+    switch (later) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory"); break;
+    }
+}
+// One global -> LDS DMA of 16 B per lane (lane i -> LDS bytes [16 i, 16 i + 16) of `l`).
+// Issued from inline asm: the waitcnt pass would otherwise put a vmcnt(0) (every stage
+// in flight) before each fragment read, as it cannot tell the ring buffers apart; the
+// waits are the explicit gx3_wait ones.
+__device__ __forceinline__ void gx3_dma(const void* g, void* l) {
+    const unsigned la =
+        __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) char*)(l));
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(g) : "memory", "m0");
+}
+
+#define GX3_BK 64
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs a) {
+    constexpr int WV = (BM / 32) * (BN / 32);           // waves, one 32 x 32 output tile each
+    constexpr int NA = BM / 4 / WV, NW = BN / 8 / WV;    // DMA instructions per wave per stage (A, W)
+    static_assert(NA * WV * 4 == BM && NW * WV * 8 == BN, "tile / wave split");
+    __shared__ __attribute__((aligned(16))) float As[NS][BM * GX3_BK];
+    __shared__ __attribute__((aligned(16))) __half Ws[NS][BN * GX3_BK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / (BN / 32), wn = w % (BN / 32);
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int r = lane & 31, hh = lane >> 5;
+    // K slice of this block: k_gemm_x2's partition (whole 128-k steps), in 64-k stages
+    const int nsplit = gridDim.z, kz = blockIdx.z;
+    const int steps_all = a.K / GX_KS;
+    const int s_lo = 2 * (kz * steps_all / nsplit), s_hi = 2 * ((kz + 1) * steps_all / nsplit);
+    const int nsteps = s_hi - s_lo;
+    // this lane's DMA sources: A instruction j covers rows 4 j + (lane >> 4), slot lane & 15
+    // (chunk slot ^ (row & 15)); W instruction j covers rows 8 j + (lane >> 3), slot lane & 7
+    // (chunk slot ^ ((row >> 1) & 7))
+    const float* asrc[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        const int row = 4 * (w + WV * i) + (lane >> 4), slot = lane & 15;
+        const int gm = min(m0 + row, a.M - 1);
+        asrc[i] = a.A + (long)gm * a.lda + (long)s_lo * GX3_BK + 4 * (slot ^ (row & 15));
+    }
+    const __half* wsrc[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const int row = 8 * (w + WV * i) + (lane >> 3), slot = lane & 7;
+        const int gn = min(n0 + row, a.N - 1);
+        wsrc[i] = reinterpret_cast<const __half*>(a.W) + (long)gn * a.ldw + (long)s_lo * GX3_BK +
+                  8 * (slot ^ ((row >> 1) & 7));
+    }
+    auto issue = [&](int st) {
+        const int k0 = st * GX3_BK, buf = st % NS;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) gx3_dma(asrc[i] + k0, &As[buf][256 * (w + WV * i)]);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) gx3_dma(wsrc[i] + k0, &Ws[buf][512 * (w + WV * i)]);
+    };
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+        if (st < nsteps) issue(st);
+    const int arow = wm * 32 + r, bcol = wn * 32 + r;
+    for (int st = 0; st < nsteps; ++st) {
+        // stage st landed (this wave's share; later ones stay in flight), then the barrier:
+        // every wave's share landed, and the buffer refilled below was consumed by all.
+        // s_barrier without __syncthreads' fence, which would wait for every DMA in flight.
+        gx3_wait<NA + NW>(min(NS - 2, nsteps - 1 - st));
+        __builtin_amdgcn_s_barrier();
+        if (st + NS - 1 < nsteps) issue(st + NS - 1);
+        const float* As_ = As[st % NS];
+        const __half* Ws_ = Ws[st % NS];
+#pragma unroll
+        for (int ks = 0; ks < GX3_BK / 16; ++ks) {
+            const int c0 = 4 * ks + 2 * hh;   // A chunks c0, c0 + 1 (4 floats each)
+            const float4 x0 = *reinterpret_cast<const float4*>(As_ + arow * GX3_BK + 4 * (c0 ^ (arow & 15)));
+            const float4 x1 = *reinterpret_cast<const float4*>(As_ + arow * GX3_BK + 4 * ((c0 + 1) ^ (arow & 15)));
+            h16x8 ahi, alo;
+            split8(x0, x1, ahi, alo);
+            const int cb = 2 * ks + hh;       // W chunk (8 halfs)
+            const h16x8 bw = *reinterpret_cast<const h16x8*>(Ws_ + bcol * GX3_BK + 8 * (cb ^ ((bcol >> 1) & 7)));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bw, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bw, acc, 0, 0, 0);
+        }
+    }
+    if (a.mode == EPI_SLAB) {
+        const int col = n0 + bcol;
+        if (col >= a.N) return;
+        float* C = a.C + (long)kz * a.slab_stride;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (row < a.M) C[(long)row * a.ldc + col] = acc[i];
+        }
+        return;
+    }
+    gemm_epilogue(a, m0 + wm * 32, n0 + bcol, lane, acc);
+}
+
+// Tile configurations of k_gemm_x3 (GENIE_GEMM_CFG picks one for benchmarks; default: by shape)
+static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
+    auto go = [&](auto kern, int bm, int bn, int threads) {
+        hipLaunchKernelGGL(kern, dim3((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, z), dim3(threads), 0, s, a);
+    };
+    switch (cfg) {
+        case 1: go(k_gemm_x3<64, 64, 4>, 64, 64, 256); break;
+        case 2: go(k_gemm_x3<32, 64, 4>, 32, 64, 128); break;
+        case 3: go(k_gemm_x3<64, 32, 4>, 64, 32, 128); break;
+        case 4: go(k_gemm_x3<32, 64, 6>, 32, 64, 128); break;
+        case 5: go(k_gemm_x3<64, 64, 6>, 64, 64, 256); break;
+        case 6: go(k_gemm_x3<32, 32, 6>, 32, 32, 64); break;
+        default: go(k_gemm_x3<64, 64, 4>, 64, 64, 256); break;
+    }
+}
+static int gemm_cfg() {
+    static const int c = [] {
+        const char* e = std::getenv("GENIE_GEMM_CFG");
+        return e ? std::atoi(e) : 0;
+    }();
+    return c;
+}
+
+static int gemm_variant() {   // GENIE_GEMM_X3=0: the register-staged k_gemm_x2
+    static const int v = [] {
+        const char* e = std::getenv("GENIE_GEMM_X3");
+        return (e && std::atoi(e) == 0) ? 2 : 3;
+    }();
+    return v;
+}
+
 static bool gemm_x2_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("GENIE_GEMM_X2");
@@ -261,7 +410,12 @@ void gemm_nt(const GemmArgs& a, hipStream_t s) {
     if (a.w_f16 && a.mode != EPI_VQDIST && a.K % GX_KS == 0 && a.lda % 4 == 0 && a.ldw % 8 == 0 &&
         gemm_x2_enabled()) {
         if (a.mode == EPI_SLAB) grid.z = a.ksplit;
-        hipLaunchKernelGGL(k_gemm_x2, grid, dim3(256), 0, s, a);
+        // the LDS-DMA pipeline reads A as stored: a slab-summing A prologue stays on k_gemm_x2
+        // (M > 512: the register-staged kernel's 128-k steps win once the grid covers the chip)
+        if (a.a_nslab == 0 && a.lda % 4 == 0 && gemm_variant() == 3 && (a.M <= 512 || gemm_cfg() != 0))
+            launch_x3(a, grid.z, s, gemm_cfg());
+        else
+            hipLaunchKernelGGL(k_gemm_x2, grid, dim3(256), 0, s, a);
         return;
     }
     if (a.w_f16)
@@ -770,19 +924,32 @@ __global__ __launch_bounds__(256) void k_attn_flash(AttnArgs a) {
     for (int r = 0; r < 4; ++r) { m[r] = -INFINITY; l[r] = 0.f; }
     const int pr = lane >> 4, pd = 2 * (lane & 15);   // P.V: this lane's row (of the wave's 4) and dims
     f32x2v o = {0.f, 0.f};
-    for (int k0 = 0; k0 < kmax; k0 += AF_KC) {
+    // K/V chunks through registers, one chunk ahead: chunk k + 1 is in flight while
+    // chunk k is scored (rows past the cache: zeros)
+    float4 pk[2], pv[2];
+    auto fetch = [&](int k0) {
         const int nk = min(AF_KC, kmax - k0);
-        for (int e = tid; e < AF_KC * 8; e += 256) {   // K/V chunk -> LDS (rows past the cache: zeros)
-            const int t = e >> 3, c = e & 7;
-            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = tid + 256 * i, t = e >> 3, c = e & 7;
+            pk[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            pv[i] = pk[i];
             if (t < nk) {
-                kv = *reinterpret_cast<const float4*>(K + (long)(k0 + t) * 32 + 4 * c);
-                vv = *reinterpret_cast<const float4*>(V + (long)(k0 + t) * 32 + 4 * c);
+                pk[i] = *reinterpret_cast<const float4*>(K + (long)(k0 + t) * 32 + 4 * c);
+                pv[i] = *reinterpret_cast<const float4*>(V + (long)(k0 + t) * 32 + 4 * c);
             }
-            *reinterpret_cast<float4*>(Ks + t * AF_KS + 4 * c) = kv;
-            *reinterpret_cast<float4*>(Vs + t * AF_KS + 4 * c) = vv;
+        }
+    };
+    if (kmax > 0) fetch(0);
+    for (int k0 = 0; k0 < kmax; k0 += AF_KC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = tid + 256 * i, t = e >> 3, c = e & 7;
+            *reinterpret_cast<float4*>(Ks + t * AF_KS + 4 * c) = pk[i];
+            *reinterpret_cast<float4*>(Vs + t * AF_KS + 4 * c) = pv[i];
         }
         __syncthreads();
+        if (k0 + AF_KC < kmax) fetch(k0 + AF_KC);
         // ---- scores: lane = key k0 + lane
         f32x2v kr[16];
 #pragma unroll
