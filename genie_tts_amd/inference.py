@@ -233,8 +233,8 @@ class GENIE:
         if not 5 <= len(utts) <= 9:
             return model.ENGINE.t2s_generate(utts, sampler)
         # 5-9 sequences fit only one layer group of the batched persistent decode; chunks of
-        # 4 run on two groups and finish sooner (profiles/r02h_batch_sweep.json: 8 = 4 + 4 in
-        # 72 ms vs 96 ms; sampled draws are keyed by the slot within each generate)
+        # 4 run on two groups and finish sooner (profiles/r03f_batch_sweep.json: 8 = 4 + 4 in
+        # 71 ms vs 96 ms; sampled draws are keyed by the slot within each generate)
         toks = []
         for i in range(0, len(utts), 4):
             toks += model.ENGINE.t2s_generate(utts[i:i + 4], sampler)
