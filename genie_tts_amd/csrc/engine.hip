@@ -1502,6 +1502,11 @@ int gsv_engine::gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t c
 
 int gsv_engine::gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len, hipStream_t caller) {
     if (gq_n == 0) return set_error(GSV_E_STATE, "no generate in flight");
+    // A vocoder call still queued here had no later generate to launch it behind (the
+    // last sentences of a stream): launch it on the vocoder CUs now, beside the decode
+    // this call waits for, instead of after it on the T2S CUs.
+    if (vqueued && vstream)
+        if (int r = vits_launch_queued(vstream)) return r;
     GenSlot& g = gq[gq_head];
     gq_head = (gq_head + 1) % 2;
     --gq_n;
