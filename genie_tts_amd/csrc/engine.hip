@@ -157,6 +157,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_ACC")) use_acc = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST")) use_persist = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST1")) use_persist1 = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_PERSIST1M")) use_persist1m = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
@@ -824,7 +825,8 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (allow_persist && use_persist && B <= 8 && persist_groups(B, decode_cus()) > 0) return decode_persistent(B, sp, st);
+    if (allow_persist && use_persist && (persist_family(B) || (B <= 8 && persist_groups(B, decode_cus()) > 0)))
+        return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -886,8 +888,18 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     return 0;
 }
 
+// B = 1: the single-sequence kernel; B = 2..56: its multi-sequence form (the live
+// sequences one after another through each layer's workgroups).  Above 56 the per-step
+// graphs are faster (tools/batch_sweep.py --compare, profiles/r03h_batch_sweep.json:
+// 56 sequences 128 vs 135 ms, 64 sequences 151 vs 143 ms per 81-step generate).
+constexpr int PERSIST1M_MAX_B = 56;
+bool gsv_engine::persist_family(int B) const {
+    return use_persist1 && decode_cus() >= persist1_grid(3) &&
+           (B == 1 || (use_persist1m && B <= std::min(PERSIST1M_MAX_B, persist1m_max_batch())));
+}
+
 int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) {
-    return decode_persistent_as(B, sp, st, B == 1 && use_persist1 && decode_cus() >= persist1_grid(3));
+    return decode_persistent_as(B, sp, st, persist_family(B));
 }
 
 // Enqueue one persistent decode launch on st (no host wait): the error word is
@@ -902,8 +914,9 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bo
     // without zeroing (re-zeroed when the epoch wraps or the layout changes).
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     if (tmax > persist_max_tokens()) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
-    const size_t need = one ? persist1_ring_bytes() : persist_ring_bytes(B);
-    const int layout = one ? -1 : B;   // ring layout key: the two kernels slot the ring differently
+    // one: the persist1 family (B = 1 single-sequence kernel, B > 1 its multi-sequence form)
+    const size_t need = one ? (B == 1 ? persist1_ring_bytes() : persist1m_ring_bytes(B)) : persist_ring_bytes(B);
+    const int layout = one ? (B == 1 ? -1 : -100 - B) : B;   // ring layout key: the kernels slot the ring differently
     if (need > pws_bytes || layout != pws_batch) {
         if (need > pws_bytes) {
             if (pws) hipFree(pws);
@@ -953,7 +966,8 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bo
     perr_zeroed = false;
     // a queued prefetch starts once this stream's prefill (same workspaces) is done
     if (pf_queued && !pf_pending) hipEventRecord(pf_fork, st);
-    const hipError_t le = one ? decode_persist1(a, st, k0, k1) : decode_persist(a, st, k0, k1);
+    const hipError_t le = one ? (B == 1 ? decode_persist1(a, st, k0, k1) : decode_persist1m(a, st, k0, k1))
+                              : decode_persist(a, st, k0, k1);
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_dst, perr, 4, hipMemcpyDeviceToHost, st);
@@ -991,7 +1005,8 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     // steps run again on the general kernel (f32 VALU arithmetic).
     if (*perr_host == 2 && one) {
         ++persist1_f16_reruns;
-        return decode_persistent_as(B, sp, st, false);
+        if (B <= 8 && persist_groups(B, decode_cus()) > 0) return decode_persistent_as(B, sp, st, false);
+        return decode_loop(B, sp, st, false);   // (the general kernel holds at most 8 sequences)
     }
     // code 1: a hand-off waited past its bound -- the launch's workgroups were not
     // all resident (other work on the device) or stalled.  Every workgroup left
@@ -1659,6 +1674,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist = value != 0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;
+    } else if (n == "persist1m") {   // B = 2..8: the multi-sequence form of persist1 (0: the general kernel)
+        eng->use_persist1m = value != 0;
     } else if (n == "persist_spin_ticks") {   // test hook: bound of a hand-off wait (100 MHz ticks)
         eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : 300000000ull;
     } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback

@@ -139,6 +139,7 @@ struct gsv_engine {
     int* perr = nullptr;               // device error word
     int* perr_host = nullptr;          // pinned error word
     bool use_persist1 = true;          // GENIE_PERSIST1=0: the general kernel at B=1 too
+    bool use_persist1m = true;         // GENIE_PERSIST1M=0: the general kernel at B = 2..8
     bool use_persist = true;           // GENIE_PERSIST=0: per-step graphs instead
     bool use_convh = true;             // GENIE_CONVH=0: MRF convs on the f32 MFMA path
     int* vovf = nullptr;               // f16-split conv overflow flag (device)
@@ -192,6 +193,7 @@ struct gsv_engine {
     unsigned long long persist_spin_ticks = 300000000ull;   // option "persist_spin_ticks" (test hook)
     int decode_persistent(int B, const gsv_sampler* sp, hipStream_t st);
     int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one);
+    bool persist_family(int B) const;
     // generate's results (ny, steps, y rows) -> pinned host memory, enqueued by the
     // persistent decode before its own sync (one host round trip per generate)
     char* res_pin = nullptr;

@@ -277,5 +277,10 @@ int persist1_grid(int groups);
 int persist1_max_groups();
 size_t persist1_ring_bytes();
 hipError_t decode_persist1(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
+// The same kernel's multi-sequence form (k_decode_persist1m): 2 <= a.B <= persist1m_max_batch() (64)
+// sequences, each layer's workgroups run the live sequences one after another.
+int persist1m_max_batch();
+size_t persist1m_ring_bytes(int B);
+hipError_t decode_persist1m(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 
 }  // namespace gsv

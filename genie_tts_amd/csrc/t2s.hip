@@ -372,6 +372,8 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
         case 4: go(k_gemm_x3<32, 64, 6>, 32, 64, 128); break;
         case 5: go(k_gemm_x3<64, 64, 6>, 64, 64, 256); break;
         case 6: go(k_gemm_x3<32, 32, 6>, 32, 32, 64); break;
+        case 7: go(k_gemm_x3<64, 64, 3>, 64, 64, 256); break;
+        case 8: go(k_gemm_x3<32, 64, 3>, 32, 64, 128); break;
         default: go(k_gemm_x3<64, 64, 4>, 64, 64, 256); break;
     }
 }

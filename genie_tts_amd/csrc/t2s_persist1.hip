@@ -105,19 +105,21 @@ struct Ws1 {
 };
 
 // One write-through 16-byte store {tag, v0, v1, v2} (buffer_store_dwordx4 ... sc1).
-__device__ __forceinline__ void st_g16(const Ws1& ws, int off, unsigned tag, float v0, float v1, float v2) {
+template <class W>
+__device__ __forceinline__ void st_g16(const W& ws, int off, unsigned tag, float v0, float v1, float v2) {
     const u32x4 v = {tag, __float_as_uint(v0), __float_as_uint(v1), __float_as_uint(v2)};
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
                                            ws.rs, off, 0, 16 /* sc1 */);
 }
-__device__ __forceinline__ u32x4 ld_g16(const Ws1& ws, int off) {   // buffer_load_dwordx4 ... sc1
+template <class W>
+__device__ __forceinline__ u32x4 ld_g16(const W& ws, int off) {   // buffer_load_dwordx4 ... sc1
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ws.rs, off, 0, 16 /* sc1 */));
 }
 
 // One lane waits for N 16-byte granules off + k * stride (k < N), all N loads in
 // flight; re-polls only the stale ones (persist.h wait_gran_n with 16-byte granules).
-template <int N>
-__device__ __forceinline__ void wait_g16_n(const Ws1& ws, int off, int stride, unsigned tag, u32x4 (&g)[N], int* err,
+template <int N, class W>
+__device__ __forceinline__ void wait_g16_n(const W& ws, int off, int stride, unsigned tag, u32x4 (&g)[N], int* err,
                                            bool& ok, unsigned long long ticks) {
 #pragma unroll
     for (int k = 0; k < N; ++k) g[k] = ld_g16(ws, off + k * stride);
@@ -190,6 +192,7 @@ struct Shared1 {
             float lp23[3][512];        // LN2 of layer 23 (b2, scale, shift), logits group
             float lfB[LROWS + 16], lfC[LROWS + 16];   // folded LN2_23 vectors of the rows (fold)
             float xr[512];             // x_l (form_x), read back by the hop-A column owners
+            uint32_t seenq[64][33];    // multi-sequence logits workgroups: each sequence's seen bitmap
             float bo[512], n1w[512];   // out-projection bias and LN1 scale of the layer (LDS-DMA)
         } ff;
         struct {                    // attention role
@@ -201,6 +204,13 @@ struct Shared1 {
             float lg[PERSIST_LGS];  // logits (sampler)
         } at;
     };
+    // multi-sequence launch (k_decode_persist1m): per-sequence state (last: the offsets of
+    // the arrays above stay as the single-sequence kernel has them)
+    struct {
+        int tok[64], act[64], ny0[64], kv0[64], st0[64], nexe[64], lstop[64], lfin[64];
+        int kstep[64];              // the step whose status of the sequence is known (seq_runs)
+        uint32_t seens[4][33];      // a sampler workgroup's sequences h, h + 16, h + 32, h + 48
+    } m;
 };
 
 #define STAMP1(i)                                                                         \
@@ -277,6 +287,9 @@ constexpr int ERR_F16_RANGE = 2;   // error word: an activation left the fp16 ra
 
 // Scores of the general case (more than 512 keys or rows beyond the LDS stage),
 // out of line so the common path keeps its registers.  Returns the lane's max.
+// (templates on V: each kernel gets its own out-of-line copy, so the multi-sequence
+// kernel does not change the single-sequence kernel's register allocation)
+template <int V>
 __device__ __noinline__ float scores_general1(Shared1& sh, const float* Kw, int kv, int T, float q0, float q1,
                                               float q2, float q3, float sc, float4 knew, int c8, int g) {
     float lmax = -INFINITY;
@@ -423,10 +436,11 @@ __device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, floa
 // The general case (more than 512 keys or rows beyond the LDS stage): scores into
 // sh.at.p, block softmax, P.V over 16 key groups, head output -> sh.osh/osl.  Out
 // of line so the common path keeps its registers.
+template <int V>
 __device__ __noinline__ void attn_general1(Shared1& sh, const float* Kw, const float* Vw, int kv, int T, float q0,
                                            float q1, float q2, float q3, float sc, float4 knew, int c8, int g, int w,
                                            int lane, int tid) {
-    const float lmax = scores_general1(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
+    const float lmax = scores_general1<V>(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
     const float wm = wave_max_dpp(lmax);
     if (lane == 0) sh.wred[0][w] = wm;
     __syncthreads();
@@ -581,7 +595,8 @@ __device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int
 // 0..7 of granule column q and thread 256 + q rows 8..16, continuing the first
 // thread's sums in row order (bit-identical to one thread summing rows 0..15).
 // Ends with a block barrier.
-__device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const Ws1& ws, int s, int l, const float* lp2,
+template <class W>
+__device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const W& ws, int s, int l, const float* lp2,
                                            Shared1& sh, bool split) {
     const int tid = threadIdx.x, q = tid & 255;
     const unsigned tag = ws.tag(s);
@@ -632,11 +647,12 @@ __device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const Ws1& ws, 
 
 // x_l for column tid: layer 0 from the token (E_audio[tok] + alpha * pe[n]),
 // otherwise LN2_{l-1}(u) with u from the hop-B gather.
-__device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, const float* lp2,
-                                       float& xv, Shared1& sh) {
+template <class W>
+__device__ __forceinline__ bool form_x(const PersistArgs& a, const W& ws, int s, int l, int pos, const float* lp2,
+                                       float& xv, Shared1& sh, int tok) {
     const int tid = threadIdx.x;
     if (l == 0) {
-        xv = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
+        xv = ldg_h(a.emb, (long)tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
         return true;
     }
     if (!gather_pfh(a, ws, s, l, lp2, sh, false)) return false;
@@ -653,12 +669,13 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const Ws1& ws, int 
 // runs on that operand while the statistics are formed: with x = (u - mean) rden
 // n2w + n2b,  W x + b = rden (W (u n2w) - mean W n2w) + (W n2b + b), the two
 // constant vectors folded per layer at load time (PersistArgs::fold).
-__device__ __forceinline__ bool form_u(const PersistArgs& a, const Ws1& ws, int s, int l, int pos, const float* lp2,
-                                       Shared1& sh) {
+template <class W>
+__device__ __forceinline__ bool form_u(const PersistArgs& a, const W& ws, int s, int l, int pos, const float* lp2,
+                                       Shared1& sh, int tok) {
     const int tid = threadIdx.x;
     if (l > 0) return gather_pfh(a, ws, s, l, lp2, sh, true);
     bool ok = true;
-    const float u = ldg_h(a.emb, (long)sh.tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
+    const float u = ldg_h(a.emb, (long)tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
     sh.lnb[0][tid] = u;
     if (!split_h(u, sh.xh[tid], sh.xl[tid]) || !(fabsf(u) < a.f16_limit)) {
         atomicCAS(a.err, 0, ERR_F16_RANGE);
@@ -671,7 +688,8 @@ __device__ __forceinline__ bool form_u(const PersistArgs& a, const Ws1& ws, int 
 // lanes < 16 in sh.pk[w][16 t + lane], leave as the blocks' 22 granules of the row at
 // byte offset `row`.  In-wave LDS order needs no fence (LDS ops of a wave complete in
 // order; the asm statement keeps the compiler from moving the reads up).
-__device__ __forceinline__ void pub64(const Ws1& ws, Shared1& sh, int row, unsigned tag, int w, int lane) {
+template <class W>
+__device__ __forceinline__ void pub64(const W& ws, Shared1& sh, int row, unsigned tag, int w, int lane) {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     if (lane < 22) {
@@ -739,7 +757,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
         for (int l = grp; l < 24; l += ng) {
             const bool probe = a.trace && ((s == 8 && (l == 12 || l == 13 || l == 23)) || (s == 9 && l == 0));
             STAMP1(0);
-            if (!form_u(a, ws, s, l, ny0 + s, &sh.p2[0][0], sh)) return;
+            if (!form_u(a, ws, s, l, ny0 + s, &sh.p2[0][0], sh, sh.tok)) return;
             STAMP1(1);
             // ---- q, k, v of head h on the MFMA: wave w < 6 -> 16 rows (C row 0 + row 1),
             // the LN2 statistics formed while the MFMAs run
@@ -799,7 +817,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 STAMP1(3);
                 merge_waves1(sh, w, lane);
             } else {
-                attn_general1(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, g, w, lane, tid);
+                attn_general1<0>(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, g, w, lane, tid);
             }
             STAMP1(4);
             // ---- out-projection slice of this head (column tid) -> partial granule
@@ -982,7 +1000,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             const bool probe = a.trace && ((s == 8 && (l == 12 || l == 13 || l == 23)) || (s == 9 && l == 0));
             STAMP1(0);
             float xv;
-            if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh)) return;
+            if (!form_x(a, ws, s, l, ny0 + s, &sh.p2[0][0], xv, sh, sh.tok)) return;
             STAMP1(1);
             // ---- v = x_l + (bo + sum_h PA[l][h]) (heads summed in order) -> lnb[1], and the
             // MFMA operand split of v * n1w: FFN1 runs on it while the LN1 statistics are
@@ -1112,7 +1130,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
             // ---- logits rows (ar_predict_layer, no bias) of x_24 = LN2_23(h1_23 + b2 + sum PF_23)
             // on the MFMA, the LN2 folded through the rows as in form_u: wave w < 4 -> rows
             // 16 w .. + 16 of this slice, wave 4 of the last slice -> the EOS row
-            if (!form_u(a, ws, s, 24, 0, &sh.ff.lp23[0][0], sh)) return;
+            if (!form_u(a, ws, s, 24, 0, &sh.ff.lp23[0][0], sh, 0)) return;
             STAMP1(1);
             if (w < 4 || (w == 4 && j == NF - 1)) {
                 const _Float16* ab = abase(sh.xh, sh.xl, lane);
@@ -1169,6 +1187,626 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
     }
 }
 
+#ifdef PERSIST1_MULTI
+// ==========================================================================
+// Several sequences in one launch (k_decode_persist1m, B = 2..MB): the same layer
+// groups, two hand-offs per layer and weights in registers as the single-sequence
+// kernel.  Each workgroup runs its owned layer for the live sequences one after
+// another with the weights it loaded once: sequence b's hand-off is in flight while
+// the workgroup works on sequence b + 1, so a step of B sequences costs about one
+// sequence's chain plus (B - 1) workgroup passes -- not B chains.  The head's K/V
+// rows of the next sequence are staged in LDS by LDS-DMA as soon as the current
+// one's attention has read them.  Every per-sequence computation is the
+// single-sequence kernel's (same code, same order), so each sequence's tokens are
+// the ones a launch of its own gives.  Granule rows are per sequence (WsSeq), the
+// token granules TK(s, b) carry each sequence's token and finished bit, and a
+// finished sequence is skipped by every workgroup from the next step on.
+// ==========================================================================
+constexpr int MB = 64;   // sequences per multi-sequence launch (Shared1::m)
+typedef unsigned long long u64m;
+
+struct WsSeq {   // one sequence's view of the multi-sequence ring: Ws1's interface
+    u64* ring;
+    unsigned epoch;
+    __amdgpu_buffer_rsrc_t rs;
+    long slot_u64, oPFH, oLG, oTK;
+    int nb, b;
+    __device__ u64* slot(int s) const { return ring + (long)(s % RING1) * slot_u64; }
+    __device__ unsigned tag(int s) const { return (epoch << 12) | (unsigned)(s + 1); }
+    __device__ int PA(int s, int l, int h) const {
+        return (int)(((long)(s % RING1) * slot_u64 + ((long)(l * nb + b) * 16 + h) * Ws1::ROW) * 8);
+    }
+    __device__ int PFH(int s, int l, int j) const {
+        return (int)(((long)(s % RING1) * slot_u64 + oPFH + ((long)(l * nb + b) * 17 + j) * Ws1::ROW) * 8);
+    }
+    __device__ const u64* at(int byte_off) const { return ring + byte_off / 8; }
+    __device__ u64* LG(int s) const { return slot(s) + oLG + (long)b * PERSIST_LGS; }
+    __device__ u64* TK(int s) const { return slot(s) + oTK + b; }
+    __device__ WsSeq seq(int bb) const { WsSeq r = *this; r.b = bb; return r; }
+};
+// ring layout per step slot for nb sequences: PA [24][nb][16][GQ], PFH [24][nb][17][GQ]
+// (16-byte granules), LG [nb][PERSIST_LGS], TK [64] (8-byte granules); < 2^31 bytes at nb = 64
+inline long wsm_oPFH(int nb) { return 24L * nb * 16 * Ws1::ROW; }
+inline long wsm_oLG(int nb) { return wsm_oPFH(nb) + 24L * nb * 17 * Ws1::ROW; }
+inline long wsm_oTK(int nb) { return wsm_oLG(nb) + (long)nb * PERSIST_LGS; }
+inline long wsm_slot(int nb) { return wsm_oTK(nb) + MB; }
+
+// Per-sequence state into LDS (thread b < nb).
+__device__ __forceinline__ void init_m(const PersistArgs& a, Shared1& sh) {
+    const int tid = threadIdx.x, nb = a.B;
+    if (tid < nb) {
+        const int b = tid, ny0 = a.ny[b];
+        sh.m.ny0[b] = ny0;
+        sh.m.kv0[b] = a.kvlen[b];
+        sh.m.st0[b] = a.steps[b];
+        sh.m.tok[b] = (int)a.y[(long)b * a.ldy + ny0 - 1];
+        sh.m.act[b] = a.done[b] ? 0 : 1;
+        sh.m.nexe[b] = 0;
+        sh.m.lstop[b] = 0;
+        sh.m.lfin[b] = a.done[b] ? 1 : 0;
+        sh.m.kstep[b] = 0;
+    }
+    if (tid == 0) sh.fail = 0;
+}
+__device__ __forceinline__ u64m live_mask(const Shared1& sh, int nb) {
+    u64m m = 0;
+    for (int b = 0; b < nb; ++b) m |= sh.m.act[b] ? 1ull << b : 0ull;
+    return m;
+}
+
+// The head's K/V rows [0, min(kv, KVL1)) of sequence b, layer l -> the LDS stage (LDS-DMA)
+__device__ __forceinline__ void stage_kv(const PersistArgs& a, Shared1& sh, int l, int b, int h, int kv, int w,
+                                         int lane) {
+    const long off = (long)b * a.sstride + (long)h * a.tmax * 32;
+    const float* K = a.kc[l] + off;
+    const float* V = a.vc[l] + off;
+    const int nr = min(kv, KVL1), nch = (nr + 7) >> 3;
+    for (int i = w; i < nch; i += PWV) {
+        if (8 * i + (lane >> 3) < nr) {
+            __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
+        }
+    }
+}
+
+// Fused greedy token of sequence b for step s - 1 (resolve_greedy's arithmetic on its
+// own candidate granules LG(s - 1, b), polled directly: in the multi-sequence pipeline
+// they are usually there already); the publisher appends it and publishes TK(s, b).
+// Sets sh.m.tok[b] and sh.m.act[b]; ends with a barrier.
+__device__ void resolve_m(const PersistArgs& a, const WsSeq& ws, int s, int b, bool publisher, Shared1& sh) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    if (tid < 64) {
+        float f[4];
+        wait_gran_n<4>(ws.LG(s - 1) + 4 * tid, 1, ws.tag(s - 1), f, a.err, ok, a.spin_ticks);
+        float gv = f[0], rv = f[2];
+        int gi = __float_as_int(f[1]), ri = __float_as_int(f[3]);
+        if (tid == 0) {
+            float e[4];
+            wait_gran_n<4>(ws.LG(s - 1) + 256, 1, ws.tag(s - 1), e, a.err, ok, a.spin_ticks);
+            argmax_merge(gv, gi, e[0], __float_as_int(e[1]));
+            argmax_merge(rv, ri, e[2], __float_as_int(e[3]));
+        }
+        const float gm = wave_max_dpp(gv), rm = wave_max_dpp(rv);
+        const int tok = wave_min_dpp(gv == gm ? gi : 0x7fffffff);
+        const int raw = wave_min_dpp(rv == rm ? ri : 0x7fffffff);
+        if (tid == 0) {
+            const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
+            const bool fin = seq_finished(a.force_b, b, a.force_steps, a.max_steps, sh.m.st0[b] + s, stop);
+            sh.m.tok[b] = tok;
+            sh.m.act[b] = fin ? 0 : 1;
+            if (publisher && ok) {
+                a.y[(long)b * a.ldy + sh.m.ny0[b] + s - 1] = tok;
+                sh.m.lstop[b] = stop;
+                sh.m.lfin[b] = fin ? 1 : 0;
+                sh.m.nexe[b] = s;
+                st_gran(ws.TK(s), ws.tag(s), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+            }
+        }
+    }
+    if (!ok) sh.fail = 1;
+    __syncthreads();
+}
+
+// Does sequence b run step s (s >= 1)?  Learned lazily, just before a workgroup's first
+// owned layer of step s touches sequence b, so step s of one sequence starts while the
+// others still finish step s - 1: group 0 with fused greedy resolves the token itself,
+// every other workgroup reads the token granule TK(s, b) (sleeping on it).  The logits
+// workgroups (`seenq`) mark the token in that sequence's seen bitmap.  Returns the
+// block-uniform answer (false also on error).
+__device__ __forceinline__ void take_tk(unsigned u, int b, int s, uint32_t (*seenq)[33], Shared1& sh) {
+    const int tok = (int)(u & 0xffff);
+    if (seenq) seenq[b][tok >> 5] |= 1u << (tok & 31);
+    sh.m.tok[b] = tok;
+    sh.m.act[b] = ((u >> 16) & 1) ? 0 : 1;
+    sh.m.kstep[b] = s;
+}
+__device__ bool seq_runs(const PersistArgs& a, const WsSeq& base, int s, int b, unsigned long long live, bool grp0,
+                         bool fused, bool publisher, uint32_t (*seenq)[33], Shared1& sh) {
+    const int tid = threadIdx.x;
+    if (fused && grp0) {
+        resolve_m(a, base.seq(b), s, b, publisher, sh);
+    } else if (sh.m.kstep[b] != s) {
+        // one look at the token granules of every later live sequence whose status is
+        // unknown (one round trip for many), then wait for sequence b's if it was not there
+        if (tid >= b && tid < a.B && ((live >> tid) & 1ull) && sh.m.kstep[tid] != s) {
+            const WsSeq ws = base.seq(tid);
+            const u64 g = ld_rlxu64(ws.TK(s));
+            if ((unsigned)(g >> 32) == ws.tag(s)) take_tk((unsigned)g, tid, s, seenq, sh);
+        }
+        __syncthreads();
+        if (sh.m.kstep[b] != s) {
+            if (tid == 0) {
+                bool ok = true;
+                const WsSeq ws = base.seq(b);
+                wait_tag_slow(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks);
+                const float v = ok ? wait_gran(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks) : 0.f;
+                if (ok) take_tk(__float_as_uint(v), b, s, seenq, sh);
+                else sh.fail = 1;
+            }
+            __syncthreads();
+        }
+    }
+    return sh.fail == 0 && sh.m.act[b] != 0;
+}
+
+__device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, int grp, int h) {
+    const int tid = threadIdx.x, lane = tid & 63, ng = a.groups, nb = a.B;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool fused = a.greedy && a.knob[0] == 0;
+    // sampled decoding: head h's workgroup of group SAMPLER_GRP samples sequences h, h + 16, ...
+    const bool sampler = !fused && grp == SAMPLER_GRP && h < nb;
+    const bool publisher = fused && grp == 0 && h == 0;
+    init_m(a, sh);
+    if (sampler)
+        for (int i = tid; i < 4 * 33; i += PT)
+            if (h + 16 * (i / 33) < nb) sh.m.seens[i / 33][i % 33] = a.seen[(long)(h + 16 * (i / 33)) * 33 + i % 33];
+    uint4 wq[16], wo[4];
+    float qfB = 0.f, qfC = 0.f;
+    auto prefetch = [&](int l) {   // the weights of owned layer l (as run_attn; no K/V)
+        const PLayer& P = a.L[l];
+        const int n16 = lane & 15, k8 = 8 * (lane >> 4);
+        if (w < 6) {
+            const int row = (w >> 1) * 512 + h * 32 + 16 * (w & 1) + n16;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) wq[c] = ldg16(P.w_in + (long)row * 512 + 32 * c + k8, 0);
+            qfB = ldg(a.fold, (long)l * FOLD_LAYER + row);
+            qfC = ldg(a.fold, (long)l * FOLD_LAYER + 1536 + row);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + h * 32 + k8, 0);
+        if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
+    };
+    auto next_live = [&](u64m live, int from) {   // the next live sequence at or after `from`, else -1
+        const u64m m = from < 64 ? live >> from : 0ull;
+        return m ? from + (int)__builtin_ctzll(m) : -1;
+    };
+    __syncthreads();
+    u64m live = live_mask(sh, nb);
+    __syncthreads();
+    if (!live) return;
+    int staged = -1;   // (layer, sequence) whose K/V rows are in the LDS stage: l * MB + b
+    prefetch(grp);
+    {
+        const int b0 = next_live(live, 0);
+        stage_kv(a, sh, grp, b0, h, sh.m.kv0[b0], w, lane);
+        staged = grp * MB + b0;
+    }
+    int n_exec = 0;
+    for (int s = 0; s < a.smax && live && sh.fail == 0; ++s) {
+        const unsigned tag = base.tag(s);
+        for (int l = grp; l < 24; l += ng) {
+            for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1)) {
+                const WsSeq ws = base.seq(b);
+                if (l == grp && s > 0 && !seq_runs(a, base, s, b, live, grp == 0, fused, publisher, nullptr, sh)) {
+                    if (sh.fail) return;
+                    live &= ~(1ull << b);   // finished: skipped from here on (by every workgroup)
+                    continue;
+                }
+                const int kv = sh.m.kv0[b] + s;
+                if (staged != l * MB + b) {   // (a sequence that finished took the stage's turn)
+                    stage_kv(a, sh, l, b, h, kv, w, lane);
+                    staged = l * MB + b;
+                }
+                if (!form_u(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], sh, sh.m.tok[b])) return;
+                if (w < 6) {
+                    const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                    float mean, rden;
+                    ln_row_stats(sh.lnb[0], mean, rden);
+                    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int cb = 0; cb < 16; cb += 8) {
+                        h8v af[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
+#pragma unroll
+                        for (int i = 0; i < 8; i += 2) {
+                            c0 = mfma16(af[i], bfrag(wq[cb + i]), c0);
+                            c1 = mfma16(af[i + 1], bfrag(wq[cb + i + 1]), c1);
+                        }
+                    }
+                    mean = l > 0 ? mean : 0.f;
+                    rden = l > 0 ? rden : 1.f;
+                    if (lane < 16) {
+                        const float val = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * qfB) + qfC;
+                        sh.qkv[16 * w + lane] = val;
+                        if (kv < KVL1 && w >= 2) {
+                            float* row = (w < 4 ? sh.at.k : sh.at.v) + kv * 32 + 16 * (w & 1);
+                            row[lane] = val;
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
+                __syncthreads();
+                const long kvoff = (long)b * a.sstride + (long)h * a.tmax * 32;
+                float* Kw = a.kc[l] + kvoff;
+                float* Vw = a.vc[l] + kvoff;
+                const float sc = a.scale;
+                const int T = kv + 1;
+                const int c8 = lane & 7, g = (w << 3) | (lane >> 3);
+                const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
+                const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
+                const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
+                // the next sequence whose K/V this layer stages (at the first owned layer of
+                // a step its status is not known yet: staged anyway, re-staged if it changed)
+                const int bn = next_live(live, b + 1);
+                if (T <= 512 && kv < KVL1) {
+                    const int nu = (T + 63) >> 6;
+                    if (nu <= 2) wave_attn1<2>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                    else if (nu <= 4) wave_attn1<4>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                    else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                    else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                    else wave_attn1<8>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
+                    __syncthreads();   // the stage is read: the next sequence's K/V may land
+                    if (bn >= 0) {
+                        stage_kv(a, sh, l, bn, h, sh.m.kv0[bn] + s, w, lane);
+                        staged = l * MB + bn;
+                    }
+                    merge_waves1(sh, w, lane);
+                } else {
+                    attn_general1<1>(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, g, w, lane, tid);
+                    __syncthreads();
+                    if (bn >= 0) {
+                        stage_kv(a, sh, l, bn, h, sh.m.kv0[bn] + s, w, lane);
+                        staged = l * MB + bn;
+                    }
+                }
+                {
+                    const h8v af = afrag(abase(sh.osh[w], sh.osl[w], lane), 0);
+                    f32x4 acc[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bfrag(wo[t]), f32x4{0.f, 0.f, 0.f, 0.f});
+                    if (lane < 16) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
+                    }
+                    pub64(ws, sh, ws.PA(s, l, h), tag, w, lane);
+                    if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
+                    else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
+                }
+                __syncthreads();   // operands consumed before the next sequence writes them
+            }
+            // ---- next owned layer (this step) or the first one of the next step
+            const int ln = l + ng < 24 ? l + ng : grp;
+            pf_wait(a.pf_delay);
+            prefetch(ln);
+            const int b0 = next_live(live, 0);
+            if (b0 >= 0 && staged != ln * MB + b0) {
+                stage_kv(a, sh, ln, b0, h, sh.m.kv0[b0] + (l + ng < 24 ? s : s + 1), w, lane);
+                staged = ln * MB + b0;
+            }
+        }
+        // ---- sampler (sampled decoding): each of this workgroup's live sequences' logits of
+        // this step -> token -> TK(s + 1, b)
+        if (sampler) {
+            for (int b = h; b < nb; b += 16) {
+                if (!((live >> b) & 1ull)) continue;
+                const WsSeq ws = base.seq(b);
+                bool ok = true;
+                if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s, 23, 0)), tag, a.err, ok, a.spin_ticks);
+                if (!block_ok1(ok, sh)) return;
+                const u64* lgg = ws.LG(s);
+                for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok, a.spin_ticks);
+                if (!block_ok1(ok, sh)) return;
+                const int st = sh.m.st0[b] + s;
+                uint32_t* seen = sh.m.seens[b >> 4];
+                int raw = 0;
+                const int tok = sample_block<PT>([&](int i) { return sh.at.lg[i]; }, seen, b, st + 1, a.top_k,
+                                                 a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw,
+                                                 sh.samp);
+                if (tid == 0) {
+                    const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
+                    const int fin = seq_finished(a.force_b, b, a.force_steps, a.max_steps, st + 1, stop) ? 1 : 0;
+                    a.y[(long)b * a.ldy + sh.m.ny0[b] + s] = tok;
+                    seen[tok >> 5] |= 1u << (tok & 31);
+                    sh.m.lstop[b] = stop;
+                    sh.m.lfin[b] = fin;
+                    sh.m.nexe[b] = s + 1;
+                    st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+                }
+                __syncthreads();   // sh.at.lg / sh.samp consumed before the next sequence's
+            }
+        }
+        ++n_exec;
+    }
+    // fused greedy at the launch's step cap: the live sequences' last tokens are unresolved
+    if (fused && grp == 0 && n_exec == a.smax && n_exec > 0 && sh.fail == 0) {
+        for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1))
+            resolve_m(a, base.seq(b), n_exec, b, publisher, sh);
+    }
+    // ---- sequence state write-back.  Fused: the publisher, every sequence (seen = the
+    // launch's input bitmap | the tokens it appended, read back from y); sampled: each
+    // sampler workgroup, its sequences (their bitmaps).
+    if ((publisher || sampler) && sh.fail == 0) {
+        if (tid == 0) __threadfence();   // the y stores of thread 0 have reached L2
+        __syncthreads();
+        for (int b = 0; b < nb; ++b) {
+            if (sampler && (b & 15) != h) continue;
+            const int ne = sh.m.nexe[b];
+            if (ne <= 0) continue;
+            if (tid < 33) {
+                uint32_t word;
+                if (sampler) {
+                    word = sh.m.seens[b >> 4][tid];
+                } else {
+                    word = a.seen[(long)b * 33 + tid];
+                    const int64_t* yb = a.y + (long)b * a.ldy + sh.m.ny0[b];
+                    for (int i = 0; i < ne; ++i) {
+                        const int t = (int)__hip_atomic_load(yb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((t >> 5) == tid) word |= 1u << (t & 31);
+                    }
+                }
+                a.seen[(long)b * 33 + tid] = word;
+            }
+            if (tid == 0) {
+                a.ny[b] = sh.m.ny0[b] + ne;
+                a.steps[b] = sh.m.st0[b] + ne;
+                a.kvlen[b] = sh.m.kv0[b] + ne;
+                a.done[b] = (uint8_t)sh.m.lfin[b];
+                if (a.stop_out) a.stop_out[b] = (uint8_t)sh.m.lstop[b];
+            }
+        }
+    }
+}
+
+__device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, int grp, int j) {
+    const int tid = threadIdx.x, lane = tid & 63, ng = a.groups, nb = a.B;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool logits = grp == LOGIT_GRP;
+    const bool fused = a.greedy && a.knob[0] == 0;
+    init_m(a, sh);
+    if (logits && fused)
+        for (int i = tid; i < nb * 33; i += PT) sh.ff.seenq[i / 33][i % 33] = a.seen[i];
+    if (logits) {
+        for (int e = tid; e < (LROWS + 1) * 64; e += PT) {
+            const int r = e >> 6, c = e & 63;
+            const int row = r < LROWS ? j * LROWS + r : 1024;
+            sh.ff.wp[r][c] = (r < LROWS || j == NF - 1) ? ldg16(a.w_pred, (long)row * 512 + 8 * c)
+                                                        : make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (tid < LROWS + 16) {
+            const int row = tid < LROWS ? j * LROWS + tid : 1024;
+            const bool live = tid < LROWS || (tid == LROWS && j == NF - 1);
+            sh.ff.lfB[tid] = live ? ldg(a.fold, LOGIT_FOLD + row) : 0.f;
+            sh.ff.lfC[tid] = live ? ldg(a.fold, LOGIT_FOLD + 1025 + row) : 0.f;
+        }
+        sh.ff.lp23[0][tid] = ldg(a.L[23].b2, tid);
+        sh.ff.lp23[1][tid] = ldg(a.L[23].n2w, tid);
+        sh.ff.lp23[2][tid] = ldg(a.L[23].n2b, tid);
+    }
+    uint4 w1r[16], w2r[16];
+    float bo = 0.f, n1w = 0.f, n1b = 0.f;
+    float ffB = 0.f, ffC = 0.f;
+    auto prefetch = [&](int l) {
+        const PLayer& P = a.L[l];
+        const int n16 = lane & 15, k8 = 8 * (lane >> 4);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) w1r[c] = ldg16(P.w1 + (long)(j * 128 + w * 16 + n16) * 512 + 32 * c + k8, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + n16) * 2048 + j * 128 + 32 * c + k8, 0);
+        ffB = ldg(a.fold, (long)l * FOLD_LAYER + 3072 + j * 128 + w * 16 + n16);
+        ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + j * 128 + w * 16 + n16);
+        bo = ldg(P.b_out, tid); n1w = ldg(P.n1w, tid); n1b = ldg(P.n1b, tid);
+        if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
+    };
+    auto next_live = [&](u64m live, int from) {
+        const u64m m = from < 64 ? live >> from : 0ull;
+        return m ? from + (int)__builtin_ctzll(m) : -1;
+    };
+    __syncthreads();
+    u64m live = live_mask(sh, nb);
+    __syncthreads();
+    if (!live) return;
+    prefetch(grp);
+    for (int s = 0; s < a.smax && live && sh.fail == 0; ++s) {
+        const unsigned tag = base.tag(s);
+        for (int l = grp; l < 24; l += ng) {
+            for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1)) {
+                const WsSeq ws = base.seq(b);
+                if (l == grp && s > 0 &&
+                    !seq_runs(a, base, s, b, live, grp == 0, fused, false, logits && fused ? sh.ff.seenq : nullptr, sh)) {
+                    if (sh.fail) return;
+                    live &= ~(1ull << b);
+                    continue;
+                }
+                float xv;
+                if (!form_x(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], xv, sh, sh.m.tok[b])) return;
+                {
+                    bool ok = true;
+                    constexpr int RB = (int)Ws1::ROW * 8;
+                    const int q = tid & 255, off = ws.PA(s, l, 0) + 16 * q;
+                    sh.ff.xr[tid] = xv;
+                    sh.ff.bo[tid] = bo;
+                    sh.ff.n1w[tid] = n1w;
+                    u32x4 g[8];
+                    if (tid < GQ) {
+                        wait_g16_n<8>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
+                        float f0 = __uint_as_float(g[0].y), f1 = __uint_as_float(g[0].z), f2 = __uint_as_float(g[0].w);
+#pragma unroll
+                        for (int r = 1; r < 8; ++r) {
+                            f0 += __uint_as_float(g[r].y);
+                            f1 += __uint_as_float(g[r].z);
+                            f2 += __uint_as_float(g[r].w);
+                        }
+                        sh.hs[3 * q] = f0; sh.hs[3 * q + 1] = f1; sh.hs[3 * q + 2] = f2;
+                    } else if (tid >= 256 && q < GQ) {
+                        wait_g16_n<8>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+                    }
+                    if (!block_ok1(ok, sh)) return;
+                    if (tid >= 256 && q < GQ) {
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            if (k == 2 && gq_n(q) == 2) break;
+                            float sum = sh.hs[3 * q + k];
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) sum += __uint_as_float(g[r][1 + k]);
+                            const int c = gq_col(q, k);
+                            const float vc = sh.ff.xr[c] + (sh.ff.bo[c] + sum);
+                            sh.lnb[1][c] = vc;
+                            const float un = vc * sh.ff.n1w[c];
+                            if (!split_h(un, sh.xh[c], sh.xl[c]) || !(fabsf(un) < a.f16_limit)) {
+                                atomicCAS(a.err, 0, ERR_F16_RANGE);
+                                ok = false;
+                            }
+                        }
+                    }
+                    if (!block_ok1(ok, sh)) return;
+                }
+                const float v = sh.lnb[1][tid];
+                {
+                    const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                    float mean, rden;
+                    ln_row_stats(sh.lnb[1], mean, rden);
+                    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int cb = 0; cb < 16; cb += 8) {
+                        h8v af[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
+#pragma unroll
+                        for (int i = 0; i < 8; i += 2) {
+                            c0 = mfma16(af[i], bfrag(w1r[cb + i]), c0);
+                            c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
+                        }
+                    }
+                    const float h1_pub = (v - mean) * rden * n1w + n1b;
+                    if ((tid >> 5) == j) sh.h1s[tid & 31] = h1_pub;
+                    if (lane < 16) {
+                        const float f = fmaxf(rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * ffB) + ffC, 0.f);
+                        split_h(f, sh.fh[w * 16 + lane], sh.fl[w * 16 + lane]);
+                        if (!(fabsf(f) < a.f16_limit)) {
+                            atomicCAS(a.err, 0, ERR_F16_RANGE);
+                            sh.fail = 1;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (sh.fail) return;
+                {
+                    f32x4 acc[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const _Float16* ab = abase(sh.fh, sh.fl, lane);
+                    h8v af[4];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) af[c] = afrag(ab, 32 * c);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) acc[t] = mfma16(af[c], bfrag(w2r[4 * t + c]), acc[t]);
+                    if (lane < 16) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
+                    }
+                    pub64(ws, sh, ws.PFH(s, l, j), tag, w, lane);
+                }
+                if (w == 0) {
+                    int ln = lane;
+                    asm volatile("" : "+v"(ln));
+                    if (ln < 11) {
+                        const float* p = sh.h1s + 3 * ln;
+                        st_g16(ws, ws.PFH(s, l, 16) + 16 * (11 * j + ln), tag, p[0], p[1], ln == 10 ? 0.f : p[2]);
+                    }
+                }
+                __syncthreads();   // operands consumed before the next sequence writes them
+            }
+            pf_wait(a.pf_delay);
+            prefetch(l + ng < 24 ? l + ng : grp);
+        }
+        if (logits) {
+            for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1)) {
+                const WsSeq ws = base.seq(b);
+                if (!form_u(a, ws, s, 24, 0, &sh.ff.lp23[0][0], sh, 0)) return;
+                if (w < 4 || (w == 4 && j == NF - 1)) {
+                    const _Float16* ab = abase(sh.xh, sh.xl, lane);
+                    float mean, rden;
+                    ln_row_stats(sh.lnb[0], mean, rden);
+                    const uint4* wb = &sh.ff.wp[min(16 * w + (lane & 15), LROWS)][lane >> 4];
+                    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int cb = 0; cb < 16; cb += 2) {
+                        c0 = mfma16(afrag(ab, 32 * cb), bfrag(wb[4 * cb]), c0);
+                        c1 = mfma16(afrag(ab, 32 * (cb + 1)), bfrag(wb[4 * (cb + 1)]), c1);
+                    }
+                    const int rl = 16 * w + lane;
+                    const float v = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * sh.ff.lfB[min(rl, LROWS)]) +
+                                    sh.ff.lfC[min(rl, LROWS)];
+                    if (!fused) {
+                        if (lane < 16 && (w < 4 || lane == 0))
+                            st_gran(ws.LG(s) + (w < 4 ? j * LROWS + rl : 1024), tag, v);
+                    } else {
+                        const int i = w < 4 ? j * LROWS + rl : 1024;
+                        const bool lv = w < 4 ? lane < 16 : lane == 0;
+                        const uint32_t* seen = sh.ff.seenq[b];
+                        float pv = ((seen[i >> 5] >> (i & 31)) & 1u) ? (v < 0.f ? v * a.rep_penalty : v / a.rep_penalty) : v;
+                        pv = pv / a.temperature;
+                        float gv = lv ? pv : -INFINITY, rv = lv ? v : -INFINITY;
+                        gv = fmaxf(gv, dpp_f<0xB1, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0xB1, 0xF>(rv));
+                        gv = fmaxf(gv, dpp_f<0x4E, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x4E, 0xF>(rv));
+                        gv = fmaxf(gv, dpp_f<0x141, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x141, 0xF>(rv));
+                        gv = fmaxf(gv, dpp_f<0x140, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x140, 0xF>(rv));
+                        const float gm = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gv)));
+                        const float rm = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rv)));
+                        int gmi = (lv && pv == gm) ? i : 0x7fffffff, rmi = (lv && v == rm) ? i : 0x7fffffff;
+                        gmi = min(gmi, dpp_i<0xB1, 0xF>(gmi)); rmi = min(rmi, dpp_i<0xB1, 0xF>(rmi));
+                        gmi = min(gmi, dpp_i<0x4E, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x4E, 0xF>(rmi));
+                        gmi = min(gmi, dpp_i<0x141, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x141, 0xF>(rmi));
+                        gmi = min(gmi, dpp_i<0x140, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x140, 0xF>(rmi));
+                        if (lane < 4) {
+                            const float out = lane == 0 ? gm : lane == 1 ? __int_as_float(gmi)
+                                            : lane == 2 ? rm : __int_as_float(rmi);
+                            st_gran(ws.LG(s) + 4 * (w < 4 ? 4 * j + w : 64) + lane, tag, out);
+                        }
+                    }
+                }
+                __syncthreads();   // operands consumed before the next sequence writes them
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(PT) void k_decode_persist1m(PersistArgs a) {
+    __shared__ Shared1 sh;
+    WsSeq ws;
+    ws.ring = a.ring;
+    ws.epoch = a.epoch;
+    ws.rs = __builtin_amdgcn_make_buffer_rsrc(a.ring, 0, 0x7fffffff, 0x00020000);
+    ws.nb = a.B;
+    ws.b = 0;
+    ws.oPFH = 24L * a.B * 16 * Ws1::ROW;
+    ws.oLG = ws.oPFH + 24L * a.B * 17 * Ws1::ROW;
+    ws.oTK = ws.oLG + (long)a.B * PERSIST_LGS;
+    ws.slot_u64 = ws.oTK + MB;
+    const int grp = blockIdx.x / GW, r = blockIdx.x - grp * GW;
+    if (r < 16) run_attn_m(a, ws, sh, grp, r);
+    else run_ffn_m(a, ws, sh, grp, r - 16);
+}
+
+#else   // the single-sequence kernel
+
 __global__ __launch_bounds__(PT) void k_decode_persist1(PersistArgs a) {
     __shared__ Shared1 sh;
     const Ws1 ws{a.ring, a.epoch, __builtin_amdgcn_make_buffer_rsrc(a.ring, 0, 0x7fffffff, 0x00020000)};
@@ -1176,18 +1814,31 @@ __global__ __launch_bounds__(PT) void k_decode_persist1(PersistArgs a) {
     if (r < 16) run_attn(a, ws, sh, grp, r);
     else run_ffn(a, ws, sh, grp, r - 16);
 }
+#endif
 
 }  // namespace
 
+#ifdef PERSIST1_MULTI
+int persist1m_max_batch() { return MB; }
+size_t persist1m_ring_bytes(int B) { return (size_t)wsm_slot(B) * RING1 * 8; }
+
+hipError_t decode_persist1m(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    if (a.groups < 3 || a.groups > NG_MAX || a.B < 2 || a.B > MB) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL(k_decode_persist1m, dim3(a.groups * GW), dim3(PT), 0, s, start, stop, 0, a);
+    return hipGetLastError();
+}
+
+#else
 int persist1_grid(int groups) { return groups * GW; }
 int persist1_max_groups() { return NG_MAX; }
 
 size_t persist1_ring_bytes() { return (size_t)Ws1::SLOT * RING1 * 8; }
-
 hipError_t decode_persist1(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     if (a.groups < 3 || a.groups > NG_MAX) return hipErrorInvalidValue;   // groups 1, 2 own the logits, sampler
     hipExtLaunchKernelGGL(k_decode_persist1, dim3(a.groups * GW), dim3(PT), 0, s, start, stop, 0, a);
     return hipGetLastError();
 }
+
+#endif
 
 }  // namespace gsv

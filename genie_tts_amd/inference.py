@@ -230,15 +230,10 @@ class GENIE:
         ssl = np.asarray(prompt_audio.ssl_content, np.float32).reshape(768, -1)
         utts = [(prompt_audio.phonemes_seq, it[0], prompt_audio.text_bert, it[1], ssl,
                  it[2] if len(it) > 2 else 0) for it in items]
-        if not 5 <= len(utts) <= 9:
-            return model.ENGINE.t2s_generate(utts, sampler)
-        # 5-9 sequences fit only one layer group of the batched persistent decode; chunks of
-        # 4 run on two groups and finish sooner (profiles/r03f_batch_sweep.json: 8 = 4 + 4 in
-        # 71 ms vs 96 ms; sampled draws are keyed by the slot within each generate)
-        toks = []
-        for i in range(0, len(utts), 4):
-            toks += model.ENGINE.t2s_generate(utts[i:i + 4], sampler)
-        return toks
+        # one generate for the whole batch: the engine's multi-sequence persistent decode
+        # (B <= 56) costs ~1.2 ms per extra sequence over a single one
+        # (profiles/r03h_batch_sweep.json), so splitting never pays
+        return model.ENGINE.t2s_generate(utts, sampler)
 
     def tts_batch_vocoder(self, items: Sequence[tuple], toks, prompt_audio: ReferenceAudio, model,
                           overlapped: bool = False):

@@ -45,13 +45,10 @@ def _resolve(spec: Optional[str]):
 
 
 def round_size(ready: int) -> int:
-    """Sentences a worker round takes out of `ready` of one character.  From the T2S time
-    per batch (tools/batch_sweep.py, profiles/r03f_batch_sweep.json): B <= 4 runs the
-    two-group persistent decode (B = 4: 36 ms), B = 5..8 fits only one layer group
-    (70-96 ms), B >= 10 the batched graph path (~100 ms, 150 ms at 64); so 5-9 ready
-    sentences go as 4 now and the rest next round (4 + 4 = 72 ms < 96 ms for 8)."""
-    if 5 <= ready <= 9:
-        return 4
+    """Sentences a worker round takes out of `ready` of one character: all of them, up to
+    MAX_BATCH.  The T2S time per batch grows monotonically and slowly with B
+    (tools/batch_sweep.py, profiles/r03h_batch_sweep.json: 16.6 ms at 1, 26 ms at 8,
+    72 ms at 32, 143 ms at 64 per 81-step generate), so a round never waits."""
     return min(ready, MAX_BATCH)
 
 

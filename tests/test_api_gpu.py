@@ -119,8 +119,8 @@ def test_api_tts_end_to_end(model):
 
 @pytest.mark.parametrize("lens", [(10, 17, 25), (10, 17, 25, 8, 13, 21)])
 def test_tts_batch_equals_single(model, lens):
-    """3 sentences: one batched generate; 6: two chunks (4 + 2) on the two-group
-    persistent decode (GENIE.tts_batch_t2s)."""
+    """3 or 6 sentences: one batched generate on the multi-sequence persistent decode
+    (GENIE.tts_batch_t2s); every sentence's audio equals its own single-sentence call."""
     from genie_tts_amd.inference import GENIE, ReferenceAudio
     m, _ = model
     ref = ReferenceAudio(phonemes_seq=synth.synth_phones(12, "b-r"), text_bert=np.zeros((12, 1024), np.float32),

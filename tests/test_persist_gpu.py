@@ -1,5 +1,6 @@
-"""GPU: the persistent decode launch (t2s_persist.hip) against the per-step
-hipGraph path and the CPU oracle.
+"""GPU: the persistent decode launches (t2s_persist1.hip at B = 1, its multi-sequence
+form at B = 2..64, t2s_persist.hip when it is off) against the per-step hipGraph path, each
+other and the CPU oracle.
 
 Both decode paths sit behind gsv_t2s_generate (the reference's 500-step loop,
 Inference.py:95-109); option "persist" selects one.  Bars: greedy token ids
@@ -145,3 +146,72 @@ def test_persistent_timeout_reruns_as_graphs(eng):
     sem, _, _ = R.t2s_generate(character("v2")["t2s_encoder"], R.T2SModel(character("v2")["t2s"]), ref, rb, txt,
                                tb, ssl, force_steps=12)
     assert out[0].tolist() == sem.reshape(-1).tolist()
+
+
+def _alone(eng, inps, sp):
+    return [eng.t2s_generate([inp], sp)[0].tolist() for inp in inps]
+
+
+@pytest.mark.parametrize("B", [2, 5, 8, 16, 40])
+def test_multi_sequence_matches_single_launches(eng, B):
+    """The multi-sequence form of the single-sequence kernel (k_decode_persist1m, B = 2..64)
+    runs every sequence through the same per-sequence arithmetic: each sequence's greedy
+    tokens are the ones a launch of its own gives (k_decode_persist1)."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=10 + 3 * i, S=8 + 2 * i, H=30 + 6 * i, tag=f"m{B}_{i}") for i in range(B)]
+    sp = make_sampler(force_steps=22)
+    eng.set_option("persist", 1)
+    got = eng.t2s_generate(inps, sp)
+    assert [g.tolist() for g in got] == _alone(eng, inps, sp)
+
+
+def test_multi_sequence_ragged_lengths(eng):
+    """Sequences that finish at different steps (per-utterance forced lengths) leave the
+    launch one by one; the others keep their tokens (vs the per-step graph path and vs
+    launches of their own)."""
+    from genie_tts_amd.engine import make_sampler
+    lens = [9, 25, 4, 17, 12]
+    inps = [t2s_inputs(R=11 + i, S=9 + i, H=32 + 4 * i, tag=f"rg{i}") + (n,) for i, n in enumerate(lens)]
+    sp = make_sampler(force_steps=30)
+    a, b = _both(eng, inps, sp)
+    for i in range(len(lens)):
+        assert a[i].tolist() == b[i].tolist(), f"utterance {i}"
+    assert len({len(x) for x in a}) == len(lens)   # every sequence stopped at its own step
+    assert [x.tolist() for x in a] == _alone(eng, inps, sp)
+
+
+def test_multi_sequence_fp16_range_fallback(eng):
+    """An activation past the fp16 range stops the multi-sequence launch (error 2) before
+    any sequence state is written; the steps run again (the general kernel up to 8
+    sequences, the per-step graphs above) with the same tokens."""
+    from genie_tts_amd.engine import make_sampler
+    for B in (3, 12):
+        inps = [t2s_inputs(R=10 + i, S=8 + i, H=30 + 2 * i, tag=f"mf{B}_{i}") for i in range(B)]
+        sp = make_sampler(force_steps=14)
+        eng.set_option("persist", 1)
+        ref = eng.t2s_generate(inps, sp)
+        before = eng.counter("persist1_f16_reruns")
+        eng.set_option("persist1_f16_limit", 1)
+        try:
+            got = eng.t2s_generate(inps, sp)
+        finally:
+            eng.set_option("persist1_f16_limit", 0)
+        assert eng.counter("persist1_f16_reruns") > before
+        assert [g.tolist() for g in got] == [r.tolist() for r in ref]
+
+
+def test_multi_sequence_sampled_matches_general_kernel(eng):
+    """Top-k sampling at B = 3: the multi-sequence kernel's sampler workgroups (one per
+    sequence) draw what the general persistent kernel draws (same Philox keys)."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=12 + i, S=9 + i, H=36 + 2 * i, tag=f"msk{i}") for i in range(3)]
+    sp = make_sampler(top_k=15, greedy=False, seed=99, force_steps=20)
+    eng.set_option("persist", 1)
+    a = eng.t2s_generate(inps, sp)
+    eng.set_option("persist1m", 0)
+    try:
+        b = eng.t2s_generate(inps, sp)
+    finally:
+        eng.set_option("persist1m", 1)
+    for i in range(len(inps)):
+        assert a[i].tolist() == b[i].tolist(), f"utterance {i}"

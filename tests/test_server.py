@@ -72,7 +72,7 @@ def test_router_endpoints_and_streaming(tmp_path):
 
 def test_round_size_policy():
     from genie_tts_amd.server import MAX_BATCH, round_size
-    assert [round_size(n) for n in range(1, 12)] == [1, 2, 3, 4, 4, 4, 4, 4, 4, 10, 11]
+    assert [round_size(n) for n in range(1, 12)] == list(range(1, 12))
     assert round_size(200) == MAX_BATCH
 
 

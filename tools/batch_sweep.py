@@ -1,7 +1,9 @@
-"""T2S generate time vs batch size (B = 1, 2, 4, 8, 16, 32, 64) on one GPU: V2 synthetic
-character, the single workload's utterance repeated B times (R=48, S=45, H=264, 81 forced
-loop steps), greedy.  Prints one JSON line: ms per generate and ms per utterance, so a
-batching front end can pick its batch policy.  Usage: python tools/batch_sweep.py"""
+"""T2S generate time vs batch size (B = 1 .. 64) on one GPU: V2 synthetic character, the
+single workload's utterance repeated B times (R=48, S=45, H=264, 81 forced loop steps),
+greedy.  Prints one JSON line: ms per generate and ms per utterance per decode path, so the
+engine's path choice and a batching front end's policy can be read off it.
+Usage: python tools/batch_sweep.py [--compare]  (--compare: also the per-step graph path
+for B > 8, i.e. with option persist1m = 0)"""
 import json
 import os
 import sys
@@ -35,11 +37,14 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3
 
-    for B in (1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 32, 64):
+    compare = "--compare" in sys.argv
+    for B in (1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 24, 32, 40, 48, 56, 64):
         ms = timed([B])
         out[B] = {"ms": round(ms, 2), "ms_per_utt": round(ms / B, 3)}
-        if 5 <= B <= 8:   # two generates of ceil(B/2), floor(B/2): the 2-group persistent kernel
-            out[B]["halves_ms"] = round(timed([(B + 1) // 2, B // 2]), 2)
+        if compare and B > 8:   # the per-step graph path at the same B
+            eng.set_option("persist1m", 0)
+            out[B]["graphs_ms"] = round(timed([B]), 2)
+            eng.set_option("persist1m", 1)
         print(B, out[B], file=sys.stderr, flush=True)
     print(json.dumps({"t2s_generate_vs_batch": out, "steps": it.force_steps}))
     eng.close()
