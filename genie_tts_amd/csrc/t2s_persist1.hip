@@ -221,6 +221,26 @@ struct Shared1 {
         }                                                                                 \
     } while (0)
 
+// A workgroup barrier without __syncthreads' memory fence: LDS writes are complete
+// (lgkmcnt(0)) but in-flight global stores are not waited for.  The multi-sequence
+// kernel's waves publish write-through granules and go on with the next sequence; a
+// fence there would hold every wave for the stores' ~1 us round trip.
+__device__ __forceinline__ void bar_nf() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+template <bool NF>
+__device__ __forceinline__ void bar_t() {
+    if (NF) bar_nf();
+    else __syncthreads();
+}
+template <bool NF = false>
+__device__ __forceinline__ bool block_ok_t(bool ok, Shared1& sh) {
+    if (!ok) sh.fail = 1;
+    bar_t<NF>();
+    return sh.fail == 0;
+}
 __device__ __forceinline__ bool block_ok1(bool ok, Shared1& sh) {
     if (!ok) sh.fail = 1;
     __syncthreads();
@@ -595,16 +615,16 @@ __device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int
 // 0..7 of granule column q and thread 256 + q rows 8..16, continuing the first
 // thread's sums in row order (bit-identical to one thread summing rows 0..15).
 // Ends with a block barrier.
-template <class W>
+template <class W, bool NF = false>
 __device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const W& ws, int s, int l, const float* lp2,
-                                           Shared1& sh, bool split) {
+                                           Shared1& sh, bool split, bool wake = true) {
     const int tid = threadIdx.x, q = tid & 255;
     const unsigned tag = ws.tag(s);
     constexpr int RB = (int)Ws1::ROW * 8;   // bytes per row
     bool ok = true;
-    if (l >= 2) {
+    if (l >= 2 && wake) {   // (a sequence that follows another through this layer polls at once)
         if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s, l - 2, 0)), tag, a.err, ok, a.spin_ticks);
-        if (!block_ok1(ok, sh)) return false;
+        if (!block_ok_t<NF>(ok, sh)) return false;
     }
     const int off = ws.PFH(s, l - 1, 0) + 16 * q;
     u32x4 g[9];
@@ -622,7 +642,7 @@ __device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const W& ws, in
     } else if (tid >= 256 && q < GQ) {
         wait_g16_n<9>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
     }
-    if (!block_ok1(ok, sh)) return false;
+    if (!block_ok_t<NF>(ok, sh)) return false;
     if (tid >= 256 && q < GQ) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -642,20 +662,20 @@ __device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const W& ws, in
             }
         }
     }
-    return block_ok1(ok, sh);
+    return block_ok_t<NF>(ok, sh);
 }
 
 // x_l for column tid: layer 0 from the token (E_audio[tok] + alpha * pe[n]),
 // otherwise LN2_{l-1}(u) with u from the hop-B gather.
-template <class W>
+template <class W, bool NF = false>
 __device__ __forceinline__ bool form_x(const PersistArgs& a, const W& ws, int s, int l, int pos, const float* lp2,
-                                       float& xv, Shared1& sh, int tok) {
+                                       float& xv, Shared1& sh, int tok, bool wake = true) {
     const int tid = threadIdx.x;
     if (l == 0) {
         xv = ldg_h(a.emb, (long)tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
         return true;
     }
-    if (!gather_pfh(a, ws, s, l, lp2, sh, false)) return false;
+    if (!gather_pfh<W, NF>(a, ws, s, l, lp2, sh, false, wake)) return false;
     const float v = sh.lnb[0][tid];
     float mean, rden;
     ln_row_stats(sh.lnb[0], mean, rden);
@@ -669,11 +689,11 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const W& ws, int s,
 // runs on that operand while the statistics are formed: with x = (u - mean) rden
 // n2w + n2b,  W x + b = rden (W (u n2w) - mean W n2w) + (W n2b + b), the two
 // constant vectors folded per layer at load time (PersistArgs::fold).
-template <class W>
+template <class W, bool NF = false>
 __device__ __forceinline__ bool form_u(const PersistArgs& a, const W& ws, int s, int l, int pos, const float* lp2,
-                                       Shared1& sh, int tok) {
+                                       Shared1& sh, int tok, bool wake = true) {
     const int tid = threadIdx.x;
-    if (l > 0) return gather_pfh(a, ws, s, l, lp2, sh, true);
+    if (l > 0) return gather_pfh<W, NF>(a, ws, s, l, lp2, sh, true, wake);
     bool ok = true;
     const float u = ldg_h(a.emb, (long)tok * 512 + tid) + ldg(a.alpha, 0) * ldg(a.pe, (long)pos * 512 + tid);
     sh.lnb[0][tid] = u;
@@ -681,7 +701,7 @@ __device__ __forceinline__ bool form_u(const PersistArgs& a, const W& ws, int s,
         atomicCAS(a.err, 0, ERR_F16_RANGE);
         ok = false;
     }
-    return block_ok1(ok, sh);
+    return block_ok_t<NF>(ok, sh);
 }
 
 // A wave's 64 published columns [64 w, 64 w + 64) (two 32-column blocks), staged by
@@ -1254,14 +1274,43 @@ __device__ __forceinline__ u64m live_mask(const Shared1& sh, int nb) {
     return m;
 }
 
-// The head's K/V rows [0, min(kv, KVL1)) of sequence b, layer l -> the LDS stage (LDS-DMA)
+// Waves 3 and 7 issue every write-through store of the multi-sequence kernel (the
+// granules, the K/V rows); the other six poll the hand-offs and run the LDS-DMA.  On
+// CDNA a wave's vmcnt covers its stores and its loads in issue order, so a wave that
+// polls next sequence's inputs right after publishing would wait for its stores'
+// write-through round trip (~1 us) on every sequence.
+__device__ __forceinline__ bool is_pub_wave(int w) { return w == 3 || w == 7; }
+
+// The 512 partial columns the 8 waves staged in sh.pk (column c at flat index c) leave
+// as the row's GQ granules at byte offset `row`, stored by waves 3 and 7 (88 each).
+template <class W>
+__device__ __forceinline__ void pub_all(const W& ws, Shared1& sh, int row, unsigned tag, int w, int lane) {
+    bar_nf();
+    if (is_pub_wave(w)) {
+        const float* pk = &sh.pk[0][0];
+        const int base = w == 3 ? 0 : 88;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int q = base + 64 * k + lane;
+            if (k == 0 || lane < 24) {
+                const int c = gq_col(q, 0);
+                st_g16(ws, row + 16 * q, tag, pk[c], pk[c + 1], gq_n(q) == 2 ? 0.f : pk[c + 2]);
+            }
+        }
+    }
+}
+
+// The head's K/V rows [0, min(kv, KVL1)) of sequence b, layer l -> the LDS stage
+// (LDS-DMA by the six non-publishing waves)
 __device__ __forceinline__ void stage_kv(const PersistArgs& a, Shared1& sh, int l, int b, int h, int kv, int w,
                                          int lane) {
+    if (is_pub_wave(w)) return;
+    const int wi = w < 3 ? w : w - 1;   // 0..5
     const long off = (long)b * a.sstride + (long)h * a.tmax * 32;
     const float* K = a.kc[l] + off;
     const float* V = a.vc[l] + off;
     const int nr = min(kv, KVL1), nch = (nr + 7) >> 3;
-    for (int i = w; i < nch; i += PWV) {
+    for (int i = wi; i < nch; i += 6) {
         if (8 * i + (lane >> 3) < nr) {
             __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, sh.at.k + i * 256, 16, 0, 0);
             __builtin_amdgcn_global_load_lds(V + (long)i * 256 + lane * 4, sh.at.v + i * 256, 16, 0, 0);
@@ -1305,7 +1354,7 @@ __device__ void resolve_m(const PersistArgs& a, const WsSeq& ws, int s, int b, b
         }
     }
     if (!ok) sh.fail = 1;
-    __syncthreads();
+    bar_nf();
 }
 
 // Does sequence b run step s (s >= 1)?  Learned lazily, just before a workgroup's first
@@ -1334,7 +1383,7 @@ __device__ bool seq_runs(const PersistArgs& a, const WsSeq& base, int s, int b, 
             const u64 g = ld_rlxu64(ws.TK(s));
             if ((unsigned)(g >> 32) == ws.tag(s)) take_tk((unsigned)g, tid, s, seenq, sh);
         }
-        __syncthreads();
+        bar_nf();
         if (sh.m.kstep[b] != s) {
             if (tid == 0) {
                 bool ok = true;
@@ -1344,7 +1393,7 @@ __device__ bool seq_runs(const PersistArgs& a, const WsSeq& base, int s, int b, 
                 if (ok) take_tk(__float_as_uint(v), b, s, seenq, sh);
                 else sh.fail = 1;
             }
-            __syncthreads();
+            bar_nf();
         }
     }
     return sh.fail == 0 && sh.m.act[b] != 0;
@@ -1403,12 +1452,16 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                     live &= ~(1ull << b);   // finished: skipped from here on (by every workgroup)
                     continue;
                 }
+                const bool probe = a.trace && s == 8 && l == grp && b < 8;   // tools/ptrace_multi.py
+                const unsigned long long t_in = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 const int kv = sh.m.kv0[b] + s;
                 if (staged != l * MB + b) {   // (a sequence that finished took the stage's turn)
                     stage_kv(a, sh, l, b, h, kv, w, lane);
                     staged = l * MB + b;
                 }
-                if (!form_u(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], sh, sh.m.tok[b])) return;
+                if (!form_u<WsSeq, true>(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], sh, sh.m.tok[b],
+                                         b == next_live(live, 0)))
+                    return;
                 if (w < 6) {
                     const _Float16* ab = abase(sh.xh, sh.xl, lane);
                     float mean, rden;
@@ -1436,8 +1489,8 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                         }
                     }
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's K/V LDS-DMA has landed
-                __syncthreads();
+                if (!is_pub_wave(w)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its K/V LDS-DMA landed
+                bar_nf();
                 const long kvoff = (long)b * a.sstride + (long)h * a.tmax * 32;
                 float* Kw = a.kc[l] + kvoff;
                 float* Vw = a.vc[l] + kvoff;
@@ -1457,7 +1510,7 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                     else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
                     else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
                     else wave_attn1<8>(sh, q0, q1, q2, q3, sc, kv, T, c8, g, w, lane);
-                    __syncthreads();   // the stage is read: the next sequence's K/V may land
+                    bar_nf();   // the stage is read: the next sequence's K/V may land
                     if (bn >= 0) {
                         stage_kv(a, sh, l, bn, h, sh.m.kv0[bn] + s, w, lane);
                         staged = l * MB + bn;
@@ -1465,7 +1518,7 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                     merge_waves1(sh, w, lane);
                 } else {
                     attn_general1<1>(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, g, w, lane, tid);
-                    __syncthreads();
+                    bar_nf();
                     if (bn >= 0) {
                         stage_kv(a, sh, l, bn, h, sh.m.kv0[bn] + s, w, lane);
                         staged = l * MB + bn;
@@ -1480,11 +1533,17 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
 #pragma unroll
                         for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
                     }
-                    pub64(ws, sh, ws.PA(s, l, h), tag, w, lane);
-                    if (tid < 32) Kw[(long)kv * 32 + tid] = sh.qkv[32 + tid];
-                    else if (tid < 64) Vw[(long)kv * 32 + tid - 32] = sh.qkv[64 + tid - 32];
+                    pub_all(ws, sh, ws.PA(s, l, h), tag, w, lane);
+                    if (w == 7) {   // the new K/V row (read by this workgroup only, next step)
+                        if (lane < 32) Kw[(long)kv * 32 + lane] = sh.qkv[32 + lane];
+                        else Vw[(long)kv * 32 + lane - 32] = sh.qkv[64 + lane - 32];
+                    }
                 }
-                __syncthreads();   // operands consumed before the next sequence writes them
+                bar_nf();   // operands consumed before the next sequence writes them
+                if (probe && tid == 0) {
+                    a.trace[blockIdx.x * 16 + 2 * b] = t_in;
+                    a.trace[blockIdx.x * 16 + 2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+                }
             }
             // ---- next owned layer (this step) or the first one of the next step
             const int ln = l + ng < 24 ? l + ng : grp;
@@ -1632,8 +1691,12 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                     live &= ~(1ull << b);
                     continue;
                 }
+                const bool probe = a.trace && s == 8 && l == grp && b < 8;   // tools/ptrace_multi.py
+                const unsigned long long t_in = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 float xv;
-                if (!form_x(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], xv, sh, sh.m.tok[b])) return;
+                if (!form_x<WsSeq, true>(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], xv, sh, sh.m.tok[b],
+                                         b == next_live(live, 0)))
+                    return;
                 {
                     bool ok = true;
                     constexpr int RB = (int)Ws1::ROW * 8;
@@ -1655,7 +1718,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                     } else if (tid >= 256 && q < GQ) {
                         wait_g16_n<8>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
                     }
-                    if (!block_ok1(ok, sh)) return;
+                    if (!block_ok_t<true>(ok, sh)) return;
                     if (tid >= 256 && q < GQ) {
 #pragma unroll
                         for (int k = 0; k < 3; ++k) {
@@ -1673,7 +1736,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                             }
                         }
                     }
-                    if (!block_ok1(ok, sh)) return;
+                    if (!block_ok_t<true>(ok, sh)) return;
                 }
                 const float v = sh.lnb[1][tid];
                 {
@@ -1703,7 +1766,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                         }
                     }
                 }
-                __syncthreads();
+                bar_nf();
                 if (sh.fail) return;
                 {
                     f32x4 acc[4];
@@ -1721,17 +1784,18 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
 #pragma unroll
                         for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
                     }
-                    pub64(ws, sh, ws.PFH(s, l, j), tag, w, lane);
+                    pub_all(ws, sh, ws.PFH(s, l, j), tag, w, lane);
                 }
-                if (w == 0) {
-                    int ln = lane;
-                    asm volatile("" : "+v"(ln));
-                    if (ln < 11) {
-                        const float* p = sh.h1s + 3 * ln;
-                        st_g16(ws, ws.PFH(s, l, 16) + 16 * (11 * j + ln), tag, p[0], p[1], ln == 10 ? 0.f : p[2]);
-                    }
+                if (w == 7 && lane >= 40 && lane < 51) {   // h1 block j (11 granules; staged before FFN1's barrier)
+                    const int q = lane - 40;
+                    const float* p = sh.h1s + 3 * q;
+                    st_g16(ws, ws.PFH(s, l, 16) + 16 * (11 * j + q), tag, p[0], p[1], q == 10 ? 0.f : p[2]);
                 }
-                __syncthreads();   // operands consumed before the next sequence writes them
+                bar_nf();   // operands consumed before the next sequence writes them
+                if (probe && tid == 0) {
+                    a.trace[blockIdx.x * 16 + 2 * b] = t_in;
+                    a.trace[blockIdx.x * 16 + 2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+                }
             }
             pf_wait(a.pf_delay);
             prefetch(l + ng < 24 ? l + ng : grp);
@@ -1739,7 +1803,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
         if (logits) {
             for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1)) {
                 const WsSeq ws = base.seq(b);
-                if (!form_u(a, ws, s, 24, 0, &sh.ff.lp23[0][0], sh, 0)) return;
+                if (!form_u<WsSeq, true>(a, ws, s, 24, 0, &sh.ff.lp23[0][0], sh, 0, b == next_live(live, 0))) return;
                 if (w < 4 || (w == 4 && j == NF - 1)) {
                     const _Float16* ab = abase(sh.xh, sh.xl, lane);
                     float mean, rden;
@@ -1755,8 +1819,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                     const float v = rden * (((c0[0] + c1[0]) + (c0[1] + c1[1])) - mean * sh.ff.lfB[min(rl, LROWS)]) +
                                     sh.ff.lfC[min(rl, LROWS)];
                     if (!fused) {
-                        if (lane < 16 && (w < 4 || lane == 0))
-                            st_gran(ws.LG(s) + (w < 4 ? j * LROWS + rl : 1024), tag, v);
+                        if (lane < 16 && (w < 4 || lane == 0)) sh.pk[w][lane] = v;   // (published by wave 7)
                     } else {
                         const int i = w < 4 ? j * LROWS + rl : 1024;
                         const bool lv = w < 4 ? lane < 16 : lane == 0;
@@ -1778,11 +1841,26 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                         if (lane < 4) {
                             const float out = lane == 0 ? gm : lane == 1 ? __int_as_float(gmi)
                                             : lane == 2 ? rm : __int_as_float(rmi);
-                            st_gran(ws.LG(s) + 4 * (w < 4 ? 4 * j + w : 64) + lane, tag, out);
+                            sh.pk[w][lane] = out;   // (published by wave 7)
                         }
                     }
                 }
-                __syncthreads();   // operands consumed before the next sequence writes them
+                bar_nf();
+                if (w == 7) {   // this slice's logits granules: 16 x 4 rows (+ the EOS row on the last slice)
+                    const bool eos = j == NF - 1;
+                    if (!fused) {
+                        if (lane < 16) {
+#pragma unroll
+                            for (int ww = 0; ww < 4; ++ww) st_gran(ws.LG(s) + j * LROWS + 16 * ww + lane, tag, sh.pk[ww][lane]);
+                        } else if (lane == 16 && eos) {
+                            st_gran(ws.LG(s) + 1024, tag, sh.pk[4][0]);
+                        }
+                    } else if (lane < 16 || (lane < 20 && eos)) {
+                        const int ww = lane >> 2, k = lane & 3;
+                        st_gran(ws.LG(s) + 4 * (ww < 4 ? 4 * j + ww : 64) + k, tag, sh.pk[ww][k]);
+                    }
+                }
+                bar_nf();   // operands consumed before the next sequence writes them
             }
         }
     }
