@@ -1,12 +1,13 @@
 """Build libgenie_engine.so (gfx950) in-tree with hipcc.
 
 One shared library, no torch dependency: C ABI in include/genie_engine.h.
-Objects are rebuilt when their source (or any header) is newer.
+Objects are rebuilt when their source, a .hip it includes, or any header is newer.
 """
 from __future__ import annotations
 
 import glob
 import os
+import re
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -39,9 +40,19 @@ def build(verbose: bool = False, force: bool = False) -> str:
     hdr = _headers_mtime()
     cc = _hipcc()
 
+    def src_mtime(src):
+        # a .hip that includes another .hip (t2s_persist1m.hip) is stale when the included one changes
+        t = os.path.getmtime(src)
+        with open(src) as f:
+            for line in f:
+                m = re.match(r'\s*#include\s+"([^"]+\.hip)"', line)
+                if m:
+                    t = max(t, os.path.getmtime(os.path.join(CSRC, m.group(1))))
+        return t
+
     def compile_one(src):
         obj = os.path.join(LIB_DIR, "obj", os.path.basename(src) + ".o")
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr):
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(src_mtime(src), hdr):
             return obj
         cmd = [cc, *FLAGS, "-c", src, "-o", obj]
         if verbose:

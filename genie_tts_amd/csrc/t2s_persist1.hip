@@ -1381,7 +1381,7 @@ __device__ bool seq_runs(const PersistArgs& a, const WsSeq& base, int s, int b, 
         if (tid >= b && tid < a.B && ((live >> tid) & 1ull) && sh.m.kstep[tid] != s) {
             const WsSeq ws = base.seq(tid);
             const u64 g = ld_rlxu64(ws.TK(s));
-            if ((unsigned)(g >> 32) == ws.tag(s)) take_tk((unsigned)g, tid, s, seenq, sh);
+            if ((unsigned)g == ws.tag(s)) take_tk((unsigned)(g >> 32), tid, s, seenq, sh);   // {tag, value}
         }
         bar_nf();
         if (sh.m.kstep[b] != s) {
