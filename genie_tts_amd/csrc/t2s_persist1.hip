@@ -221,6 +221,16 @@ struct Shared1 {
         }                                                                                 \
     } while (0)
 
+// threadIdx.x as a value the compiler cannot see through: the lane-derived LDS / ring
+// offsets of a pass are recomputed from it (a few VALU operations) instead
+// of hoisted out of the layer / sequence loops and spilled (a chain of dependent scratch reloads
+// costs ~1 us per pass)
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // A workgroup barrier without __syncthreads' memory fence: LDS writes are complete
 // (lgkmcnt(0)) but in-flight global stores are not waited for.  The multi-sequence
 // kernel's waves publish write-through granules and go on with the next sequence; a
@@ -271,6 +281,10 @@ __device__ __forceinline__ void ln_row_stats(const float* buf, float& mean, floa
     const float q = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[1]), 63)) * (1.0f / 512.0f);
     mean = c + d;
     rden = __builtin_amdgcn_rsqf(fmaxf(q - d * d, 0.f) + 1e-5f);   // 1 / sqrt(var + eps), v_rsq_f32
+}
+
+__device__ __forceinline__ float ln_apply(float v, float mean, float rden, float w, float b) {
+    return (v - mean) * rden * w + b;
 }
 
 // Batch-1 GEMV on the 16x16x32 f16 MFMA (v_mfma_f32_16x16x32_f16).  The weights
@@ -679,7 +693,7 @@ __device__ __forceinline__ bool form_x(const PersistArgs& a, const W& ws, int s,
     const float v = sh.lnb[0][tid];
     float mean, rden;
     ln_row_stats(sh.lnb[0], mean, rden);
-    xv = (v - mean) * rden * lp2[512 + tid] + lp2[1024 + tid];
+    xv = ln_apply(v, mean, rden, lp2[512 + tid], lp2[1024 + tid]);
     return true;
 }
 
@@ -1146,6 +1160,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
         }
         if (logits) {
             const bool probe = a.trace && s == 8;   // step-end trace (tools/knob_sweep.py)
+            const int lane = opaque_tid() & 63;   // (the row / LDS offsets below: no spilled copies)
             STAMP1(0);
             // ---- logits rows (ar_predict_layer, no bias) of x_24 = LN2_23(h1_23 + b2 + sum PF_23)
             // on the MFMA, the LN2 folded through the rows as in form_u: wave w < 4 -> rows
@@ -1233,8 +1248,8 @@ struct WsSeq {   // one sequence's view of the multi-sequence ring: Ws1's interf
     int nb, b;
     __device__ u64* slot(int s) const { return ring + (long)(s % RING1) * slot_u64; }
     __device__ unsigned tag(int s) const { return (epoch << 12) | (unsigned)(s + 1); }
-    __device__ int PA(int s, int l, int h) const {
-        return (int)(((long)(s % RING1) * slot_u64 + ((long)(l * nb + b) * 16 + h) * Ws1::ROW) * 8);
+    __device__ int PA(int s, int l, int h) const {   // rows 0..15: head partials; 16: x_l
+        return (int)(((long)(s % RING1) * slot_u64 + ((long)(l * nb + b) * 17 + h) * Ws1::ROW) * 8);
     }
     __device__ int PFH(int s, int l, int j) const {
         return (int)(((long)(s % RING1) * slot_u64 + oPFH + ((long)(l * nb + b) * 17 + j) * Ws1::ROW) * 8);
@@ -1244,12 +1259,13 @@ struct WsSeq {   // one sequence's view of the multi-sequence ring: Ws1's interf
     __device__ u64* TK(int s) const { return slot(s) + oTK + b; }
     __device__ WsSeq seq(int bb) const { WsSeq r = *this; r.b = bb; return r; }
 };
-// ring layout per step slot for nb sequences: PA [24][nb][16][GQ], PFH [24][nb][17][GQ]
-// (16-byte granules), LG [nb][PERSIST_LGS], TK [64] (8-byte granules); < 2^31 bytes at nb = 64
-inline long wsm_oPFH(int nb) { return 24L * nb * 16 * Ws1::ROW; }
-inline long wsm_oLG(int nb) { return wsm_oPFH(nb) + 24L * nb * 17 * Ws1::ROW; }
-inline long wsm_oTK(int nb) { return wsm_oLG(nb) + (long)nb * PERSIST_LGS; }
-inline long wsm_slot(int nb) { return wsm_oTK(nb) + MB; }
+// ring layout per step slot for nb sequences: PA [24][nb][17][GQ] (16 head partials + x_l),
+// PFH [24][nb][17][GQ] (16-byte granules), LG [nb][PERSIST_LGS], TK [64] (8-byte granules);
+// < 2^31 bytes at nb = 64
+__host__ __device__ inline long wsm_oPFH(int nb) { return 24L * nb * 17 * Ws1::ROW; }
+__host__ __device__ inline long wsm_oLG(int nb) { return wsm_oPFH(nb) + 24L * nb * 17 * Ws1::ROW; }
+__host__ __device__ inline long wsm_oTK(int nb) { return wsm_oLG(nb) + (long)nb * PERSIST_LGS; }
+__host__ __device__ inline long wsm_slot(int nb) { return wsm_oTK(nb) + MB; }
 
 // Per-sequence state into LDS (thread b < nb).
 __device__ __forceinline__ void init_m(const PersistArgs& a, Shared1& sh) {
@@ -1281,22 +1297,38 @@ __device__ __forceinline__ u64m live_mask(const Shared1& sh, int nb) {
 // write-through round trip (~1 us) on every sequence.
 __device__ __forceinline__ bool is_pub_wave(int w) { return w == 3 || w == 7; }
 
+
 // The 512 partial columns the 8 waves staged in sh.pk (column c at flat index c) leave
-// as the row's GQ granules at byte offset `row`, stored by waves 3 and 7 (88 each).
+// as the row's GQ granules at byte offset `row`, stored by waves 3 and 7 (88 each: two
+// stores per lane); wave 7's idle lanes 40..50 of the second store carry the 11
+// granules of the 32-column block in sh.h1s to byte offset blk (the FFN: its h1 block;
+// attention: its block of x_l).  Every operand is read and held in registers before
+// the first store: a spill reload after an sc1 store waits for it (~1 us).
 template <class W>
-__device__ __forceinline__ void pub_all(const W& ws, Shared1& sh, int row, unsigned tag, int w, int lane) {
+__device__ __forceinline__ void pub_all(const W& ws, Shared1& sh, int row, unsigned tag, int w, int lane, int blk) {
     bar_nf();
     if (is_pub_wave(w)) {
         const float* pk = &sh.pk[0][0];
-        const int base = w == 3 ? 0 : 88;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int q = base + 64 * k + lane;
-            if (k == 0 || lane < 24) {
-                const int c = gq_col(q, 0);
-                st_g16(ws, row + 16 * q, tag, pk[c], pk[c + 1], gq_n(q) == 2 ? 0.f : pk[c + 2]);
-            }
+        const int q0 = (w == 3 ? 0 : 88) + lane, q1 = q0 + 64;
+        const int c0 = gq_col(q0, 0);
+        float a0 = pk[c0], a1 = pk[c0 + 1], a2 = gq_n(q0) == 2 ? 0.f : pk[c0 + 2];
+        float b0 = 0.f, b1 = 0.f, b2 = 0.f;
+        int o0 = row + 16 * q0, o1 = row + 16 * q1;
+        bool second = lane < 24;
+        if (second) {
+            const int c1 = gq_col(q1, 0);
+            b0 = pk[c1]; b1 = pk[c1 + 1]; b2 = gq_n(q1) == 2 ? 0.f : pk[c1 + 2];
         }
+        if (w == 7 && lane >= 40 && lane < 51) {
+            const int r = lane - 40;
+            const float* p = sh.h1s + 3 * r;
+            b0 = p[0]; b1 = p[1]; b2 = r == 10 ? 0.f : p[2];
+            o1 = blk + 16 * r;
+            second = true;
+        }
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(o0), "+v"(o1));
+        st_g16(ws, o0, tag, a0, a1, a2);
+        if (second) st_g16(ws, o1, tag, b0, b1, b2);
     }
 }
 
@@ -1447,18 +1479,22 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
         for (int l = grp; l < 24; l += ng) {
             for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1)) {
                 const WsSeq ws = base.seq(b);
+                const int tid = opaque_tid(), lane = tid & 63;
                 if (l == grp && s > 0 && !seq_runs(a, base, s, b, live, grp == 0, fused, publisher, nullptr, sh)) {
                     if (sh.fail) return;
                     live &= ~(1ull << b);   // finished: skipped from here on (by every workgroup)
                     continue;
                 }
-                const bool probe = a.trace && s == 8 && l == grp && b < 8;   // tools/ptrace_multi.py
+                const bool probe = a.trace && s == 8 && l == grp && b < 4;   // tools/ptrace_multi.py
+                const bool pd = probe && b == 1;
+#define MSTAMP(k) if (pd && tid == 0) sh.stamp[k] = __builtin_amdgcn_s_memrealtime()
                 const unsigned long long t_in = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 const int kv = sh.m.kv0[b] + s;
                 if (staged != l * MB + b) {   // (a sequence that finished took the stage's turn)
                     stage_kv(a, sh, l, b, h, kv, w, lane);
                     staged = l * MB + b;
                 }
+                MSTAMP(0);
                 if (!form_u<WsSeq, true>(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], sh, sh.m.tok[b],
                                          b == next_live(live, 0)))
                     return;
@@ -1478,6 +1514,11 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                             c1 = mfma16(af[i + 1], bfrag(wq[cb + i + 1]), c1);
                         }
                     }
+                    if (w == 0 && lane < 32) {   // x_l block h (form_x's arithmetic) for the FFN's PA row 16
+                        const int c = 32 * h + lane;
+                        sh.h1s[lane] = l > 0 ? ln_apply(sh.lnb[0][c], mean, rden, sh.p2[1][c], sh.p2[2][c])
+                                             : sh.lnb[0][c];
+                    }
                     mean = l > 0 ? mean : 0.f;
                     rden = l > 0 ? rden : 1.f;
                     if (lane < 16) {
@@ -1489,8 +1530,10 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                         }
                     }
                 }
+                MSTAMP(1);
                 if (!is_pub_wave(w)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its K/V LDS-DMA landed
                 bar_nf();
+                MSTAMP(2);
                 const long kvoff = (long)b * a.sstride + (long)h * a.tmax * 32;
                 float* Kw = a.kc[l] + kvoff;
                 float* Vw = a.vc[l] + kvoff;
@@ -1516,7 +1559,9 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                         staged = l * MB + bn;
                     }
                     merge_waves1(sh, w, lane);
+                    MSTAMP(3);
                 } else {
+                    MSTAMP(3);
                     attn_general1<1>(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, g, w, lane, tid);
                     bar_nf();
                     if (bn >= 0) {
@@ -1533,7 +1578,9 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
 #pragma unroll
                         for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
                     }
-                    pub_all(ws, sh, ws.PA(s, l, h), tag, w, lane);
+                    MSTAMP(4);
+                    pub_all(ws, sh, ws.PA(s, l, h), tag, w, lane, ws.PA(s, l, 16) + 16 * 11 * h);
+                    MSTAMP(5);
                     if (w == 7) {   // the new K/V row (read by this workgroup only, next step)
                         if (lane < 32) Kw[(long)kv * 32 + lane] = sh.qkv[32 + lane];
                         else Vw[(long)kv * 32 + lane - 32] = sh.qkv[64 + lane - 32];
@@ -1543,6 +1590,8 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                 if (probe && tid == 0) {
                     a.trace[blockIdx.x * 16 + 2 * b] = t_in;
                     a.trace[blockIdx.x * 16 + 2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+                    if (pd)
+                        for (int k = 0; k < 8; ++k) a.trace[blockIdx.x * 16 + 8 + k] = sh.stamp[k];
                 }
             }
             // ---- next owned layer (this step) or the first one of the next step
@@ -1685,40 +1734,47 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
         for (int l = grp; l < 24; l += ng) {
             for (int b = next_live(live, 0); b >= 0; b = next_live(live, b + 1)) {
                 const WsSeq ws = base.seq(b);
+                const int tid = opaque_tid(), lane = tid & 63;
                 if (l == grp && s > 0 &&
                     !seq_runs(a, base, s, b, live, grp == 0, fused, false, logits && fused ? sh.ff.seenq : nullptr, sh)) {
                     if (sh.fail) return;
                     live &= ~(1ull << b);
                     continue;
                 }
-                const bool probe = a.trace && s == 8 && l == grp && b < 8;   // tools/ptrace_multi.py
+                const bool probe = a.trace && s == 8 && l == grp && b < 4;   // tools/ptrace_multi.py
+                const bool pd = probe && b == 1;
                 const unsigned long long t_in = probe ? __builtin_amdgcn_s_memrealtime() : 0ull;
-                float xv;
-                if (!form_x<WsSeq, true>(a, ws, s, l, sh.m.ny0[b] + s, &sh.p2[0][0], xv, sh, sh.m.tok[b],
-                                         b == next_live(live, 0)))
-                    return;
                 {
                     bool ok = true;
+                    // the first live sequence: a sleeping lane waits for the layer's attention
+                    // input (the head partials follow about one pass later), then all poll
+                    if (b == next_live(live, 0)) {
+                        if (tid == 0) wait_tag16_slow(ws.at(l > 0 ? ws.PFH(s, l - 1, 0) : ws.PA(s, 0, 0)), tag, a.err,
+                                                      ok, a.spin_ticks);
+                        if (!block_ok_t<true>(ok, sh)) return;
+                    }
+                    MSTAMP(0);
                     constexpr int RB = (int)Ws1::ROW * 8;
                     const int q = tid & 255, off = ws.PA(s, l, 0) + 16 * q;
-                    sh.ff.xr[tid] = xv;
                     sh.ff.bo[tid] = bo;
                     sh.ff.n1w[tid] = n1w;
-                    u32x4 g[8];
+                    u32x4 g[9];   // (second half: rows 8..15 and x_l)
                     if (tid < GQ) {
-                        wait_g16_n<8>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
-                        float f0 = __uint_as_float(g[0].y), f1 = __uint_as_float(g[0].z), f2 = __uint_as_float(g[0].w);
+                        u32x4 h8[8];
+                        wait_g16_n<8>(ws, off, RB, tag, h8, a.err, ok, a.spin_ticks);
+                        float f0 = __uint_as_float(h8[0].y), f1 = __uint_as_float(h8[0].z), f2 = __uint_as_float(h8[0].w);
 #pragma unroll
                         for (int r = 1; r < 8; ++r) {
-                            f0 += __uint_as_float(g[r].y);
-                            f1 += __uint_as_float(g[r].z);
-                            f2 += __uint_as_float(g[r].w);
+                            f0 += __uint_as_float(h8[r].y);
+                            f1 += __uint_as_float(h8[r].z);
+                            f2 += __uint_as_float(h8[r].w);
                         }
                         sh.hs[3 * q] = f0; sh.hs[3 * q + 1] = f1; sh.hs[3 * q + 2] = f2;
                     } else if (tid >= 256 && q < GQ) {
-                        wait_g16_n<8>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+                        wait_g16_n<9>(ws, off + 8 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
                     }
                     if (!block_ok_t<true>(ok, sh)) return;
+                    MSTAMP(1);
                     if (tid >= 256 && q < GQ) {
 #pragma unroll
                         for (int k = 0; k < 3; ++k) {
@@ -1727,7 +1783,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
 #pragma unroll
                             for (int r = 0; r < 8; ++r) sum += __uint_as_float(g[r][1 + k]);
                             const int c = gq_col(q, k);
-                            const float vc = sh.ff.xr[c] + (sh.ff.bo[c] + sum);
+                            const float vc = __uint_as_float(g[8][1 + k]) + (sh.ff.bo[c] + sum);
                             sh.lnb[1][c] = vc;
                             const float un = vc * sh.ff.n1w[c];
                             if (!split_h(un, sh.xh[c], sh.xl[c]) || !(fabsf(un) < a.f16_limit)) {
@@ -1738,6 +1794,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                     }
                     if (!block_ok_t<true>(ok, sh)) return;
                 }
+                MSTAMP(6);
                 const float v = sh.lnb[1][tid];
                 {
                     const _Float16* ab = abase(sh.xh, sh.xl, lane);
@@ -1755,6 +1812,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                             c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
                         }
                     }
+                    MSTAMP(7);
                     const float h1_pub = (v - mean) * rden * n1w + n1b;
                     if ((tid >> 5) == j) sh.h1s[tid & 31] = h1_pub;
                     if (lane < 16) {
@@ -1767,6 +1825,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
                     }
                 }
                 bar_nf();
+                MSTAMP(2);
                 if (sh.fail) return;
                 {
                     f32x4 acc[4];
@@ -1784,18 +1843,20 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
 #pragma unroll
                         for (int t = 0; t < 4; ++t) sh.pk[w][16 * t + lane] = acc[t][0] + acc[t][1];
                     }
-                    pub_all(ws, sh, ws.PFH(s, l, j), tag, w, lane);
-                }
-                if (w == 7 && lane >= 40 && lane < 51) {   // h1 block j (11 granules; staged before FFN1's barrier)
-                    const int q = lane - 40;
-                    const float* p = sh.h1s + 3 * q;
-                    st_g16(ws, ws.PFH(s, l, 16) + 16 * (11 * j + q), tag, p[0], p[1], q == 10 ? 0.f : p[2]);
+                    MSTAMP(3);
+                    // with h1 block j (11 granules; staged before FFN1's barrier)
+                    pub_all(ws, sh, ws.PFH(s, l, j), tag, w, lane, ws.PFH(s, l, 16) + 16 * 11 * j);
+                    MSTAMP(4);
                 }
                 bar_nf();   // operands consumed before the next sequence writes them
+                MSTAMP(5);
                 if (probe && tid == 0) {
                     a.trace[blockIdx.x * 16 + 2 * b] = t_in;
                     a.trace[blockIdx.x * 16 + 2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+                    if (pd)
+                        for (int k = 0; k < 8; ++k) a.trace[blockIdx.x * 16 + 8 + k] = sh.stamp[k];
                 }
+#undef MSTAMP
             }
             pf_wait(a.pf_delay);
             prefetch(l + ng < 24 ? l + ng : grp);
@@ -1874,10 +1935,10 @@ __global__ __launch_bounds__(PT) void k_decode_persist1m(PersistArgs a) {
     ws.rs = __builtin_amdgcn_make_buffer_rsrc(a.ring, 0, 0x7fffffff, 0x00020000);
     ws.nb = a.B;
     ws.b = 0;
-    ws.oPFH = 24L * a.B * 16 * Ws1::ROW;
-    ws.oLG = ws.oPFH + 24L * a.B * 17 * Ws1::ROW;
-    ws.oTK = ws.oLG + (long)a.B * PERSIST_LGS;
-    ws.slot_u64 = ws.oTK + MB;
+    ws.oPFH = wsm_oPFH(a.B);
+    ws.oLG = wsm_oLG(a.B);
+    ws.oTK = wsm_oTK(a.B);
+    ws.slot_u64 = wsm_slot(a.B);
     const int grp = blockIdx.x / GW, r = blockIdx.x - grp * GW;
     if (r < 16) run_attn_m(a, ws, sh, grp, r);
     else run_ffn_m(a, ws, sh, grp, r - 16);

@@ -1,7 +1,11 @@
 """Per-sequence timeline of the multi-sequence persistent decode (k_decode_persist1m): B = 8
 copies of the bench utterance, step 8; for each layer group's attention / FFN workgroups
-(first owned layer = the group index) the start and end of each sequence's pass, in us
-from the first stamp.  Usage: python tools/ptrace_multi.py [B]"""
+(first owned layer = the group index) the start and end of sequences 0..3's passes, then
+the phase stamps of sequence 1's pass (attention: stage checked, x formed, q/k/v + K/V
+landed, attention merged, before / after publishing; FFN: x formed, head partials summed,
+FFN1 done, before / after publishing, end, LN1 input formed, FFN1 MFMA done), in us from
+the first stamp.
+Usage: python tools/ptrace_multi.py [B]"""
 import sys
 sys.path.insert(0, ".")
 import numpy as np
@@ -27,6 +31,8 @@ us = lambda x: (x - t0) * 10 / 1000.0
 for g in range(G):
     for role, off in (("attn", 0), ("ffn", 16)):
         rows = tr[32 * g + off: 32 * g + off + 16]
-        st = [us(np.median(rows[:, 2 * b])) for b in range(min(B, 8))]
-        en = [us(np.median(rows[:, 2 * b + 1])) for b in range(min(B, 8))]
-        print(f"group {g} {role:4s} " + " ".join(f"[{a:7.2f} {z:7.2f}]" for a, z in zip(st, en)))
+        st = [us(np.median(rows[:, 2 * b])) for b in range(min(B, 4))]
+        en = [us(np.median(rows[:, 2 * b + 1])) for b in range(min(B, 4))]
+        ph = [us(np.median(rows[:, 8 + k])) for k in range(8 if role == "ffn" else 6)]
+        print(f"group {g} {role:4s} " + " ".join(f"[{a:7.2f} {z:7.2f}]" for a, z in zip(st, en))
+              + "  seq1: " + " ".join(f"{p:7.2f}" for p in ph))
