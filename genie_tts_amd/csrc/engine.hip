@@ -888,11 +888,11 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     return 0;
 }
 
-// B = 1: the single-sequence kernel; B = 2..56: its multi-sequence form (the live
-// sequences one after another through each layer's workgroups).  Above 56 the per-step
-// graphs are faster (tools/batch_sweep.py --compare, profiles/r03h_batch_sweep.json:
-// 56 sequences 128 vs 135 ms, 64 sequences 151 vs 143 ms per 81-step generate).
-constexpr int PERSIST1M_MAX_B = 56;
+// B = 1: the single-sequence kernel; B = 2..64: its multi-sequence form (the live
+// sequences one after another through each layer's workgroups), faster than the
+// per-step graphs at every batch size (tools/batch_sweep.py --compare,
+// profiles/r03i_batch_sweep.json).
+constexpr int PERSIST1M_MAX_B = 64;
 bool gsv_engine::persist_family(int B) const {
     return use_persist1 && decode_cus() >= persist1_grid(3) &&
            (B == 1 || (use_persist1m && B <= std::min(PERSIST1M_MAX_B, persist1m_max_batch())));

@@ -152,7 +152,7 @@ def _alone(eng, inps, sp):
     return [eng.t2s_generate([inp], sp)[0].tolist() for inp in inps]
 
 
-@pytest.mark.parametrize("B", [2, 5, 8, 16, 40])
+@pytest.mark.parametrize("B", [2, 5, 8, 16, 40, 64])
 def test_multi_sequence_matches_single_launches(eng, B):
     """The multi-sequence form of the single-sequence kernel (k_decode_persist1m, B = 2..64)
     runs every sequence through the same per-sequence arithmetic: each sequence's greedy
