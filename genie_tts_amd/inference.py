@@ -231,8 +231,8 @@ class GENIE:
         utts = [(prompt_audio.phonemes_seq, it[0], prompt_audio.text_bert, it[1], ssl,
                  it[2] if len(it) > 2 else 0) for it in items]
         # one generate for the whole batch: the engine's multi-sequence persistent decode
-        # (B <= 56) costs ~1.2 ms per extra sequence over a single one
-        # (profiles/r03h_batch_sweep.json), so splitting never pays
+        # (B <= 64) costs ~2 ms per extra sequence over a single one
+        # (profiles/r03i_batch_sweep.json), so splitting never pays
         return model.ENGINE.t2s_generate(utts, sampler)
 
     def tts_batch_vocoder(self, items: Sequence[tuple], toks, prompt_audio: ReferenceAudio, model,

@@ -47,8 +47,8 @@ def _resolve(spec: Optional[str]):
 def round_size(ready: int) -> int:
     """Sentences a worker round takes out of `ready` of one character: all of them, up to
     MAX_BATCH.  The T2S time per batch grows monotonically and slowly with B
-    (tools/batch_sweep.py, profiles/r03h_batch_sweep.json: 16.6 ms at 1, 26 ms at 8,
-    72 ms at 32, 143 ms at 64 per 81-step generate), so a round never waits."""
+    (tools/batch_sweep.py, profiles/r03i_batch_sweep.json: 16.7 ms at 1, 27 ms at 8,
+    69 ms at 32, 129 ms at 64 per 81-step generate), so a round never waits."""
     return min(ready, MAX_BATCH)
 
 
