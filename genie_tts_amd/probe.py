@@ -46,17 +46,21 @@ def persist_algorithmic_bytes(n0: int, steps: int, B: int = 1) -> int:
     return sum(W16 + B * (KV_ROW * (n0 + s) + KV_ROW) for s in range(steps))
 
 
+# The translation unit k_decode_persist1 is compiled from: its HBM traffic depends on
+# these files only, so a PMC count stays valid while other kernels change.
+DECODE_TU = ("t2s_persist1.hip", "common.h", "kernels.h", "sampler.h", "persist.h")
+
+
 def kernel_source_sha() -> str:
-    """sha256 (16 hex) over the engine's HIP sources and headers: identifies the
-    kernel build a PMC measurement belongs to."""
-    import glob
+    """sha256 (16 hex) over the decode kernel's translation unit (DECODE_TU):
+    identifies the kernel build a PMC measurement belongs to."""
     import hashlib
     import os
     csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
-        h.update(os.path.basename(f).encode())
-        h.update(open(f, "rb").read())
+    for f in DECODE_TU:
+        h.update(f.encode())
+        h.update(open(os.path.join(csrc, f), "rb").read())
     return h.hexdigest()[:16]
 
 
