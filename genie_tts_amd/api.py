@@ -86,6 +86,13 @@ def load_roberta(model=None) -> None:
     model_manager.load_roberta_model(model)
 
 
+def load_sv_model(model=None) -> None:
+    """Speaker-verification weights (V2ProPlus sv_emb): GenieData speaker_encoder.onnx
+    (or its directory) or a dict of arrays (weights.sv_spec names); runs on the engine
+    (gsv_sv).  `g/ModelManager.py:155-170`."""
+    model_manager.load_sv_model(model)
+
+
 def set_sv_extractor(fn: Optional[Callable]) -> None:
     """fn(audio_16k f32 [1,N]) -> sv_emb f32 [1,20480] (the reference's speaker-verification session)."""
     global _sv_extractor
@@ -203,13 +210,27 @@ def _sentences(text, split_sentence: bool) -> List:
     return [np.asarray(text, np.int64)]               # phoneme ids: one utterance
 
 
+def _ensure_sv_emb(m, ref) -> None:
+    """V2ProPlus: the reference clip's speaker embedding, once per clip
+    (ReferenceAudio.update_global_emb, `g/Audio/ReferenceAudio.py:68-76`): a plugged
+    extractor, else the engine's SV model (load_sv_model() or $SV_MODEL_PATH)."""
+    if m.PROMPT_ENCODER is None or ref.sv_emb is not None:
+        return
+    if getattr(ref, "sv_fn", None) is not None:
+        ref.sv_emb = np.asarray(ref.sv_fn(ref.audio_16k), np.float32).reshape(1, -1)
+    elif getattr(ref, "audio_16k", None) is not None and (model_manager.speaker_verification_model is not None
+                                                          or os.getenv("SV_MODEL_PATH")):
+        model_manager.load_sv_model()
+        sv = model_manager.speaker_verification_model.run(None, {"waveform": ref.audio_16k})[0]
+        ref.sv_emb = np.asarray(sv, np.float32).reshape(1, -1)
+
+
 def _synthesize(character_name: str, sentence, text_bert=None, sampler=None) -> np.ndarray:
     m = model_manager.get(character_name)
     if m is None:
         raise ValueError(f"character '{character_name}' is not loaded")
     ref = _reference_audios[character_name]
-    if m.PROMPT_ENCODER is not None and ref.sv_emb is None and getattr(ref, "sv_fn", None) is not None:
-        ref.sv_emb = np.asarray(ref.sv_fn(ref.audio_16k), np.float32).reshape(1, -1)
+    _ensure_sv_emb(m, ref)
     tts_client.stop_event.clear()
     return tts_client.tts(sentence, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER, m.VITS,
                           m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p, sampler=sampler)
@@ -224,8 +245,7 @@ def _synthesize_all(character_name: str, sentences: List, text_bert=None, sample
     if m is None:
         raise ValueError(f"character '{character_name}' is not loaded")
     ref = _reference_audios[character_name]
-    if m.PROMPT_ENCODER is not None and ref.sv_emb is None and getattr(ref, "sv_fn", None) is not None:
-        ref.sv_emb = np.asarray(ref.sv_fn(ref.audio_16k), np.float32).reshape(1, -1)
+    _ensure_sv_emb(m, ref)
     tts_client.stop_event.clear()
     return list(tts_client.tts_stream(sentences, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER,
                                       m.VITS, m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p,

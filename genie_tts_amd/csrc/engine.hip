@@ -71,6 +71,7 @@ gsv_engine::~gsv_engine() {
     if (pws) hipFree(pws);
     if (hubert.ws) hipFree(hubert.ws);
     if (bert.ws) hipFree(bert.ws);
+    if (sv_ws) hipFree(sv_ws);
     if (perr_host) hipHostFree(perr_host);
     if (res_pin) hipHostFree(res_pin);
     for (GenSlot& g : gq) {
@@ -1251,7 +1252,8 @@ extern "C" int gsv_finalize_weights(gsv_engine* eng) {
     if (eng->finalized) return set_error(GSV_E_STATE, "already finalized");
     const bool has_hubert = eng->find("feature_extractor.conv_layers.0.conv.weight") != nullptr;
     const bool has_roberta = eng->find("embeddings.word_embeddings.weight") != nullptr;
-    if (!(has_hubert || has_roberta) || eng->find("ar_audio_embedding.word_embeddings.weight")) {
+    const bool has_sv = eng->find("layer3_ds.weight") != nullptr;
+    if (!(has_hubert || has_roberta || has_sv) || eng->find("ar_audio_embedding.word_embeddings.weight")) {
         if (int e = eng->finalize_t2s()) return e;
     }
     if (has_hubert) {   // CN-HuBERT (a GenieData model, usually an engine of its own)
@@ -1259,6 +1261,9 @@ extern "C" int gsv_finalize_weights(gsv_engine* eng) {
     }
     if (has_roberta) {  // RoBERTa (GenieData, Chinese BERT features)
         if (int e = eng->finalize_roberta()) return e;
+    }
+    if (has_sv) {       // speaker verification (GenieData speaker_encoder, V2ProPlus sv_emb)
+        if (int e = eng->finalize_sv()) return e;
     }
     if (eng->find("vq_model.dec.conv_pre.weight")) {
         if (int e = eng->finalize_vits()) return e;

@@ -58,6 +58,24 @@ struct BertWeights {
     float* ws = nullptr;
     size_t ws_floats = 0;
 };
+// Speaker verification (sv.hip): ERes2NetV2 convs, BatchNorm folded, weights [co][tap][ci] f32
+struct SvConv {
+    float *w = nullptr, *b = nullptr;
+    int cin = 0, cout = 0, k = 1;
+};
+struct SvBlock {
+    SvConv conv1, convs[4], conv3, sc, aff_a[3], aff_b[3];
+    int width = 0, stride = 1;
+    bool aff = false, has_sc = false;
+};
+struct SvWeights {
+    bool ready = false;
+    float *stem_w = nullptr, *stem_b = nullptr;     // conv1 (1 -> 64, 3x3) + bn1 folded
+    std::vector<SvBlock> blocks;                     // layer1..4: 3 + 4 + 6 + 3
+    SvConv ds34, fuse_a, fuse_b;                     // layer3_ds, fuse34 local_att convs
+    float *win = nullptr, *cos_tab = nullptr, *banks = nullptr;   // fbank tables
+};
+int sv_frames(int n_samples);
 }  // namespace gsv
 
 struct gsv_engine {
@@ -112,6 +130,9 @@ struct gsv_engine {
     gsv::PromptEncWeights penc;
     gsv::HubertWeights hubert;
     gsv::BertWeights bert;
+    gsv::SvWeights sv;
+    float* sv_ws = nullptr;           // SV workspace (grown per call)
+    size_t sv_ws_n = 0;
 
     std::map<std::string, hipGraphExec_t> graphs;
     bool timing = false;
@@ -162,6 +183,10 @@ struct gsv_engine {
     float* hubert_ws(size_t floats);
     int hubert_forward(const float* audio, int n, float* out, hipStream_t st);
     int finalize_roberta();
+    int finalize_sv();
+    int sv_conv_upload(const std::string& wname, const std::string& bname, const std::string& bn, gsv::SvConv* c);
+    size_t sv_ws_floats(int frames);
+    int sv_forward(const float* wav, int n, float* out, hipStream_t st);
     // RoBERTa over N token rows; rows[n_out]: the token row of each output row.  Packed
     // sentences: row_pos (host [N], position within its sentence) and row_seg (host [N][2],
     // {first row, rows} of its sentence), else one sentence.

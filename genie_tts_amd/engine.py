@@ -120,6 +120,8 @@ def lib():
         L.gsv_get_counter.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
         L.gsv_hubert_frames.argtypes = [ctypes.c_int32]
         L.gsv_hubert.argtypes = [vp, vp, ctypes.c_int32, vp, vp]
+        L.gsv_sv_frames.argtypes = [ctypes.c_int32]
+        L.gsv_sv.argtypes = [vp, vp, ctypes.c_int32, vp, vp]
         L.gsv_roberta.argtypes = [vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
         L.gsv_roberta_batch.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
         _lib = L
@@ -133,7 +135,8 @@ EXPORTED = (
     "gsv_set_timing", "gsv_get_timing", "gsv_debug_copy", "gsv_debug_conv1d",
     "gsv_probe", "gsv_get_kernel_timing", "gsv_debug_sample", "gsv_debug_ktrace",
     "gsv_set_option", "gsv_debug_ptrace", "gsv_debug_conv1d_h", "gsv_vits_decode_batch",
-    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_roberta", "gsv_vits_decode_async",
+    "gsv_get_counter", "gsv_hubert", "gsv_hubert_frames", "gsv_sv", "gsv_sv_frames", "gsv_roberta",
+    "gsv_vits_decode_async",
     "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
     "gsv_vits_decode_batch_async", "gsv_vits_batch_wait", "gsv_ref_encode", "gsv_roberta_batch",
 )
@@ -522,6 +525,16 @@ class Engine:
             raise EngineError(f"audio of {a.numel()} samples is too short for CN-HuBERT")
         out = t.empty((768, T), dtype=t.float32, device=self.dev)
         _check(lib().gsv_hubert(self.h, _ptr(a), a.numel(), _ptr(out), _stream()), "gsv_hubert")
+        return out
+
+    def sv(self, audio_16k):
+        """Speaker verification (gsv_sv): 16 kHz audio [N] -> sv_emb [1, 20480] on the device."""
+        t = self.torch
+        a = self._dev(audio_16k, t.float32).reshape(-1)
+        if lib().gsv_sv_frames(a.numel()) < 1:
+            raise EngineError(f"audio of {a.numel()} samples is too short for the SV fbank (400 needed)")
+        out = t.empty((1, 20480), dtype=t.float32, device=self.dev)
+        _check(lib().gsv_sv(self.h, _ptr(a), a.numel(), _ptr(out), _stream()), "gsv_sv")
         return out
 
     def roberta(self, input_ids, repeats, attention_mask=None):

@@ -73,6 +73,7 @@ class ModelManager:
         self.vits_noise = "philox"       # z_p noise of new characters' vocoders ("zero": deterministic tests)
         self.cn_hubert = None            # HubertSession (ModelManager.py:127,172-195)
         self.roberta = None              # RobertaSession (ModelManager.py:129,132-150)
+        self.speaker_verification_model = None   # SvSession (ModelManager.py:128,155-170)
 
     def _put(self, name: str, model: GSVModel) -> None:
         self.character_to_model[name] = model
@@ -136,6 +137,27 @@ class ModelManager:
         self.roberta = RobertaSession(Engine({"roberta": w}, "v2", device=self.device))
         logger.info("RoBERTa loaded")
         return True
+
+    def load_sv_model(self, model: Union[str, Dict[str, np.ndarray], None] = None) -> bool:
+        """Speaker verification on its own engine (`g/ModelManager.py:155-170`): `model`
+        is GenieData's speaker_encoder.onnx (or its directory) or in-memory weights
+        (sv_spec names); default: $SV_MODEL_PATH."""
+        if self.speaker_verification_model is not None:
+            return True
+        from .sessions import SvSession
+        if model is None:
+            model = os.getenv("SV_MODEL_PATH")
+            if not model:
+                raise FileNotFoundError("SV model: pass speaker_encoder.onnx or weights, or set SV_MODEL_PATH")
+        w = W.load_sv_weights(model) if isinstance(model, (str, os.PathLike)) else model
+        self.speaker_verification_model = SvSession(Engine({"sv": w}, "v2", device=self.device))
+        logger.info("Speaker Verification model loaded")
+        return True
+
+    def unload_sv_model(self) -> None:
+        if self.speaker_verification_model is not None:
+            self.speaker_verification_model.engine.close()
+            self.speaker_verification_model = None
 
     def unload_cn_hubert(self) -> None:
         if self.cn_hubert is not None:

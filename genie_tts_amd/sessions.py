@@ -256,6 +256,17 @@ class HubertSession(_Session):
         return self._select(output_names, {"ssl_content": _np(ssl)[None]})
 
 
+class SvSession(_Session):
+    """speaker_encoder.onnx, V2ProPlus speaker verification (reference call:
+    ReferenceAudio.py:71-72): waveform = 16 kHz clip [1, N] -> sv_emb [1, 20480]."""
+    INPUTS = (NodeArg("waveform", (1, "N"), "tensor(float)"),)
+    OUTPUTS = (NodeArg("sv_emb", (1, 20480), "tensor(float)"),)
+
+    def run(self, output_names, input_feed):
+        self._need(input_feed, "waveform")
+        return self._select(output_names, {"sv_emb": _np(self.engine.sv(input_feed["waveform"]))})
+
+
 class RobertaSession(_Session):
     """RoBERTa.onnx, Chinese BERT features (reference call: GetPhonesAndBert.py:64-74):
     input_ids [1, N], attention_mask [1, N], repeats = word2ph [n_chars] ->

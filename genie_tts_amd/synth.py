@@ -84,6 +84,27 @@ def synth_weights(spec, seed: int = WEIGHT_SEED, fp16: bool = True) -> Dict[str,
     return {k: synth_tensor(k, s, seed, fp16) for k, s in spec.items()}
 
 
+def synth_sv_weights(seed: int = WEIGHT_SEED) -> Dict[str, np.ndarray]:
+    """fp32 weights for the SV model (weights.sv_spec): convs uniform with variance
+    1/fan_in; BatchNorm weight 1 +- 0.2, bias and running_mean +- 0.1, running_var
+    in [0.5, 1.5] (the real speaker_encoder.onnx ships fp32, so nothing is rounded)."""
+    out = {}
+    for name, shape in W.sv_spec().items():
+        n = int(np.prod(shape))
+        u = 2.0 * uniform01(name, n, seed) - 1.0
+        leaf = name.rsplit(".", 1)[-1]
+        if len(shape) == 4:
+            v = u * np.sqrt(3.0 / int(np.prod(shape[1:])))
+        elif leaf == "running_var":
+            v = 1.0 + 0.5 * u
+        elif leaf == "weight":
+            v = 1.0 + 0.2 * u
+        else:
+            v = 0.1 * u
+        out[name] = v.reshape(shape).astype(np.float32)
+    return out
+
+
 def synthetic_character(version: str = "v2", seed: int = WEIGHT_SEED):
     """Weights of a synthetic character in the same form `load_character_weights` returns."""
     w = {

@@ -316,6 +316,69 @@ def load_roberta_weights(model_dir: str) -> Dict[str, np.ndarray]:
     return read_initializer_values(os.path.join(model_dir, "RoBERTa.onnx"), roberta_spec())
 
 
+SV_STAGES = ((64, 3, 1, False), (128, 4, 2, False), (256, 6, 2, True), (512, 3, 2, True))
+
+
+def sv_spec() -> Spec:
+    """Speaker-verification model (GenieData speaker_encoder.onnx, V2ProPlus `sv_emb`;
+    loaded at `g/ModelManager.py:155-170`, run at `g/Audio/ReferenceAudio.py:71-72`):
+    GPT-SoVITS's ERes2NetV2(baseWidth=24, scale=4, expansion=4) state_dict names,
+    BatchNorm unfolded (weight, bias, running_mean, running_var; eps 1e-5).  Stages
+    (planes, blocks, stride, AFF) = SV_STAGES; width = floor(planes * 24 / 64).  The
+    real graph is absent: this layout is not pinned to its initializer table."""
+    s: Spec = OrderedDict()
+
+    def bn(p, c):
+        for leaf in ("weight", "bias", "running_mean", "running_var"):
+            s[f"{p}.{leaf}"] = (c,)
+
+    def aff(p, c):
+        inter = c // 4
+        s[p + ".local_att.0.weight"] = (inter, 2 * c, 1, 1)
+        s[p + ".local_att.0.bias"] = (inter,)
+        bn(p + ".local_att.1", inter)
+        s[p + ".local_att.3.weight"] = (c, inter, 1, 1)
+        s[p + ".local_att.3.bias"] = (c,)
+        bn(p + ".local_att.4", c)
+
+    s["conv1.weight"] = (64, 1, 3, 3)
+    bn("bn1", 64)
+    cin = 64
+    for li, (planes, nb, stride, use_aff) in enumerate(SV_STAGES, start=1):
+        width = planes * 24 // 64
+        for b in range(nb):
+            p = f"layer{li}.{b}"
+            st = stride if b == 0 else 1
+            s[p + ".conv1.weight"] = (width * 4, cin, 1, 1)
+            bn(p + ".bn1", width * 4)
+            for i in range(4):
+                s[p + f".convs.{i}.weight"] = (width, width, 3, 3)
+                bn(p + f".bns.{i}", width)
+            if use_aff:
+                for i in range(3):
+                    aff(p + f".fuse_models.{i}", width)
+            s[p + ".conv3.weight"] = (planes * 4, width * 4, 1, 1)
+            bn(p + ".bn3", planes * 4)
+            if st != 1 or cin != planes * 4:
+                s[p + ".shortcut.0.weight"] = (planes * 4, cin, 1, 1)
+                bn(p + ".shortcut.1", planes * 4)
+            cin = planes * 4
+    s["layer3_ds.weight"] = (2048, 1024, 3, 3)
+    aff("fuse34", 2048)
+    return s
+
+
+def load_sv_weights(path: str) -> Dict[str, np.ndarray]:
+    """GenieData speaker_encoder.onnx (`g/ModelManager.py:155-170`, plain ONNX with
+    fp32 initializers, no fp16 bin) read through the initializer table by sv_spec
+    names.  Unverified against a real file (none offline): an export that folded
+    BatchNorm into the convs under other initializer names is not readable here."""
+    from .onnx_table import read_initializer_values
+    if os.path.isdir(path):
+        path = os.path.join(path, "speaker_encoder.onnx")
+    return read_initializer_values(path, sv_spec())
+
+
 def spec_numel(spec: Spec) -> int:
     return int(sum(int(np.prod(v)) for v in spec.values()))
 

@@ -238,6 +238,17 @@ int gsv_prompt_encode(gsv_engine* eng, const float* ref_audio, int32_t n_audio,
 int gsv_hubert_frames(int32_t n_samples);
 int gsv_hubert(gsv_engine* eng, const float* audio_16k, int32_t n_samples, float* ssl_content, void* stream);
 
+/* speaker_encoder.onnx (V2ProPlus speaker verification, ReferenceAudio.py:71-72:
+ * speaker_verification_model.run(None, {'waveform': audio_16k}); session loaded at
+ * ModelManager.py:155-170): waveform = the 16 kHz reference clip (device
+ * [n_samples]) -> sv_emb (device [20480], the graph's [1, 20480] output), the
+ * prompt encoder's sv_emb input.  Kaldi fbank (80 mel bins, 25/10 ms frames,
+ * snip edges) -> ERes2NetV2 (GPT-SoVITS sv.py, baseWidth 24 / scale 4 / expansion 4)
+ * forward3.  gsv_sv_frames(n) is the fbank frame count (0: too short, GSV_E_ARG).
+ * Needs an engine whose weights include the SV tensors (weights.sv_spec names). */
+int gsv_sv_frames(int32_t n_samples);
+int gsv_sv(gsv_engine* eng, const float* audio_16k, int32_t n_samples, float* sv_emb, void* stream);
+
 /* RoBERTa.onnx (chinese-roberta-wwm-ext-large BERT features for Chinese text,
  * GetPhonesAndBert.py:64-74; session ModelManager.py:132-150): input_ids (device
  * i64 [n_tokens], CLS .. SEP), attention_mask (host i64 [n_tokens], all ones, or

@@ -1,0 +1,91 @@
+"""CPU: the SV oracle (oracle/sv.py) and the SV weight table (weights.sv_spec).
+
+The Kaldi fbank restatement is checked against a second, independent one (numpy,
+float64, direct DFT over the frame instead of torch.fft), and every sv_spec tensor
+must be read by the ERes2NetV2 restatement (and nothing else).  Parity with the
+absent speaker_encoder.onnx stays unpinned."""
+import numpy as np
+import pytest
+
+from genie_tts_amd import synth, weights as W
+from oracle import sv as S
+
+
+def _fbank_f64(wav):
+    x = np.asarray(wav, np.float64)
+    T = 1 + (len(x) - 400) // 160
+    out = np.empty((T, 80))
+    n = np.arange(400)
+    win = (0.5 - 0.5 * np.cos(2 * np.pi * n / 399)) ** 0.85
+    k = np.arange(257)[:, None]
+    basis = np.exp(-2j * np.pi * k * n[None, :] / 512)
+    banks = S.mel_banks().astype(np.float64)
+    for t in range(T):
+        f = x[160 * t:160 * t + 400].copy()
+        f -= f.mean()
+        f = (f - 0.97 * np.concatenate([f[:1], f[:-1]])) * win
+        p = np.abs(basis @ f) ** 2
+        out[t] = np.log(np.maximum(banks @ p, np.finfo(np.float32).eps))
+    return out
+
+
+def test_fbank_matches_independent_restatement():
+    r = synth.rng_for("sv-fb")
+    a = (0.3 * np.sin(np.arange(8000) * 0.07) + 0.05 * r.standard_normal(8000)).astype(np.float32)
+    got = S.fbank(a).numpy()
+    want = _fbank_f64(a)
+    assert got.shape == want.shape == (S.n_frames(8000), 80)
+    assert np.abs(got - want).max() < 2e-3, np.abs(got - want).max()
+
+
+def test_fbank_silence_is_log_eps():
+    f = S.fbank(np.zeros(1200, np.float32)).numpy()
+    assert np.allclose(f, np.log(np.finfo(np.float32).eps))
+
+
+def test_mel_banks_shape_and_support():
+    b = S.mel_banks()
+    assert b.shape == (80, 257)
+    assert np.all(b[:, 256] == 0) and np.all(b >= 0) and np.all(b <= 1)
+    assert np.all(b.sum(axis=1) > 0)
+    assert np.all(b[:, 0] == 0)          # 0 Hz is below the 20 Hz low edge
+
+
+@pytest.mark.parametrize("n,T", [(399, 0), (400, 1), (559, 1), (560, 2), (89600, 558)])
+def test_frame_count(n, T):
+    assert S.n_frames(n) == T
+
+
+class _Track(dict):
+    def __init__(self, d):
+        super().__init__(d)
+        self.read = set()
+
+    def __getitem__(self, k):
+        self.read.add(k)
+        return super().__getitem__(k)
+
+
+def test_spec_is_exactly_what_the_model_reads():
+    import torch
+    w = synth.synth_sv_weights()
+    spec = W.sv_spec()
+    assert list(w) == list(spec)
+    for k, shp in spec.items():
+        assert w[k].shape == shp and w[k].dtype == np.float32
+    tw = _Track(S.torch_weights(w))
+    feat = torch.from_numpy(np.random.default_rng(0).standard_normal((17, 80)).astype(np.float32))
+    out = S.forward3(tw, feat)
+    assert out.shape == (1, 20480)
+    assert tw.read == set(spec)
+    assert np.all(w["layer1.0.bn1.running_var"] > 0)
+
+
+def test_embedding_depends_on_audio():
+    w = synth.synth_sv_weights()
+    r = synth.rng_for("sv-dep")
+    a = (0.1 * r.standard_normal(4000)).astype(np.float32)
+    e1 = S.sv_embedding(w, a)
+    e2 = S.sv_embedding(w, a * 0.5)
+    assert e1.shape == (1, 20480) and np.isfinite(e1).all()
+    assert np.abs(e1 - e2).max() > 1e-3

@@ -57,4 +57,42 @@ out["roberta"] = {"tokens": int(N), "layers_run": 22, "ms": ms, "gflop": flops /
                   "weights_mb": 22 * 12.6e6 * 2 / 1e6 / 2,
                   "frac_hbm_weights": (22 * (1024 * 3072 + 1024 * 1024 + 2 * 1024 * 4096) * 2) / 8e12 / (ms * 1e-3)}
 er.close()
+# ---- speaker verification (V2ProPlus sv_emb, ReferenceAudio.py:71-72): 5.3 s + 0.3 s silence at 16 kHz
+es = Engine({"sv": synth.synth_sv_weights()}, "v2")
+audio = torch.as_tensor(synth.rng_for("sv").standard_normal(89600).astype(np.float32) * 0.1, device="cuda")
+for _ in range(3):
+    es.sv(audio)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(n):
+    es.sv(audio)
+torch.cuda.synchronize()
+ms = (time.perf_counter() - t0) / n * 1e3
+T = lib().gsv_sv_frames(audio.numel())
+
+
+def down(x):
+    return (x - 1) // 2 + 1
+
+
+flops, P, cin = 0, 80 * T, 64
+flops += 2 * P * 64 * 9
+F_, T_ = 80, T
+for planes, nb, stride, aff in W.SV_STAGES:
+    w = planes * 24 // 64
+    for b in range(nb):
+        s_ = stride if b == 0 else 1
+        if s_ == 2:
+            F_, T_ = down(F_), down(T_)
+        P = F_ * T_
+        flops += 2 * P * (cin * 4 * w + 4 * w * w * 9 + 4 * w * planes * 4)
+        if b == 0 and (s_ != 1 or cin != planes * 4):
+            flops += 2 * P * cin * planes * 4
+        if aff:
+            flops += 3 * 2 * P * (2 * w * (w // 4) + (w // 4) * w)
+        cin = planes * 4
+flops += 2 * P * 1024 * 9 * 2048 + 2 * P * (4096 * 512 + 512 * 2048)
+out["sv"] = {"audio_s": 5.6, "frames": int(T), "ms": ms, "gflop": flops / 1e9,
+             "frac_f32_peak": flops / 157.3e12 / (ms * 1e-3)}
+es.close()
 print(json.dumps(out), flush=True)
