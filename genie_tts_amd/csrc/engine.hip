@@ -826,8 +826,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (allow_persist && use_persist && (persist_family(B) || (B <= 8 && persist_groups(B, decode_cus()) > 0)))
-        return decode_persistent(B, sp, st);
+    if (allow_persist && use_persist && persist_family(B)) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -900,7 +899,7 @@ bool gsv_engine::persist_family(int B) const {
 }
 
 int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) {
-    return decode_persistent_as(B, sp, st, persist_family(B));
+    return decode_persistent_as(B, sp, st);
 }
 
 // Enqueue one persistent decode launch on st (no host wait): the error word is
@@ -908,16 +907,16 @@ int gsv_engine::decode_persistent(int B, const gsv_sampler* sp, hipStream_t st) 
 // (enqueue_results layout) behind it; queued vocoder / prefetch work is launched
 // on the vocoder CUs right after the kernel.  one: the single-sequence kernel
 // (t2s_persist1.hip) instead of the general one.
-int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bool one, int* perr_dst,
+int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, int* perr_dst,
                                 hipEvent_t k0, hipEvent_t k1, char* res_dst, int res_b) {
-    // One launch runs every loop step (t2s_persist.hip).  Hand-offs are tagged
+    // One launch runs every loop step (t2s_persist1.hip).  Hand-offs are tagged
     // granules in a ring; the launch epoch in the tag makes the ring reusable
     // without zeroing (re-zeroed when the epoch wraps or the layout changes).
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (tmax > persist_max_tokens()) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
+    if (tmax > PERSIST_TMAX) return set_error(GSV_E_CAPACITY, "persistent decode: tokens exceed 4096");
     // one: the persist1 family (B = 1 single-sequence kernel, B > 1 its multi-sequence form)
-    const size_t need = one ? (B == 1 ? persist1_ring_bytes() : persist1m_ring_bytes(B)) : persist_ring_bytes(B);
-    const int layout = one ? (B == 1 ? -1 : -100 - B) : B;   // ring layout key: the kernels slot the ring differently
+    const size_t need = B == 1 ? persist1_ring_bytes() : persist1m_ring_bytes(B);
+    const int layout = B == 1 ? -1 : -100 - B;   // ring layout key: the kernels slot the ring differently
     if (need > pws_bytes || layout != pws_batch) {
         if (need > pws_bytes) {
             if (pws) hipFree(pws);
@@ -939,8 +938,8 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bo
     a.B = B;
     // layer groups: as many as the engine stream's CUs hold (all of them unless the
     // vocoder is overlapped on its own CUs)
-    a.groups = one ? std::min(persist1_max_groups(), decode_cus() / persist1_grid(1)) : persist_groups(B, decode_cus());
-    if (const char* e = std::getenv("GENIE_PERSIST_GROUPS")) a.groups = std::max(one ? 3 : 1, std::min(a.groups, std::atoi(e)));
+    a.groups = std::min(persist1_max_groups(), decode_cus() / persist1_grid(1));
+    if (const char* e = std::getenv("GENIE_PERSIST_GROUPS")) a.groups = std::max(3, std::min(a.groups, std::atoi(e)));
     for (int l = 0; l < 24; ++l) {
         const T2SLayerW& W = layers[l];
         a.L[l] = PLayer{W.w_in, W.w_out, W.w1, W.w2, W.b_in, W.b_out, W.b1, W.b2, W.n1w, W.n1b, W.n2w, W.n2b};
@@ -967,8 +966,7 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bo
     perr_zeroed = false;
     // a queued prefetch starts once this stream's prefill (same workspaces) is done
     if (pf_queued && !pf_pending) hipEventRecord(pf_fork, st);
-    const hipError_t le = one ? (B == 1 ? decode_persist1(a, st, k0, k1) : decode_persist1m(a, st, k0, k1))
-                              : decode_persist(a, st, k0, k1);
+    const hipError_t le = B == 1 ? decode_persist1(a, st, k0, k1) : decode_persist1m(a, st, k0, k1);
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     hipMemcpyAsync(perr_dst, perr, 4, hipMemcpyDeviceToHost, st);
@@ -992,22 +990,21 @@ void gsv_engine::probe_sample(hipEvent_t k0, hipEvent_t k1) {
     }
 }
 
-int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one) {
+int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st) {
     if (!perr_host && hipHostMalloc((void**)&perr_host, 64, hipHostMallocDefault) != hipSuccess)
         return set_error(GSV_E_HIP, "pinned alloc");
     const bool probe = timing && kev[0] != nullptr;
-    if (int r = persist_enqueue(B, sp, st, one, perr_host, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr,
+    if (int r = persist_enqueue(B, sp, st, perr_host, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr,
                                 res_batch ? res_pin : nullptr, res_batch))
         return r;
     if (host_wait(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
-    // code 2: the single-sequence kernel met an activation beyond the fp16 range of
-    // its split-operand MFMA GEMVs.  It stopped before writing the sequence state
-    // back (KV rows and tokens of the partial run are rewritten), so the same
-    // steps run again on the general kernel (f32 VALU arithmetic).
-    if (*perr_host == 2 && one) {
+    // code 2: the kernel met an activation beyond the fp16 range of its split-operand
+    // MFMA GEMVs.  It stopped before writing the sequence state back (KV rows and
+    // tokens of the partial run are rewritten), so the same steps run again as
+    // per-step graphs (t2s_decode.hip: f32 activations on the VALU, no fp16 operand).
+    if (*perr_host == 2) {
         ++persist1_f16_reruns;
-        if (B <= 8 && persist_groups(B, decode_cus()) > 0) return decode_persistent_as(B, sp, st, false);
-        return decode_loop(B, sp, st, false);   // (the general kernel holds at most 8 sequences)
+        return decode_loop(B, sp, st, false);
     }
     // code 1: a hand-off waited past its bound -- the launch's workgroups were not
     // all resident (other work on the device) or stalled.  Every workgroup left
@@ -1501,7 +1498,7 @@ int gsv_engine::gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t c
     const bool persist_ok = use_persist && use_persist1 && decode_cus() >= persist1_grid(3);
     int rc = 0;
     if (persist_ok) {
-        rc = persist_enqueue(1, &sp, st, true, g.perr_h, timing ? g.k0 : nullptr, timing ? g.k1 : nullptr, g.res, 1);
+        rc = persist_enqueue(1, &sp, st, g.perr_h, timing ? g.k0 : nullptr, timing ? g.k1 : nullptr, g.res, 1);
     } else {   // no persistent path: this one runs to completion now
         res_batch = 1;
         res_ready = false;
@@ -1679,7 +1676,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist = value != 0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;
-    } else if (n == "persist1m") {   // B = 2..8: the multi-sequence form of persist1 (0: the general kernel)
+    } else if (n == "persist1m") {   // B = 2..64: the multi-sequence form of persist1 (0: per-step graphs)
         eng->use_persist1m = value != 0;
     } else if (n == "persist_spin_ticks") {   // test hook: bound of a hand-off wait (100 MHz ticks)
         eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : 300000000ull;

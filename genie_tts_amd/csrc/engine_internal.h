@@ -152,15 +152,15 @@ struct gsv_engine {
     long long* acc64 = nullptr;   // per sequence [24 layers][FFN out, attn out][512] fixed-point hand-offs
     bool use_acc = true;          // GENIE_ACC=0: split-K partial slabs instead   // GENIE_KTRACE: phase stamps [3][256][8] of layer probe_layer
     hipEvent_t poll_ev[2] = {};
-    // ---- persistent decode (t2s_persist.hip)
+    // ---- persistent decode (t2s_persist1.hip)
     void* pws = nullptr;               // granule ring
     size_t pws_bytes = 0;
     int pws_batch = 0;                 // batch the ring is laid out for
     unsigned pepoch = 0;               // launch epoch (granule tags)
     int* perr = nullptr;               // device error word
     int* perr_host = nullptr;          // pinned error word
-    bool use_persist1 = true;          // GENIE_PERSIST1=0: the general kernel at B=1 too
-    bool use_persist1m = true;         // GENIE_PERSIST1M=0: the general kernel at B = 2..8
+    bool use_persist1 = true;          // GENIE_PERSIST1=0: per-step graphs at every batch size
+    bool use_persist1m = true;         // GENIE_PERSIST1M=0: per-step graphs at B = 2..64
     bool use_persist = true;           // GENIE_PERSIST=0: per-step graphs instead
     bool use_convh = true;             // GENIE_CONVH=0: MRF convs on the f32 MFMA path
     int* vovf = nullptr;               // f16-split conv overflow flag (device)
@@ -217,7 +217,7 @@ struct gsv_engine {
     long persist_timeouts = 0;         // persistent launches that timed out (co-running work) and re-ran as graphs
     unsigned long long persist_spin_ticks = 300000000ull;   // option "persist_spin_ticks" (test hook)
     int decode_persistent(int B, const gsv_sampler* sp, hipStream_t st);
-    int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st, bool one);
+    int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st);
     bool persist_family(int B) const;
     // generate's results (ny, steps, y rows) -> pinned host memory, enqueued by the
     // persistent decode before its own sync (one host round trip per generate)
@@ -228,7 +228,7 @@ struct gsv_engine {
     int ensure_res_pin(int batch);
     void enqueue_results(int batch, hipStream_t st, char* dst);
     int trim_results(const char* res, int batch, int64_t* out_tokens, int out_stride, int32_t* out_len);
-    int persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, bool one, int* perr_dst, hipEvent_t k0,
+    int persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, int* perr_dst, hipEvent_t k0,
                         hipEvent_t k1, char* res_dst, int res_b);
     void probe_sample(hipEvent_t k0, hipEvent_t k1);
     // asynchronous single-utterance generate (gsv_t2s_generate_start / _finish): up to
@@ -249,7 +249,7 @@ struct gsv_engine {
     int gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t caller);
     int gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len, hipStream_t caller);
     int gen_drain();                   // wait for every started generate (their results stay queued)
-    long persist1_f16_reruns = 0;      // single-sequence launches re-run on the general kernel (fp16 range)
+    long persist1_f16_reruns = 0;      // persistent launches re-run as per-step graphs (fp16 range)
     int persist1_f16_limit = 0;
     int persist1_pf_delay = 0;         // GENIE_PF_DELAY: s_sleep(32) ticks before the next-layer prefetch
     int persist1_knob[4] = {0, 0, 0, 0};   // options "knob0".."knob3": single-sequence kernel tuning variants

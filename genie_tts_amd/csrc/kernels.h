@@ -231,7 +231,7 @@ void seq_state_init(int b, const int64_t* prompts, int P, int L, int64_t* y, lon
 
 
 // ---------------------------------------------------------------------------
-// Persistent decode (t2s_persist.hip): the whole AR loop in one launch.
+// Persistent decode (t2s_persist1.hip): the whole AR loop in one launch.
 // ---------------------------------------------------------------------------
 struct PLayer {
     const __half *w_in, *w_out, *w1, *w2;   // fp16, the graph's [out][in] layouts
@@ -247,7 +247,7 @@ struct PersistArgs {
     int64_t* y; long ldy; int* ny; int* kvlen; int* steps; uint8_t* done; uint8_t* stop_out; uint32_t* seen;
     int top_k; float temperature; float rep_penalty; int greedy; uint64_t seed; int max_steps; int force_steps;
     const int* force_b;                           // optional per-sequence force_steps (>0 overrides)
-    unsigned long long* ring;                     // granule ring (persist_ring_bytes)
+    unsigned long long* ring;                     // granule ring (persist1_ring_bytes / persist1m_ring_bytes)
     unsigned epoch;                               // launch epoch (tag high bits), 1 .. 2^20-1
     int* err;                                     // zeroed per launch; non-zero: a hand-off timed out
     int smax;                                     // step cap of the launch
@@ -265,11 +265,7 @@ struct PersistArgs {
                                                   // layer 0: 0 | b_in), so a GEMV can run beside its LayerNorm stats;
                                                   // then [W_pred n2w_23 | W_pred n2b_23] (1025 each, the logits)
 };
-int persist_groups(int B, int n_cu);   // 0: the grid does not fit
-int persist_grid(int B, int groups);
-size_t persist_ring_bytes(int B);
-int persist_max_tokens();
-hipError_t decode_persist(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
+constexpr int PERSIST_TMAX = 4096;   // longest key range of the persistent decode (its PE table)
 // Single-sequence persistent decode (t2s_persist1.hip): a.groups (3..8) layer
 // groups x 32 workgroups, two hand-offs per layer.  Needs persist1_grid(groups)
 // resident CUs; B must be 1.

@@ -1,5 +1,5 @@
-// Device helpers shared by the persistent decode kernels (t2s_persist.hip,
-// t2s_persist1.hip): tagged-granule hand-offs, global-address-space loads,
+// Device helpers of the persistent decode kernel (t2s_persist1.hip, B = 1 and its
+// multi-sequence form): tagged-granule hand-offs, global-address-space loads,
 // ILP DPP reductions and the graph-order LayerNorm statistics.
 //
 // Hand-offs are 8-byte {tag, value} granules written by ONE write-through (sc1)

@@ -1,5 +1,5 @@
 // Sampler device body shared by the per-step sampler kernel (t2s.hip) and the
-// persistent decode kernel (t2s_persist.hip).
+// persistent decode kernel (t2s_persist1.hip).
 #pragma once
 #include "common.h"
 #include "kernels.h"

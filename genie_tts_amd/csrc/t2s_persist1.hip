@@ -15,8 +15,8 @@
 //     h1_l = LN1(x_l + bo + sum_h PA[l][h]), publishes h1_l (32 columns per
 //     slice), FFN1 rows of the slice (ReLU), FFN2 partial -> granules PF[l][j].
 // So a token costs 2 hand-offs per layer + logits + sampler + token = 50 hops
-// (the general kernel, t2s_persist.hip, needs 3 per layer because every
-// workgroup tracks the residual stream).  Everything else is local.
+// (a design in which every workgroup tracks the residual stream needs 3 per
+// layer).  Everything else is local.
 //
 // Grid: G layer groups x 32 workgroups (one per CU; LDS forces it): G = 8 fills
 // the chip (256); with the vocoder overlapped on its own CUs (engine option

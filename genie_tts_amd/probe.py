@@ -1,7 +1,7 @@
 """Roofline of the dominant kernel, from the engine's live in-loop timing.
 
-Persistent decode (default, t2s_persist.hip): the dominant kernel is
-`k_decode_persist`, ONE launch per utterance that runs every decode step.  Its
+Persistent decode (default, t2s_persist1.hip): the dominant kernel is
+`k_decode_persist1`, ONE launch per utterance that runs every decode step.  Its
 algorithmic bytes (per sequence per step): the fp16 weights read
 once, W16 = 24 layers x (1536+512+2048+2048) x 512 x 2 B + the 1025x512 fp16
 logits head = 152,044,544 B, plus the fp32 K/V cache rows read, 98,304 B per

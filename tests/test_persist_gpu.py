@@ -1,6 +1,6 @@
 """GPU: the persistent decode launches (t2s_persist1.hip at B = 1, its multi-sequence
-form at B = 2..64, t2s_persist.hip when it is off) against the per-step hipGraph path, each
-other and the CPU oracle.
+form at B = 2..64) against the per-step hipGraph path (t2s_decode.hip), each other and
+the CPU oracle.
 
 Both decode paths sit behind gsv_t2s_generate (the reference's 500-step loop,
 Inference.py:95-109); option "persist" selects one.  Bars: greedy token ids
@@ -100,8 +100,8 @@ def test_persistent_natural_stop_max_steps(eng):
 
 def test_persistent_fp16_range_fallback(eng, oracle_model):
     """An FFN activation beyond the fp16 range of the single-sequence kernel's split
-    MFMA operands stops it (error code 2) and the host re-runs the steps on the general
-    kernel.  The hook lowers the limit to 1.0 so that the fallback fires; the tokens
+    MFMA operands stops it (error code 2) and the host re-runs the steps as per-step
+    graphs.  The hook lowers the limit to 1.0 so that the fallback fires; the tokens
     stay bit-exact vs the oracle."""
     from genie_tts_amd.engine import make_sampler
     from oracle import restate as R
@@ -182,8 +182,8 @@ def test_multi_sequence_ragged_lengths(eng):
 
 def test_multi_sequence_fp16_range_fallback(eng):
     """An activation past the fp16 range stops the multi-sequence launch (error 2) before
-    any sequence state is written; the steps run again (the general kernel up to 8
-    sequences, the per-step graphs above) with the same tokens."""
+    any sequence state is written; the steps run again as per-step graphs with the
+    same tokens."""
     from genie_tts_amd.engine import make_sampler
     for B in (3, 12):
         inps = [t2s_inputs(R=10 + i, S=8 + i, H=30 + 2 * i, tag=f"mf{B}_{i}") for i in range(B)]
@@ -200,9 +200,10 @@ def test_multi_sequence_fp16_range_fallback(eng):
         assert [g.tolist() for g in got] == [r.tolist() for r in ref]
 
 
-def test_multi_sequence_sampled_matches_general_kernel(eng):
+def test_multi_sequence_sampled_matches_graph_path(eng):
     """Top-k sampling at B = 3: the multi-sequence kernel's sampler workgroups (one per
-    sequence) draw what the general persistent kernel draws (same Philox keys)."""
+    sequence) draw what the per-step graphs' sampler draws (same Philox keys; option
+    persist1m = 0 sends B > 1 to the graphs)."""
     from genie_tts_amd.engine import make_sampler
     inps = [t2s_inputs(R=12 + i, S=9 + i, H=36 + 2 * i, tag=f"msk{i}") for i in range(3)]
     sp = make_sampler(top_k=15, greedy=False, seed=99, force_steps=20)
