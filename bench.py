@@ -374,6 +374,9 @@ def main():
                     help="batched workloads: HIP stream priority of the vocoder lanes (lower = first)")
     ap.add_argument("--t2s-priority", type=int, default=None,
                     help="batched workloads: HIP stream priority of the engine (T2S) stream")
+    ap.add_argument("--shard", type=str, default="",
+                    help="mixed100 on one GPU: run only LPT shard R of an N-rank job (R/N), to time "
+                         "one rank of an N-GPU run (tools/shard_projection.py)")
     ap.add_argument("--stub-ms", type=float, default=0.0,
                     help=argparse.SUPPRESS)   # tests: a CPU stub replica whose step sleeps this long
     args = ap.parse_args()
@@ -407,9 +410,16 @@ def main():
     if args.workload == "mixed100":
         reqs = [replicas.Request(i, it.text_seq, it.text_bert, it.force_steps, it.bert_ids, it.word2ph)
                 for i, it in enumerate(wl.items)]
-        shard = replicas.lpt_assign([replicas.predicted_cost(r) for r in reqs], world)[rank]
+        if args.shard:
+            if world > 1:
+                raise SystemExit("--shard is a one-process measurement of one rank's shard")
+            sr, sn = (int(x) for x in args.shard.split("/"))
+            shard = replicas.lpt_assign([replicas.predicted_cost(r) for r in reqs], sn)[sr]
+        else:
+            shard = replicas.lpt_assign([replicas.predicted_cost(r) for r in reqs], world)[rank]
         items = [wl.items[i] for i in shard]
-        units_per_step = len(wl.items)            # the whole set per step, over all ranks
+        # the whole set per step, over all ranks (a --shard run: its own sentences only)
+        units_per_step = len(items) if args.shard else len(wl.items)
     else:
         items = wl.items
         units_per_step = world * len(items)       # every replica runs the workload (weak scaling)
@@ -533,6 +543,8 @@ def main():
                          (" (LPT shards)" if args.workload == "mixed100" else ""),
                          "pipelined": pipelined,
                          "vits_f32_reruns": run.eng.counter("vits_f32_reruns")}
+        if args.shard:
+            out["config"]["shard"] = args.shard
         ph = {k: v / args.steps * 1e3 for k, v in run.phase.items()}
         out["phase_ms"] = ph
         out["roofline_utterance"] = composite_roofline(ms_per_step, n0s, [it.force_steps for it in items], tokens,
