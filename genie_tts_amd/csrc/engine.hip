@@ -72,6 +72,8 @@ gsv_engine::~gsv_engine() {
     if (hubert.ws) hipFree(hubert.ws);
     if (bert.ws) hipFree(bert.ws);
     if (sv_ws) hipFree(sv_ws);
+    if (sv_ovf) hipFree(sv_ovf);
+    if (sv_ovf_host) hipHostFree(sv_ovf_host);
     if (perr_host) hipHostFree(perr_host);
     if (res_pin) hipHostFree(res_pin);
     for (GenSlot& g : gq) {
@@ -1728,6 +1730,10 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
             }
     } else if (n == "vocoder_cus") {   // overlapped vocoder: CUs reserved for gsv_vits_decode_async
         return eng->set_vocoder_cus(value);
+    } else if (n == "sv_f16") {   // speaker verification on the split-fp16 MFMA convs (0: the f32 MFMA path)
+        eng->sv_f16 = value != 0;
+    } else if (n == "sv_f16_limit") {   // tests: force the f32 re-run (0: the fp16 range)
+        eng->sv_f16_limit = value > 0 ? (float)value : 65000.f;
     } else if (n == "convh") {   // a queued or pending vocoder call finishes under the mode it began with
         if (int r = eng->vits_wait(nullptr)) return r;
         if (int r = eng->vits_batch_finish(nullptr)) return r;
@@ -1753,6 +1759,7 @@ extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value
     if (n == "persist_timeouts") *value = eng->persist_timeouts;
     else if (n == "persist1_f16_reruns") *value = eng->persist1_f16_reruns;
     else if (n == "vits_f32_reruns") *value = eng->vits_f32_reruns;
+    else if (n == "sv_f32_reruns") *value = eng->sv_f32_reruns;
     else return set_error(GSV_E_ARG, "unknown counter " + n);
     return 0;
 }

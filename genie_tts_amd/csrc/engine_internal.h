@@ -61,6 +61,7 @@ struct BertWeights {
 // Speaker verification (sv.hip): ERes2NetV2 convs, BatchNorm folded, weights [co][tap][ci] f32
 struct SvConv {
     float *w = nullptr, *b = nullptr;
+    __half *wh = nullptr, *wl = nullptr;   // w split into fp16 hi + lo (null: |w| beyond the fp16 range)
     int cin = 0, cout = 0, k = 1;
 };
 struct SvBlock {
@@ -133,6 +134,11 @@ struct gsv_engine {
     gsv::SvWeights sv;
     float* sv_ws = nullptr;           // SV workspace (grown per call)
     size_t sv_ws_n = 0;
+    bool sv_f16 = true;               // option "sv_f16": split-fp16 MFMA convs (else f32 MFMA)
+    float sv_f16_limit = 65000.f;     // option "sv_f16_limit" (> 0): largest activation the f16 path takes
+    int* sv_ovf = nullptr;            // device flag: an activation beyond the fp16 range
+    int* sv_ovf_host = nullptr;       // pinned copy
+    int sv_f32_reruns = 0;            // SV calls re-run on the f32 path after an overflow
 
     std::map<std::string, hipGraphExec_t> graphs;
     bool timing = false;
@@ -186,7 +192,7 @@ struct gsv_engine {
     int finalize_sv();
     int sv_conv_upload(const std::string& wname, const std::string& bname, const std::string& bn, gsv::SvConv* c);
     size_t sv_ws_floats(int frames);
-    int sv_forward(const float* wav, int n, float* out, hipStream_t st);
+    int sv_forward(const float* wav, int n, float* out, hipStream_t st, int* ovf, float lim);
     // RoBERTa over N token rows; rows[n_out]: the token row of each output row.  Packed
     // sentences: row_pos (host [N], position within its sentence) and row_seg (host [N][2],
     // {first row, rows} of its sentence), else one sentence.

@@ -11,11 +11,15 @@
 // (C innermost), so a 1x1 conv is a GEMM over positions and a 3x3 / stride-2 conv is
 // an implicit GEMM whose A rows gather the tap's input position -- no im2col.
 // Every conv is k_sv_conv: 64 positions x 64 output channels per block, K = taps x Cin
-// in steps of 32 staged through LDS, f32 MFMA (v_mfma_f32_32x32x2f32; the weights are
-// arbitrary fp32 with BatchNorm folded in at load, so there is no fp16 split).  The
+// in steps of 32 staged through LDS, on the f16 MFMA with both operands split into fp16
+// hi + lo (the weights are arbitrary fp32 with BatchNorm folded in at load, so they are
+// split too: three MFMAs per product, f32-level accuracy); an activation beyond the fp16
+// range re-runs the call on the f32 MFMA (v_mfma_f32_32x32x2f32).  The
 // Res2Net pieces fold into the A gather (sp + spx[i]; cat(x, y) of the AFF convs) and
 // into the epilogue (bias, residual, ReLU / Hardtanh(0, 20) / SiLU, the AFF mix
 // x (1 + tanh v) + y (1 - tanh v)), so each block is its convs and nothing else.
+#include <cmath>
+
 #include "common.h"
 #include "engine_internal.h"
 
@@ -41,6 +45,9 @@ struct SvConvArgs {
     const float* src2; long lda2;
     int amode, csplit;
     const float* w;            // [cout][K] fp32, BatchNorm folded
+    const __half *wh, *wl;     // the same split into fp16 hi + lo (non-null: the f16 MFMA path)
+    int* ovf;                  // f16 path: set when an activation is beyond the fp16 range
+    float lim;                 // f16 path: largest |activation| it accepts (65000; tests lower it)
     const float* bias;         // [cout] (folded)
     const float* res; long ldr;     // optional residual added before the activation
     int act;
@@ -49,9 +56,20 @@ struct SvConvArgs {
     float* out; long ldo;
 };
 
+typedef _Float16 svh8 __attribute__((ext_vector_type(8)));
+
+// H = false: f32 MFMA (v_mfma_f32_32x32x2f32) on f32 tiles.  H = true: the same tiles on
+// the f16 MFMA (v_mfma_f32_32x32x16_f16, 16x the f32 rate) with both operands split
+// into fp16 hi + lo -- the weights once at load (wh, wl planes), the activations as
+// they leave LDS -- and C += Ah Wh + Al Wh + Ah Wl (the dropped Al Wl term is
+// ~2^-22 relative, f32-level).  An activation beyond the fp16 range sets *ovf and the
+// host runs the model again on the f32 path.
+template <bool H>
 __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
-    __shared__ float As[64][33];
-    __shared__ float Ws[64][33];
+    constexpr int AP = H ? 36 : 33;   // H: 16-byte aligned rows for the fragment reads
+    __shared__ __attribute__((aligned(16))) float As[64][AP];
+    __shared__ __attribute__((aligned(16))) float Ws[H ? 1 : 64][33];
+    __shared__ __attribute__((aligned(16))) _Float16 Wh[H ? 64 : 1][40], Wl[H ? 64 : 1][40];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv >> 1, wn = wv & 1;
     const int M = a.Fo * a.To;
@@ -68,11 +86,12 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    bool big = false;
     for (int k0 = 0; k0 < a.K; k0 += 32) {
         const int kk = k0 + sc;       // 8 consecutive k of one tap (cin % 8 == 0)
-        float av[8], wv8[8];
+        float av[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { av[i] = 0.f; wv8[i] = 0.f; }
+        for (int i = 0; i < 8; ++i) av[i] = 0.f;
         if (gm < M && kk < a.K) {
             const int tap = kk / a.cin, ci = kk - tap * a.cin;
             const int dy = tap / a.k, dx = tap - dy * a.k;
@@ -93,26 +112,66 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
                 }
             }
         }
-        if (gn < a.cout && kk < a.K) {
-            const float4* p = reinterpret_cast<const float4*>(a.w + (long)gn * a.K + kk);
-            const float4 x0 = p[0], x1 = p[1];
-            wv8[0] = x0.x; wv8[1] = x0.y; wv8[2] = x0.z; wv8[3] = x0.w;
-            wv8[4] = x1.x; wv8[5] = x1.y; wv8[6] = x1.z; wv8[7] = x1.w;
-        }
+        if (H) {
+            uint4 hw = make_uint4(0u, 0u, 0u, 0u), lw = make_uint4(0u, 0u, 0u, 0u);
+            if (gn < a.cout && kk < a.K) {
+                hw = *reinterpret_cast<const uint4*>(a.wh + (long)gn * a.K + kk);
+                lw = *reinterpret_cast<const uint4*>(a.wl + (long)gn * a.K + kk);
+            }
+            *reinterpret_cast<float4*>(&As[sr][sc]) = make_float4(av[0], av[1], av[2], av[3]);
+            *reinterpret_cast<float4*>(&As[sr][sc + 4]) = make_float4(av[4], av[5], av[6], av[7]);
+            *reinterpret_cast<uint4*>(&Wh[sr][sc]) = hw;
+            *reinterpret_cast<uint4*>(&Wl[sr][sc]) = lw;
+        } else {
+            float wv8[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            As[sr][sc + i] = av[i];
-            Ws[sr][sc + i] = wv8[i];
+            for (int i = 0; i < 8; ++i) wv8[i] = 0.f;
+            if (gn < a.cout && kk < a.K) {
+                const float4* p = reinterpret_cast<const float4*>(a.w + (long)gn * a.K + kk);
+                const float4 x0 = p[0], x1 = p[1];
+                wv8[0] = x0.x; wv8[1] = x0.y; wv8[2] = x0.z; wv8[3] = x0.w;
+                wv8[4] = x1.x; wv8[5] = x1.y; wv8[6] = x1.z; wv8[7] = x1.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                As[sr][sc + i] = av[i];
+                Ws[sr][sc + i] = wv8[i];
+            }
         }
         __syncthreads();
+        if (H) {
+            const int r = lane & 31, hh = lane >> 5;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float x = As[wm * 32 + (lane & 31)][2 * j + (lane >> 5)];
-            const float y = Ws[wn * 32 + (lane & 31)][2 * j + (lane >> 5)];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
+            for (int ks = 0; ks < 2; ++ks) {
+                const float* ap = &As[wm * 32 + r][ks * 16 + 8 * hh];
+                const float4 x0 = *reinterpret_cast<const float4*>(ap);
+                const float4 x1 = *reinterpret_cast<const float4*>(ap + 4);
+                const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                svh8 ahi, alo;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    big |= !(fabsf(v[j]) < a.lim);
+                    const _Float16 hj = (_Float16)v[j];
+                    ahi[j] = hj;
+                    alo[j] = (_Float16)(v[j] - (float)hj);
+                }
+                const svh8 bh = *reinterpret_cast<const svh8*>(&Wh[wn * 32 + r][ks * 16 + 8 * hh]);
+                const svh8 bl = *reinterpret_cast<const svh8*>(&Wl[wn * 32 + r][ks * 16 + 8 * hh]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bh, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bh, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bl, acc, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float x = As[wm * 32 + (lane & 31)][2 * j + (lane >> 5)];
+                const float y = Ws[wn * 32 + (lane & 31)][2 * j + (lane >> 5)];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
+            }
         }
         __syncthreads();
     }
+    if (H && big) atomicOr(a.ovf, 1);
     const int col = n0 + wn * 32 + (lane & 31);
     if (col >= a.cout) return;
     const float bv = a.bias ? a.bias[col] : 0.f;
@@ -261,6 +320,21 @@ int gsv_engine::sv_conv_upload(const std::string& wname, const std::string& bnam
     c->b = (float*)dalloc((size_t)co * 4);
     if (!c->w || !c->b) return set_error(GSV_E_HIP, "hipMalloc failed for " + wname);
     hipMemcpy(c->w, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    // fp16 hi + lo planes for the f16 MFMA path, unless a weight is beyond the fp16 range
+    bool fits = true;
+    for (float v : h) fits = fits && std::fabs(v) < 65000.f;
+    if (fits) {
+        std::vector<__half> hi(h.size()), lo(h.size());
+        for (size_t i = 0; i < h.size(); ++i) {
+            hi[i] = __float2half(h[i]);
+            lo[i] = __float2half(h[i] - __half2float(hi[i]));
+        }
+        c->wh = (__half*)dalloc(hi.size() * 2);
+        c->wl = (__half*)dalloc(lo.size() * 2);
+        if (!c->wh || !c->wl) return set_error(GSV_E_HIP, "hipMalloc failed for " + wname);
+        hipMemcpy(c->wh, hi.data(), hi.size() * 2, hipMemcpyHostToDevice);
+        hipMemcpy(c->wl, lo.data(), lo.size() * 2, hipMemcpyHostToDevice);
+    }
     hipMemcpy(c->b, shift.data(), (size_t)co * 4, hipMemcpyHostToDevice);
     c->cin = ci;
     c->cout = co;
@@ -355,7 +429,8 @@ struct SvMap {   // a feature map in the workspace
     long ld;     // row stride (channels of the buffer it lives in)
 };
 
-SvConvArgs sv_args(const SvConv& c, const SvMap& in, int stride, int pad, float* out, long ldo) {
+SvConvArgs sv_args(const SvConv& c, const SvMap& in, int stride, int pad, float* out, long ldo, int* ovf,
+                   float lim) {
     SvConvArgs a{};
     a.Fi = in.F; a.Ti = in.T;
     a.k = c.k; a.stride = stride; a.pad = pad;
@@ -365,6 +440,9 @@ SvConvArgs sv_args(const SvConv& c, const SvMap& in, int stride, int pad, float*
     a.src = in.p; a.lda = in.ld;
     a.amode = SV_A_PLAIN;
     a.w = c.w; a.bias = c.b;
+    if (ovf && c.wh) {   // the split-fp16 path (ovf: its range flag)
+        a.wh = c.wh; a.wl = c.wl; a.ovf = ovf; a.lim = lim;
+    }
     a.act = SV_ACT_NONE;
     a.out = out; a.ldo = ldo;
     return a;
@@ -372,7 +450,9 @@ SvConvArgs sv_args(const SvConv& c, const SvMap& in, int stride, int pad, float*
 
 void sv_conv(const SvConvArgs& a, hipStream_t st) {
     const int M = a.Fo * a.To;
-    hipLaunchKernelGGL(k_sv_conv, dim3((a.cout + 63) / 64, (M + 63) / 64), dim3(256), 0, st, a);
+    const dim3 grid((a.cout + 63) / 64, (M + 63) / 64);
+    if (a.wh) hipLaunchKernelGGL(k_sv_conv<true>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_sv_conv<false>, grid, dim3(256), 0, st, a);
 }
 }  // namespace
 
@@ -383,7 +463,7 @@ size_t gsv_engine::sv_ws_floats(int T) {
     return P1 + 3 * P1 * 256 + 2 * P1 * 96 + P1 * 24 + P1 * 24 + 2 * (size_t)10 * T4 * 2048 + (size_t)10 * T4 * 512 + 64;
 }
 
-int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st) {
+int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, int* ovf, float lim) {
     const SvWeights& S = sv;
     const int T = sv_frames(n);
     const size_t P1 = (size_t)SV_NMEL * T;
@@ -419,14 +499,14 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st) 
             int ob = 0;
             while (ob == cur_buf || ob == keep_buf) ++ob;
             // conv1 (1x1, stride) + BN + Hardtanh -> H [P][4w]
-            SvConvArgs c1 = sv_args(B.conv1, cur, B.stride, 0, H, w4);
+            SvConvArgs c1 = sv_args(B.conv1, cur, B.stride, 0, H, w4, ovf, lim);
             c1.act = SV_ACT_RELU20;
             sv_conv(c1, st);
             const SvMap hmap{H, c1.Fo, c1.To, w4, w4};
             // the split chain: sp_0 = conv(spx_0); sp_i = conv(sp_{i-1} + spx_i) or conv(AFF(sp_{i-1}, spx_i))
             for (int i = 0; i < 4; ++i) {
                 SvMap in{H + i * w, hmap.F, hmap.T, w, w4};
-                SvConvArgs c = sv_args(B.convs[i], in, 1, 1, O + i * w, w4);
+                SvConvArgs c = sv_args(B.convs[i], in, 1, 1, O + i * w, w4, ovf, lim);
                 if (i > 0 && !B.aff) {
                     c.amode = SV_A_ADD;
                     c.src = O + (i - 1) * w; c.lda = w4;
@@ -434,13 +514,13 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st) 
                 } else if (i > 0) {
                     // AFF: t = SiLU(conv_a(cat(sp, spx_i))), z = sp (1 + tanh conv_b(t)) + spx_i (1 - tanh ...)
                     SvMap cat{O + (i - 1) * w, hmap.F, hmap.T, 2 * w, w4};
-                    SvConvArgs ca = sv_args(B.aff_a[i - 1], cat, 1, 0, A, w / 4);
+                    SvConvArgs ca = sv_args(B.aff_a[i - 1], cat, 1, 0, A, w / 4, ovf, lim);
                     ca.amode = SV_A_CAT;
                     ca.src2 = H + i * w; ca.lda2 = w4; ca.csplit = w;
                     ca.act = SV_ACT_SILU;
                     sv_conv(ca, st);
                     SvMap tm{A, hmap.F, hmap.T, w / 4, w / 4};
-                    SvConvArgs cb = sv_args(B.aff_b[i - 1], tm, 1, 0, Z, w);
+                    SvConvArgs cb = sv_args(B.aff_b[i - 1], tm, 1, 0, Z, w, ovf, lim);
                     cb.ax = O + (i - 1) * w; cb.ldx = w4;
                     cb.ay = H + i * w; cb.ldy = w4;
                     sv_conv(cb, st);
@@ -455,13 +535,13 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st) 
             const float* res = cur.p;
             long ldr = cur.ld;
             if (B.has_sc) {
-                SvConvArgs sc = sv_args(B.sc, cur, B.stride, 0, y, cout);
+                SvConvArgs sc = sv_args(B.sc, cur, B.stride, 0, y, cout, ovf, lim);
                 sv_conv(sc, st);
                 res = y;
                 ldr = cout;
             }
             const SvMap omap{O, hmap.F, hmap.T, w4, w4};
-            SvConvArgs c3 = sv_args(B.conv3, omap, 1, 0, y, cout);
+            SvConvArgs c3 = sv_args(B.conv3, omap, 1, 0, y, cout, ovf, lim);
             c3.res = res; c3.ldr = ldr;
             c3.act = SV_ACT_RELU20;
             sv_conv(c3, st);
@@ -474,17 +554,17 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st) 
         }
     }
     // layer3_ds (3x3 stride 2, no BN) and fuse34 = AFF(out4, out3_ds)
-    SvConvArgs d = sv_args(S.ds34, out3, 2, 1, ds, 2048);
+    SvConvArgs d = sv_args(S.ds34, out3, 2, 1, ds, 2048, ovf, lim);
     sv_conv(d, st);
     if (d.Fo != cur.F || d.To != cur.T) return set_error(GSV_E_ARG, "SV layer3_ds / layer4 shape mismatch");
     SvMap cat{cur.p, cur.F, cur.T, 4096, cur.ld};
-    SvConvArgs fa_ = sv_args(S.fuse_a, cat, 1, 0, fa, 512);
+    SvConvArgs fa_ = sv_args(S.fuse_a, cat, 1, 0, fa, 512, ovf, lim);
     fa_.amode = SV_A_CAT;
     fa_.src2 = ds; fa_.lda2 = 2048; fa_.csplit = 2048;
     fa_.act = SV_ACT_SILU;
     sv_conv(fa_, st);
     SvMap tm{fa, cur.F, cur.T, 512, 512};
-    SvConvArgs fb = sv_args(S.fuse_b, tm, 1, 0, fuse, 2048);
+    SvConvArgs fb = sv_args(S.fuse_b, tm, 1, 0, fuse, 2048, ovf, lim);
     fb.ax = cur.p; fb.ldx = cur.ld;
     fb.ay = ds; fb.ldy = 2048;
     sv_conv(fb, st);
@@ -501,5 +581,18 @@ extern "C" int gsv_sv(gsv_engine* eng, const float* audio_16k, int n_samples, fl
     if (sv_frames(n_samples) < 1) return set_error(GSV_E_ARG, "audio too short for the SV fbank (< 400 samples)");
     hipSetDevice(eng->device);
     StreamScope sc(eng, stream);
-    return eng->sv_forward(audio_16k, n_samples, sv_emb, sc.st());
+    if (!eng->sv_f16) return eng->sv_forward(audio_16k, n_samples, sv_emb, sc.st(), nullptr, 0.f);
+    if (!eng->sv_ovf) {
+        if (hipMalloc((void**)&eng->sv_ovf, 4) != hipSuccess ||
+            hipHostMalloc((void**)&eng->sv_ovf_host, 4, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "SV overflow flag");
+    }
+    hipMemsetAsync(eng->sv_ovf, 0, 4, sc.st());
+    if (int r = eng->sv_forward(audio_16k, n_samples, sv_emb, sc.st(), eng->sv_ovf, eng->sv_f16_limit)) return r;
+    hipMemcpyAsync(eng->sv_ovf_host, eng->sv_ovf, 4, hipMemcpyDeviceToHost, sc.st());
+    if (hipStreamSynchronize(sc.st()) != hipSuccess) return set_error(GSV_E_HIP, "SV sync");
+    if (*eng->sv_ovf_host == 0) return 0;
+    // an activation beyond the fp16 range: the same call on the f32 MFMA path
+    ++eng->sv_f32_reruns;
+    return eng->sv_forward(audio_16k, n_samples, sv_emb, sc.st(), nullptr, 0.f);
 }

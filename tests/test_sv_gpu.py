@@ -1,8 +1,9 @@
 """GPU: the V2ProPlus speaker-verification model on the engine (gsv_sv, sv.hip) against
 the oracle's restatement of GPT-SoVITS's SV (Kaldi fbank -> ERes2NetV2.forward3,
 oracle/sv.py) on the same synthetic fp32 weights.  ONNX-level parity is unpinned
-(speaker_encoder.onnx is absent); the bar is the fp32 model within f32-MFMA
-accumulation order: RMS <= 1e-4 x max(1, std) of the 20480-d embedding."""
+(speaker_encoder.onnx is absent); the bar is the fp32 model within the split-fp16
+MFMA's accuracy (and the f32 MFMA path's): RMS <= 1e-4 x max(1, std) of the 20480-d
+embedding."""
 import numpy as np
 import pytest
 
@@ -45,6 +46,39 @@ def test_sv_vs_oracle(svm, n):
     e, w = svm
     a = _clip(n, f"sv-{n}") if n > 4800 else (0.2 * synth.rng_for("sv-min").standard_normal(n)).astype(np.float32)
     _check(e.sv(a).cpu().numpy(), S.sv_embedding(w, a))
+
+
+def test_sv_f32_path_vs_oracle(svm):
+    """Option sv_f16 = 0: every conv on the f32 MFMA (no fp16 split) -- same bar."""
+    from oracle import sv as S
+    e, w = svm
+    a = _clip(16077, "sv-f32")
+    e.set_option("sv_f16", 0)
+    try:
+        got = e.sv(a).cpu().numpy()
+    finally:
+        e.set_option("sv_f16", 1)
+    _check(got, S.sv_embedding(w, a))
+
+
+def test_sv_fp16_range_fallback(svm):
+    """An activation beyond the fp16 range (limit lowered to 1 here) sets the flag and the
+    call runs again on the f32 path: the result is that path's, bit for bit."""
+    e, _ = svm
+    a = _clip(16077, "sv-ovf")
+    e.set_option("sv_f16", 0)
+    try:
+        want = e.sv(a).cpu().numpy()
+    finally:
+        e.set_option("sv_f16", 1)
+    before = e.counter("sv_f32_reruns")
+    e.set_option("sv_f16_limit", 1)
+    try:
+        got = e.sv(a).cpu().numpy()
+    finally:
+        e.set_option("sv_f16_limit", 0)
+    assert e.counter("sv_f32_reruns") == before + 1
+    assert np.array_equal(got, want)
 
 
 def test_sv_too_short(svm):
