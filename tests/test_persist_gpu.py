@@ -98,6 +98,19 @@ def test_persistent_natural_stop_max_steps(eng):
     assert len(a[0]) > 0
 
 
+@pytest.mark.parametrize("B", [1, 4])
+def test_persistent_full_500_step_loop(eng, B):
+    """The reference's whole loop (Inference.py:95, range(500)) with no EOS (random
+    weights): 500 steps, the keys growing past the LDS stage (N0 ~ 150 + 500 > 448
+    rows) -- the persistent kernels equal the per-step graphs at the maximum length."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=40 + 3 * i, S=30 + 2 * i, H=160 + 8 * i, tag=f"f500_{B}_{i}") for i in range(B)]
+    a, b = _both(eng, inps, make_sampler())
+    for i in range(B):
+        assert a[i].tolist() == b[i].tolist(), f"utterance {i}"
+        assert len(a[i]) >= 450       # no EOS under random weights: (nearly) the whole loop
+
+
 def test_persistent_fp16_range_fallback(eng, oracle_model):
     """An FFN activation beyond the fp16 range of the single-sequence kernel's split
     MFMA operands stops it (error code 2) and the host re-runs the steps as per-step
