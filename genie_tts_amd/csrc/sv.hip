@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv >> 1, wn = wv & 1;
     const int M = a.Fo * a.To;
-    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;   // positions on x: long clips exceed 65535 tiles
     const int sr = tid >> 2, sc = (tid & 3) * 8;
     const int gm = m0 + sr, gn = n0 + sr;
     // this thread's A row: output position (fo, to) -> top-left input position
@@ -450,7 +450,7 @@ SvConvArgs sv_args(const SvConv& c, const SvMap& in, int stride, int pad, float*
 
 void sv_conv(const SvConvArgs& a, hipStream_t st) {
     const int M = a.Fo * a.To;
-    const dim3 grid((a.cout + 63) / 64, (M + 63) / 64);
+    const dim3 grid((M + 63) / 64, (a.cout + 63) / 64);
     if (a.wh) hipLaunchKernelGGL(k_sv_conv<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_sv_conv<false>, grid, dim3(256), 0, st, a);
 }

@@ -39,8 +39,8 @@ def _check(got, ref):
 
 
 # 400 samples = one fbank frame (the minimum); a ragged 1 s; the nominal 5.3 s reference
-# clip + 0.3 s of silence at 16 kHz
-@pytest.mark.parametrize("n", [400, 16077, 89600])
+# clip + 0.3 s of silence at 16 kHz; a 30 s clip (2998 frames)
+@pytest.mark.parametrize("n", [400, 16077, 89600, 480000])
 def test_sv_vs_oracle(svm, n):
     from oracle import sv as S
     e, w = svm
