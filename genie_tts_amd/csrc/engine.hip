@@ -992,6 +992,19 @@ void gsv_engine::probe_sample(hipEvent_t k0, hipEvent_t k1) {
     }
 }
 
+// A persistent launch whose hand-off outwaited its bound: its grid was not all resident
+// (placement, other work on the CUs) and the steps re-run as per-step graphs.  Two in a
+// row mean the condition persists: the engine stays on the graphs (option "persist" = 1
+// re-enables) instead of paying the bound on every utterance.
+void gsv_engine::note_persist_timeout() {
+    ++persist_timeouts;
+    if (++persist_timeout_run >= 2 && use_persist) {
+        use_persist = false;
+        std::fprintf(stderr, "[genie] persistent decode timed out %d times in a row: using per-step graphs\n",
+                     persist_timeout_run);
+    }
+}
+
 int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st) {
     if (!perr_host && hipHostMalloc((void**)&perr_host, 64, hipHostMallocDefault) != hipSuccess)
         return set_error(GSV_E_HIP, "pinned alloc");
@@ -1013,11 +1026,12 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     // before the sequence state was written back, so the same steps run again as
     // per-step graphs, which need no co-residency.
     if (*perr_host == 1) {
-        ++persist_timeouts;
+        note_persist_timeout();
         return decode_loop(B, sp, st, false);
     }
     if (*perr_host != 0)
         return set_error(GSV_E_HIP, "persistent decode failed (code " + std::to_string(*perr_host) + ")");
+    persist_timeout_run = 0;
     res_ready = res_batch > 0;
     if (probe) probe_sample(kev[0], kev[1]);
     return 0;
@@ -1542,7 +1556,7 @@ int gsv_engine::gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len
         // sequence state was not written back; drain and run this utterance again on
         // the synchronous path, which handles both (its own prefill, slot 0)
         if (*g.perr_h == 2) ++persist1_f16_reruns;
-        else if (*g.perr_h == 1) ++persist_timeouts;
+        else if (*g.perr_h == 1) note_persist_timeout();
         if (int e = gen_drain()) return e;
         const int saved_n = gq_n;
         gq_n = 0;   // the synchronous path must not see the queue
@@ -1681,7 +1695,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "persist1m") {   // B = 2..64: the multi-sequence form of persist1 (0: per-step graphs)
         eng->use_persist1m = value != 0;
     } else if (n == "persist_spin_ticks") {   // test hook: bound of a hand-off wait (100 MHz ticks)
-        eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : 300000000ull;
+        eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : gsv_engine::PERSIST_SPIN_TICKS;
     } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback
         eng->persist1_f16_limit = value;
     } else if (n == "pf_delay") {   // single-sequence decode: s_sleep(32) ticks before the next-layer prefetch

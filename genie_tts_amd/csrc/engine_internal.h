@@ -221,7 +221,12 @@ struct gsv_engine {
     hipGraphExec_t step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st);
     int decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool allow_persist = true);
     long persist_timeouts = 0;         // persistent launches that timed out (co-running work) and re-ran as graphs
-    unsigned long long persist_spin_ticks = 300000000ull;   // option "persist_spin_ticks" (test hook)
+    int persist_timeout_run = 0;       // consecutive ones (2: the engine stays on the graphs)
+    void note_persist_timeout();
+    // hand-off wait bound, 100 MHz ticks: 200 ms, >100x the longest legitimate wait (a
+    // workgroup waiting out one step of a 64-sequence decode, ~1.6 ms)
+    static constexpr unsigned long long PERSIST_SPIN_TICKS = 20000000ull;
+    unsigned long long persist_spin_ticks = PERSIST_SPIN_TICKS;   // option "persist_spin_ticks" (test hook)
     int decode_persistent(int B, const gsv_sampler* sp, hipStream_t st);
     int decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st);
     bool persist_family(int B) const;

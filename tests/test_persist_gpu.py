@@ -161,6 +161,28 @@ def test_persistent_timeout_reruns_as_graphs(eng):
     assert out[0].tolist() == sem.reshape(-1).tolist()
 
 
+def test_repeated_timeouts_leave_the_persistent_path(eng):
+    """Two timed-out launches in a row (the grid cannot be co-resident) make the engine stay
+    on the per-step graphs, so later utterances do not pay the wait bound; option persist = 1
+    re-enables the persistent path."""
+    from genie_tts_amd.engine import make_sampler
+    inp = t2s_inputs(R=12, S=10, H=41, tag="tmo2")
+    sp = make_sampler(force_steps=10)
+    eng.set_option("persist", 1)
+    want = eng.t2s_generate([inp], sp)[0].tolist()
+    before = eng.counter("persist_timeouts")
+    eng.set_option("persist_spin_ticks", 50)
+    try:
+        for _ in range(3):
+            assert eng.t2s_generate([inp], sp)[0].tolist() == want
+    finally:
+        eng.set_option("persist_spin_ticks", 0)
+    assert eng.counter("persist_timeouts") == before + 2     # the third ran on the graphs directly
+    eng.set_option("persist", 1)
+    assert eng.t2s_generate([inp], sp)[0].tolist() == want
+    assert eng.counter("persist_timeouts") == before + 2
+
+
 def _alone(eng, inps, sp):
     return [eng.t2s_generate([inp], sp)[0].tolist() for inp in inps]
 
