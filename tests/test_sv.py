@@ -89,3 +89,19 @@ def test_embedding_depends_on_audio():
     e2 = S.sv_embedding(w, a * 0.5)
     assert e1.shape == (1, 20480) and np.isfinite(e1).all()
     assert np.abs(e1 - e2).max() > 1e-3
+
+
+def test_sv_loader_reads_speaker_encoder_onnx(tmp_path):
+    """load_sv_weights reads GenieData's speaker_encoder.onnx (inline fp32 initializers,
+    ModelManager.py:155-170) by sv_spec names, from the file or its directory; tensors
+    the model does not use are ignored (written here by tests/onnx_writer.py)."""
+    from tests.onnx_writer import model_inline
+    w = synth.synth_sv_weights()
+    arrs = dict(w)
+    arrs["seg_1.weight"] = np.zeros((192, 8), np.float32)       # the pooling head forward3 skips
+    (tmp_path / "speaker_encoder.onnx").write_bytes(model_inline(arrs))
+    for path in (str(tmp_path / "speaker_encoder.onnx"), str(tmp_path)):
+        got = W.load_sv_weights(path)
+        assert list(got) == list(W.sv_spec())
+        for k in ("conv1.weight", "layer4.2.fuse_models.2.local_att.4.running_var", "fuse34.local_att.3.weight"):
+            np.testing.assert_array_equal(np.asarray(got[k], np.float32), w[k])
