@@ -381,6 +381,8 @@ def main():
                     help=argparse.SUPPRESS)   # tests: a CPU stub replica whose step sleeps this long
     args = ap.parse_args()
 
+    if args.shard and args.workload != "mixed100":
+        ap.error("--shard applies to --workload mixed100 (the LPT-sharded set)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.stub_ms > 0:
