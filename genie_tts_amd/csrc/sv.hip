@@ -54,7 +54,23 @@ struct SvConvArgs {
     const float* ax; long ldx;      // AFF mix: out = ax (1 + tanh v) + ay (1 - tanh v)
     const float* ay; long ldy;
     float* out; long ldo;
+    int ksplit;                // > 1: K split over blockIdx.z, raw sums into slab[z][M][cout] (k_sv_reduce)
+    float* slab;
 };
+
+// The epilogue of one output element: bias (folded BN), residual, activation, AFF mix.
+__device__ __forceinline__ void sv_epilogue(const SvConvArgs& a, int row, int col, float acc) {
+    float v = acc + (a.bias ? a.bias[col] : 0.f);
+    if (a.res) v += a.res[(long)row * a.ldr + col];
+    if (a.act == SV_ACT_RELU) v = fmaxf(v, 0.f);
+    else if (a.act == SV_ACT_RELU20) v = fminf(fmaxf(v, 0.f), 20.f);
+    else if (a.act == SV_ACT_SILU) v = v / (1.f + expf(-v));
+    if (a.ax) {
+        const float t = tanhf(v);
+        v = a.ax[(long)row * a.ldx + col] * (1.f + t) + a.ay[(long)row * a.ldy + col] * (1.f - t);
+    }
+    a.out[(long)row * a.ldo + col] = v;
+}
 
 typedef _Float16 svh8 __attribute__((ext_vector_type(8)));
 
@@ -87,7 +103,10 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     bool big = false;
-    for (int k0 = 0; k0 < a.K; k0 += 32) {
+    // this block's K range: whole 32-k steps, split over blockIdx.z
+    const int steps = (a.K + 31) / 32, kz = blockIdx.z, ks = a.ksplit > 1 ? a.ksplit : 1;
+    const int k_lo = 32 * (int)((long)steps * kz / ks), k_hi = min(a.K, 32 * (int)((long)steps * (kz + 1) / ks));
+    for (int k0 = k_lo; k0 < k_hi; k0 += 32) {
         const int kk = k0 + sc;       // 8 consecutive k of one tap (cin % 8 == 0)
         float av[8];
 #pragma unroll
@@ -174,22 +193,24 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
     if (H && big) atomicOr(a.ovf, 1);
     const int col = n0 + wn * 32 + (lane & 31);
     if (col >= a.cout) return;
-    const float bv = a.bias ? a.bias[col] : 0.f;
+    float* slab = ks > 1 ? a.slab + (long)kz * M * a.cout : nullptr;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row >= M) continue;
-        float v = acc[r] + bv;
-        if (a.res) v += a.res[(long)row * a.ldr + col];
-        if (a.act == SV_ACT_RELU) v = fmaxf(v, 0.f);
-        else if (a.act == SV_ACT_RELU20) v = fminf(fmaxf(v, 0.f), 20.f);
-        else if (a.act == SV_ACT_SILU) v = v / (1.f + expf(-v));
-        if (a.ax) {
-            const float t = tanhf(v);
-            v = a.ax[(long)row * a.ldx + col] * (1.f + t) + a.ay[(long)row * a.ldy + col] * (1.f - t);
-        }
-        a.out[(long)row * a.ldo + col] = v;
+        if (slab) slab[(long)row * a.cout + col] = acc[r];
+        else sv_epilogue(a, row, col, acc[r]);
     }
+}
+
+// Split-K reduce: the slabs summed in z order, then the conv's epilogue.
+__global__ __launch_bounds__(256) void k_sv_reduce(SvConvArgs a) {
+    const long M = (long)a.Fo * a.To, e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= M * a.cout) return;
+    const long stride = M * a.cout;
+    float v = a.slab[e];
+    for (int z = 1; z < a.ksplit; ++z) v += a.slab[z * stride + e];
+    sv_epilogue(a, (int)(e / a.cout), (int)(e % a.cout), v);
 }
 
 // Kaldi fbank, one block per frame: remove DC, pre-emphasis 0.97, povey window, zero pad
@@ -275,6 +296,7 @@ __global__ __launch_bounds__(256) void k_sv_pool(const float* x, int F, int T, i
 }
 
 int sv_down(int n) { return (n - 1) / 2 + 1; }   // 1x1 stride 2 pad 0 == 3x3 stride 2 pad 1
+constexpr size_t SV_SLAB_CAP = (size_t)8 << 20;   // split-K slab floats (32 MB)
 
 }  // namespace
 
@@ -448,11 +470,21 @@ SvConvArgs sv_args(const SvConv& c, const SvMap& in, int stride, int pad, float*
     return a;
 }
 
-void sv_conv(const SvConvArgs& a, hipStream_t st) {
+// A conv with few blocks (stages 3-4: 33-352 for 256 CUs) waits out a memory round trip
+// per 32-k step on few CUs; it splits K over up to 8 blocks (>= 4 steps each, up to ~512
+// blocks) when the slabs fit (slab_cap floats), and k_sv_reduce applies the epilogue.
+void sv_conv(SvConvArgs a, hipStream_t st, float* slab, size_t slab_cap) {
     const int M = a.Fo * a.To;
-    const dim3 grid((M + 63) / 64, (a.cout + 63) / 64);
+    const int blocks = ((M + 63) / 64) * ((a.cout + 63) / 64), steps = (a.K + 31) / 32;
+    int ks = 1;
+    while (ks < 8 && blocks * ks < 512 && steps / (2 * ks) >= 4 && (size_t)2 * ks * M * a.cout <= slab_cap) ks *= 2;
+    a.ksplit = ks;
+    a.slab = slab;
+    const dim3 grid((M + 63) / 64, (a.cout + 63) / 64, ks);
     if (a.wh) hipLaunchKernelGGL(k_sv_conv<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_sv_conv<false>, grid, dim3(256), 0, st, a);
+    if (ks > 1)
+        hipLaunchKernelGGL(k_sv_reduce, dim3((unsigned)(((long)M * a.cout + 255) / 256)), dim3(256), 0, st, a);
 }
 }  // namespace
 
@@ -460,7 +492,8 @@ size_t gsv_engine::sv_ws_floats(int T) {
     const size_t P1 = (size_t)SV_NMEL * T;
     // x (fbank) + 3 block buffers [P1][256] + H, O [P1][96] + Z [P1][24] + AFF tmp + ds / fuse maps
     const int T4 = sv_down(sv_down(sv_down(T)));
-    return P1 + 3 * P1 * 256 + 2 * P1 * 96 + P1 * 24 + P1 * 24 + 2 * (size_t)10 * T4 * 2048 + (size_t)10 * T4 * 512 + 64;
+    return P1 + 3 * P1 * 256 + 2 * P1 * 96 + P1 * 24 + P1 * 24 + 2 * (size_t)10 * T4 * 2048 + (size_t)10 * T4 * 512 + 64 +
+           SV_SLAB_CAP;
 }
 
 int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, int* ovf, float lim) {
@@ -485,6 +518,8 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
     float* ds = A + P1 * 24;
     float* fuse = ds + (size_t)10 * T4 * 2048;
     float* fa = fuse + (size_t)10 * T4 * 2048;
+    float* slab = fa + (size_t)10 * T4 * 512 + 64;
+    auto conv = [&](const SvConvArgs& c) { sv_conv(c, st, slab, SV_SLAB_CAP); };
 
     hipLaunchKernelGGL(k_sv_fbank, dim3(T), dim3(256), 0, st, wav, T, S.win, S.cos_tab, S.banks, x);
     hipLaunchKernelGGL(k_sv_stem, dim3((unsigned)((P1 + 3) / 4)), dim3(256), 0, st, x, T, S.stem_w, S.stem_b, big[0]);
@@ -501,7 +536,7 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
             // conv1 (1x1, stride) + BN + Hardtanh -> H [P][4w]
             SvConvArgs c1 = sv_args(B.conv1, cur, B.stride, 0, H, w4, ovf, lim);
             c1.act = SV_ACT_RELU20;
-            sv_conv(c1, st);
+            conv(c1);
             const SvMap hmap{H, c1.Fo, c1.To, w4, w4};
             // the split chain: sp_0 = conv(spx_0); sp_i = conv(sp_{i-1} + spx_i) or conv(AFF(sp_{i-1}, spx_i))
             for (int i = 0; i < 4; ++i) {
@@ -518,16 +553,16 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
                     ca.amode = SV_A_CAT;
                     ca.src2 = H + i * w; ca.lda2 = w4; ca.csplit = w;
                     ca.act = SV_ACT_SILU;
-                    sv_conv(ca, st);
+                    conv(ca);
                     SvMap tm{A, hmap.F, hmap.T, w / 4, w / 4};
                     SvConvArgs cb = sv_args(B.aff_b[i - 1], tm, 1, 0, Z, w, ovf, lim);
                     cb.ax = O + (i - 1) * w; cb.ldx = w4;
                     cb.ay = H + i * w; cb.ldy = w4;
-                    sv_conv(cb, st);
+                    conv(cb);
                     c.src = Z; c.lda = w;
                 }
                 c.act = SV_ACT_RELU20;
-                sv_conv(c, st);
+                conv(c);
             }
             // shortcut (1x1 conv + BN, or identity) and conv3 + BN + residual + Hardtanh
             float* y = big[ob];
@@ -536,7 +571,7 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
             long ldr = cur.ld;
             if (B.has_sc) {
                 SvConvArgs sc = sv_args(B.sc, cur, B.stride, 0, y, cout, ovf, lim);
-                sv_conv(sc, st);
+                conv(sc);
                 res = y;
                 ldr = cout;
             }
@@ -544,7 +579,7 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
             SvConvArgs c3 = sv_args(B.conv3, omap, 1, 0, y, cout, ovf, lim);
             c3.res = res; c3.ldr = ldr;
             c3.act = SV_ACT_RELU20;
-            sv_conv(c3, st);
+            conv(c3);
             cur = SvMap{y, hmap.F, hmap.T, (int)cout, cout};
             cur_buf = ob;
         }
@@ -555,19 +590,19 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
     }
     // layer3_ds (3x3 stride 2, no BN) and fuse34 = AFF(out4, out3_ds)
     SvConvArgs d = sv_args(S.ds34, out3, 2, 1, ds, 2048, ovf, lim);
-    sv_conv(d, st);
+    conv(d);
     if (d.Fo != cur.F || d.To != cur.T) return set_error(GSV_E_ARG, "SV layer3_ds / layer4 shape mismatch");
     SvMap cat{cur.p, cur.F, cur.T, 4096, cur.ld};
     SvConvArgs fa_ = sv_args(S.fuse_a, cat, 1, 0, fa, 512, ovf, lim);
     fa_.amode = SV_A_CAT;
     fa_.src2 = ds; fa_.lda2 = 2048; fa_.csplit = 2048;
     fa_.act = SV_ACT_SILU;
-    sv_conv(fa_, st);
+    conv(fa_);
     SvMap tm{fa, cur.F, cur.T, 512, 512};
     SvConvArgs fb = sv_args(S.fuse_b, tm, 1, 0, fuse, 2048, ovf, lim);
     fb.ax = cur.p; fb.ldx = cur.ld;
     fb.ay = ds; fb.ldy = 2048;
-    sv_conv(fb, st);
+    conv(fb);
     hipLaunchKernelGGL(k_sv_pool, dim3((2048 * cur.F + 255) / 256), dim3(256), 0, st, fuse, cur.F, cur.T, 2048, out);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "SV launch");
 }
