@@ -329,6 +329,23 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
                        (long)T * 768, H.pos_b, tmp, T * 768);
     layernorm_rows_d(tmp, h, T, 768, H.enc_ln_w, H.enc_ln_b, 1e-5f, st);
     // ---- 12 post-norm encoder layers
+    // h = LN(h + A W^T + b).  A short clip's out-projection / FFN2 (768 outputs: 12 column
+    // tiles x ceil(T / 64) row tiles, < 256 blocks) splits K into slabs that the LayerNorm
+    // reduces in order (as RoBERTa's), so the GEMM covers the chip.
+    const bool split = ((T + 63) / 64) * 12 < 256;
+    auto resid_ln = [&](const float* A, int K, const __half* W, const float* bias, int z, const float* lw,
+                        const float* lb) {
+        if (split) {
+            GemmArgs g = gemm_f16(T, 768, K, A, K, W, nullptr, slabs, 768, EPI_SLAB);
+            g.ksplit = z;
+            g.slab_stride = (long)T * 768;
+            gemm_nt(g, st);
+            layernorm_rows_d_slabs(slabs, z, (long)T * 768, bias, h, h, T, 768, lw, lb, 1e-5f, st);
+        } else {
+            gemm_nt(gemm_f16(T, 768, K, A, K, W, bias, tmp, 768, EPI_RESID, h, 768), st);
+            layernorm_rows_d(tmp, h, T, 768, lw, lb, 1e-5f, st);
+        }
+    };
     for (int l = 0; l < 12; ++l) {
         const HubertLayerW& L = H.L[l];
         gemm_nt(gemm_f16(T, 2304, 768, h, 768, L.wqkv, L.bqkv, qkv, 2304, EPI_STORE), st);
@@ -340,11 +357,9 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
         m.nq = T; m.nk = T; m.heads = 12; m.dk = 64;
         m.postdiv = 0; m.scale = 8.f;   // q * 64^-0.5 (exact: a power of two)
         mha(m, st);
-        gemm_nt(gemm_f16(T, 768, 768, att, 768, L.wo, L.bo, tmp, 768, EPI_RESID, h, 768), st);
-        layernorm_rows_d(tmp, h, T, 768, L.ln1w, L.ln1b, 1e-5f, st);
+        resid_ln(att, 768, L.wo, L.bo, 4, L.ln1w, L.ln1b);
         gemm_nt(gemm_f16(T, 3072, 768, h, 768, L.w1, L.b1, f, 3072, EPI_GELU), st);
-        gemm_nt(gemm_f16(T, 768, 3072, f, 3072, L.w2, L.b2, tmp, 768, EPI_RESID, h, 768), st);
-        layernorm_rows_d(tmp, h, T, 768, L.ln2w, L.ln2b, 1e-5f, st);
+        resid_ln(f, 3072, L.w2, L.b2, NZ_POS, L.ln2w, L.ln2b);
     }
     hipLaunchKernelGGL(k_hb_transpose, dim3((T + 31) / 32, 24), dim3(256), 0, st, h, T, out);
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "hubert launch");
