@@ -55,7 +55,8 @@ class ReferenceAudio:
         if self.sv_emb is None and self.sv_fn is not None and self.audio_16k is not None:
             self.sv_emb = np.asarray(self.sv_fn(self.audio_16k), np.float32).reshape(1, -1)
         if self.sv_emb is None:
-            raise ValueError("V2ProPlus needs the speaker-verification embedding (sv_emb) of the reference")
+            raise ValueError("V2ProPlus needs the speaker-verification embedding (sv_emb) of the reference: "
+                             "load_sv_model(), set_sv_extractor() or pass sv_emb")
         self.global_emb, self.global_emb_advanced = prompt_encoder.run(None, {
             "ref_audio": self.audio_32k, "sv_emb": self.sv_emb})
 
