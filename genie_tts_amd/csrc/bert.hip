@@ -9,11 +9,13 @@
 // from this container; the op order follows transformers' BertModel:
 //   x = LayerNorm(word[id] + position[t] + token_type[0])            eps 1e-12
 //   L - 2 x post-norm layers: MHA (16 x 64) + residual -> LN; FFN 4096 GELU + residual -> LN
-// Activations time-major [N][1024]; GEMMs k_gemm_x2 (fp16 weights, split-fp16
-// MFMA), attention k_mha.
+// Activations time-major [N][1024]; GEMMs k_gemm_x3 on the f16 MFMA with the f32
+// activations split hi + lo and the fp32 weights split hi + lo 2^-11 (W16: three MFMAs
+// per product, ~22 significant bits of each weight kept); attention k_mha.
 #include "common.h"
 #include "engine_internal.h"
 
+#include <algorithm>
 #include <numeric>
 
 namespace gsv {
@@ -79,7 +81,10 @@ int gsv_engine::finalize_roberta() {
     for (int l = 0; l < n - 2; ++l) {
         const std::string p = "encoder.layer." + std::to_string(l) + ".";
         BertLayerW& L = B.L[l];
-        std::vector<__half> wqkv((size_t)3072 * 1024);
+        // q, k, v fused into one [3072][1024] weight; every projection keeps the
+        // initializers' fp32 values (RoBERTa.onnx is fp32, ModelManager.py:139-142):
+        // fp16-exact tensors take one plane, others the hi + lo split (W16)
+        std::vector<float> wqkv((size_t)3072 * 1024);
         std::vector<float> bqkv(3072);
         const char* nm[3] = {"query", "key", "value"};
         for (int m = 0; m < 3; ++m) {
@@ -87,20 +92,19 @@ int gsv_engine::finalize_roberta() {
             const Staged* b = find(p + "attention.self." + nm[m] + ".bias");
             if (!w || !b || w->data.size() != (size_t)1024 * 1024 || b->data.size() != 1024)
                 return set_error(GSV_E_WEIGHT, "missing/bad weight " + p + "attention.self." + nm[m]);
-            for (size_t e = 0; e < (size_t)1024 * 1024; ++e) wqkv[(size_t)m * 1024 * 1024 + e] = __float2half(w->data[e]);
+            std::copy(w->data.begin(), w->data.end(), wqkv.begin() + (size_t)m * 1024 * 1024);
             for (int e = 0; e < 1024; ++e) bqkv[m * 1024 + e] = b->data[e];
         }
-        L.wqkv = (__half*)dalloc(wqkv.size() * 2);
-        hipMemcpy(L.wqkv, wqkv.data(), wqkv.size() * 2, hipMemcpyHostToDevice);
+        L.wqkv = upload_w16(p + "attention.self.{query,key,value}.weight", wqkv, &err);
         L.bqkv = (float*)dalloc(bqkv.size() * 4);
         hipMemcpy(L.bqkv, bqkv.data(), bqkv.size() * 4, hipMemcpyHostToDevice);
-        L.wo = up_f16(p + "attention.output.dense.weight", &err);
+        L.wo = up_w16(p + "attention.output.dense.weight", &err);
         L.bo = up_f32(p + "attention.output.dense.bias", &err);
         L.ln1w = up_f32(p + "attention.output.LayerNorm.weight", &err);
         L.ln1b = up_f32(p + "attention.output.LayerNorm.bias", &err);
-        L.w1 = up_f16(p + "intermediate.dense.weight", &err);
+        L.w1 = up_w16(p + "intermediate.dense.weight", &err);
         L.b1 = up_f32(p + "intermediate.dense.bias", &err);
-        L.w2 = up_f16(p + "output.dense.weight", &err);
+        L.w2 = up_w16(p + "output.dense.weight", &err);
         L.b2 = up_f32(p + "output.dense.bias", &err);
         L.ln2w = up_f32(p + "output.LayerNorm.weight", &err);
         L.ln2b = up_f32(p + "output.LayerNorm.bias", &err);
@@ -140,7 +144,7 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
     hipLaunchKernelGGL(k_bert_embed, dim3(N), dim3(256), 0, st, ids, B.word, B.pos, B.type, B.ln_w, B.ln_b, EPS,
                        row_pos ? dpos : nullptr, h);
     for (const BertLayerW& L : B.L) {
-        gemm_nt(gemm_f16(N, 3072, 1024, h, 1024, L.wqkv, L.bqkv, qkv, 3072, EPI_STORE), st);
+        gemm_nt(gemm_w16(N, 3072, 1024, h, 1024, L.wqkv, L.bqkv, qkv, 3072, EPI_STORE), st);
         MhaArgs m{};
         m.q = qkv; m.q_ts = 3072; m.q_cs = 1;
         m.k = qkv + 1024; m.k_ts = 3072; m.k_cs = 1;
@@ -150,21 +154,21 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
         m.postdiv = 0; m.scale = 8.f;   // scores / sqrt(64) (exact: a power of two)
         m.row_seg = row_seg ? dseg : nullptr;   // packed: each sentence attends within itself
         mha(m, st);
-        auto resid_ln = [&](const float* A, int K, const void* W, const float* bias, int z, const float* lw,
+        auto resid_ln = [&](const float* A, int K, const W16& W, const float* bias, int z, const float* lw,
                             const float* lb) {
             if (z > 1) {
-                GemmArgs g = gemm_f16(N, 1024, K, A, K, W, nullptr, slabs, 1024, EPI_SLAB);
+                GemmArgs g = gemm_w16(N, 1024, K, A, K, W, nullptr, slabs, 1024, EPI_SLAB);
                 g.ksplit = z;
                 g.slab_stride = (long)N * 1024;
                 gemm_nt(g, st);
                 layernorm_rows_d_slabs(slabs, z, (long)N * 1024, bias, h, h, N, 1024, lw, lb, EPS, st);
             } else {
-                gemm_nt(gemm_f16(N, 1024, K, A, K, W, bias, tmp, 1024, EPI_RESID, h, 1024), st);
+                gemm_nt(gemm_w16(N, 1024, K, A, K, W, bias, tmp, 1024, EPI_RESID, h, 1024), st);
                 layernorm_rows_d(tmp, h, N, 1024, lw, lb, EPS, st);
             }
         };
         resid_ln(att, 1024, L.wo, L.bo, zo, L.ln1w, L.ln1b);
-        gemm_nt(gemm_f16(N, 4096, 1024, h, 1024, L.w1, L.b1, f, 4096, EPI_GELU), st);
+        gemm_nt(gemm_w16(N, 4096, 1024, h, 1024, L.w1, L.b1, f, 4096, EPI_GELU), st);
         resid_ln(f, 4096, L.w2, L.b2, z2, L.ln2w, L.ln2b);
     }
     hipLaunchKernelGGL(k_bert_repeat, dim3(n_out), dim3(256), 0, st, h, drows, out);

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -75,6 +76,7 @@ gsv_engine::~gsv_engine() {
     if (sv_ovf) hipFree(sv_ovf);
     if (sv_ovf_host) hipHostFree(sv_ovf_host);
     if (perr_host) hipHostFree(perr_host);
+    if (stop_word) hipHostFree(stop_word);
     if (res_pin) hipHostFree(res_pin);
     for (GenSlot& g : gq) {
         if (g.res) hipHostFree(g.res);
@@ -115,9 +117,32 @@ float* gsv_engine::up_f32(const std::string& n, int* err) {
     return d;
 }
 
+// fp16 copies never round: a tensor bound for an fp16-only path must be fp16-exact (the
+// Genie fp16 bins are); an fp32 tensor of a split-weight path goes through up_w16.
+static int64_t first_non_f16(const float* v, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (__half2float(__float2half(v[i])) != v[i] && !(v[i] != v[i])) return (int64_t)i;
+    return -1;
+}
+
+extern "C" int gsv_f16_exact(const float* v, int64_t n, int64_t* first_bad) {
+    if (!v && n > 0) return set_error(GSV_E_ARG, "null values");
+    const int64_t b = n > 0 ? first_non_f16(v, (size_t)n) : -1;
+    if (first_bad) *first_bad = b;
+    return b < 0 ? 1 : 0;
+}
+
+int gsv::f16_inexact_error(const std::string& n, const float* v, int64_t i) {
+    char buf[96];
+    std::snprintf(buf, sizeof buf, " is not fp16-exact (element %lld = %.9g)", (long long)i, (double)v[i]);
+    return set_error(GSV_E_WEIGHT, "weight " + n + buf + "; its path takes fp16 weights only");
+}
+
 __half* gsv_engine::up_f16(const std::string& n, int* err) {
     const Staged* s = find(n);
     if (!s) { *err = set_error(GSV_E_WEIGHT, "missing weight " + n); return nullptr; }
+    const int64_t bad = first_non_f16(s->data.data(), s->data.size());
+    if (bad >= 0) { *err = f16_inexact_error(n, s->data.data(), bad); return nullptr; }
     std::vector<__half> h(s->data.size());
     for (size_t i = 0; i < h.size(); ++i) h[i] = __float2half(s->data[i]);
     __half* d = (__half*)dalloc(h.size() * 2);
@@ -129,6 +154,8 @@ __half* gsv_engine::up_f16(const std::string& n, int* err) {
 __half* gsv_engine::up_f16_t(const std::string& n, int* err) {
     const Staged* s = find(n);
     if (!s || s->dims.size() != 2) { *err = set_error(GSV_E_WEIGHT, "missing 2-D weight " + n); return nullptr; }
+    const int64_t bad = first_non_f16(s->data.data(), s->data.size());
+    if (bad >= 0) { *err = f16_inexact_error(n, s->data.data(), bad); return nullptr; }
     const size_t R = s->dims[0], C = s->dims[1];
     std::vector<__half> h(R * C);
     for (size_t r = 0; r < R; ++r)
@@ -137,6 +164,37 @@ __half* gsv_engine::up_f16_t(const std::string& n, int* err) {
     if (!d) { *err = set_error(GSV_E_HIP, "hipMalloc failed for " + n); return nullptr; }
     hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice);
     return d;
+}
+
+// W16 planes of v (already in the kernel's layout): hi only when every value is fp16-exact,
+// else hi = fp16(w) and lo = fp16((w - hi) 2^11).  |w| beyond the fp16 range has no split.
+W16 gsv_engine::upload_w16(const std::string& n, const std::vector<float>& v, int* err) {
+    W16 w;
+    if (*err) return w;
+    std::vector<__half> hi(v.size()), lo;
+    const bool exact = first_non_f16(v.data(), v.size()) < 0;
+    if (!exact) lo.resize(v.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (!(std::fabs(v[i]) <= 65504.f)) {
+            *err = set_error(GSV_E_WEIGHT, "weight " + n + " has a value beyond the fp16 range");
+            return w;
+        }
+        hi[i] = __float2half(v[i]);
+        if (!exact) lo[i] = __float2half((v[i] - __half2float(hi[i])) * W16_LO_SCALE);
+    }
+    w.hi = (__half*)dalloc(hi.size() * 2);
+    if (!exact) w.lo = (__half*)dalloc(lo.size() * 2);
+    if (!w.hi || (!exact && !w.lo)) { *err = set_error(GSV_E_HIP, "hipMalloc failed for " + n); return W16{}; }
+    hipMemcpy(w.hi, hi.data(), hi.size() * 2, hipMemcpyHostToDevice);
+    if (!exact) hipMemcpy(w.lo, lo.data(), lo.size() * 2, hipMemcpyHostToDevice);
+    if (!exact) ++w16_split_tensors;
+    return w;
+}
+
+W16 gsv_engine::up_w16(const std::string& n, int* err) {
+    const Staged* s = find(n);
+    if (!s) { *err = set_error(GSV_E_WEIGHT, "missing weight " + n); return W16{}; }
+    return upload_w16(n, s->data, err);
 }
 
 static std::vector<float> default_div_term() {
@@ -682,6 +740,7 @@ SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
     sa.force_steps = sp ? sp->force_steps : 0;
     sa.force_b = forceb;
     sa.prefill = 0;
+    sa.stop_req = stop_word;
     return sa;
 }
 
@@ -828,7 +887,8 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     // graphs so forced lengths run no extra step).  The host polls the done flags
     // of chunk k while chunk k+1 already runs, so the GPU never waits on the host.
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
-    if (allow_persist && use_persist && persist_family(B)) return decode_persistent(B, sp, st);
+    if (stop_requested()) return stopped_error();
+    if (allow_persist && use_persist && persist_family(B) && persist_admit()) return decode_persistent(B, sp, st);
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -846,6 +906,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     // queue behind the running chunk and execute back to back, as inside the graph.
     bool probe_pending = timing && kev[0] != nullptr;
     while (launched < limit && !finished) {
+        if (stop_requested()) break;   // the queued chunks finish their sequences at the sampler
         int n = std::min(chunk, limit - launched);
         if (probe_pending && launched == chunk) {
             n = 1;
@@ -875,6 +936,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
         }
     }
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "decode sync");
+    if (stop_requested()) return stopped_error();
     if (probed) {
         // one sample per decode loop: the probed step's layer-`probe_layer` FFN launch
         float ms = 0.f;
@@ -957,6 +1019,7 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, in
     a.ring = (unsigned long long*)pws;
     a.epoch = pepoch;
     a.err = perr;
+    a.stop_req = stop_word;
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
     a.pf_delay = persist1_pf_delay;
@@ -971,6 +1034,7 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, in
     const hipError_t le = B == 1 ? decode_persist1(a, st, k0, k1) : decode_persist1m(a, st, k0, k1);
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
+    ++persist_launches;
     hipMemcpyAsync(perr_dst, perr, 4, hipMemcpyDeviceToHost, st);
     if (res_dst) enqueue_results(res_b, st, res_dst);   // valid if this launch succeeds
     // a queued overlapped vocoder call and T2S prefetch: enqueue them now (vocoder
@@ -994,15 +1058,47 @@ void gsv_engine::probe_sample(hipEvent_t k0, hipEvent_t k1) {
 
 // A persistent launch whose hand-off outwaited its bound: its grid was not all resident
 // (placement, other work on the CUs) and the steps re-run as per-step graphs.  Two in a
-// row mean the condition persists: the engine stays on the graphs (option "persist" = 1
-// re-enables) instead of paying the bound on every utterance.
+// row mean the condition persists: a hold begins -- the next persist_backoff generates
+// (or persist_backoff_s seconds, whichever ends first) run on the graphs, then the
+// persistent path is probed again.  A probe that times out again starts a hold twice as
+// long; a launch that completes ends the back-off.
+static double steady_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 void gsv_engine::note_persist_timeout() {
     ++persist_timeouts;
-    if (++persist_timeout_run >= 2 && use_persist) {
-        use_persist = false;
-        std::fprintf(stderr, "[genie] persistent decode timed out %d times in a row: using per-step graphs\n",
-                     persist_timeout_run);
+    if (++persist_timeout_run >= 2) {
+        const int n = persist_backoff > 0 ? persist_backoff : persist_backoff_base;
+        const double sec = persist_backoff_s * n / std::max(1, persist_backoff_base);
+        persist_hold = n;
+        persist_hold_end = steady_s() + std::min(60.0, sec);
+        persist_backoff = std::min(4096, 2 * n);
+        ++persist_disabled;
+        std::fprintf(stderr,
+                     "[genie] persistent decode timed out %d times in a row: per-step graphs for the next %d "
+                     "generates (%.1f s at most)\n",
+                     persist_timeout_run, n, std::min(60.0, sec));
     }
+}
+
+void gsv_engine::note_persist_ok() {
+    persist_timeout_run = 0;
+    persist_backoff = 0;
+}
+
+bool gsv_engine::persist_admit() {
+    if (persist_hold <= 0) return true;
+    if (--persist_hold <= 0 || steady_s() >= persist_hold_end) {
+        persist_hold = 0;   // probe the persistent path again
+        return true;
+    }
+    return false;
+}
+
+int gsv_engine::stopped_error() {
+    ++stops;
+    return set_error(GSV_E_STOPPED, "stopped by gsv_request_stop");
 }
 
 int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t st) {
@@ -1013,6 +1109,8 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
                                 res_batch ? res_pin : nullptr, res_batch))
         return r;
     if (host_wait(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
+    // code 3 (or any code under a pending stop): a stop request abandoned the launch
+    if (*perr_host == 3 || (*perr_host != 0 && stop_requested())) return stopped_error();
     // code 2: the kernel met an activation beyond the fp16 range of its split-operand
     // MFMA GEMVs.  It stopped before writing the sequence state back (KV rows and
     // tokens of the partial run are rewritten), so the same steps run again as
@@ -1031,7 +1129,8 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     }
     if (*perr_host != 0)
         return set_error(GSV_E_HIP, "persistent decode failed (code " + std::to_string(*perr_host) + ")");
-    persist_timeout_run = 0;
+    note_persist_ok();
+    if (stop_requested()) return stopped_error();
     res_ready = res_batch > 0;
     if (probe) probe_sample(kev[0], kev[1]);
     return 0;
@@ -1222,6 +1321,12 @@ extern "C" int gsv_engine_create(int device, int version, gsv_engine** out) {
         return set_error(GSV_E_HIP, "stream create failed");
     }
     e->own_stream = true;
+    if (hipHostMalloc((void**)&e->stop_word, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        hipStreamDestroy(e->stream);
+        delete e;
+        return set_error(GSV_E_HIP, "stop word alloc failed");
+    }
+    *e->stop_word = 0;
     for (auto& x : e->ev) hipEventCreate(&x);
     hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming);
     hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming);
@@ -1390,6 +1495,7 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (batch <= 0 || !utts || !out_tokens || !out_len) return set_error(GSV_E_ARG, "bad args");
     gsv_sampler sp;
     if (int e = norm_sampler(s, sp)) return e;
+    if (eng->stop_requested()) return eng->stopped_error();   // Inference.py:96-97 at step 0
     if (int e = eng->gen_drain()) return e;   // started generates finish first (results stay queued)
     // prefetched (gsv_t2s_prefetch, launched into slot 1 during the last decode)?  A
     // queued prefetch is for a later call: it stays queued (launched during this
@@ -1511,14 +1617,15 @@ int gsv_engine::gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t c
         if (int e = prefill_slot(0, pH, L, prompts_buf, P, &sp, nullptr, st)) return e;
     }
     hipEventRecord(g.d0, st);
-    const bool persist_ok = use_persist && use_persist1 && decode_cus() >= persist1_grid(3);
+    const bool persist_ok = use_persist && use_persist1 && decode_cus() >= persist1_grid(3) && !stop_requested() &&
+                            persist_admit();
     int rc = 0;
     if (persist_ok) {
         rc = persist_enqueue(1, &sp, st, g.perr_h, timing ? g.k0 : nullptr, timing ? g.k1 : nullptr, g.res, 1);
-    } else {   // no persistent path: this one runs to completion now
+    } else {   // no persistent path (or a stop is pending): this one runs to completion now
         res_batch = 1;
         res_ready = false;
-        rc = decode_loop(1, &sp, st);
+        rc = decode_loop(1, &sp, st, false);
         res_batch = 0;
         perr_zeroed = false;
         if (rc == 0) enqueue_results(1, st, g.res);
@@ -1543,7 +1650,8 @@ int gsv_engine::gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len
     GenSlot& g = gq[gq_head];
     gq_head = (gq_head + 1) % 2;
     --gq_n;
-    if (g.sync && g.sync_rc) return g.sync_rc;
+    if (g.sync && g.sync_rc) return g.sync_rc == GSV_E_STOPPED ? set_error(GSV_E_STOPPED, "stopped by gsv_request_stop")
+                                                               : g.sync_rc;
     for (;;) {   // poll, as host_wait
         const hipError_t e = hipEventQuery(g.done);
         if (e == hipSuccess) break;
@@ -1551,6 +1659,8 @@ int gsv_engine::gen_finish(int64_t* out_tokens, int out_stride, int32_t* out_len
         if (spin_wait) std::this_thread::yield();
         else if (hipEventSynchronize(g.done) != hipSuccess) return set_error(GSV_E_HIP, "generate");
     }
+    if (!g.sync && (*g.perr_h == 3 || stop_requested())) return stopped_error();
+    if (!g.sync && *g.perr_h == 0) note_persist_ok();
     if (*g.perr_h != 0) {
         // the launch met an fp16-range activation (2) or a hand-off timeout (1): the
         // sequence state was not written back; drain and run this utterance again on
@@ -1688,8 +1798,16 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     const std::string n(name);
     if (n == "packed") {          // batched generate: one packed prefill over all utterances
         eng->use_packed = value != 0;
-    } else if (n == "persist") {
+    } else if (n == "persist") {   // also ends a timeout back-off
         eng->use_persist = value != 0;
+        eng->persist_hold = 0;
+        eng->note_persist_ok();
+    } else if (n == "persist_backoff") {   // generates of the first back-off hold (default 64)
+        if (value < 1) return set_error(GSV_E_ARG, "persist_backoff: >= 1");
+        eng->persist_backoff_base = value;
+    } else if (n == "persist_backoff_ms") {   // its time bound (default 5000)
+        if (value < 1) return set_error(GSV_E_ARG, "persist_backoff_ms: >= 1");
+        eng->persist_backoff_s = value / 1000.0;
     } else if (n == "persist1") {
         eng->use_persist1 = value != 0;
     } else if (n == "persist1m") {   // B = 2..64: the multi-sequence form of persist1 (0: per-step graphs)
@@ -1766,6 +1884,12 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     return 0;
 }
 
+extern "C" int gsv_request_stop(gsv_engine* eng, int32_t on) {
+    ENG_CHECK(eng);
+    __atomic_store_n(eng->stop_word, on ? 1 : 0, __ATOMIC_RELEASE);
+    return 0;
+}
+
 extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value) {
     ENG_CHECK(eng);
     if (!name || !value) return set_error(GSV_E_ARG, "null arg");
@@ -1774,6 +1898,11 @@ extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value
     else if (n == "persist1_f16_reruns") *value = eng->persist1_f16_reruns;
     else if (n == "vits_f32_reruns") *value = eng->vits_f32_reruns;
     else if (n == "sv_f32_reruns") *value = eng->sv_f32_reruns;
+    else if (n == "w16_split_tensors") *value = eng->w16_split_tensors;
+    else if (n == "persist_disabled") *value = eng->persist_disabled;
+    else if (n == "persist_launches") *value = eng->persist_launches;
+    else if (n == "persist_hold") *value = eng->persist_hold;
+    else if (n == "stops") *value = eng->stops;
     else return set_error(GSV_E_ARG, "unknown counter " + n);
     return 0;
 }

@@ -15,6 +15,7 @@
 
 namespace gsv {
 int set_error(int code, const std::string& msg);
+int f16_inexact_error(const std::string& weight, const float* v, int64_t index);
 struct StreamScope;
 constexpr long ACC_SEQ = 24 * 2 * 512;   // fixed-point hand-off accumulators per sequence
 
@@ -31,17 +32,17 @@ struct T2SLayerW {
 };
 // CN-HuBERT (hubert.hip): chinese-hubert-base, transformers HubertModel layout
 struct HubertLayerW {
-    __half *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
+    W16 wqkv, wo, w1, w2;
     float *bqkv = nullptr, *bo = nullptr, *b1 = nullptr, *b2 = nullptr;
     float *ln1w = nullptr, *ln1b = nullptr, *ln2w = nullptr, *ln2b = nullptr;
 };
 struct HubertWeights {
     bool ready = false;
     float *conv0_w = nullptr, *gn_w = nullptr, *gn_b = nullptr;
-    __half* conv_w[7] = {};           // conv 1..6 as [co][tap][ci]
+    W16 conv_w[7];                    // conv 1..6 as [co][tap][ci]
     float *fp_ln_w = nullptr, *fp_ln_b = nullptr, *fp_b = nullptr;
-    __half* fp_w = nullptr;
-    __half* pos_w = nullptr;          // [768][tap 128][ci 48] (16 groups of 48 rows)
+    W16 fp_w;
+    W16 pos_w;                        // [768][tap 128][ci 48] (16 groups of 48 rows)
     float *pos_b = nullptr, *enc_ln_w = nullptr, *enc_ln_b = nullptr;
     HubertLayerW L[12];
     float* ws = nullptr;              // workspace (grown per call)
@@ -182,6 +183,11 @@ struct gsv_engine {
     float* up_f32(const std::string& n, int* err);
     __half* up_f16(const std::string& n, int* err);
     __half* up_f16_t(const std::string& n, int* err);   // transposed 2-D upload
+    // up_f16 / up_f16_t refuse a tensor that is not fp16-exact (GSV_E_WEIGHT); the W16
+    // uploads split such a tensor into hi + lo planes for the split-weight GEMM
+    gsv::W16 upload_w16(const std::string& n, const std::vector<float>& v, int* err);
+    gsv::W16 up_w16(const std::string& n, int* err);
+    long w16_split_tensors = 0;        // tensors uploaded as hi + lo planes (counter "w16_split_tensors")
     int finalize_t2s();
     int finalize_vits();
     int finalize_prompt_encoder();
@@ -221,8 +227,25 @@ struct gsv_engine {
     hipGraphExec_t step_graph(int B, const gsv_sampler* sp, int chunk, hipStream_t st);
     int decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool allow_persist = true);
     long persist_timeouts = 0;         // persistent launches that timed out (co-running work) and re-ran as graphs
-    int persist_timeout_run = 0;       // consecutive ones (2: the engine stays on the graphs)
+    int persist_timeout_run = 0;       // consecutive ones (2: a back-off hold on the graphs begins)
+    // back-off after repeated timeouts: the next persist_hold generates (or until persist_hold_end,
+    // whichever comes first) run on the per-step graphs, then the persistent path is probed again;
+    // each hold that ends in another timeout doubles the next one (64 generates / 5 s up to 4096 / 60 s)
+    int persist_hold = 0;
+    double persist_hold_end = 0.0;     // steady-clock seconds
+    int persist_backoff = 0;           // length of the next hold (0: persist_backoff_base)
+    int persist_backoff_base = 64;     // option "persist_backoff" (generates; tests shorten it)
+    double persist_backoff_s = 5.0;    // option "persist_backoff_ms"
+    long persist_disabled = 0;         // holds begun (counter "persist_disabled")
+    long persist_launches = 0;         // persistent decode launches enqueued (counter "persist_launches")
     void note_persist_timeout();
+    void note_persist_ok();
+    bool persist_admit();              // once per generate: false while a hold lasts
+    // stop word (gsv_request_stop): host-coherent pinned int, read by the decode kernels
+    int* stop_word = nullptr;
+    bool stop_requested() const { return stop_word && __atomic_load_n(stop_word, __ATOMIC_ACQUIRE) != 0; }
+    long stops = 0;                    // generates abandoned by a stop request (counter "stops")
+    int stopped_error();
     // hand-off wait bound, 100 MHz ticks: 200 ms, >100x the longest legitimate wait (a
     // workgroup waiting out one step of a 64-sequence decode, ~1.6 ms)
     static constexpr unsigned long long PERSIST_SPIN_TICKS = 20000000ull;

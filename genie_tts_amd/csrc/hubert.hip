@@ -16,12 +16,16 @@
 // Layout: activations time-major [T][C] in HBM.  A stride-s conv over a
 // time-major input is a plain GEMM with no im2col: output row t reads the k
 // consecutive input rows starting at s t, i.e. A = X with lda = s C and K = k C
-// (weights re-ordered to [co][tap][ci] at load).  Every GEMM is k_gemm_x2
-// (fp16 weights, split-fp16 MFMA, t2s.hip); attention is k_mha (vits.hip).
+// (weights re-ordered to [co][tap][ci] at load).  Every GEMM is gemm_nt (t2s.hip):
+// split-fp16 activations on the f16 MFMA, weights as W16 planes -- the fp16 bin's
+// exact values as one plane, an fp32 export's values as hi + lo; attention is k_mha
+// (vits.hip).
 // The grouped positional conv is 16 GEMMs over per-group im2col rows (K = 6144)
 // split over K into slabs, reduced with bias + GELU + the residual add.
 #include "common.h"
 #include "engine_internal.h"
+
+#include <algorithm>
 
 namespace gsv {
 namespace {
@@ -164,6 +168,13 @@ GemmArgs gemm_f16(int M, int N, int K, const float* A, long lda, const void* W, 
     return a;
 }
 
+GemmArgs gemm_w16(int M, int N, int K, const float* A, long lda, const W16& W, const float* bias, float* C,
+                  long ldc, int mode, const float* res, long ldr) {
+    GemmArgs a = gemm_f16(M, N, K, A, lda, W.hi, bias, C, ldc, mode, res, ldr);
+    a.Wl = W.lo;
+    return a;
+}
+
 void layernorm_rows_d(const float* in, float* out, int rows, int D, const float* g, const float* b, float eps,
                       hipStream_t s) {
     hipLaunchKernelGGL(k_ln_rows_d, dim3(rows), dim3(256), 0, s, in, out, D, g, b, eps, 0, 0L, nullptr, nullptr);
@@ -202,30 +213,26 @@ int gsv_engine::finalize_hubert() {
         const Staged* s = find(n);
         const int k = HB_KS[i];
         if (!s || s->data.size() != (size_t)512 * 512 * k) return set_error(GSV_E_WEIGHT, "missing/bad weight " + n);
-        std::vector<__half> h((size_t)512 * 512 * k);
+        std::vector<float> h((size_t)512 * 512 * k);
         for (int co = 0; co < 512; ++co)
             for (int ci = 0; ci < 512; ++ci)
-                for (int j = 0; j < k; ++j)
-                    h[((size_t)co * k + j) * 512 + ci] = __float2half(s->data[((size_t)co * 512 + ci) * k + j]);
-        H.conv_w[i] = (__half*)dalloc(h.size() * 2);
-        hipMemcpy(H.conv_w[i], h.data(), h.size() * 2, hipMemcpyHostToDevice);
+                for (int j = 0; j < k; ++j) h[((size_t)co * k + j) * 512 + ci] = s->data[((size_t)co * 512 + ci) * k + j];
+        H.conv_w[i] = upload_w16(n, h, &err);
     }
     H.fp_ln_w = up_f32("feature_projection.layer_norm.weight", &err);
     H.fp_ln_b = up_f32("feature_projection.layer_norm.bias", &err);
-    H.fp_w = up_f16("feature_projection.projection.weight", &err);
+    H.fp_w = up_w16("feature_projection.projection.weight", &err);
     H.fp_b = up_f32("feature_projection.projection.bias", &err);
     {
         // [768][48][128] -> per group g: [48 o][128 j][48 i] (im2col K order j, i)
         const std::string n = "encoder.pos_conv_embed.conv.weight";
         const Staged* s = find(n);
         if (!s || s->data.size() != (size_t)768 * 48 * 128) return set_error(GSV_E_WEIGHT, "missing/bad weight " + n);
-        std::vector<__half> h((size_t)768 * 6144);
+        std::vector<float> h((size_t)768 * 6144);
         for (int co = 0; co < 768; ++co)
             for (int i = 0; i < 48; ++i)
-                for (int j = 0; j < 128; ++j)
-                    h[(size_t)co * 6144 + j * 48 + i] = __float2half(s->data[((size_t)co * 48 + i) * 128 + j]);
-        H.pos_w = (__half*)dalloc(h.size() * 2);
-        hipMemcpy(H.pos_w, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+                for (int j = 0; j < 128; ++j) h[(size_t)co * 6144 + j * 48 + i] = s->data[((size_t)co * 48 + i) * 128 + j];
+        H.pos_w = upload_w16(n, h, &err);
     }
     H.pos_b = up_f32("encoder.pos_conv_embed.conv.bias", &err);
     H.enc_ln_w = up_f32("encoder.layer_norm.weight", &err);
@@ -234,7 +241,7 @@ int gsv_engine::finalize_hubert() {
         const std::string p = "encoder.layers." + std::to_string(l) + ".";
         HubertLayerW& L = H.L[l];
         // q, k, v projections fused into one [2304][768] weight
-        std::vector<__half> wqkv((size_t)2304 * 768);
+        std::vector<float> wqkv((size_t)2304 * 768);
         std::vector<float> bqkv(2304);
         const char* nm[3] = {"q_proj", "k_proj", "v_proj"};
         for (int m = 0; m < 3; ++m) {
@@ -242,20 +249,19 @@ int gsv_engine::finalize_hubert() {
             const Staged* b = find(p + "attention." + nm[m] + ".bias");
             if (!w || !b || w->data.size() != (size_t)768 * 768 || b->data.size() != 768)
                 return set_error(GSV_E_WEIGHT, "missing/bad weight " + p + "attention." + nm[m]);
-            for (size_t e = 0; e < (size_t)768 * 768; ++e) wqkv[(size_t)m * 768 * 768 + e] = __float2half(w->data[e]);
+            std::copy(w->data.begin(), w->data.end(), wqkv.begin() + (size_t)m * 768 * 768);
             for (int e = 0; e < 768; ++e) bqkv[m * 768 + e] = b->data[e];
         }
-        L.wqkv = (__half*)dalloc(wqkv.size() * 2);
-        hipMemcpy(L.wqkv, wqkv.data(), wqkv.size() * 2, hipMemcpyHostToDevice);
+        L.wqkv = upload_w16(p + "attention.{q,k,v}_proj.weight", wqkv, &err);
         L.bqkv = (float*)dalloc(bqkv.size() * 4);
         hipMemcpy(L.bqkv, bqkv.data(), bqkv.size() * 4, hipMemcpyHostToDevice);
-        L.wo = up_f16(p + "attention.out_proj.weight", &err);
+        L.wo = up_w16(p + "attention.out_proj.weight", &err);
         L.bo = up_f32(p + "attention.out_proj.bias", &err);
         L.ln1w = up_f32(p + "layer_norm.weight", &err);
         L.ln1b = up_f32(p + "layer_norm.bias", &err);
-        L.w1 = up_f16(p + "feed_forward.intermediate_dense.weight", &err);
+        L.w1 = up_w16(p + "feed_forward.intermediate_dense.weight", &err);
         L.b1 = up_f32(p + "feed_forward.intermediate_dense.bias", &err);
-        L.w2 = up_f16(p + "feed_forward.output_dense.weight", &err);
+        L.w2 = up_w16(p + "feed_forward.output_dense.weight", &err);
         L.b2 = up_f32(p + "feed_forward.output_dense.bias", &err);
         L.ln2w = up_f32(p + "final_layer_norm.weight", &err);
         L.ln2b = up_f32(p + "final_layer_norm.bias", &err);
@@ -307,18 +313,18 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
     hipLaunchKernelGGL(k_hb_gn_gelu, dim3(T0), dim3(512), 0, st, cA, 512, gmean, grstd, H.gn_w, H.gn_b);
     float *src = cA, *dst = cB;
     for (int i = 1; i < 7; ++i) {
-        gemm_nt(gemm_f16(Ts[i + 1], 512, HB_KS[i] * 512, src, (long)HB_SS[i] * 512, H.conv_w[i], nullptr, dst, 512,
+        gemm_nt(gemm_w16(Ts[i + 1], 512, HB_KS[i] * 512, src, (long)HB_SS[i] * 512, H.conv_w[i], nullptr, dst, 512,
                         EPI_GELU),
                 st);
         std::swap(src, dst);
     }
     // ---- feature projection: LayerNorm(512) -> Linear(512 -> 768)
     layernorm_rows_d(src, dst, T, 512, H.fp_ln_w, H.fp_ln_b, 1e-5f, st);
-    gemm_nt(gemm_f16(T, 768, 512, dst, 512, H.fp_w, H.fp_b, xproj, 768, EPI_STORE), st);
+    gemm_nt(gemm_w16(T, 768, 512, dst, 512, H.fp_w, H.fp_b, xproj, 768, EPI_STORE), st);
     // ---- positional conv embedding: h = x + GELU(conv(x)), then LayerNorm(768)
     hipLaunchKernelGGL(k_hb_pos_im2col, dim3(T, 16), dim3(256), 0, st, xproj, T, im);
     for (int g = 0; g < 16; ++g) {
-        GemmArgs a = gemm_f16(T, 48, 6144, im + (size_t)g * T * 6144, 6144, H.pos_w + (size_t)g * 48 * 6144,
+        GemmArgs a = gemm_w16(T, 48, 6144, im + (size_t)g * T * 6144, 6144, H.pos_w.at((size_t)g * 48 * 6144),
                              nullptr, slabs + 48 * g, 768, EPI_SLAB);
         a.ksplit = NZ_POS;
         a.slab_stride = (long)T * 768;
@@ -333,22 +339,22 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
     // tiles x ceil(T / 64) row tiles, < 256 blocks) splits K into slabs that the LayerNorm
     // reduces in order (as RoBERTa's), so the GEMM covers the chip.
     const bool split = ((T + 63) / 64) * 12 < 256;
-    auto resid_ln = [&](const float* A, int K, const __half* W, const float* bias, int z, const float* lw,
+    auto resid_ln = [&](const float* A, int K, const W16& W, const float* bias, int z, const float* lw,
                         const float* lb) {
         if (split) {
-            GemmArgs g = gemm_f16(T, 768, K, A, K, W, nullptr, slabs, 768, EPI_SLAB);
+            GemmArgs g = gemm_w16(T, 768, K, A, K, W, nullptr, slabs, 768, EPI_SLAB);
             g.ksplit = z;
             g.slab_stride = (long)T * 768;
             gemm_nt(g, st);
             layernorm_rows_d_slabs(slabs, z, (long)T * 768, bias, h, h, T, 768, lw, lb, 1e-5f, st);
         } else {
-            gemm_nt(gemm_f16(T, 768, K, A, K, W, bias, tmp, 768, EPI_RESID, h, 768), st);
+            gemm_nt(gemm_w16(T, 768, K, A, K, W, bias, tmp, 768, EPI_RESID, h, 768), st);
             layernorm_rows_d(tmp, h, T, 768, lw, lb, 1e-5f, st);
         }
     };
     for (int l = 0; l < 12; ++l) {
         const HubertLayerW& L = H.L[l];
-        gemm_nt(gemm_f16(T, 2304, 768, h, 768, L.wqkv, L.bqkv, qkv, 2304, EPI_STORE), st);
+        gemm_nt(gemm_w16(T, 2304, 768, h, 768, L.wqkv, L.bqkv, qkv, 2304, EPI_STORE), st);
         MhaArgs m{};
         m.q = qkv; m.q_ts = 2304; m.q_cs = 1;
         m.k = qkv + 768; m.k_ts = 2304; m.k_cs = 1;
@@ -358,7 +364,7 @@ int gsv_engine::hubert_forward(const float* audio, int n, float* out, hipStream_
         m.postdiv = 0; m.scale = 8.f;   // q * 64^-0.5 (exact: a power of two)
         mha(m, st);
         resid_ln(att, 768, L.wo, L.bo, 4, L.ln1w, L.ln1b);
-        gemm_nt(gemm_f16(T, 3072, 768, h, 768, L.w1, L.b1, f, 3072, EPI_GELU), st);
+        gemm_nt(gemm_w16(T, 3072, 768, h, 768, L.w1, L.b1, f, 3072, EPI_GELU), st);
         resid_ln(f, 3072, L.w2, L.b2, NZ_POS, L.ln2w, L.ln2b);
     }
     hipLaunchKernelGGL(k_hb_transpose, dim3((T + 31) / 32, 24), dim3(256), 0, st, h, T, out);

@@ -1,6 +1,7 @@
 // Host-side launchers of the engine's HIP kernels (gfx950).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 #include <stdint.h>
 
 namespace gsv {
@@ -31,10 +32,21 @@ struct KVScatter {
     const uint8_t* row_skip; // optional: per-row "done" flags (no cache write)
 };
 
+// A GEMM weight as fp16 planes.  fp16-exact tensors (the Genie fp16 bins) have hi only.
+// Any other fp32 tensor is split: hi = fp16(w), lo = fp16((w - hi) 2^11), so that lo stays
+// a normal fp16 number down to |w| ~ 2^-14 and w = hi + lo 2^-11 to ~22 significant bits.
+constexpr float W16_LO_SCALE = 2048.f, W16_LO_INV = 1.f / 2048.f;
+struct W16 {
+    __half* hi = nullptr;
+    __half* lo = nullptr;   // null: the tensor is fp16-exact
+    W16 at(size_t e) const { return W16{hi + e, lo ? lo + e : nullptr}; }   // element offset e
+};
+
 struct GemmArgs {
     int M, N, K;
     const float* A; long lda;
     const void* W; long ldw; int w_f16;
+    const void* Wl;                  // optional lo plane of split fp32 weights (W16), same layout as W
     const float* bias;
     float* C; long ldc;
     int mode;
@@ -49,8 +61,13 @@ void gemm_nt(const GemmArgs& a, hipStream_t s);
 // Args of a GEMM with fp16 weights W[N][K] (ldw = K): C = epi(A W^T + bias)
 GemmArgs gemm_f16(int M, int N, int K, const float* A, long lda, const void* W, const float* bias, float* C,
                   long ldc, int mode, const float* res = nullptr, long ldr = 0);
+// ... with W16 weights (lo plane, if any, in a.Wl)
+GemmArgs gemm_w16(int M, int N, int K, const float* A, long lda, const W16& W, const float* bias, float* C,
+                  long ldc, int mode, const float* res = nullptr, long ldr = 0);
 // EPI_SLAB (split-K into slabs) is available for fp16 weights with these shapes
 bool gemm_slabs_supported(int K, long lda, long ldw);
+// shapes the split-weight (W16 with lo) GEMM runs
+bool gemm_w16_supported(int K, long lda, long ldw);
 
 // --------------------------------------------------------- row kernels
 void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,
@@ -221,6 +238,7 @@ struct SampleArgs {
     int ablate;                        // probe only: 1 skip top-k, 2 also skip softmax, 3 loads + tail
     long long* acc_zero; long acc_n;   // per-sequence fixed-point accumulators zeroed for the next step
     int threads;                       // 256 (default) or 512: block size of the sampler body
+    const int* stop_req;               // host-mapped stop word (gsv_request_stop): set -> the sequence finishes
 };
 void sample_tokens(const SampleArgs& a, hipStream_t s);
 
@@ -250,6 +268,8 @@ struct PersistArgs {
     unsigned long long* ring;                     // granule ring (persist1_ring_bytes / persist1m_ring_bytes)
     unsigned epoch;                               // launch epoch (tag high bits), 1 .. 2^20-1
     int* err;                                     // zeroed per launch; non-zero: a hand-off timed out
+    const int* stop_req;                          // host-mapped stop word (gsv_request_stop), or null: once
+                                                  // set, every sequence finishes at its next token (<= 2 steps)
     int smax;                                     // step cap of the launch
     int groups;                                   // layer groups (layer l -> group l % groups)
     unsigned long long* trace;                    // optional [grid][16] phase stamps (step 8, layer 12)

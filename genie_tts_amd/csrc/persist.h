@@ -18,6 +18,11 @@ constexpr unsigned long long SPIN_TICKS = 300000000ull;   // 3 s of the 100 MHz 
 __device__ __forceinline__ int ld_rlx(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The engine's stop word (gsv_request_stop): host-coherent pinned memory, read at system
+// scope (a PCIe round trip, so the decode kernels read it off their critical path)
+__device__ __forceinline__ int ld_stop(const int* p) {
+    return p ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+}
 __device__ __forceinline__ u64 ld_rlxu64(const u64* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

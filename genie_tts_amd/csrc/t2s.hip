@@ -7,6 +7,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
+#include <cstdio>
 #include <cstdlib>
 
 namespace gsv {
@@ -276,13 +277,19 @@ __device__ __forceinline__ void gx3_dma(const void* g, void* l) {
 }
 
 #define GX3_BK 64
-template <int BM, int BN, int NS>
+// SW (split weights, a.Wl set): fp32 weights w = hi + lo 2^-11 as two fp16 planes
+// (W16, kernels.h).  Each product is three MFMAs, a_hi w_hi + a_lo w_hi into acc and
+// a_hi w_lo into accl, and the result is acc + accl 2^-11: a weight keeps ~22 of its
+// 24 significant bits (the reference runs such models with fp32 initializers).
+template <int BM, int BN, int NS, bool SW = false>
 __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs a) {
     constexpr int WV = (BM / 32) * (BN / 32);           // waves, one 32 x 32 output tile each
     constexpr int NA = BM / 4 / WV, NW = BN / 8 / WV;    // DMA instructions per wave per stage (A, W)
     static_assert(NA * WV * 4 == BM && NW * WV * 8 == BN, "tile / wave split");
+    constexpr int NWL = SW ? NW : 0;                     // ... of the lo plane
     __shared__ __attribute__((aligned(16))) float As[NS][BM * GX3_BK];
     __shared__ __attribute__((aligned(16))) __half Ws[NS][BN * GX3_BK];
+    __shared__ __attribute__((aligned(16))) __half Wls[SW ? NS : 1][SW ? BN * GX3_BK : 8];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w / (BN / 32), wn = w % (BN / 32);
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
@@ -310,16 +317,19 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs
         wsrc[i] = reinterpret_cast<const __half*>(a.W) + (long)gn * a.ldw + (long)s_lo * GX3_BK +
                   8 * (slot ^ ((row >> 1) & 7));
     }
+    const long wl_off = SW ? reinterpret_cast<const __half*>(a.Wl) - reinterpret_cast<const __half*>(a.W) : 0;
     auto issue = [&](int st) {
         const int k0 = st * GX3_BK, buf = st % NS;
 #pragma unroll
         for (int i = 0; i < NA; ++i) gx3_dma(asrc[i] + k0, &As[buf][256 * (w + WV * i)]);
 #pragma unroll
         for (int i = 0; i < NW; ++i) gx3_dma(wsrc[i] + k0, &Ws[buf][512 * (w + WV * i)]);
-    };
-    f32x16 acc;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        for (int i = 0; i < NWL; ++i) gx3_dma(wsrc[i] + wl_off + k0, &Wls[buf][512 * (w + WV * i)]);
+    };
+    f32x16 acc, accl;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = accl[i] = 0.f;
 #pragma unroll
     for (int st = 0; st < NS - 1; ++st)
         if (st < nsteps) issue(st);
@@ -328,11 +338,12 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs
         // stage st landed (this wave's share; later ones stay in flight), then the barrier:
         // every wave's share landed, and the buffer refilled below was consumed by all.
         // s_barrier without __syncthreads' fence, which would wait for every DMA in flight.
-        gx3_wait<NA + NW>(min(NS - 2, nsteps - 1 - st));
+        gx3_wait<NA + NW + NWL>(min(NS - 2, nsteps - 1 - st));
         __builtin_amdgcn_s_barrier();
         if (st + NS - 1 < nsteps) issue(st + NS - 1);
         const float* As_ = As[st % NS];
         const __half* Ws_ = Ws[st % NS];
+        const __half* Wls_ = Wls[SW ? st % NS : 0];
 #pragma unroll
         for (int ks = 0; ks < GX3_BK / 16; ++ks) {
             const int c0 = 4 * ks + 2 * hh;   // A chunks c0, c0 + 1 (4 floats each)
@@ -341,10 +352,19 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs
             h16x8 ahi, alo;
             split8(x0, x1, ahi, alo);
             const int cb = 2 * ks + hh;       // W chunk (8 halfs)
-            const h16x8 bw = *reinterpret_cast<const h16x8*>(Ws_ + bcol * GX3_BK + 8 * (cb ^ ((bcol >> 1) & 7)));
+            const int wo = bcol * GX3_BK + 8 * (cb ^ ((bcol >> 1) & 7));
+            const h16x8 bw = *reinterpret_cast<const h16x8*>(Ws_ + wo);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bw, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bw, acc, 0, 0, 0);
+            if (SW) {
+                const h16x8 bl = *reinterpret_cast<const h16x8*>(Wls_ + wo);
+                accl = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bl, accl, 0, 0, 0);
+            }
         }
+    }
+    if (SW) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = fmaf(accl[i], W16_LO_INV, acc[i]);
     }
     if (a.mode == EPI_SLAB) {
         const int col = n0 + bcol;
@@ -365,6 +385,10 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
     auto go = [&](auto kern, int bm, int bn, int threads) {
         hipLaunchKernelGGL(kern, dim3((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, z), dim3(threads), 0, s, a);
     };
+    if (a.Wl) {   // split weights: one configuration (4 x 32 KB stages)
+        go(k_gemm_x3<64, 64, 4, true>, 64, 64, 256);
+        return;
+    }
     switch (cfg) {
         case 1: go(k_gemm_x3<64, 64, 4>, 64, 64, 256); break;
         case 2: go(k_gemm_x3<32, 64, 4>, 32, 64, 128); break;
@@ -401,12 +425,24 @@ static bool gemm_x2_enabled() {
     return on;
 }
 
+bool gemm_w16_supported(int K, long lda, long ldw) { return K % GX_KS == 0 && lda % 4 == 0 && ldw % 8 == 0; }
+
 bool gemm_slabs_supported(int K, long lda, long ldw) {
     return K % GX_KS == 0 && lda % 4 == 0 && ldw % 8 == 0 && gemm_x2_enabled();
 }
 
 void gemm_nt(const GemmArgs& a, hipStream_t s) {
     dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
+    if (a.Wl) {
+        // split fp32 weights run only on k_gemm_x3 (every M: its partition does not depend
+        // on M, so packed and per-sentence rows stay identical); the loaders check the shapes
+        if (!gemm_w16_supported(a.K, a.lda, a.ldw) || a.a_nslab != 0 || a.mode == EPI_VQDIST) {
+            std::fprintf(stderr, "gemm_nt: split-weight GEMM with unsupported shape K=%d lda=%ld\n", a.K, a.lda);
+            std::abort();
+        }
+        launch_x3(a, a.mode == EPI_SLAB ? a.ksplit : 1, s, 0);
+        return;
+    }
     // fp16 weights -> split-activation f16 MFMA; the VQ distance GEMM stays on the
     // exact f32 path (its argmin must see the f32 dot products).
     if (a.w_f16 && a.mode != EPI_VQDIST && a.K % GX_KS == 0 && a.lda % 4 == 0 && a.ldw % 8 == 0 &&
@@ -1231,10 +1267,14 @@ __global__ __launch_bounds__(NT) void k_sample(SampleArgs a) {
             *reinterpret_cast<longlong2*>(z + i) = make_longlong2(0, 0);
     }
     // sequence state for the tail, read up front (no dependent round trips at the end)
-    int st_ny = 0, st_steps = 0, st_kv = 0;
+    int st_ny = 0, st_steps = 0, st_kv = 0, st_stop = 0;
     if (tid == 0) {
         st_ny = a.ny[b];
-        if (!a.prefill) { st_steps = a.steps[b]; st_kv = a.kvlen[b]; }
+        if (!a.prefill) {
+            st_steps = a.steps[b];
+            st_kv = a.kvlen[b];
+            if (a.stop_req) st_stop = __hip_atomic_load(a.stop_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     if (tid < 33) seen_s[tid] = seen[tid];
     const bool skip = !a.prefill && a.done[b];
@@ -1253,6 +1293,7 @@ __global__ __launch_bounds__(NT) void k_sample(SampleArgs a) {
     if (tid == 0) {
         if (a.ablate == 3) { a.y[(long)b * a.ldy + st_ny] = raw; a.ny[b] = st_ny + 1; return; }
         sample_commit(a, b, tok, raw, st_ny, st_steps, st_kv, seen_s);
+        if (st_stop) a.done[b] = 1;   // gsv_request_stop: the sequence ends here (the host returns STOPPED)
     }
 }
 

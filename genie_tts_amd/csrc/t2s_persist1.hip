@@ -183,6 +183,7 @@ struct Shared1 {
     float wred[2][PWV];
     uint32_t seen[33];
     int tok, fin, fail;
+    int stopreq;                    // the stop word as last read (gsv_request_stop; fills the 8-byte padding)
     unsigned long long stamp[16];   // [0,8) 100 MHz realtime, [8,16) shader clock
     SampleLds<PT> samp;
     union {
@@ -209,6 +210,7 @@ struct Shared1 {
     struct {
         int tok[64], act[64], ny0[64], kv0[64], st0[64], nexe[64], lstop[64], lfin[64];
         int kstep[64];              // the step whose status of the sequence is known (seq_runs)
+        int stop_s;                 // the step the stop word was last read at (resolve_m)
         uint32_t seens[4][33];      // a sampler workgroup's sequences h, h + 16, h + 32, h + 48
     } m;
 };
@@ -521,6 +523,17 @@ __device__ __noinline__ void attn_general1(Shared1& sh, const float* Kw, const f
 // at once (its layer 0 starts from it) and sleeps on the layer-23 output of the
 // previous step first; the other groups only need the stop bit and poll slowly.
 // Returns false when the loop is over (or on error: sh.fail).
+
+// A stop request (gsv_request_stop, the reference's stop_event checked once per loop
+// step, Inference.py:96-97) seen at a token: the launch is abandoned as a timed-out
+// one is -- error word 3, so every workgroup leaves at its next wait and no sequence
+// state is written back (the host returns GSV_E_STOPPED; the sentence yields None).
+// Only a token resolver reads the stop word, and only once per step, so workgroups
+// never disagree about a sequence's tokens.
+__device__ __forceinline__ void stop_launch(const PersistArgs& a, bool& ok) {
+    atomicCAS(a.err, 0, 3);
+    ok = false;
+}
 // Fused greedy step end (group 0, s >= 1): the token of step s - 1 from the logits
 // workgroups' local argmaxes (LG(s - 1): candidate q's {penalised max, its index, raw
 // max, its index} at 4 q .. 4 q + 3; q = 4 j + w covers rows 64 j + 16 w .. + 16, q =
@@ -533,6 +546,7 @@ __device__ void resolve_greedy(const PersistArgs& a, const Ws1& ws, int s, int n
     const int tid = threadIdx.x;
     bool ok = true;
     if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s - 1, 23, 0)), ws.tag(s - 1), a.err, ok, a.spin_ticks);
+    if (tid == 64) sh.stopreq = ld_stop(a.stop_req);   // wave 1: beside wave 0's (longer) wait
     if (!block_ok1(ok, sh)) return;
     if (tid < 64) {
         // lane q: candidate q's {penalised max, its index, raw max, its index} (16 rows of
@@ -553,6 +567,7 @@ __device__ void resolve_greedy(const PersistArgs& a, const Ws1& ws, int s, int n
         if (tid == 0) {
             const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
             const bool fin = seq_finished(a.force_b, 0, a.force_steps, a.max_steps, st0 + s, stop);
+            if (sh.stopreq) stop_launch(a, ok);
             sh.tok = tok;
             sh.fin = fin ? 1 : 0;
             if (publisher && ok) {
@@ -882,6 +897,7 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
             const bool probe = a.trace && s == 8;   // step-end trace (tools/knob_sweep.py)
             bool ok = true;
             if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s, 23, 0)), tag, a.err, ok, a.spin_ticks);
+            if (tid == 64) sh.stopreq = ld_stop(a.stop_req);
             if (!block_ok1(ok, sh)) return;
             STAMP1(0);
             const u64* lgg = ws.LG(s);
@@ -941,7 +957,9 @@ __device__ void run_attn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int g
                 const bool fin = seq_finished(a.force_b, 0, a.force_steps, a.max_steps, nst, stop);
                 last_stop = stop;
                 last_fin = fin ? 1 : 0;
-                st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+                bool go = true;
+                if (sh.stopreq) stop_launch(a, go);   // no token: every waiting workgroup sees the error word
+                else st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
             }
             STAMP1(2);
             if (probe && tid < 16) a.trace[blockIdx.x * 16 + tid] = sh.stamp[tid];
@@ -1282,7 +1300,11 @@ __device__ __forceinline__ void init_m(const PersistArgs& a, Shared1& sh) {
         sh.m.lfin[b] = a.done[b] ? 1 : 0;
         sh.m.kstep[b] = 0;
     }
-    if (tid == 0) sh.fail = 0;
+    if (tid == 0) {
+        sh.fail = 0;
+        sh.stopreq = 0;
+        sh.m.stop_s = -1;
+    }
 }
 __device__ __forceinline__ u64m live_mask(const Shared1& sh, int nb) {
     u64m m = 0;
@@ -1357,6 +1379,12 @@ __device__ __forceinline__ void stage_kv(const PersistArgs& a, Shared1& sh, int 
 __device__ void resolve_m(const PersistArgs& a, const WsSeq& ws, int s, int b, bool publisher, Shared1& sh) {
     const int tid = threadIdx.x;
     bool ok = true;
+    // the stop word, once per step (wave 1; tid 0 below may still see the previous step's
+    // value: a stop takes effect within two steps)
+    if (tid == 64 && sh.m.stop_s != s) {
+        sh.stopreq = ld_stop(a.stop_req);
+        sh.m.stop_s = s;
+    }
     if (tid < 64) {
         float f[4];
         wait_gran_n<4>(ws.LG(s - 1) + 4 * tid, 1, ws.tag(s - 1), f, a.err, ok, a.spin_ticks);
@@ -1374,6 +1402,7 @@ __device__ void resolve_m(const PersistArgs& a, const WsSeq& ws, int s, int b, b
         if (tid == 0) {
             const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
             const bool fin = seq_finished(a.force_b, b, a.force_steps, a.max_steps, sh.m.st0[b] + s, stop);
+            if (sh.stopreq) stop_launch(a, ok);
             sh.m.tok[b] = tok;
             sh.m.act[b] = fin ? 0 : 1;
             if (publisher && ok) {
@@ -1612,6 +1641,7 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                 const WsSeq ws = base.seq(b);
                 bool ok = true;
                 if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s, 23, 0)), tag, a.err, ok, a.spin_ticks);
+                if (tid == 64) sh.stopreq = ld_stop(a.stop_req);
                 if (!block_ok1(ok, sh)) return;
                 const u64* lgg = ws.LG(s);
                 for (int i = tid; i < 1025; i += PT) sh.at.lg[i] = wait_gran(lgg + i, tag, a.err, ok, a.spin_ticks);
@@ -1630,7 +1660,9 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
                     sh.m.lstop[b] = stop;
                     sh.m.lfin[b] = fin;
                     sh.m.nexe[b] = s + 1;
-                    st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+                    bool go = true;
+                    if (sh.stopreq) stop_launch(a, go);
+                    else st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
                 }
                 __syncthreads();   // sh.at.lg / sh.samp consumed before the next sequence's
             }

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -25,8 +26,32 @@ GSV_V2, GSV_V2PP = 0, 1
 MAX_BATCH = 64           # gsv_reserve: sequences decoded together
 
 
+GSV_E_STOPPED = -6       # a generate abandoned by gsv_request_stop
+
+
 class EngineError(RuntimeError):
     pass
+
+
+class EngineStopped(EngineError):
+    """A T2S generate was abandoned by a stop request (gsv_request_stop); the reference's
+    loop returns None for the sentence then (Inference.py:96-97)."""
+
+
+# Every live engine, so one stop request reaches them all (GENIE.stop_event is process-wide
+# in the reference, Core/Inference.py:13-14), and the current request state for new engines.
+_engines: "weakref.WeakSet" = weakref.WeakSet()
+_stop_on = False
+
+
+def request_stop_all(on: bool) -> None:
+    """Set (or clear) the stop word of every engine of this process (gsv_request_stop).
+    Writes one host word per engine: safe from any thread while a generate runs."""
+    global _stop_on
+    _stop_on = bool(on)
+    for e in list(_engines):
+        if getattr(e, "h", None):
+            lib().gsv_request_stop(e.h, int(on))
 
 
 class Utt(ctypes.Structure):
@@ -124,6 +149,8 @@ def lib():
         L.gsv_sv.argtypes = [vp, vp, ctypes.c_int32, vp, vp]
         L.gsv_roberta.argtypes = [vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
         L.gsv_roberta_batch.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
+        L.gsv_f16_exact.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+        L.gsv_request_stop.argtypes = [vp, ctypes.c_int32]
         _lib = L
     return _lib
 
@@ -139,12 +166,28 @@ EXPORTED = (
     "gsv_vits_decode_async",
     "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
     "gsv_vits_decode_batch_async", "gsv_vits_batch_wait", "gsv_ref_encode", "gsv_roberta_batch",
+    "gsv_f16_exact", "gsv_request_stop",
 )
+
+
+def f16_exact(values) -> int:
+    """gsv_f16_exact: -1 when every value is exactly an fp16 number (what the engine's
+    fp16-only weight paths require), else the index of the first one that is not.
+    A host-only check: needs the library, not a GPU."""
+    import numpy as np
+    v = np.ascontiguousarray(values, np.float32).reshape(-1)
+    bad = ctypes.c_int64(0)
+    rc = lib().gsv_f16_exact(v.ctypes.data_as(ctypes.c_void_p), v.size, ctypes.byref(bad))
+    if rc < 0:
+        _check(rc, "gsv_f16_exact")
+    return int(bad.value)
 
 
 def _check(rc: int, what: str):
     if rc != 0:
         msg = lib().gsv_last_error().decode(errors="replace")
+        if rc == GSV_E_STOPPED:
+            raise EngineStopped(f"{what}: {msg}")
         raise EngineError(f"{what} failed ({rc}): {msg}")
 
 
@@ -226,6 +269,14 @@ class Engine:
             self._set("pe.div_term", np.asarray(pe_div_term, np.float32))
         _check(lib().gsv_finalize_weights(self.h), "gsv_finalize_weights")
         self.dev = torch.device("cuda", device)
+        _engines.add(self)
+        if _stop_on:
+            lib().gsv_request_stop(self.h, 1)
+
+    def request_stop(self, on: bool = True):
+        """gsv_request_stop: while set, T2S generates raise EngineStopped (a running decode
+        leaves within two loop steps).  Callable from another thread."""
+        _check(lib().gsv_request_stop(self.h, int(on)), "gsv_request_stop")
 
     def _set(self, name: str, arr: np.ndarray):
         a = np.ascontiguousarray(arr)
@@ -596,7 +647,9 @@ class Engine:
         _check(lib().gsv_set_option(self.h, name.encode(), int(value)), "gsv_set_option")
 
     def counter(self, name: str) -> int:
-        """Engine counter (gsv_get_counter): persist_timeouts, persist1_f16_reruns, vits_f32_reruns."""
+        """Engine counter (gsv_get_counter): persist_timeouts, persist1_f16_reruns, vits_f32_reruns,
+        sv_f32_reruns, w16_split_tensors, persist_disabled (timeout back-off holds begun),
+        persist_launches, persist_hold (generates left in the current hold), stops."""
         v = ctypes.c_int64()
         _check(lib().gsv_get_counter(self.h, name.encode(), ctypes.byref(v)), "gsv_get_counter")
         return v.value

@@ -5,8 +5,9 @@ reference-audio features and the five sessions of a `GSVModel`, runs T2S, the
 EOS filter and the vocoder, and returns `audio f32 [1280*G]`.  When the
 sessions are this package's engine-backed ones (always, through
 `model_manager`), T2S is one `gsv_t2s_generate` call: encoder, prefill, the
-decode loop on the device as replayed hipGraphs, and the reference's trim +
-EOS filter (Inference.py:41-44,108-109) -- no per-step host round trip.
+whole decode loop as one persistent kernel launch (per-step hipGraphs only as
+the fp16-range / co-residency fallback), and the reference's trim + EOS filter
+(Inference.py:41-44,108-109) -- no per-step host round trip.
 `GENIE.t2s_cpu` is the reference's own session-by-session loop
 (Inference.py:63-109) over the same sessions, kept for parity tests.
 
@@ -23,7 +24,7 @@ from typing import Callable, List, Optional, Sequence, Union
 
 import numpy as np
 
-from .engine import Sampler
+from .engine import EngineStopped, Sampler, request_stop_all
 from .sessions import (EncoderSession, FirstStageDecoderSession, StageDecoderSession, VitsSession,
                        PromptEncoderSession)
 
@@ -77,9 +78,24 @@ def _engine_of(*sessions):
     return None
 
 
+class StopEvent(threading.Event):
+    """GENIE.stop_event (Inference.py:13-14): a threading.Event whose set()/clear() also
+    set/clear the stop word of every engine (gsv_request_stop), so a decode running on
+    the device leaves within two loop steps, as the reference's per-step check
+    (Inference.py:96-97) does."""
+
+    def set(self):
+        super().set()
+        request_stop_all(True)
+
+    def clear(self):
+        super().clear()
+        request_stop_all(False)
+
+
 class GENIE:
     def __init__(self):
-        self.stop_event = threading.Event()
+        self.stop_event = StopEvent()
 
     def tts(self, text: Union[str, np.ndarray], prompt_audio: ReferenceAudio, encoder, first_stage_decoder,
             stage_decoder, vocoder, prompt_encoder=None, language: str = "japanese",
@@ -97,6 +113,8 @@ class GENIE:
         if eng is not None:
             sem = self.t2s(prompt_audio.phonemes_seq, prompt_audio.text_bert, text_seq, text_bert,
                            prompt_audio.ssl_content, eng, sampler or first_stage_decoder.sampler)
+            if sem is None:            # stopped (Inference.py:96-97)
+                return None
         else:
             sem = self.t2s_cpu(prompt_audio.phonemes_seq, prompt_audio.text_bert, text_seq, text_bert,
                                prompt_audio.ssl_content, encoder, first_stage_decoder, stage_decoder)
@@ -131,12 +149,17 @@ class GENIE:
         prev_cus = eng.vocoder_cus     # restored when the stream ends: later single-sentence and
         if prev_cus != vocoder_cus:    # batched calls keep every CU (decode groups, lanes)
             eng.set_vocoder_cus(vocoder_cus)
-        if prompt_encoder is None:
-            cond = (vocoder.v2_cond(prompt_audio.audio_32k) if getattr(vocoder, "engine", None) is eng
-                    else {"ref_audio": prompt_audio.audio_32k})
-        else:
-            prompt_audio.update_global_emb(prompt_encoder)
-            cond = {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced}
+        try:
+            if prompt_encoder is None:
+                cond = (vocoder.v2_cond(prompt_audio.audio_32k) if getattr(vocoder, "engine", None) is eng
+                        else {"ref_audio": prompt_audio.audio_32k})
+            else:
+                prompt_audio.update_global_emb(prompt_encoder)
+                cond = {"ge": prompt_audio.global_emb, "ge_advanced": prompt_audio.global_emb_advanced}
+        except BaseException:          # e.g. a V2ProPlus clip without sv_emb: the CU split is undone
+            if eng.vocoder_cus != prev_cus:
+                eng.set_vocoder_cus(prev_cus)
+            raise
         # every sentence's inputs up front: sentence i+1's T2S is queued behind sentence
         # i's, its encoder + prefill run on the vocoder CUs while sentence i decodes
         seqs = []
@@ -163,7 +186,10 @@ class GENIE:
                     if i + 2 < n:
                         eng.t2s_prefetch(utts[i + 2], sp)
                     eng.t2s_generate_start(utts[i + 1], sp)
-                sem = eng.t2s_generate_finish().reshape(1, 1, -1)
+                try:
+                    sem = eng.t2s_generate_finish().reshape(1, 1, -1)
+                except EngineStopped:          # stop_event during sentence i's decode
+                    break
                 if pending is not None:
                     eng.vits_wait()
                     done, pending = pending, None
@@ -193,10 +219,15 @@ class GENIE:
             if eng.vocoder_cus != prev_cus:
                 eng.set_vocoder_cus(prev_cus)
 
-    def t2s(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, engine, sampler: Sampler) -> np.ndarray:
-        """Whole T2S on the device; returns the trimmed, EOS-filtered [1,1,G] tokens."""
-        tok = engine.t2s_generate([(ref_seq, text_seq, ref_bert, text_bert,
-                                    np.asarray(ssl_content, np.float32).reshape(768, -1))], sampler)[0]
+    def t2s(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, engine,
+            sampler: Sampler) -> Optional[np.ndarray]:
+        """Whole T2S on the device; returns the trimmed, EOS-filtered [1,1,G] tokens, or
+        None when stop_event interrupted it (Inference.py:96-97)."""
+        try:
+            tok = engine.t2s_generate([(ref_seq, text_seq, ref_bert, text_bert,
+                                        np.asarray(ssl_content, np.float32).reshape(768, -1))], sampler)[0]
+        except EngineStopped:
+            return None
         return tok.reshape(1, 1, -1)
 
     def t2s_cpu(self, ref_seq, ref_bert, text_seq, text_bert, ssl_content, encoder, first_stage_decoder,

@@ -132,6 +132,8 @@ def mixed100(n: int = 100, tag: str = "m100") -> Workload:
 
 
 def roberta_weights(n_layers: int = 24):
-    """Synthetic RoBERTa (chinese-roberta-wwm-ext-large shapes) for the ZH sentences."""
+    """Synthetic RoBERTa (chinese-roberta-wwm-ext-large shapes) for the ZH sentences,
+    fp32-valued: the reference loads RoBERTa.onnx with its fp32 initializers
+    (ModelManager.py:139-142), with no fp16 bin."""
     from . import weights as W
-    return synth.synth_weights(W.roberta_spec(n_layers))
+    return synth.synth_weights(W.roberta_spec(n_layers), fp16=False)

@@ -54,6 +54,7 @@ extern "C" {
 #define GSV_E_STATE -3
 #define GSV_E_WEIGHT -4
 #define GSV_E_CAPACITY -5
+#define GSV_E_STOPPED -6   /* the generate was abandoned by gsv_request_stop (the reference returns None) */
 
 typedef struct gsv_engine gsv_engine;
 
@@ -79,8 +80,18 @@ int gsv_set_weight(gsv_engine* eng, const char* name, const void* host, int dtyp
                    const int64_t* dims, int ndim);
 
 /* Fold weight norm (w = v/||v|| * g), convert, upload; must follow the last
- * gsv_set_weight.  Missing tensors are an error (GSV_E_WEIGHT). */
+ * gsv_set_weight.  Missing tensors are an error (GSV_E_WEIGHT).  No weight is ever
+ * rounded silently: the T2S / VITS / prompt-encoder paths take fp16 weights (the
+ * Genie fp16 bins, ModelManager.py:59-114) and refuse a tensor that is not
+ * fp16-exact (GSV_E_WEIGHT naming it); RoBERTa and CN-HuBERT keep fp32 values
+ * (RoBERTa.onnx is loaded as fp32, ModelManager.py:139-142) as fp16 hi + lo planes
+ * (counter "w16_split_tensors"). */
 int gsv_finalize_weights(gsv_engine* eng);
+
+/* Host-only check used by those loaders: 1 if all n values are exactly fp16 numbers,
+ * else 0 with *first_bad = the first index that is not (-1 when all are).  Needs no
+ * device. */
+int gsv_f16_exact(const float* values, int64_t n, int64_t* first_bad);
 
 /* Reserve decode capacity: up to `max_batch` sequences of up to `max_tokens`
  * positions (x + prompts + generated) each.  Allocates the KV cache. */
@@ -312,6 +323,16 @@ int gsv_get_timing(gsv_engine* eng, float* ms4);
  * (hipExtLaunchKernelGGL).  Average microseconds and number of samples; a
  * negative count is -(hipError_t) of a failed hipEventElapsedTime. */
 int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples);
+
+/* Stop (the reference's GENIE.stop_event, checked before every loop step:
+ * Inference.py:96-97 returns None for the sentence).  on = 1 sets the engine's stop
+ * word, 0 clears it (TTSPlayer.py:86 clears the event when a new job starts).  While it
+ * is set, T2S generates (gsv_t2s_generate, _start/_finish) return GSV_E_STOPPED: a
+ * running decode leaves within two loop steps -- the persistent kernels read the word
+ * once per step at token resolution, the per-step graphs' sampler every step -- and a
+ * new one returns at once.  The engine stays usable.  The only entry point that may be
+ * called from another thread while a call on the engine runs: it writes one word. */
+int gsv_request_stop(gsv_engine* eng, int32_t on);
 
 /* Engine options (no reference counterpart; the reference's session options are
  * ORT's).  "persist": 1 (default) runs gsv_t2s_generate's decode loop as ONE

@@ -98,3 +98,23 @@ def test_api_requires_reference_and_gpu():
     assert G.tts("nobody", [3, 4, 5]) is None            # Internal.py:292-294: logs, returns
     with pytest.raises(ValueError):
         G.load_character("x", "/nonexistent", "klingon")
+
+
+def test_fp16_only_weight_paths_refuse_fp32_values():
+    """The engine's fp16-only loaders (up_f16 / up_f16_t) refuse any value that is not
+    fp16-exact instead of rounding it; gsv_f16_exact is the check they apply."""
+    from genie_tts_amd.build import LIB, build
+    if not os.path.exists(LIB):
+        build()
+    from genie_tts_amd import engine
+    h = np.array([0.5, -3.25, 65504.0, 2.0 ** -24, 0.0], np.float32)
+    assert engine.f16_exact(h) == -1
+    w = h.copy()
+    w[3] = np.float32(0.1)                       # 0.1 has no fp16 representation
+    assert engine.f16_exact(w) == 3
+    assert engine.f16_exact(np.float32([1.0 + 2.0 ** -20])) == 0
+    assert engine.f16_exact(np.zeros(0, np.float32)) == -1
+    # the synthetic RoBERTa of the tests carries fp32 values, as RoBERTa.onnx does
+    from genie_tts_amd import synth, weights as W
+    q = synth.synth_tensor("encoder.layer.0.attention.self.query.weight", (1024, 1024), fp16=False)
+    assert engine.f16_exact(q) >= 0

@@ -70,3 +70,22 @@ def test_hubert_session_and_reference_audio(hub, tmp_path):
         genie.set_g2p(None)
         genie.unload_character("hb")
         genie.clear_reference_audio_cache()
+
+
+def test_hubert_fp32_weights_vs_transformers():
+    """load_cn_hubert(model_path) without the fp16 bin loads a plain fp32 graph
+    (ModelManager.py:183-187): fp32-valued weights run on the split-weight GEMMs."""
+    from genie_tts_amd.engine import Engine
+    from oracle import hubert as H
+    w = synth.synth_weights(W.hubert_spec(), fp16=False)
+    e = Engine({"hubert": w}, "v2")
+    try:
+        assert e.counter("w16_split_tensors") == 6 + 2 + 4 * 12   # convs 1-6, projection, pos conv, layers
+        a = (0.1 * synth.rng_for("hb-f32").standard_normal(24000)).astype(np.float32)
+        got = e.hubert(a).cpu().numpy()
+        ref = H.ssl_content(H.hubert_model(w), a)[0]
+        rms = float(np.sqrt(np.mean((got - ref) ** 2)))
+        print(f"fp32 weights: rms {rms:.2e} ref std {ref.std():.3f}")
+        assert rms <= RMS_TOL * max(1.0, float(ref.std())), rms
+    finally:
+        e.close()

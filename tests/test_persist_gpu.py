@@ -162,9 +162,9 @@ def test_persistent_timeout_reruns_as_graphs(eng):
 
 
 def test_repeated_timeouts_leave_the_persistent_path(eng):
-    """Two timed-out launches in a row (the grid cannot be co-resident) make the engine stay
-    on the per-step graphs, so later utterances do not pay the wait bound; option persist = 1
-    re-enables the persistent path."""
+    """Two timed-out launches in a row (the grid cannot be co-resident) start a back-off hold
+    on the per-step graphs, so the next utterances do not pay the wait bound; option
+    persist = 1 ends the hold."""
     from genie_tts_amd.engine import make_sampler
     inp = t2s_inputs(R=12, S=10, H=41, tag="tmo2")
     sp = make_sampler(force_steps=10)
@@ -251,3 +251,117 @@ def test_multi_sequence_sampled_matches_graph_path(eng):
         eng.set_option("persist1m", 1)
     for i in range(len(inps)):
         assert a[i].tolist() == b[i].tolist(), f"utterance {i}"
+
+
+def test_timeout_backoff_reprobes_the_persistent_path(eng):
+    """After two timeouts in a row the engine holds on the per-step graphs for a bounded
+    number of generates (option persist_backoff), then probes the persistent path again:
+    once the condition has cleared, it is back (persist_launches grows again); tokens are
+    bit-exact throughout.  A probe that times out again starts a longer hold."""
+    from genie_tts_amd.engine import make_sampler
+    inp = t2s_inputs(R=12, S=10, H=41, tag="bko")
+    sp = make_sampler(force_steps=10)
+    eng.set_option("persist", 1)
+    eng.set_option("persist_backoff", 3)
+    eng.set_option("persist_backoff_ms", 600000)
+    try:
+        want = eng.t2s_generate([inp], sp)[0].tolist()
+        t0, d0 = eng.counter("persist_timeouts"), eng.counter("persist_disabled")
+        eng.set_option("persist_spin_ticks", 50)
+        try:
+            for _ in range(2):
+                assert eng.t2s_generate([inp], sp)[0].tolist() == want
+        finally:
+            eng.set_option("persist_spin_ticks", 0)
+        assert eng.counter("persist_timeouts") == t0 + 2
+        assert eng.counter("persist_disabled") == d0 + 1 and eng.counter("persist_hold") == 3
+        n0 = eng.counter("persist_launches")
+        for _ in range(2):                       # the hold: per-step graphs, no launch
+            assert eng.t2s_generate([inp], sp)[0].tolist() == want
+        assert eng.counter("persist_launches") == n0
+        for k in (1, 2):                         # the probe succeeds; the path stays
+            assert eng.t2s_generate([inp], sp)[0].tolist() == want
+            assert eng.counter("persist_launches") == n0 + k
+        assert eng.counter("persist_timeouts") == t0 + 2 and eng.counter("persist_hold") == 0
+        # the condition returns: two timeouts -> a hold of 3 (the successful launches reset
+        # the back-off); its probe times out again -> a hold twice as long
+        eng.set_option("persist_spin_ticks", 50)
+        try:
+            for _ in range(2):
+                assert eng.t2s_generate([inp], sp)[0].tolist() == want
+            assert eng.counter("persist_hold") == 3
+            for _ in range(3):                   # 2 on the graphs, then the failing probe
+                assert eng.t2s_generate([inp], sp)[0].tolist() == want
+        finally:
+            eng.set_option("persist_spin_ticks", 0)
+        assert eng.counter("persist_timeouts") == t0 + 5
+        assert eng.counter("persist_hold") == 6
+    finally:
+        eng.set_option("persist_backoff", 64)
+        eng.set_option("persist_backoff_ms", 5000)
+        eng.set_option("persist", 1)
+
+
+def _stop_during(eng, inps, sp, persist, delay_s):
+    """Request a stop `delay_s` into a generate; returns (raised EngineStopped, seconds from
+    the request to the generate's return, seconds the generate ran)."""
+    import threading
+    import time
+    from genie_tts_amd.engine import EngineStopped
+    eng.set_option("persist", persist)
+    res = {}
+
+    def run():
+        t = time.perf_counter()
+        try:
+            eng.t2s_generate(inps, sp)
+            res["stopped"] = False
+        except EngineStopped:
+            res["stopped"] = True
+        res["end"] = time.perf_counter()
+        res["ran"] = res["end"] - t
+    th = threading.Thread(target=run)
+    th.start()
+    time.sleep(delay_s)
+    t_req = time.perf_counter()
+    eng.request_stop(True)
+    th.join(timeout=30)
+    assert not th.is_alive()
+    eng.request_stop(False)
+    eng.set_option("persist", 1)
+    return res["stopped"], res["end"] - t_req, res["ran"]
+
+
+@pytest.mark.parametrize("B,persist", [(1, 1), (8, 1), (1, 0)])
+def test_stop_interrupts_a_running_decode(eng, B, persist):
+    """gsv_request_stop during a forced 500-step decode (the reference's stop_event,
+    checked every loop step, Inference.py:96-97): the generate raises EngineStopped within
+    a few steps of the request (a step is ~0.2 ms at B = 1), the stop counter grows, and
+    the engine decodes the same utterances bit-exactly afterwards."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=12 + i, S=10 + i, H=41, tag=f"stp{i}") for i in range(B)]
+    sp = make_sampler(force_steps=500)
+    eng.set_option("persist", 1)
+    full = eng.t2s_generate(inps, sp)                 # warm, and the uninterrupted tokens
+    import time
+    t = time.perf_counter()
+    eng.t2s_generate(inps, sp)
+    t_full = time.perf_counter() - t
+    s0 = eng.counter("stops")
+    stopped, latency, ran = _stop_during(eng, inps, sp, persist, 0.3 * t_full)
+    print(f"B={B} persist={persist}: full {t_full * 1e3:.1f} ms, stopped after {ran * 1e3:.1f} ms, "
+          f"{latency * 1e3:.2f} ms after the request")
+    assert stopped and eng.counter("stops") == s0 + 1
+    assert ran < 0.8 * t_full
+    # two loop steps of this decode plus the host's wake-up; the graph path checks its
+    # stop word per step too, but its host loop notices only between 8-step chunks
+    step = t_full / 500
+    assert latency < 2 * step + (8 * step if persist == 0 else 0) + 2e-3, latency
+    # a request before the call: nothing runs
+    eng.request_stop(True)
+    from genie_tts_amd.engine import EngineStopped
+    with pytest.raises(EngineStopped):
+        eng.t2s_generate(inps, sp)
+    eng.request_stop(False)
+    again = eng.t2s_generate(inps, sp)
+    assert [a.tolist() for a in again] == [f.tolist() for f in full]

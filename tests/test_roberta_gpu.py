@@ -2,7 +2,9 @@
 oracle, transformers' BertModel (the published chinese-roberta-wwm-ext-large
 architecture GPT-SoVITS exports) on the same synthetic weights:
 hidden_states[-3], CLS/SEP dropped, rows repeated by word2ph
-(GetPhonesAndBert.py:64-74).  ONNX-level parity unpinned (RoBERTa.onnx absent)."""
+(GetPhonesAndBert.py:64-74).  The weights are fp32-valued like RoBERTa.onnx's
+initializers, so the engine runs its split-weight GEMMs (W16 hi + lo planes).
+ONNX-level parity unpinned (RoBERTa.onnx absent)."""
 import numpy as np
 import pytest
 
@@ -12,11 +14,15 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 
-def _setup(n_layers):
+def _setup(n_layers, fp16=False):
+    """fp32-valued weights by default, as RoBERTa.onnx ships (ModelManager.py:139-142)."""
     from genie_tts_amd.engine import Engine
     from oracle import bert as B
-    w = synth.synth_weights(W.roberta_spec(n_layers))
-    return Engine({"roberta": w}, "v2"), B, B.bert_model(w, n_layers)
+    w = synth.synth_weights(W.roberta_spec(n_layers), fp16=fp16)
+    e = Engine({"roberta": w}, "v2")
+    # every projection of the layers that run (0 .. L-3) is an fp32 tensor -> hi + lo planes
+    assert e.counter("w16_split_tensors") == (0 if fp16 else 4 * (n_layers - 2))
+    return e, B, B.bert_model(w, n_layers)
 
 
 @pytest.mark.parametrize("n_layers,n_chars", [(4, 9), (24, 20)])   # reduced; the real 24-layer model
@@ -72,5 +78,31 @@ def test_roberta_batch_equals_single_calls():
             assert np.array_equal(g.cpu().numpy(), one)
         ref = B.bert_features(m, sents[1][0], sents[1][1])
         assert float(np.sqrt(np.mean((got[1].cpu().numpy() - ref) ** 2))) <= RMS_TOL
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("fp16", [True, False])
+def test_roberta_weight_precision(fp16):
+    """fp16-valued weights take one plane; fp32 ones keep their low bits: rounding the
+    fp32 weights to fp16 (what the engine did before) moves the output measurably more
+    than the split path's error against the fp32 oracle."""
+    e, B, m = _setup(4, fp16)
+    try:
+        r = synth.rng_for("rb-prec")
+        ids = np.concatenate([[101], r.integers(672, 8000, size=12), [102]]).astype(np.int64)
+        w2p = np.ones(12, np.int64)
+        got = e.roberta(ids, w2p).cpu().numpy()
+        ref = B.bert_features(m, ids, w2p)
+        rms = float(np.sqrt(np.mean((got - ref) ** 2)))
+        print(f"fp16={fp16}: rms {rms:.2e}")
+        assert rms <= 5e-6 * max(1.0, float(ref.std())), rms
+        if not fp16:
+            w16 = {k: v.astype(np.float16).astype(np.float32)
+                   for k, v in synth.synth_weights(W.roberta_spec(4), fp16=False).items()}
+            rounded = B.bert_features(B.bert_model(w16, 4), ids, w2p)
+            gap = float(np.sqrt(np.mean((rounded - ref) ** 2)))
+            print(f"fp16-rounded weights: rms {gap:.2e}")
+            assert gap > 10 * rms, (gap, rms)
     finally:
         e.close()
