@@ -315,12 +315,17 @@ int gsv_engine::sv_conv_upload(const std::string& wname, const std::string& bnam
     const int co = (int)w->dims[0], ci = (int)w->dims[1], k = (int)w->dims[2];
     if (w->dims[3] != k || ci % 8) return set_error(GSV_E_WEIGHT, "bad SV conv shape " + wname);
     std::vector<float> scale(co, 1.f), shift(co, 0.f);
-    if (!bname.empty()) {
-        const Staged* b = find(bname);
-        if (!b || (int)b->data.size() != co) return set_error(GSV_E_WEIGHT, "missing/bad SV weight " + bname);
+    // the conv's own bias (optional: the state-dict layout has none on BatchNorm'd convs;
+    // an export that folded the BatchNorm carries it there instead)
+    const Staged* b = bname.empty() ? nullptr : find(bname);
+    if (b) {
+        if ((int)b->data.size() != co) return set_error(GSV_E_WEIGHT, "bad SV weight " + bname);
         for (int o = 0; o < co; ++o) shift[o] = b->data[o];
     }
-    if (!bn.empty()) {
+    const bool has_bn = !bn.empty() && find(bn + ".weight");
+    if (!bn.empty() && !has_bn && !b)
+        return set_error(GSV_E_WEIGHT, "missing SV BatchNorm " + bn + " (and no folded bias " + bname + ")");
+    if (has_bn) {
         const Staged *g = find(bn + ".weight"), *be = find(bn + ".bias"), *mu = find(bn + ".running_mean"),
                      *var = find(bn + ".running_var");
         if (!g || !be || !mu || !var || (int)g->data.size() != co || (int)be->data.size() != co ||
@@ -370,13 +375,20 @@ int gsv_engine::finalize_sv() {
         const Staged* w = find("conv1.weight");
         if (!w || w->data.size() != 64 * 9) return set_error(GSV_E_WEIGHT, "missing/bad SV weight conv1.weight");
         const Staged *g = find("bn1.weight"), *be = find("bn1.bias"), *mu = find("bn1.running_mean"),
-                     *var = find("bn1.running_var");
-        if (!g || !be || !mu || !var) return set_error(GSV_E_WEIGHT, "missing SV BatchNorm bn1");
+                     *var = find("bn1.running_var"), *cb = find("conv1.bias");
+        if ((!g || !be || !mu || !var) && !cb) return set_error(GSV_E_WEIGHT, "missing SV BatchNorm bn1");
+        if (cb && cb->data.size() != 64) return set_error(GSV_E_WEIGHT, "bad SV weight conv1.bias");
         std::vector<float> hw(64 * 9), hb(64);
         for (int o = 0; o < 64; ++o) {
-            const float s = g->data[o] / sqrtf(var->data[o] + 1e-5f);
-            for (int t = 0; t < 9; ++t) hw[o * 9 + t] = w->data[o * 9 + t] * s;
-            hb[o] = be->data[o] - mu->data[o] * s;
+            const float b0 = cb ? cb->data[o] : 0.f;
+            if (g && be && mu && var) {
+                const float s = g->data[o] / sqrtf(var->data[o] + 1e-5f);
+                for (int t = 0; t < 9; ++t) hw[o * 9 + t] = w->data[o * 9 + t] * s;
+                hb[o] = (b0 - mu->data[o]) * s + be->data[o];
+            } else {   // BatchNorm folded into the conv by the export
+                for (int t = 0; t < 9; ++t) hw[o * 9 + t] = w->data[o * 9 + t];
+                hb[o] = b0;
+            }
         }
         S.stem_w = (float*)dalloc(hw.size() * 4);
         S.stem_b = (float*)dalloc(hb.size() * 4);
@@ -393,9 +405,10 @@ int gsv_engine::finalize_sv() {
             B.stride = b == 0 ? SV_STAGE_STRIDE[s] : 1;
             B.aff = SV_STAGE_AFF[s];
             const std::string p = "layer" + std::to_string(s + 1) + "." + std::to_string(b);
-            if (int e = sv_conv_upload(p + ".conv1.weight", "", p + ".bn1", &B.conv1)) return e;
+            if (int e = sv_conv_upload(p + ".conv1.weight", p + ".conv1.bias", p + ".bn1", &B.conv1)) return e;
             for (int i = 0; i < 4; ++i)
-                if (int e = sv_conv_upload(p + ".convs." + std::to_string(i) + ".weight", "",
+                if (int e = sv_conv_upload(p + ".convs." + std::to_string(i) + ".weight",
+                                           p + ".convs." + std::to_string(i) + ".bias",
                                            p + ".bns." + std::to_string(i), &B.convs[i]))
                     return e;
             if (B.aff)
@@ -404,17 +417,17 @@ int gsv_engine::finalize_sv() {
                     if (int e = sv_conv_upload(q + "0.weight", q + "0.bias", q + "1", &B.aff_a[i])) return e;
                     if (int e = sv_conv_upload(q + "3.weight", q + "3.bias", q + "4", &B.aff_b[i])) return e;
                 }
-            if (int e = sv_conv_upload(p + ".conv3.weight", "", p + ".bn3", &B.conv3)) return e;
+            if (int e = sv_conv_upload(p + ".conv3.weight", p + ".conv3.bias", p + ".bn3", &B.conv3)) return e;
             B.has_sc = find(p + ".shortcut.0.weight") != nullptr;
             if (B.has_sc)
-                if (int e = sv_conv_upload(p + ".shortcut.0.weight", "", p + ".shortcut.1", &B.sc)) return e;
+                if (int e = sv_conv_upload(p + ".shortcut.0.weight", p + ".shortcut.0.bias", p + ".shortcut.1", &B.sc)) return e;
             if (B.conv1.cin != cin || B.conv3.cout != planes * 4 || (!B.has_sc && (B.stride != 1 || cin != planes * 4)))
                 return set_error(GSV_E_WEIGHT, "SV block " + p + " shape mismatch");
             S.blocks.push_back(B);
             cin = planes * 4;
         }
     }
-    if (int e = sv_conv_upload("layer3_ds.weight", "", "", &S.ds34)) return e;
+    if (int e = sv_conv_upload("layer3_ds.weight", "layer3_ds.bias", "", &S.ds34)) return e;
     if (int e = sv_conv_upload("fuse34.local_att.0.weight", "fuse34.local_att.0.bias", "fuse34.local_att.1", &S.fuse_a))
         return e;
     if (int e = sv_conv_upload("fuse34.local_att.3.weight", "fuse34.local_att.3.bias", "fuse34.local_att.4", &S.fuse_b))

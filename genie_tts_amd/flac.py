@@ -210,6 +210,73 @@ _RATES = {1: 88200, 2: 176400, 3: 192000, 4: 8000, 5: 16000, 6: 22050, 7: 24000,
 _SIZES = {1: 8, 2: 12, 4: 16, 5: 20, 6: 24, 7: 32}
 
 
+def _next_sync(data: bytes, pos: int) -> int:
+    """Byte offset of the next frame sync code (0xFFF8 / 0xFFF9) at or after pos, or -1."""
+    while True:
+        i = data.find(b"\xff", pos)
+        if i < 0 or i + 1 >= len(data):
+            return -1
+        if data[i + 1] in (0xF8, 0xF9):
+            return i
+        pos = i + 1
+
+
+def _frame(r: "_Bits", data: bytes, start: int, info: dict, rate: int):
+    """One frame after its sync code -> (sample rate, bits per sample, channel samples)."""
+    r.read(1)                                # blocking strategy (fixed / variable)
+    bcode, rcode, chmode, scode = r.read(4), r.read(4), r.read(4), r.read(3)
+    r.read(1)
+    _utf8_number(r)
+    if bcode == 0:
+        raise FlacError("reserved block size")
+    block = (192 if bcode == 1 else 576 << (bcode - 2) if bcode <= 5 else
+             r.read(8) + 1 if bcode == 6 else r.read(16) + 1 if bcode == 7 else 256 << (bcode - 8))
+    if rcode == 12:
+        rate = r.read(8) * 1000
+    elif rcode == 13:
+        rate = r.read(16)
+    elif rcode == 14:
+        rate = r.read(16) * 10
+    elif rcode == 15:
+        raise FlacError("invalid sample rate code")
+    elif rcode:
+        rate = _RATES[rcode]
+    fbps = info["bps"] if scode == 0 else _SIZES.get(scode)
+    if fbps is None:
+        raise FlacError("reserved sample size")
+    hcrc = r.read(8)
+    if crc8(data[start:r.byte - 1]) != hcrc:
+        raise FlacError(f"frame header CRC mismatch at byte {start}")
+    if chmode <= 7:
+        n_ch = chmode + 1
+        sub = [_subframe(r, block, fbps) for _ in range(n_ch)]
+    elif chmode <= 10:
+        n_ch = 2
+        side_first = chmode == 9
+        a = _subframe(r, block, fbps + (1 if side_first else 0))
+        b = _subframe(r, block, fbps + (0 if side_first else 1))
+        if chmode == 8:                      # left, side
+            sub = [a, [l - s for l, s in zip(a, b)]]
+        elif chmode == 9:                    # side, right
+            sub = [[s + rr for s, rr in zip(a, b)], b]
+        else:                                # mid, side
+            left, right = [], []
+            for m, s in zip(a, b):
+                m = (m << 1) | (s & 1)
+                left.append((m + s) >> 1)
+                right.append((m - s) >> 1)
+            sub = [left, right]
+    else:
+        raise FlacError("reserved channel assignment")
+    if n_ch != info["channels"]:
+        raise FlacError("channel count differs from STREAMINFO")
+    r.align()
+    fcrc = r.read(16)
+    if crc16(data[start:r.byte - 2]) != fcrc:
+        raise FlacError(f"frame CRC mismatch at byte {start}")
+    return rate, fbps, sub
+
+
 def decode(data: bytes) -> Tuple[np.ndarray, int, int]:
     """FLAC bytes -> (int32 samples [frames, channels], sample rate, bits per sample)."""
     if data[:4] != b"fLaC":
@@ -235,63 +302,28 @@ def decode(data: bytes) -> Tuple[np.ndarray, int, int]:
     r = _Bits(data, pos)
     rate, bps = info["rate"], info["bps"]
     while r.byte + 2 <= len(data):
+        if info["total"] and len(chans[0]) >= info["total"]:
+            break                                # every sample STREAMINFO announced: trailing
+                                                 # bytes (an ID3v1 'TAG' block, padding) are not audio
         start = r.byte
-        if r.read(15) != 0x7FFC:                 # sync 0b11111111111110 + reserved 0
-            raise FlacError(f"lost frame sync at byte {start}")
-        r.read(1)                                # blocking strategy (fixed / variable)
-        bcode, rcode, chmode, scode = r.read(4), r.read(4), r.read(4), r.read(3)
-        r.read(1)
-        _utf8_number(r)
-        if bcode == 0:
-            raise FlacError("reserved block size")
-        block = (192 if bcode == 1 else 576 << (bcode - 2) if bcode <= 5 else
-                 r.read(8) + 1 if bcode == 6 else r.read(16) + 1 if bcode == 7 else 256 << (bcode - 8))
-        if rcode == 12:
-            rate = r.read(8) * 1000
-        elif rcode == 13:
-            rate = r.read(16)
-        elif rcode == 14:
-            rate = r.read(16) * 10
-        elif rcode == 15:
-            raise FlacError("invalid sample rate code")
-        elif rcode:
-            rate = _RATES[rcode]
-        fbps = info["bps"] if scode == 0 else _SIZES.get(scode)
-        if fbps is None:
-            raise FlacError("reserved sample size")
-        bps = fbps
-        hcrc = r.read(8)
-        if crc8(data[start:r.byte - 1]) != hcrc:
-            raise FlacError(f"frame header CRC mismatch at byte {start}")
-        if chmode <= 7:
-            n_ch = chmode + 1
-            sub = [_subframe(r, block, fbps) for _ in range(n_ch)]
-        elif chmode <= 10:
-            n_ch = 2
-            side_first = chmode == 9
-            a = _subframe(r, block, fbps + (1 if side_first else 0))
-            b = _subframe(r, block, fbps + (0 if side_first else 1))
-            if chmode == 8:                      # left, side
-                sub = [a, [l - s for l, s in zip(a, b)]]
-            elif chmode == 9:                    # side, right
-                sub = [[s + rr for s, rr in zip(a, b)], b]
-            else:                                # mid, side
-                left, right = [], []
-                for m, s in zip(a, b):
-                    m = (m << 1) | (s & 1)
-                    left.append((m + s) >> 1)
-                    right.append((m - s) >> 1)
-                sub = [left, right]
-        else:
-            raise FlacError("reserved channel assignment")
-        if n_ch != info["channels"]:
-            raise FlacError("channel count differs from STREAMINFO")
-        r.align()
-        fcrc = r.read(16)
-        if crc16(data[start:r.byte - 2]) != fcrc:
-            raise FlacError(f"frame CRC mismatch at byte {start}")
+        try:
+            if r.read(15) != 0x7FFC:             # sync 0b11111111111110 + reserved 0
+                raise FlacError(f"lost frame sync at byte {start}")
+            rate, bps, sub = _frame(r, data, start, info, rate)
+        except FlacError:
+            if not chans[0]:
+                raise
+            # after audio: bytes that are no frame (a tag, padding, junk holding a sync code);
+            # libFLAC searches for the next frame, so do we
+            nxt = _next_sync(data, start + 1)
+            if nxt < 0:
+                break
+            r = _Bits(data, nxt)
+            continue
         for c, x in zip(chans, sub):
             c.extend(x)
+    if info["total"] and len(chans[0]) < info["total"]:
+        raise FlacError(f"{len(chans[0])} samples decoded, STREAMINFO announces {info['total']}")
     pcm = np.asarray(chans, np.int64).T
     if info["total"]:
         pcm = pcm[:info["total"]]

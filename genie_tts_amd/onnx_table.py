@@ -129,3 +129,57 @@ def read_initializer_values(path: str, spec) -> Dict[str, "object"]:
             raise ValueError(f"{name}: shape {found[name].shape} in graph, expected {shape}")
         out[name] = found[name]
     return out
+
+
+def _inline_array(v2):
+    """(name, ndarray or None) of an inline TensorProto (FLOAT / FLOAT16 raw_data)."""
+    import numpy as np
+    name, dims, dtype, raw = "", [], 0, b""
+    for f3, wt, v3 in _walk(v2):
+        if f3 == 1:
+            if wt == 0:
+                dims.append(v3)
+            else:
+                q = 0
+                while q < len(v3):
+                    d, q = _varint(v3, q)
+                    dims.append(d)
+        elif f3 == 2:
+            dtype = v3
+        elif f3 == 8:
+            name = bytes(v3).decode()
+        elif f3 == 9:
+            raw = bytes(v3)
+    dt = {1: np.float32, 10: np.float16}.get(dtype)
+    arr = np.frombuffer(raw, dtype=dt).reshape(dims) if dt is not None and raw else None
+    return name, arr
+
+
+def read_graph(path: str):
+    """Inline initializers and nodes of a graph: ({name: ndarray}, [(op_type, inputs,
+    outputs, node name)] in file order, which torch.onnx.export writes topologically).
+    NodeProto: input=1, output=2, name=3, op_type=4; GraphProto: node=1, initializer=5."""
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    inits, nodes = {}, []
+    for f, _, v in _walk(buf):
+        if f != 7:
+            continue
+        for f2, _, v2 in _walk(v):
+            if f2 == 5:
+                name, arr = _inline_array(v2)
+                if arr is not None:
+                    inits[name] = arr
+            elif f2 == 1:
+                ins, outs, nm, op = [], [], "", ""
+                for f3, _, v3 in _walk(v2):
+                    if f3 == 1:
+                        ins.append(bytes(v3).decode())
+                    elif f3 == 2:
+                        outs.append(bytes(v3).decode())
+                    elif f3 == 3:
+                        nm = bytes(v3).decode()
+                    elif f3 == 4:
+                        op = bytes(v3).decode()
+                nodes.append((op, ins, outs, nm))
+    return inits, nodes

@@ -276,6 +276,11 @@ class Router:
             except (EOFError, OSError):
                 self._worker_died(i)
                 return
+            if msg.get("kind") != "chunk":   # a final reply: worker i owes this request nothing more
+                with self.state_lock:
+                    ws = self.sent_to.get(msg["id"])
+                    if ws is not None:
+                        ws.discard(i)
             q = self.queues.get(msg["id"])
             if q is not None:
                 self.loop.call_soon_threadsafe(q.put_nowait, (i, msg))
@@ -315,7 +320,11 @@ class Router:
                 self.sent_to[rid] = set(live)
             for i in live:
                 self._send(i, dict(cmd=cmd, id=rid, **kw))
-            return [(await q.get())[1] for _ in live]
+            got: Dict[int, dict] = {}
+            while len(got) < len(live):         # one reply per worker (a dying worker's error
+                i, msg = await q.get()          # may follow its own final reply: keep the first)
+                got.setdefault(i, msg)
+            return [got[i] for i in live]
         finally:
             self.queues.pop(rid, None)
             with self.state_lock:
@@ -326,9 +335,15 @@ class Router:
         rid = next(self.ids)
         q: asyncio.Queue = asyncio.Queue()
         self.queues[rid] = q
-        i = min(self._live(), key=lambda k: self.load[k])
-        self.load[i] += 1
+        # pick the worker and record what it owes under one lock: a worker that dies before
+        # is not picked, one that dies after finds this request in sent_to (_worker_died)
         with self.state_lock:
+            live = [k for k in range(len(self.conns)) if k not in self.dead]
+            if not live:
+                self.queues.pop(rid, None)
+                raise RuntimeError("no live engine worker")
+            i = min(live, key=lambda k: self.load[k])
+            self.load[i] += 1
             self.sent_to[rid] = {i}
         try:
             self._send(i, dict(cmd="tts", id=rid, **kw))

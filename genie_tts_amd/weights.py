@@ -17,7 +17,7 @@ from __future__ import annotations
 import os
 from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -368,15 +368,81 @@ def sv_spec() -> Spec:
     return s
 
 
+def sv_conv_order() -> List[Tuple[str, Optional[str]]]:
+    """The SV model's convs in forward3's execution order (the order torch.onnx.export
+    writes their Conv nodes): (conv prefix, BatchNorm prefix applied to its output or
+    None).  Stem; per block conv1, convs.0, [fuse_models.i-1 local_att.0 / .3,] convs.i,
+    conv3, shortcut.0; then layer3_ds (computed after layer4) and fuse34."""
+    order: List[Tuple[str, Optional[str]]] = [("conv1", "bn1")]
+    cin = 64
+    for li, (planes, nb, stride, use_aff) in enumerate(SV_STAGES, start=1):
+        for b in range(nb):
+            p = f"layer{li}.{b}"
+            order.append((p + ".conv1", p + ".bn1"))
+            for i in range(4):
+                if i > 0 and use_aff:
+                    order.append((p + f".fuse_models.{i - 1}.local_att.0", p + f".fuse_models.{i - 1}.local_att.1"))
+                    order.append((p + f".fuse_models.{i - 1}.local_att.3", p + f".fuse_models.{i - 1}.local_att.4"))
+                order.append((p + f".convs.{i}", p + f".bns.{i}"))
+            order.append((p + ".conv3", p + ".bn3"))
+            st = stride if b == 0 else 1
+            if st != 1 or cin != planes * 4:
+                order.append((p + ".shortcut.0", p + ".shortcut.1"))
+            cin = planes * 4
+    order.append(("layer3_ds", None))
+    order.append(("fuse34.local_att.0", "fuse34.local_att.1"))
+    order.append(("fuse34.local_att.3", "fuse34.local_att.4"))
+    return order
+
+
 def load_sv_weights(path: str) -> Dict[str, np.ndarray]:
     """GenieData speaker_encoder.onnx (`g/ModelManager.py:155-170`, plain ONNX with
-    fp32 initializers, no fp16 bin) read through the initializer table by sv_spec
-    names.  Unverified against a real file (none offline): an export that folded
-    BatchNorm into the convs under other initializer names is not readable here."""
-    from .onnx_table import read_initializer_values
+    fp32 initializers, no fp16 bin).  Two layouts are read:
+
+      * initializers under sv_spec's state-dict names (BatchNorm unfolded);
+      * an export that renamed them (onnx::Conv_N ...), with or without BatchNorm
+        folded into the convs: its Conv nodes, in the file's (topological) order, are
+        mapped onto sv_conv_order() with every weight shape checked; a conv's own bias
+        input becomes '<conv>.bias', and a BatchNormalization node reading a conv's
+        output gives that conv's BatchNorm tensors (folded exports have none: the
+        engine then takes the conv bias alone).
+
+    Neither fits -> KeyError naming the missing tensors.  Unverified against the real
+    file (none offline): SV parity at the ONNX level is unpinned."""
+    from .onnx_table import read_graph, read_initializer_values
     if os.path.isdir(path):
         path = os.path.join(path, "speaker_encoder.onnx")
-    return read_initializer_values(path, sv_spec())
+    spec = sv_spec()
+    try:
+        return read_initializer_values(path, spec)
+    except KeyError:
+        pass
+    inits, nodes = read_graph(path)
+    missing = [n for n in spec if n not in inits]
+    convs = [nd for nd in nodes if nd[0] == "Conv"]
+    order = sv_conv_order()
+    if len(convs) != len(order):
+        raise KeyError(f"{path}: {len(missing)} SV initializers missing by name (e.g. {missing[:4]}) and "
+                       f"{len(convs)} Conv nodes where the renamed layout has {len(order)}")
+    bn_of = {nd[1][0]: nd for nd in nodes if nd[0] == "BatchNormalization"}
+    out: Dict[str, np.ndarray] = {}
+    for k, ((conv, bn), nd) in enumerate(zip(order, convs)):
+        w = inits.get(nd[1][1]) if len(nd[1]) > 1 else None
+        want = spec[conv + ".weight"]
+        if w is None or tuple(w.shape) != tuple(want):
+            raise KeyError(f"{path}: Conv node {k} ({nd[3] or nd[1][1]}) has weight shape "
+                           f"{None if w is None else tuple(w.shape)}, expected {conv}.weight {want}")
+        out[conv + ".weight"] = np.asarray(w, np.float32)
+        b = inits.get(nd[1][2]) if len(nd[1]) > 2 and nd[1][2] else None
+        if b is not None:
+            out[conv + ".bias"] = np.asarray(b, np.float32).reshape(-1)
+        bnode = bn_of.get(nd[2][0]) if nd[2] else None
+        if bn is not None and bnode is not None:
+            for leaf, name in zip(("weight", "bias", "running_mean", "running_var"), bnode[1][1:5]):
+                out[f"{bn}.{leaf}"] = np.asarray(inits[name], np.float32).reshape(-1)
+        elif bn is not None and b is None:
+            raise KeyError(f"{path}: {conv} has neither a bias (folded BatchNorm) nor a BatchNormalization node")
+    return out
 
 
 def spec_numel(spec: Spec) -> int:

@@ -82,6 +82,8 @@ def fbank(wav: np.ndarray) -> torch.Tensor:
 
 
 def _bn(x, w, p):
+    if p + ".weight" not in w:     # an export with BatchNorm folded into the conv (its bias)
+        return x
     return F.batch_norm(x, w[p + ".running_mean"], w[p + ".running_var"], w[p + ".weight"], w[p + ".bias"],
                         training=False, eps=BN_EPS)
 
@@ -101,7 +103,7 @@ def _aff(w, p, x, y):
 
 def _block(w, p, x, planes, stride, aff):
     width = int(math.floor(planes * (BASE_WIDTH / 64.0)))
-    out = _relu20(_bn(F.conv2d(x, w[p + ".conv1.weight"], stride=stride), w, p + ".bn1"))
+    out = _relu20(_bn(F.conv2d(x, w[p + ".conv1.weight"], w.get(p + ".conv1.bias"), stride=stride), w, p + ".bn1"))
     spx = torch.split(out, width, 1)
     outs = []
     sp = None
@@ -112,11 +114,11 @@ def _block(w, p, x, planes, stride, aff):
             sp = _aff(w, f"{p}.fuse_models.{i - 1}", sp, spx[i])
         else:
             sp = sp + spx[i]
-        sp = _relu20(_bn(F.conv2d(sp, w[f"{p}.convs.{i}.weight"], padding=1), w, f"{p}.bns.{i}"))
+        sp = _relu20(_bn(F.conv2d(sp, w[f"{p}.convs.{i}.weight"], w.get(f"{p}.convs.{i}.bias"), padding=1), w, f"{p}.bns.{i}"))
         outs.append(sp)
-    out = _bn(F.conv2d(torch.cat(outs, 1), w[p + ".conv3.weight"]), w, p + ".bn3")
+    out = _bn(F.conv2d(torch.cat(outs, 1), w[p + ".conv3.weight"], w.get(p + ".conv3.bias")), w, p + ".bn3")
     if p + ".shortcut.0.weight" in w:
-        res = _bn(F.conv2d(x, w[p + ".shortcut.0.weight"], stride=stride), w, p + ".shortcut.1")
+        res = _bn(F.conv2d(x, w[p + ".shortcut.0.weight"], w.get(p + ".shortcut.0.bias"), stride=stride), w, p + ".shortcut.1")
     else:
         res = x
     return _relu20(out + res)
@@ -126,13 +128,13 @@ def _block(w, p, x, planes, stride, aff):
 def forward3(w: Dict[str, torch.Tensor], feat: torch.Tensor) -> torch.Tensor:
     """ERes2NetV2.forward3 on feat [T, 80] -> [1, 20480] (channel-major c * 10 + f)."""
     x = feat.T.contiguous()[None, None]                       # (B, 1, F=80, T)
-    out = F.relu(_bn(F.conv2d(x, w["conv1.weight"], padding=1), w, "bn1"))
+    out = F.relu(_bn(F.conv2d(x, w["conv1.weight"], w.get("conv1.bias"), padding=1), w, "bn1"))
     outs = []
     for s, (planes, nb, stride, aff) in enumerate(STAGES, start=1):
         for b in range(nb):
             out = _block(w, f"layer{s}.{b}", out, planes, stride if b == 0 else 1, aff)
         outs.append(out)
-    out3_ds = F.conv2d(outs[2], w["layer3_ds.weight"], stride=2, padding=1)
+    out3_ds = F.conv2d(outs[2], w["layer3_ds.weight"], w.get("layer3_ds.bias"), stride=2, padding=1)
     fuse = _aff(w, "fuse34", outs[3], out3_ds)
     return torch.flatten(fuse, start_dim=1, end_dim=2).mean(-1)
 

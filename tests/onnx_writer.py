@@ -59,3 +59,18 @@ def model_inline(arrays) -> bytes:
     for name, a in arrays.items():
         graph += _field(5, 2, tensor_inline(name, a))
     return _field(1, 0, _varint(9)) + _field(7, 2, graph)
+
+
+def node(op: str, inputs, outputs, name: str = "") -> bytes:
+    body = b"".join(_str(1, i) for i in inputs) + b"".join(_str(2, o) for o in outputs)
+    if name:
+        body += _str(3, name)
+    return body + _str(4, op)
+
+
+def model_graph(arrays, nodes) -> bytes:
+    """Inline initializers plus nodes [(op_type, inputs, outputs, name)] in order."""
+    graph = b"".join(_field(1, 2, node(*n)) for n in nodes) + _str(2, "g")
+    for name, a in arrays.items():
+        graph += _field(5, 2, tensor_inline(name, a))
+    return _field(1, 0, _varint(9)) + _field(7, 2, graph)

@@ -82,3 +82,22 @@ def test_load_audio_flac_equals_wav(tmp_path):
     a, b = A.load_audio(str(fl), 32000), A.load_audio(str(wv), 32000)
     assert a.shape == b.shape == (int(np.ceil(3 * 32000)) + int(0.3 * 32000),)
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("tail", [b"TAG" + bytes(125), bytes(64), b"\xff\xf8junk\xff\xf9\x00\x00"])
+def test_trailing_bytes_after_the_last_frame(tail):
+    """an ID3v1 'TAG' block, zero padding or junk holding a sync pattern after
+    the last frame is not audio (libsndfile reads such files): decoding stops at
+    STREAMINFO's sample count, or resynchronises and finds no further frame."""
+    x = _sig(1024 + 576, 1, 16)
+    frames = [dict(n=1024, mode=0, sub=[dict(LPC)]), dict(n=576, mode=0, sub=[dict(kind="fixed", order=2)])]
+    data = encode(x, 32000, 16, frames)
+    pcm, _, _ = flac.decode(data + tail)
+    assert np.array_equal(pcm, x)
+    # STREAMINFO total 0 (unknown): the same bytes end at the last real frame too
+    i = data.index(b"fLaC") + 4 + 4 + 13             # STREAMINFO body byte 13: total samples start
+    body = bytearray(data)
+    body[i] &= 0xF0
+    body[i + 1:i + 5] = bytes(4)
+    pcm, _, _ = flac.decode(bytes(body) + tail)
+    assert np.array_equal(pcm, x)

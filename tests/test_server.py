@@ -183,3 +183,35 @@ def test_router_fails_requests_of_a_dead_worker():
         finally:
             router.close()
     asyncio.run(run())
+
+
+def reply_then_die_worker(index, conn, cfg):
+    """Worker 0 answers the 'stop' broadcast and then exits; worker 1 answers it late."""
+    import time
+    conn.send(dict(kind="ready", id=-1, index=index))
+    while True:
+        msg = conn.recv()
+        if msg is None:
+            return
+        if index == 1:
+            time.sleep(0.5)
+        conn.send(dict(kind="ok", id=msg["id"], index=index))
+        if index == 0:
+            conn.close()
+            os._exit(0)
+
+
+def test_broadcast_keeps_the_reply_of_a_worker_that_dies_after_answering():
+    """a worker's final reply clears what it owes, so its later death adds no
+    error for that request, and a broadcast waits for one reply from every worker."""
+    from genie_tts_amd.server import Router
+
+    async def run():
+        router = Router([0, 1], worker=reply_then_die_worker)
+        router.start(asyncio.get_running_loop(), timeout=120)
+        try:
+            res = await asyncio.wait_for(router.broadcast("stop"), 60)
+            assert [(r["kind"], r.get("index")) for r in res] == [("ok", 0), ("ok", 1)]
+        finally:
+            router.close()
+    asyncio.run(run())

@@ -105,3 +105,35 @@ def test_sv_loader_reads_speaker_encoder_onnx(tmp_path):
         assert list(got) == list(W.sv_spec())
         for k in ("conv1.weight", "layer4.2.fuse_models.2.local_att.4.running_var", "fuse34.local_att.3.weight"):
             np.testing.assert_array_equal(np.asarray(got[k], np.float32), w[k])
+
+
+def test_sv_loader_reads_renamed_exports(tmp_path):
+    """speaker_encoder.onnx exports that renamed the initializers
+    (onnx::Conv_N) are read by Conv node order: with BatchNormalization nodes the
+    state-dict tensors come back exactly; with BatchNorm folded into the convs the
+    oracle's forward over the loaded tensors equals the unfolded model's."""
+    from tests.sv_export import export
+    w = synth.synth_sv_weights()
+    p = str(tmp_path / "bn.onnx")
+    export(w, p, folded=False)
+    got = W.load_sv_weights(p)
+    assert set(got) == set(W.sv_spec()) and all(np.array_equal(got[k], w[k]) for k in got)
+    p = str(tmp_path / "folded.onnx")
+    export(w, p, folded=True)
+    got = W.load_sv_weights(p)
+    assert not any(k.endswith("running_var") for k in got) and "layer1.0.conv1.bias" in got
+    a = (0.1 * synth.rng_for("sv-fold").standard_normal(16000)).astype(np.float32)
+    ref, fol = S.sv_embedding(w, a), S.sv_embedding(got, a)
+    # fp32 folding reorders the rounding; a wrong conv mapping would differ by O(1)
+    rel = float(np.sqrt(np.mean((fol - ref) ** 2)) / np.sqrt(np.mean(ref ** 2)))
+    assert rel <= 1e-4, rel
+
+
+def test_sv_loader_names_what_is_missing(tmp_path):
+    from tests.onnx_writer import model_graph
+    p = str(tmp_path / "bad.onnx")
+    with open(p, "wb") as f:
+        f.write(model_graph({"onnx::Conv_0": np.zeros((64, 1, 3, 3), np.float32)},
+                            [("Conv", ["x", "onnx::Conv_0"], ["y"], "/conv1/Conv")]))
+    with pytest.raises(KeyError, match="conv1.weight|missing"):
+        W.load_sv_weights(p)

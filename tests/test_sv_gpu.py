@@ -144,3 +144,26 @@ def test_reference_audio_gets_sv_from_engine(svm, tmp_path):
         model_manager.speaker_verification_model = None
         model_manager.character_to_model.pop("svc", None)
         genie.clear_reference_audio_cache()
+
+
+@pytest.mark.parametrize("folded", [False, True])
+def test_sv_renamed_export_on_the_engine(svm, tmp_path, folded):
+    """An export with renamed initializers (weights.load_sv_weights' Conv-order mapping):
+    with BatchNormalization nodes the engine gets the very same tensors; with BatchNorm
+    folded into the convs it takes their biases instead and gives the same embedding
+    (the engine folds BatchNorm in the same fp32 arithmetic)."""
+    from genie_tts_amd import weights as W
+    from genie_tts_amd.engine import Engine
+    from tests.sv_export import export
+    e0, w = svm
+    p = str(tmp_path / "speaker_encoder.onnx")
+    export(w, p, folded=folded)
+    e = Engine({"sv": W.load_sv_weights(p)}, "v2")
+    try:
+        a = _clip(48000, "sv-renamed")
+        got, ref = e.sv(a).cpu().numpy().reshape(1, -1), e0.sv(a).cpu().numpy().reshape(1, -1)
+        rel = float(np.sqrt(np.mean((got - ref) ** 2)) / np.sqrt(np.mean(ref ** 2)))
+        print(f"folded={folded}: rel rms {rel:.2e}")
+        assert rel <= 1e-6, rel
+    finally:
+        e.close()
