@@ -84,6 +84,13 @@ gsv_engine::~gsv_engine() {
         for (hipEvent_t e : {g.d0, g.done, g.k0, g.k1})
             if (e) hipEventDestroy(e);
     }
+    for (float* p : {sgb.z, sgb.dcond, sgb.audio, sgb.g[0], sgb.g[1], sgb.g[2], sgb.g[3], sgb.g[4]})
+        if (p) hipFree(p);
+    for (int* p : {sgb.seg[0], sgb.seg[1], sgb.seg[2], sgb.seg[3], sgb.seg[4], sgb.seg[5], sgb.off, sgb.len, sgb.ovf})
+        if (p) hipFree(p);
+    if (sgb.ovf_host) hipHostFree(sgb.ovf_host);
+    if (sgb.h_pin) hipHostFree(sgb.h_pin);
+    if (sgb.done) hipEventDestroy(sgb.done);
     if (vovf_host) hipHostFree(vovf_host);
     if (vovf) hipFree(vovf);
     for (auto& L : vlanes) {
@@ -1846,6 +1853,9 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
             eng->stream = ns;
             eng->t2s_priority = p;
         }
+    } else if (n == "seg_vocoder") {   // batched vocoder: one generator pass over the batch (0: per-lane passes)
+        if (int r = eng->vits_batch_finish(nullptr)) return r;
+        eng->seg_vocoder = value != 0;
     } else if (n == "vits_threads") {   // vocoder lanes issued by one host thread each (default 1)
         eng->vits_threads = value != 0;
     } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)

@@ -294,6 +294,32 @@ struct gsv_engine {
                          const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
                          const float* eps, uint64_t noise_seed, float noise_scale, float* audio, hipStream_t st,
                          int* ovf, bool timed);
+    int vits_front(gsv::VitsWorkspace& W, const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
+                   const float* ref_audio, int n_audio, const float* ge, const float* ge_adv, const float* eps,
+                   uint64_t noise_seed, float noise_scale, float* dcond_out, hipStream_t st);
+    // segmented vocoder batch (option "seg_vocoder", default 1): every utterance's front part
+    // (vits_front) on the lanes, then ONE generator pass over all of them laid out back to
+    // back along time with zero gaps (gsv::ConvArgs::seg), on lane 0's stream
+    struct SegBatch {
+        size_t cap_t = 0;              // frames (rate T) of the buffers
+        int cap_n = 0;
+        float *z = nullptr, *dcond = nullptr, *audio = nullptr;
+        float* g[5] = {};
+        int* seg[6] = {};
+        int *off = nullptr, *len = nullptr;
+        int* ovf = nullptr;
+        int* ovf_host = nullptr;
+        int* h_pin = nullptr;          // pinned staging of the offset / length tables
+        std::vector<int> h_off, h_len;
+        int T = 0;                     // frames of the current batch (incl. gaps)
+        hipEvent_t done = nullptr;
+        hipStream_t st = nullptr;      // the stream the generator ran on
+    } sgb;
+    bool seg_vocoder = true;
+    static constexpr int SEG_GAP = 4;  // zero frames between utterances (>= every conv halo at rate T)
+    int seg_reserve(int n, int T);
+    int seg_generate(hipStream_t st, bool f16);
+    void seg_copy_out(hipStream_t st);
     // concurrent vocoder lanes (gsv_vits_decode_batch)
     int vits_lanes = 4;                    // option "vits_lanes" (1..16): concurrent vocoder streams;
                                            // 4 = HIP's default hardware queues per process
@@ -315,6 +341,7 @@ struct gsv_engine {
     std::vector<int> vb_rcs;
     std::vector<std::string> vb_errs;   // each failed lane thread's error text
     int vb_k = 0;
+    bool vb_seg = false;               // the running batch is a segmented one (sgb)
     float vb_scale = 0.f;
     bool vb_active = false;
     int vits_batch_launch(float noise_scale, hipStream_t s, bool join);

@@ -54,8 +54,16 @@ struct ConvArgs {
     // scale (weight norm g/||v||, 1 without it), overflow flag set when an
     // input does not fit fp16.  wh == nullptr -> f32 path.
     const __half* wh; const float* wscale; int* ovf;
+    // segmented batch (several utterances back to back along time, zero gaps between
+    // them): seg[tp] = the utterance of output time tp, or -1 in a gap, where the
+    // output is written as 0 (so every buffer keeps zero gaps, and a conv whose halo
+    // reaches into a gap reads the zero padding a single-utterance call sees);
+    // CV_VEC / CV_RESID_VEC read vec + seg[tp] * vec_sstride
+    const int* seg; long vec_sstride;
 };
 void conv1d(const ConvArgs& a, hipStream_t s);
+// seg[t] for t < n: i with off[i] * f <= t < (off[i] + len[i]) * f, else -1 (off ascending)
+void seg_fill(int* seg, long n, const int* off, const int* len, int nseg, int f, hipStream_t s);
 // f16-split path; returns false (nothing launched) when the shape is not covered.
 bool conv1d_h(const ConvArgs& a, hipStream_t s);
 

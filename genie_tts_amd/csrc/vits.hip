@@ -219,6 +219,25 @@ void conv1d(const ConvArgs& a, hipStream_t s) {
     }
 }
 
+// ------------------------------------------------------------ segment table
+__global__ __launch_bounds__(256) void k_seg_fill(int* seg, long n, const int* off, const int* len, int nseg,
+                                                   int f) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n) return;
+    int lo = 0, hi = nseg - 1;   // last segment with off * f <= t
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((long)off[mid] * f <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    const long a = (long)off[lo] * f;
+    seg[t] = (t >= a && t < a + (long)len[lo] * f) ? lo : -1;
+}
+
+void seg_fill(int* seg, long n, const int* off, const int* len, int nseg, int f, hipStream_t s) {
+    hipLaunchKernelGGL(k_seg_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, seg, n, off, len, nseg, f);
+}
+
 // ----------------------------------------------------------------- LN over C
 // modules.LayerNorm: transpose -> layer_norm(channels, eps 1e-5) -> transpose.
 // Block = 64 time columns x 4 channel groups; each thread keeps its channel

@@ -590,6 +590,75 @@ int gsv_engine::vits_wait(hipStream_t caller) {
     return 0;
 }
 
+// The HiFi-GAN generator (vits_fp32.onnx dec.*) on z [192][T]: conv_pre + the
+// conditioning vector dcond, 5 x (ConvTranspose1d up + 3 MRF resblocks), conv_post + tanh
+// -> audio [T * prod(up_rate)].  gb: five buffers of >= upc * T * 20 floats.  seg
+// (segmented batch, else null): the time tables of the 6 rates (T, T u0, ...), and
+// dcond holds one vector per utterance (stride dcond_sstride); gaps stay zero.
+static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const float* z, int T, const float* dcond,
+                           long dcond_sstride, const int* const* seg, float* audio, hipStream_t s) {
+    float* x = gb[0];
+    // x = conv_pre(z) + cond(ge)   (dec#: Conv -> Add(cond))
+    ConvArgs c2 = cargs(V.conv_pre, z, T, x, CV_VEC);
+    c2.vec = dcond;
+    if (seg) { c2.seg = seg[0]; c2.vec_sstride = dcond_sstride; }
+    conv1d(c2, s);
+    int C = V.upc, Tc = T;
+    float* const* bufs = gb + 1;
+    for (int i = 0; i < 5; ++i) {
+        const Conv& up = V.ups[i];
+        const int u = V.up_rate[i], kfull = V.up_k[i], padT = (kfull - u) / 2;
+        const int Tn = (Tc - 1) * u - 2 * padT + kfull;
+        const int* sg = seg ? seg[i + 1] : nullptr;
+        float* yb = bufs[0];
+        ConvArgs ct{};
+        ct.x = x; ct.x_cs = Tc; ct.x_ts = 1; ct.Cin = C; ct.Tin = Tc;
+        ct.w = up.w; ct.Cout = up.cout; ct.K = up.k; ct.dil = 1; ct.pad = up.k - 1;
+        ct.bias = up.b; ct.out = yb; ct.o_cs = Tn; ct.o_ts = 1;
+        ct.n_t = (Tn + padT + u - 1) / u; ct.o_tstride = u; ct.o_toff = -padT; ct.o_len = Tn;
+        ct.in_act = 1; ct.in_slope = 0.1f; ct.mode = CV_STORE;
+        ct.phases = u; ct.w_phase_stride = (long)up.cout * up.cin * up.k;
+        ct.seg = sg;
+        conv1d(ct, s);
+        C = up.cout;
+        Tc = Tn;
+        float* rbuf = bufs[1];
+        float* xt = bufs[2];
+        float* accb = bufs[3];
+        for (int j = 0; j < 3; ++j) {
+            const int kk = V.rb_k[j];
+            const float* rcur = yb;
+            for (int mi = 0; mi < 3; ++mi) {
+                const int d = V.rb_d[mi];
+                const Conv& c1 = V.rb[i * 3 + j][0][mi];
+                const Conv& c2w = V.rb[i * 3 + j][1][mi];
+                ConvArgs a1 = cargs(c1, rcur, Tc, xt);
+                a1.dil = d; a1.pad = (kk * d - d) / 2; a1.in_act = 1; a1.in_slope = 0.1f;
+                a1.seg = sg;
+                conv1d(a1, s);
+                ConvArgs a2 = cargs(c2w, xt, Tc, rbuf);
+                a2.in_act = 1; a2.in_slope = 0.1f; a2.res = rcur;
+                a2.seg = sg;
+                if (mi < 2) {
+                    a2.mode = CV_RESID;
+                } else if (j == 0) {
+                    a2.mode = CV_ACC_FIRST; a2.acc = accb;
+                } else if (j == 1) {
+                    a2.mode = CV_ACC_ADD; a2.acc = accb;
+                } else {
+                    a2.mode = CV_ACC_MEAN; a2.acc = accb; a2.div = 3.0f; a2.out = x;
+                }
+                conv1d(a2, s);
+                rcur = rbuf;
+            }
+        }
+    }
+    ConvArgs cp = cargs(V.conv_post, x, Tc, audio, CV_TANH);
+    cp.in_act = 1; cp.in_slope = 0.01f;
+    cp.seg = seg ? seg[5] : nullptr;
+    conv1d(cp, s);
+}
+
 // One utterance on stream s with workspace W.  ovf != NULL: the MRF convs run on
 // the f16-split path and OR 1 into *ovf on an fp16-range overflow.  noise: eps
 // (device [192, 2G]) if given, else Philox N(0,1) keyed by noise_seed when it is
@@ -598,6 +667,32 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
                                  const float* ref_audio, int n_audio, const float* ge_in,
                                  const float* ge_adv_in, const float* eps, uint64_t noise_seed, float noise_scale,
                                  float* audio, hipStream_t s, int* ovf, bool timed) {
+    if (!vits.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
+    if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
+    if (2 * G > MHA_MAXK_HOST || n_text > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
+    if (int r = ensure_vits_ws(this, W, 2 * G, n_text, version == GSV_V2PP ? 0 : n_audio)) return r;
+    SplitkScope sk(W.splitk, W.splitk_cap);
+    tls_ovf = ovf;
+    struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
+    (void)hipGetLastError();   // the launches below are checked as one batch at the end
+    if (timed) hipEventRecord(ev[4], s);
+    if (int r = vits_front(W, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
+                           noise_scale, W.dcond, s))
+        return r;
+    float* const gb[5] = {W.g0, W.g1, W.g2, W.g3, W.g4};
+    vits_generator(vits, gb, W.z, 2 * G, W.dcond, 0, nullptr, audio, s);
+    if (timed) hipEventRecord(ev[5], s);   // read by vits_read_ms once the pass is known to be final
+    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vits launch");
+}
+
+// Everything of vits_fp32.onnx before the generator, for one utterance: conditioning,
+// enc_p (codebook decode, ssl_proj, encoder_ssl, text encoder), MRTE, z_p, the reverse
+// flow -> z in W.z [192][2G]; and the generator's conditioning vector dcond_out [upc] =
+// dec.cond(ge).  The caller set the split-K scope.
+int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text, const int64_t* sem, int G,
+                           const float* ref_audio, int n_audio, const float* ge_in, const float* ge_adv_in,
+                           const float* eps, uint64_t noise_seed, float noise_scale, float* dcond_out,
+                           hipStream_t s) {
     const VitsWeights& V = vits;
     if (!V.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
     if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
@@ -607,11 +702,6 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     const int T = 2 * G, S = n_text;
     if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, W, T, S, pp ? 0 : n_audio)) return r;
-    SplitkScope sk(W.splitk, W.splitk_cap);
-    tls_ovf = ovf;
-    struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
-    (void)hipGetLastError();   // the launches below are checked as one batch at the end
-    if (timed) hipEventRecord(ev[4], s);
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
     const float* ge;
     const float* ge_m;
@@ -685,66 +775,8 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
         conv1d(po, s);
         float* t = W.z; W.z = W.z2; W.z2 = t;
     }
-    // ---- generator
-    {
-        float* x = W.g0;
-        // x = conv_pre(z) + cond(ge)   (dec#: Conv -> Add(cond))
-        conv1d(cargs(V.cond, ge, 1, W.dcond), s);
-        ConvArgs c2 = cargs(V.conv_pre, W.z, T, x, CV_VEC);
-        c2.vec = W.dcond;
-        conv1d(c2, s);
-        int C = V.upc, Tc = T;
-        float* bufs[4] = {W.g1, W.g2, W.g3, W.g4};
-        for (int i = 0; i < 5; ++i) {
-            const Conv& up = V.ups[i];
-            const int u = V.up_rate[i], kfull = V.up_k[i], padT = (kfull - u) / 2;
-            const int Tn = (Tc - 1) * u - 2 * padT + kfull;
-            float* yb = bufs[0];
-            ConvArgs ct{};
-            ct.x = x; ct.x_cs = Tc; ct.x_ts = 1; ct.Cin = C; ct.Tin = Tc;
-            ct.w = up.w; ct.Cout = up.cout; ct.K = up.k; ct.dil = 1; ct.pad = up.k - 1;
-            ct.bias = up.b; ct.out = yb; ct.o_cs = Tn; ct.o_ts = 1;
-            ct.n_t = (Tn + padT + u - 1) / u; ct.o_tstride = u; ct.o_toff = -padT; ct.o_len = Tn;
-            ct.in_act = 1; ct.in_slope = 0.1f; ct.mode = CV_STORE;
-            ct.phases = u; ct.w_phase_stride = (long)up.cout * up.cin * up.k;
-            conv1d(ct, s);
-            C = up.cout;
-            Tc = Tn;
-            float* rbuf = bufs[1];
-            float* xt = bufs[2];
-            float* accb = bufs[3];
-            for (int j = 0; j < 3; ++j) {
-                const int kk = V.rb_k[j];
-                const float* rcur = yb;
-                for (int mi = 0; mi < 3; ++mi) {
-                    const int d = V.rb_d[mi];
-                    const Conv& c1 = V.rb[i * 3 + j][0][mi];
-                    const Conv& c2w = V.rb[i * 3 + j][1][mi];
-                    ConvArgs a1 = cargs(c1, rcur, Tc, xt);
-                    a1.dil = d; a1.pad = (kk * d - d) / 2; a1.in_act = 1; a1.in_slope = 0.1f;
-                    conv1d(a1, s);
-                    ConvArgs a2 = cargs(c2w, xt, Tc, rbuf);
-                    a2.in_act = 1; a2.in_slope = 0.1f; a2.res = rcur;
-                    if (mi < 2) {
-                        a2.mode = CV_RESID;
-                    } else if (j == 0) {
-                        a2.mode = CV_ACC_FIRST; a2.acc = accb;
-                    } else if (j == 1) {
-                        a2.mode = CV_ACC_ADD; a2.acc = accb;
-                    } else {
-                        a2.mode = CV_ACC_MEAN; a2.acc = accb; a2.div = 3.0f; a2.out = x;
-                    }
-                    conv1d(a2, s);
-                    rcur = rbuf;
-                }
-            }
-        }
-        ConvArgs cp = cargs(V.conv_post, x, Tc, audio, CV_TANH);
-        cp.in_act = 1; cp.in_slope = 0.01f;
-        conv1d(cp, s);
-    }
-    if (timed) hipEventRecord(ev[5], s);   // read by vits_read_ms once the pass is known to be final
-    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vits launch");
+    conv1d(cargs(V.cond, ge, 1, dcond_out), s);
+    return 0;
 }
 
 // Several utterances at once: utterance i runs on lane i % K (its own stream and
@@ -766,6 +798,74 @@ int gsv_engine::vits_decode_batch(int n, const gsv_vits_item* it, float noise_sc
     vb_items.assign(it, it + n);
     if (int r = vits_batch_launch(noise_scale, s, true)) return r;
     return vits_batch_finish(s);
+}
+
+// ---------------------------------------------------------------- segmented batch
+// Buffers for n utterances of T frames in total (gaps included).
+int gsv_engine::seg_reserve(int n, int T) {
+    SegBatch& B = sgb;
+    const VitsWeights& V = vits;
+    if ((size_t)T > B.cap_t) {
+        const size_t t = std::max((size_t)T, B.cap_t + B.cap_t / 4);
+        for (float** p : {&B.z, &B.audio}) {
+            if (*p) hipFree(*p);
+            *p = nullptr;
+        }
+        for (auto& g : B.g) { if (g) hipFree(g); g = nullptr; }
+        for (auto& q : B.seg) { if (q) hipFree(q); q = nullptr; }
+        B.cap_t = 0;
+        long f = 1;
+        for (int i = 0; i < 5; ++i) f *= V.up_rate[i];
+        bool ok = hipMalloc(&B.z, (size_t)192 * t * 4) == hipSuccess &&
+                  hipMalloc(&B.audio, (size_t)f * t * 4) == hipSuccess;
+        for (auto& g : B.g) ok = ok && hipMalloc(&g, (size_t)V.upc * t * 20 * 4) == hipSuccess;
+        long fs = 1;
+        for (int i = 0; i < 6; ++i) {
+            ok = ok && hipMalloc(&B.seg[i], (size_t)fs * t * 4) == hipSuccess;
+            if (i < 5) fs *= V.up_rate[i];
+        }
+        if (!ok) return set_error(GSV_E_HIP, "segmented vocoder buffers");
+        B.cap_t = t;
+    }
+    if (n > B.cap_n) {
+        for (float** p : {&B.dcond}) { if (*p) hipFree(*p); *p = nullptr; }
+        for (int** p : {&B.off, &B.len, &B.ovf}) { if (*p) hipFree(*p); *p = nullptr; }
+        if (B.ovf_host) hipHostFree(B.ovf_host);
+        if (B.h_pin) hipHostFree(B.h_pin);
+        B.ovf_host = nullptr;
+        B.h_pin = nullptr;
+        B.cap_n = 0;
+        if (hipMalloc(&B.dcond, (size_t)n * V.upc * 4) != hipSuccess || hipMalloc(&B.off, (size_t)n * 4) != hipSuccess ||
+            hipMalloc(&B.len, (size_t)n * 4) != hipSuccess || hipMalloc(&B.ovf, 64) != hipSuccess ||
+            hipHostMalloc((void**)&B.ovf_host, 64, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&B.h_pin, (size_t)n * 8, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "segmented vocoder tables");
+        B.cap_n = n;
+    }
+    if (!B.done && hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
+        return set_error(GSV_E_HIP, "segmented vocoder event");
+    return 0;
+}
+
+// One generator pass over the batch on stream st (f16: the MRF convs on the split-fp16
+// path, flagging an fp16-range input in sgb.ovf).
+int gsv_engine::seg_generate(hipStream_t st, bool f16) {
+    SegBatch& B = sgb;
+    tls_ovf = f16 ? B.ovf : nullptr;
+    struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
+    const int* seg[6] = {B.seg[0], B.seg[1], B.seg[2], B.seg[3], B.seg[4], B.seg[5]};
+    float* const gb[5] = {B.g[0], B.g[1], B.g[2], B.g[3], B.g[4]};
+    vits_generator(vits, gb, B.z, B.T, B.dcond, vits.upc, seg, B.audio, st);
+    return 0;
+}
+
+// Each utterance's audio out of the batch buffer (stream st).
+void gsv_engine::seg_copy_out(hipStream_t st) {
+    long f = 1;
+    for (int i = 0; i < 5; ++i) f *= vits.up_rate[i];
+    for (size_t i = 0; i < vb_items.size(); ++i)
+        hipMemcpyAsync(vb_items[i].audio, sgb.audio + f * sgb.h_off[i], (size_t)f * sgb.h_len[i] * 4,
+                       hipMemcpyDeviceToDevice, st);
 }
 
 // Fork the batch in vb_items over the lanes (ordered after stream s) and issue it:
@@ -796,23 +896,68 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
             return set_error(GSV_E_HIP, "vocoder flags");
         vflag_cap = n;
     }
+    // segmented: utterances back to back along time (zero gaps), one generator pass
+    const VitsWeights& V = vits;
+    bool seg = seg_vocoder && n > 1;
+    for (int i = 0; i < 5 && seg; ++i) seg = (V.up_k[i] - V.up_rate[i]) % 2 == 0;   // output = u x input
+    if (seg) {
+        sgb.h_off.resize(n);
+        sgb.h_len.resize(n);
+        int T = 0;
+        for (int i = 0; i < n; ++i) {
+            if (vb_items[i].n_sem <= 0) return set_error(GSV_E_ARG, "empty VITS input");
+            sgb.h_off[i] = T;
+            sgb.h_len[i] = 2 * vb_items[i].n_sem;
+            T += sgb.h_len[i] + (i + 1 < n ? SEG_GAP : 0);
+        }
+        if (int r = seg_reserve(n, T)) return r;
+        sgb.T = T;
+        std::memcpy(sgb.h_pin, sgb.h_off.data(), (size_t)n * 4);   // pinned staging: the copies stay async
+        std::memcpy(sgb.h_pin + n, sgb.h_len.data(), (size_t)n * 4);
+        hipMemcpyAsync(sgb.off, sgb.h_pin, (size_t)n * 4, hipMemcpyHostToDevice, s);
+        hipMemcpyAsync(sgb.len, sgb.h_pin + n, (size_t)n * 4, hipMemcpyHostToDevice, s);
+        hipMemsetAsync(sgb.z, 0, (size_t)192 * T * 4, s);
+        hipMemsetAsync(sgb.ovf, 0, 4, s);
+        long f = 1;
+        for (int i = 0; i < 6; ++i) {
+            seg_fill(sgb.seg[i], f * T, sgb.off, sgb.len, n, (int)f, s);
+            if (i < 5) f *= V.up_rate[i];
+        }
+    }
     if (timing) hipEventRecord(ev[4], s);
     hipMemsetAsync(vflags, 0, (size_t)n * 4, s);
     hipEventRecord(vfork, s);
     for (int l = 0; l < K; ++l) hipStreamWaitEvent(vlanes[l].st, vfork, 0);
     vb_k = K;
+    vb_seg = seg;
     vb_scale = noise_scale;
-    vb_rcs.assign(K, 0);
-    vb_errs.assign(K, std::string());
-    auto lane_work = [this, K, n](int l) {
+    vb_rcs.assign(K + 1, 0);
+    vb_errs.assign(K + 1, std::string());
+    auto lane_work = [this, K, n, seg](int l) {
         hipSetDevice(device);
         VitsLane& L = vlanes[l];
         for (int i = l; i < n; i += K) {
             const gsv_vits_item& u = vb_items[i];
-            if (int r = vits_decode_pass(L.ws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
-                                         u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
-                                         u.noise_mode == 2 ? u.noise_seed : 0, vb_scale, u.audio, L.st,
-                                         use_convh ? vflags + i : nullptr, false)) {
+            int r = 0;
+            if (seg) {   // the front part; z and dec.cond(ge) into the batch buffers
+                VitsWorkspace& W = L.ws;
+                r = ensure_vits_ws(this, W, 2 * u.n_sem, u.n_text, version == GSV_V2PP ? 0 : u.n_audio);
+                if (!r) {
+                    SplitkScope sk(W.splitk, W.splitk_cap);
+                    r = vits_front(W, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge, u.ge_adv,
+                                   u.noise_mode == 1 ? u.eps : nullptr, u.noise_mode == 2 ? u.noise_seed : 0,
+                                   vb_scale, sgb.dcond + (size_t)i * vits.upc, L.st);
+                }
+                if (!r)
+                    hipMemcpy2DAsync(sgb.z + sgb.h_off[i], (size_t)sgb.T * 4, W.z, (size_t)sgb.h_len[i] * 4,
+                                     (size_t)sgb.h_len[i] * 4, 192, hipMemcpyDeviceToDevice, L.st);
+            } else {
+                r = vits_decode_pass(L.ws, u.text_seq, u.n_text, u.sem, u.n_sem, u.ref_audio, u.n_audio, u.ge,
+                                     u.ge_adv, u.noise_mode == 1 ? u.eps : nullptr,
+                                     u.noise_mode == 2 ? u.noise_seed : 0, vb_scale, u.audio, L.st,
+                                     use_convh ? vflags + i : nullptr, false);
+            }
+            if (r) {
                 vb_rcs[l] = r;
                 vb_errs[l] = gsv_last_error();   // g_err is thread-local: keep the lane thread's text
                 return;
@@ -820,9 +965,40 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
         }
         hipEventRecord(L.join, L.st);
     };
+    // the generator of a segmented batch: on lane 0's stream after every lane's front part
+    auto gen_work = [this, K]() {
+        hipSetDevice(device);
+        for (int l = 0; l < K; ++l)
+            if (vb_rcs[l]) return;
+        hipStream_t gs = vlanes[0].st;
+        for (int l = 1; l < K; ++l) hipStreamWaitEvent(gs, vlanes[l].join, 0);
+        (void)hipGetLastError();
+        seg_generate(gs, use_convh);
+        if (use_convh) hipMemcpyAsync(sgb.ovf_host, sgb.ovf, 4, hipMemcpyDeviceToHost, gs);
+        seg_copy_out(gs);
+        sgb.st = gs;
+        hipEventRecord(sgb.done, gs);
+        if (hipGetLastError() != hipSuccess) {
+            vb_rcs[K] = set_error(GSV_E_HIP, "segmented generator launch");
+            vb_errs[K] = gsv_last_error();
+        }
+    };
     vb_active = true;
     if (!vits_threads) {
         for (int l = 0; l < K; ++l) lane_work(l);
+        if (seg) gen_work();
+    } else if (seg) {
+        // one coordinating thread: lane threads issue the front parts, then it issues the generator
+        vb_threads.emplace_back([this, K, lane_work, gen_work]() {
+            std::vector<std::thread> lanes;
+            for (int l = 0; l < K; ++l) lanes.emplace_back(lane_work, l);
+            for (auto& t : lanes) t.join();
+            gen_work();
+        });
+        if (join) {
+            for (auto& t : vb_threads) t.join();
+            vb_threads.clear();
+        }
     } else {
         for (int l = 0; l < K; ++l) vb_threads.emplace_back(lane_work, l);
         if (join) {
@@ -843,13 +1019,24 @@ int gsv_engine::vits_batch_finish(hipStream_t s) {
     if (!s) s = stream;
     const int n = (int)vb_items.size(), K = vb_k;
     for (int l = 0; l < K; ++l) hipStreamWaitEvent(s, vlanes[l].join, 0);
-    for (int l = 0; l < K; ++l)
-        if (vb_rcs[l]) {   // the other lanes may still write their audio: drain them before reporting
+    if (vb_seg) hipStreamWaitEvent(s, sgb.done, 0);
+    for (int l = 0; l <= K; ++l)
+        if (l < (int)vb_rcs.size() && vb_rcs[l]) {   // the other lanes may still write: drain them before reporting
             hipStreamSynchronize(s);
             for (int k = 0; k < K; ++k) hipStreamSynchronize(vlanes[k].st);
-            return set_error(vb_rcs[l], "vocoder lane " + std::to_string(l) + ": " + vb_errs[l]);
+            return set_error(vb_rcs[l], (l < K ? "vocoder lane " + std::to_string(l) : std::string("generator")) +
+                                            ": " + vb_errs[l]);
         }
-    if (use_convh) {
+    if (vb_seg) {
+        if (use_convh) {
+            if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vocoder batch sync");
+            if (*sgb.ovf_host) {   // an fp16-range input: the generator again on the f32 path
+                ++vits_f32_reruns;
+                seg_generate(s, false);
+                seg_copy_out(s);
+            }
+        }
+    } else if (use_convh) {
         hipMemcpyAsync(vflags_host, vflags, (size_t)n * 4, hipMemcpyDeviceToHost, s);
         if (hipStreamSynchronize(s) != hipSuccess) return set_error(GSV_E_HIP, "vocoder batch sync");
         for (int i = 0; i < n; ++i) {

@@ -12,11 +12,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int co, int t, 
     if (tp < 0 || tp >= a.o_len) return;
     const float v = a.bias ? a.bias[co] + acc : acc;
     const long oi = (long)co * a.o_cs + (long)tp * a.o_ts;
+    const float* vec = a.vec;
+    if (a.seg) {   // segmented batch: gaps stay zero
+        const int sg = a.seg[tp];
+        if (sg < 0) {
+            (a.mode == CV_ACC_FIRST || a.mode == CV_ACC_ADD ? a.acc : a.out)[oi] = 0.f;
+            return;
+        }
+        if (vec) vec += (long)sg * a.vec_sstride;
+    }
     switch (a.mode) {
         case CV_STORE: a.out[oi] = v; break;
         case CV_RELU: a.out[oi] = fmaxf(v, 0.f); break;
         case CV_RESID: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
-        case CV_VEC: a.out[oi] = v + a.vec[co]; break;
+        case CV_VEC: a.out[oi] = v + vec[co]; break;
         case CV_SUB: a.out[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] - v; break;
         case CV_TANH: a.out[oi] = tanhf(v); break;
         case CV_ACC_FIRST: a.acc[oi] = a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v; break;
@@ -25,7 +34,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int co, int t, 
             a.out[oi] = (a.acc[oi] + (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v)) / a.div;
             break;
         case CV_RESID_VEC:
-            a.out[oi] = (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v) + a.vec[co];
+            a.out[oi] = (a.res[(long)co * a.r_cs + (long)tp * a.r_ts] + v) + vec[co];
             break;
         case CV_SPLIT_RESID:
             if (co < a.split) {
@@ -48,6 +57,22 @@ template <bool FULL>
 __device__ __forceinline__ void conv_epilogue16_(const ConvArgs& a, int cobase, int tp, int t, int ph,
                                                  const float (&val)[16]) {
     const int mode = a.mode;
+    const float* vecp = a.vec;
+    if (a.seg) {   // segmented batch: a gap column is written as zeros
+        const int sg = a.seg[tp];
+        if (sg < 0) {
+            const int nrow = FULL ? 32 : a.Cout - cobase;
+            float* dst = (mode == CV_ACC_FIRST || mode == CV_ACC_ADD ? a.acc : a.out) + (long)cobase * a.o_cs +
+                         (long)tp * a.o_ts;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = (r & 3) + 8 * (r >> 2);
+                if (d < nrow) dst[(long)d * a.o_cs] = 0.f;
+            }
+            return;
+        }
+        if (vecp) vecp += (long)sg * a.vec_sstride;
+    }
     if (mode == CV_SPLIT_RESID) {
         for (int r = 0; r < 16; ++r) {
             const int co = cobase + (r & 3) + 8 * (r >> 2);
@@ -107,7 +132,7 @@ __device__ __forceinline__ void conv_epilogue16_(const ConvArgs& a, int cobase, 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int d = (r & 3) + 8 * (r >> 2);
-            vv[r] = d < nrow ? a.vec[cobase + d] : 0.f;
+            vv[r] = d < nrow ? vecp[cobase + d] : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) y[r] = y[r] + vv[r];

@@ -251,8 +251,9 @@ class GENIE:
     def tts_batch(self, items: Sequence[tuple], prompt_audio: ReferenceAudio, model, sampler: Sampler) -> List[np.ndarray]:
         """Batched synthesis for one character and reference: items are
         (text_seq, text_bert|None[, force_steps]).  All sequences decode together
-        (one batched step per token, ragged: a finished sequence drops out); the
-        vocoder runs per utterance."""
+        (one multi-sequence persistent launch, ragged: a finished sequence drops out);
+        the vocoder runs each utterance's text/flow part on concurrent lanes and the
+        generator once over the whole batch (gsv_vits_decode_batch)."""
         toks = self.tts_batch_t2s(items, prompt_audio, model, sampler)
         wavs = self.tts_batch_vocoder(items, toks, prompt_audio, model)
         return [w if isinstance(w, np.ndarray) else w.cpu().numpy() for w in wavs]

@@ -1,7 +1,7 @@
 """Roofline of the dominant kernel, from the engine's live in-loop timing.
 
-Persistent decode (default, t2s_persist1.hip): the dominant kernel is
-`k_decode_persist1`, ONE launch per utterance that runs every decode step.  Its
+The dominant kernel is the persistent decode `k_decode_persist1`
+(t2s_persist1.hip): ONE launch per utterance that runs every decode step.  Its
 algorithmic bytes (per sequence per step): the fp16 weights read
 once, W16 = 24 layers x (1536+512+2048+2048) x 512 x 2 B + the 1025x512 fp16
 logits head = 152,044,544 B, plus the fp32 K/V cache rows read, 98,304 B per
@@ -9,31 +9,10 @@ cached position (24 layers x K,V x 512 x 4 B), plus the new row written,
 98,304 B.  Summed over the launch's steps (key count N0 + s at step s).
 The duration is the launch's own dispatch-packet start/stop events
 (hipExtLaunchKernelGGL), averaged over the timed utterances.
-
-Per-step hipGraph path (option persist=0):
-
-Dominant kernel (rocprofv3, profiles/): the fused decode FFN (`k_ffn`, one
-launch per layer per step) -- HBM-bound weight streaming.  Its algorithmic
-bytes per launch at batch B (the unique bytes the math needs, each once):
-  W1 fp16 2048x512 + W2^T fp16 2048x512          4,194,304
-  b1 f32 2048 + bo/ln1 gamma/beta f32 3x512       14,336
-  per sequence: attention partials 16x512 f32 read (32,768), residual h 512
-  f32 read (2,048), FFN2 partials 64x512 f32 written (131,072), h1 written (2,048)
-The duration is the average, over the timed region, of start/stop HIP events
-that hipExtLaunchKernelGGL stamps from the dispatch packet of that launch: one
-launch per utterance (layer 12 of the 9th decode step, run eagerly because graph
-event nodes are not timing events on HIP; see engine.hip decode_loop).
 """
 from __future__ import annotations
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-
-
-def ffn_algorithmic_bytes(B: int = 1, slices: int = 64) -> int:
-    weights = 2 * 2048 * 512 * 2
-    params = 2048 * 4 + 3 * 512 * 4
-    per_seq = 16 * 512 * 4 + 512 * 4 + slices * 512 * 4 + 512 * 4
-    return weights + params + B * per_seq
 
 
 W16 = 24 * (1536 + 512 + 2048 + 2048) * 512 * 2 + 1025 * 512 * 2   # 152,044,544
@@ -108,36 +87,23 @@ def persist_roofline(eng, n0: int, steps: int, B: int = 1):
     }
 
 
-def dominant_kernel_roofline(eng, B: int = 1):
-    us, n = eng.kernel_timing()
-    if n <= 0 or us <= 0:
-        return {"error": f"no live kernel samples (hipEventElapsedTime error {-n})"}
-    bytes_ = ffn_algorithmic_bytes(B)
-    achieved = bytes_ / (us * 1e-6) / 1e9
-    return {
-        "kernel": "k_ffn (fused FFN1+FFN2 split-K, decode, layer 12, B=%d)" % B,
-        "bound": "hbm",
-        "achieved": achieved,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS,
-        "traffic": None,
-        "algorithmic_bytes_per_launch": bytes_,
-        "avg_launch_us": us,
-        "samples": n,
-    }
-
-
 # ------------------------------------------------------------------ composite
 # roofline.achieved of the whole utterance = sum over phases of the
 # phase's minimum time on its own bound, over the measured time.
 #   decode : algorithmic bytes (above) / HBM peak
 #   prefill: 2 N0 x 24 x 3,145,728 (q/k/v, out, FFN1, FFN2 weights) + 4 N0^2 x 512 x 24
-#            (dense scores and P.V) FLOP / the FP32 peak (the reference computes in
-#            fp32; our split-fp16 MFMA GEMMs reproduce fp32 products)
+#            (dense scores and P.V) FLOP
 #   vits   : 135.5 GFLOP (V2) / 298 GFLOP (V2ProPlus) per 80 tokens, linear in the
-#            token count (the generator, 96 % of it, is linear in G) / the FP32 peak
+#            token count (the generator, 96 % of it, is linear in G)
+# Two compute ceilings, both reported:
+#   f32       : the FP32 matrix peak (the reference computes in fp32);
+#   split_f16 : the precision the kernels actually run at -- the f16 MFMA (2.5 PF dense)
+#               divided by the MFMAs each product costs: fp16 weights x (hi, lo) activation
+#               = 2 (k_gemm_x3, k_conv_h; the prefill's attention and VITS' few f32-MFMA
+#               convs are priced at this rate too, a lower bound on their time).
 F32_PEAK_TFS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak
+F16_PEAK_TFS = 2500.0   # MI355X_MICROARCH.md: BF16/FP16 MFMA, dense
+SPLIT_F16_TFS = F16_PEAK_TFS / 2   # 2 MFMAs per product (activation hi + lo)
 VITS_FLOP_PER_TOKEN = {"v2": 135.5e9 / 80, "v2ProPlus": 298.0e9 / 80}
 
 
@@ -156,13 +122,22 @@ def batch_decode_bytes(n0s, steps) -> int:
 
 
 def composite_roofline(ms_total: float, n0s, steps, tokens, version: str = "v2", phase_ms=None):
-    """Sum of per-phase minimum times / measured time for one job (ms_total)."""
+    """Sum of per-phase minimum times / measured time for one job (ms_total), with the
+    compute phases priced at the FP32 peak (frac) and at the split-fp16 MFMA ceiling
+    the kernels run on (frac_split_f16)."""
     t_dec = batch_decode_bytes(n0s, steps) / (HBM_PEAK_GBS * 1e9) * 1e3
-    t_pre = sum(prefill_flop(n0) for n0 in n0s) / (F32_PEAK_TFS * 1e12) * 1e3
-    t_voc = sum(VITS_FLOP_PER_TOKEN[version] * g for g in tokens) / (F32_PEAK_TFS * 1e12) * 1e3
-    out = {"t_min_ms": {"decode_hbm": t_dec, "prefill_f32": t_pre, "vits_f32": t_voc},
-           "t_measured_ms": ms_total, "frac": (t_dec + t_pre + t_voc) / ms_total}
+    f_pre = sum(prefill_flop(n0) for n0 in n0s)
+    f_voc = sum(VITS_FLOP_PER_TOKEN[version] * g for g in tokens)
+    t_pre, t_voc = f_pre / (F32_PEAK_TFS * 1e12) * 1e3, f_voc / (F32_PEAK_TFS * 1e12) * 1e3
+    h_pre, h_voc = f_pre / (SPLIT_F16_TFS * 1e12) * 1e3, f_voc / (SPLIT_F16_TFS * 1e12) * 1e3
+    out = {"t_min_ms": {"decode_hbm": t_dec, "prefill_f32": t_pre, "vits_f32": t_voc,
+                        "prefill_split_f16": h_pre, "vits_split_f16": h_voc},
+           "t_measured_ms": ms_total, "frac": (t_dec + t_pre + t_voc) / ms_total,
+           "frac_split_f16": (t_dec + h_pre + h_voc) / ms_total,
+           "peaks": {"hbm_GBs": HBM_PEAK_GBS, "f32_TFs": F32_PEAK_TFS, "split_f16_TFs": SPLIT_F16_TFS}}
     if phase_ms:
         mins = {"decode": t_dec, "prefill": t_pre, "vits": t_voc}
+        mins_h = {"decode": t_dec, "prefill": h_pre, "vits": h_voc}
         out["phase_frac"] = {k: mins[k] / v for k, v in phase_ms.items() if k in mins and v > 0}
+        out["phase_frac_split_f16"] = {k: mins_h[k] / v for k, v in phase_ms.items() if k in mins_h and v > 0}
     return out

@@ -13,7 +13,8 @@
  *   encoder.run            (Inference.py:76-85)      gsv_t2s_encode
  *   first_stage_decoder.run(Inference.py:88-90)      gsv_t2s_prefill
  *   stage_decoder.run      (Inference.py:102)        gsv_t2s_decode_steps (k steps)
- *   the 500-step loop + trim (Inference.py:95-109)   gsv_t2s_generate (on device, hipGraph)
+ *   the 500-step loop + trim (Inference.py:95-109)   gsv_t2s_generate (the whole loop as ONE persistent
+ *                                                    kernel launch; per-step hipGraphs only as a fallback)
  *   vocoder.run            (Inference.py:47-60)      gsv_vits_decode
  *   prompt_encoder.run     (ReferenceAudio.py:73)    gsv_prompt_encode
  *   vocoder.run's refer branch (Inference.py:50, V2)  gsv_ref_encode (once per reference)
@@ -22,6 +23,7 @@
  *   per-sentence tts loop  (TTSPlayer.py:56-107)     gsv_t2s_prefetch, gsv_t2s_generate_start /
  *                                                    _finish, gsv_vits_decode_async / gsv_vits_wait
  *                                                    (option "vocoder_cus")
+ *   stop_event.set()/.clear() (Inference.py:13-14,96-97) gsv_request_stop
  *
  * Conventions
  *   - All functions return 0 on success, a negative GSV_E* code on failure;
@@ -30,9 +32,9 @@
  *     marked (device) is a caller-owned device buffer (e.g. a torch tensor's
  *     data_ptr()); (host) arguments are read before the call returns.
  *   - `stream` is the caller's hipStream_t passed as void* (NULL = the HIP null
- *     stream).  The engine runs on its own stream (so its decode loop can be
- *     graph-captured), ordered after `stream` on entry and before it on exit
- *     by events: results are stream-ordered for the caller.
+ *     stream).  The engine runs on its own stream, ordered after `stream` on
+ *     entry and before it on exit by events: results are stream-ordered for
+ *     the caller.
  *     Calls on one engine are serialised by the caller (one engine per GPU
  *     process, as the reference serialises on its single TTS worker thread,
  *     Core/TTSPlayer.py:55).
@@ -126,10 +128,15 @@ typedef struct {
  * x (device, [n_ref+n_text, 512] f32), prompts (device, [n_ssl/2] i64). */
 int gsv_t2s_encode(gsv_engine* eng, const gsv_utt* u, float* x, int64_t* prompts, void* stream);
 
-/* Full T2S of a batch: encoder, prefill, decode loop on device, and the
- * reference's token trim + EOS filter (Inference.py:41-44,108-109).
- * out_tokens (host) [batch][out_stride] i64, out_len (host) [batch].
- * Returns the trimmed semantic tokens per utterance. */
+/* Full T2S of a batch: encoder, prefill (one packed pass over the batch), the decode
+ * loop on the device, and the reference's token trim + EOS filter
+ * (Inference.py:41-44,108-109).  The loop is one persistent kernel launch: B = 1 on
+ * k_decode_persist1, B = 2..64 on its multi-sequence form k_decode_persist1m (each
+ * layer's workgroups run the live sequences one after another); B > 64, an activation
+ * beyond the fp16 range, or a launch whose grid could not be co-resident (a hand-off
+ * timeout) re-run on replayed per-step hipGraphs.  out_tokens (host)
+ * [batch][out_stride] i64, out_len (host) [batch].  Returns the trimmed semantic tokens
+ * per utterance; GSV_E_STOPPED when gsv_request_stop interrupted it. */
 int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts, const gsv_sampler* s,
                      int64_t* out_tokens, int32_t out_stride, int32_t* out_len, void* stream);
 
@@ -158,9 +165,15 @@ int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
                     const float* ge, const float* ge_adv, const float* eps, float noise_scale,
                     float* audio, void* stream);
 
-/* Several vocoder calls at once (the same graph per utterance, vits_fp32.onnx):
- * utterances run concurrently on the engine's internal streams, each with its
- * own workspace; results are stream-ordered for the caller like gsv_vits_decode.
+/* Several vocoder calls at once (the same graph per utterance, vits_fp32.onnx).  Option
+ * "seg_vocoder" 1 (default): each utterance's text/flow part runs on the engine's lanes
+ * (internal streams, own workspaces), then the HiFi-GAN generator runs ONCE over all of
+ * them laid out back to back along time with zero gaps between utterances (every conv
+ * treats a gap as the zero padding a single call sees), so its ~400 launches serve the
+ * whole batch; each utterance matches its own gsv_vits_decode to fp32 rounding (the
+ * batch's larger tiles order the reductions differently).  0: whole utterances on the
+ * lanes, bit-identical to single calls.  Results are stream-ordered for the caller like
+ * gsv_vits_decode.
  * Noise for z_p (vits(v2)#6490 RandomNormalLike x noise_scale):
  *   noise_mode 0: zeros; 1: eps (device [192, 2*n_sem]); 2: the engine's Philox
  *   N(0,1) stream keyed by noise_seed (counter = element index; Box-Muller). */
@@ -317,11 +330,12 @@ int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us, void* str
  * [0]=encode [1]=prefill [2]=decode [3]=vits.  Filled when timing is enabled. */
 int gsv_set_timing(gsv_engine* eng, int enabled);
 int gsv_get_timing(gsv_engine* eng, float* ms4);
-/* Live duration of the dominant decode kernel (fused FFN of layer 12): while
- * timing is enabled, the 9th step of each decode loop runs eagerly and that
+/* Live duration of the dominant kernel, the persistent decode launch (k_decode_persist1 /
+ * k_decode_persist1m: the whole decode loop of a generate): while timing is enabled each
  * launch carries start/stop events stamped from its dispatch packet
- * (hipExtLaunchKernelGGL).  Average microseconds and number of samples; a
- * negative count is -(hipError_t) of a failed hipEventElapsedTime. */
+ * (hipExtLaunchKernelGGL).  On the per-step graph path the sample is one eagerly run step's
+ * FFN launch instead.  Average microseconds and number of samples; a negative count is
+ * -(hipError_t) of a failed hipEventElapsedTime. */
 int gsv_get_kernel_timing(gsv_engine* eng, float* avg_us, int32_t* samples);
 
 /* Stop (the reference's GENIE.stop_event, checked before every loop step:
@@ -336,15 +350,24 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
 
 /* Engine options (no reference counterpart; the reference's session options are
  * ORT's).  "persist": 1 (default) runs gsv_t2s_generate's decode loop as ONE
- * persistent launch (B <= 8), 0 as replayed per-step hipGraphs.  "ptrace": 1
- * allocates per-workgroup phase stamps of the persistent launch (step 8, layer 12),
- * read back with gsv_debug_ptrace ([256 workgroups][16 slots]: 8 stamps of the
- * 100 MHz clock, then the same 8 of the shader clock).
+ * persistent launch (B <= 64), 0 as replayed per-step hipGraphs; setting it also ends
+ * a timeout back-off.  "persist_backoff" / "persist_backoff_ms": the first back-off hold
+ * after two timed-out launches in a row (64 generates / 5 s, doubling per failed re-probe).
+ * "vocoder_cus" (CU split for the sentence pipeline), "decode_cus" / "decode_cu_offset",
+ * "vits_lanes", "seg_vocoder" (1, default: a vocoder batch runs its generator as ONE pass
+ * over all utterances laid out back to back), "convh" (MRF convs on the split-fp16 MFMA),
+ * "sv_f16", "packed", test hooks ("persist_spin_ticks", "persist1_f16_limit",
+ * "sv_f16_limit").  "ptrace": 1 allocates per-workgroup phase stamps of the persistent
+ * launch (step 8, layer 12), read back with gsv_debug_ptrace ([256 workgroups][16
+ * slots]: 8 stamps of the 100 MHz clock, then the same 8 of the shader clock).
  * GSV_E_ARG for an unknown name. */
 int gsv_set_option(gsv_engine* eng, const char* name, int value);
 /* Engine counters: "persist_timeouts" (persistent decode launches whose hand-offs
  * timed out -- e.g. other work on the device -- and re-ran as per-step graphs),
- * "persist1_f16_reruns" (fp16-range fallbacks), "vits_f32_reruns". */
+ * "persist_disabled" (back-off holds begun), "persist_hold" (generates left in the
+ * current hold), "persist_launches", "persist1_f16_reruns" (fp16-range fallbacks),
+ * "vits_f32_reruns", "sv_f32_reruns", "w16_split_tensors" (fp32 weights kept as hi + lo
+ * planes), "stops" (generates abandoned by gsv_request_stop). */
 int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value);
 int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);
 

@@ -2,7 +2,11 @@
 CN-HuBERT on a 5.3 s reference clip (ReferenceAudio.py:48-52, once per reference) and the
 24-layer Chinese RoBERTa on a 20-character sentence (GetPhonesAndBert.py:64-74, once per
 sentence), synthetic weights of the real shapes.  Prints one JSON line; the FLOP counts
-are the dense-matmul work of each model (T_min at the 157.3 TF/s f32 MFMA peak)."""
+are the dense-matmul work of each model, priced at the 157.3 TF/s f32 MFMA peak and at the
+ceiling of the precision each kernel runs at: the f16 MFMA (2.5 PF dense) / MFMAs per product
+(CN-HuBERT fp16 weights x split activations: 2; RoBERTa fp32 weights as hi + lo planes x
+split activations: 3; SV fp32 weights: 3).  RoBERTa runs with fp32-valued weights, as
+RoBERTa.onnx ships them (ModelManager.py:139-142)."""
 import json
 import sys
 import time
@@ -35,10 +39,11 @@ layers = 12 * 2 * T * (768 * 2304 + 768 * 768 + 2 * 768 * 3072) + 12 * 4 * T * T
 pos = 2 * T * 768 * 48 * 128
 flops = conv + layers + pos + 2 * T * 512 * 768
 out["cn_hubert"] = {"audio_s": 5.3, "frames": int(T), "ms": ms, "gflop": flops / 1e9,
-                    "frac_f32_peak": flops / 157.3e12 / (ms * 1e-3)}
+                    "frac_f32_peak": flops / 157.3e12 / (ms * 1e-3),
+                    "frac_split_f16_peak": flops / (2500e12 / 2) / (ms * 1e-3)}
 eh.close()
 # ---- RoBERTa, 24 layers (hidden_states[-3]: 22 run), 20 characters
-er = Engine({"roberta": synth.synth_weights(W.roberta_spec(24))}, "v2")
+er = Engine({"roberta": synth.synth_weights(W.roberta_spec(24), fp16=False)}, "v2")
 r = synth.rng_for("rbb")
 n_chars = 20
 ids = np.concatenate([[101], r.integers(672, 8000, size=n_chars), [102]]).astype(np.int64)
@@ -53,9 +58,12 @@ torch.cuda.synchronize()
 ms = (time.perf_counter() - t0) / n * 1e3
 N = ids.size
 flops = 22 * (2 * N * (1024 * 3072 + 1024 * 1024 + 2 * 1024 * 4096) + 4 * N * N * 1024)
+wbytes = 22 * (1024 * 3072 + 1024 * 1024 + 2 * 1024 * 4096) * 4   # hi + lo fp16 planes = fp32 bytes
 out["roberta"] = {"tokens": int(N), "layers_run": 22, "ms": ms, "gflop": flops / 1e9,
-                  "weights_mb": 22 * 12.6e6 * 2 / 1e6 / 2,
-                  "frac_hbm_weights": (22 * (1024 * 3072 + 1024 * 1024 + 2 * 1024 * 4096) * 2) / 8e12 / (ms * 1e-3)}
+                  "weight_planes_mb": wbytes / 1e6,
+                  "frac_hbm_weights": wbytes / 8e12 / (ms * 1e-3),
+                  "frac_split_f16_peak": flops / (2500e12 / 3) / (ms * 1e-3),
+                  "w16_split_tensors": er.counter("w16_split_tensors")}
 er.close()
 # ---- speaker verification (V2ProPlus sv_emb, ReferenceAudio.py:71-72): 5.3 s + 0.3 s silence at 16 kHz
 es = Engine({"sv": synth.synth_sv_weights()}, "v2")
@@ -93,6 +101,7 @@ for planes, nb, stride, aff in W.SV_STAGES:
         cin = planes * 4
 flops += 2 * P * 1024 * 9 * 2048 + 2 * P * (4096 * 512 + 512 * 2048)
 out["sv"] = {"audio_s": 5.6, "frames": int(T), "ms": ms, "gflop": flops / 1e9,
-             "frac_f32_peak": flops / 157.3e12 / (ms * 1e-3)}
+             "frac_f32_peak": flops / 157.3e12 / (ms * 1e-3),
+             "frac_split_f16_peak": flops / (2500e12 / 3) / (ms * 1e-3)}
 es.close()
 print(json.dumps(out), flush=True)

@@ -21,6 +21,13 @@ for s in $STEPS; do
              timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > gpurun_out/${TAG}_$w.json 2> gpurun_out/${TAG}_$w.err || { tail -30 gpurun_out/${TAG}_$w.err; exit 1; }
              cat gpurun_out/${TAG}_$w.json
            done ;;
+    mfma)  # MFMA busy cycles per kernel (SQ_VALU_MFMA_BUSY_CYCLES; GRBM_GUI_ACTIVE sums the 8 XCDs)
+           for w in bench aux; do
+             if [ $w = bench ]; then cmd="python3 bench.py --no-cpu-baseline --concurrent-streams 0 --steps 3 --warmup 1"; else cmd="python3 tools/aux_models_bench.py"; fi
+             rm -rf gpurun_out/pmc_${TAG}_mfma_$w
+             timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_${TAG}_mfma_$w -o pmc -- $cmd > gpurun_out/${TAG}_pmc_mfma_$w.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_mfma_$w.log; exit 1; }
+             python tools/mfma_util.py gpurun_out/pmc_${TAG}_mfma_$w > gpurun_out/${TAG}_mfma_$w.txt 2>&1; head -30 gpurun_out/${TAG}_mfma_$w.txt
+           done ;;
     pmc)   for c in FETCH_SIZE WRITE_SIZE; do
              rm -rf gpurun_out/pmc_${TAG}_$c
              timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$c -o pmc -- python3 bench.py --no-cpu-baseline --concurrent-streams 0 --steps 3 --warmup 1 > gpurun_out/${TAG}_pmc_$c.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_$c.log; exit 1; }
