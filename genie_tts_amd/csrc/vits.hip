@@ -59,10 +59,8 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
             if (e < CI * XW) {
                 const int ci = e / XW, u = e - ci * XW;
                 const int tin = t0 - a.pad + u;
-                if (ci0 + ci < a.Cin && tin >= 0 && tin < a.Tin) {
-                    v = a.x[(long)(ci0 + ci) * a.x_cs + (long)tin * a.x_ts];
-                    if (a.in_act) v = v >= 0.f ? v : v * a.in_slope;
-                }
+                if (ci0 + ci < a.Cin && tin >= 0 && tin < a.Tin)
+                    v = a.x[(long)(ci0 + ci) * a.x_cs + (long)tin * a.x_ts];   // pre-activation in store()
             }
             xr[i] = v;
         }
@@ -93,7 +91,8 @@ __global__ __launch_bounds__(256) void k_conv1d(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             const int e = tid + i * 256;
-            if (e < CI * XW) Xs[buf][e] = xr[i];
+            const float v = a.in_act && xr[i] < 0.f ? xr[i] * a.in_slope : xr[i];
+            if (e < CI * XW) Xs[buf][e] = v;
         }
 #pragma unroll
         for (int i = 0; i < NW; ++i) {

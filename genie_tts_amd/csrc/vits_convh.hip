@@ -96,12 +96,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
             const int tin = t0 - a.pad + xu[i];
             const bool ok = xc[i] >= 0 && tin >= 0 && tin < a.Tin;
             const float* src = X + (long)(ci0 + xc[i] * 8) * a.x_cs + tin;
+            // raw values only: the pre-activation is applied in store(), so these loads stay
+            // in flight across the current chunk's MFMAs (an activation here made the
+            // compiler wait vmcnt(0) for them before the MFMAs, serialising every chunk)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float v = ok ? src[(long)j * a.x_cs] : 0.f;
-                if (a.in_act) v = v >= 0.f ? v : v * a.in_slope;
-                xr[i][j] = v;
-            }
+            for (int j = 0; j < 8; ++j) xr[i][j] = ok ? src[(long)j * a.x_cs] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < C::NWI; ++i) {
@@ -121,6 +120,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < C::NXI; ++i) {
             if (xc[i] < 0) continue;
+            if (a.in_act) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xr[i][j] = xr[i][j] >= 0.f ? xr[i][j] : xr[i][j] * a.in_slope;
+            }
             float m = 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(xr[i][j]));
