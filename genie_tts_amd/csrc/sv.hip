@@ -106,11 +106,15 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
     // this block's K range: whole 32-k steps, split over blockIdx.z
     const int steps = (a.K + 31) / 32, kz = blockIdx.z, ks = a.ksplit > 1 ? a.ksplit : 1;
     const int k_lo = 32 * (int)((long)steps * kz / ks), k_hi = min(a.K, 32 * (int)((long)steps * (kz + 1) / ks));
-    for (int k0 = k_lo; k0 < k_hi; k0 += 32) {
+    // The next 32-k step's operands are loaded into registers while the current step's
+    // MFMAs run (raw values; the Res2Net add is done when they are staged, so the loads
+    // stay in flight across the MFMAs)
+    float av[8], av2[8], wv8[8];
+    uint4 hw, lw;
+    auto load = [&](int k0) {
         const int kk = k0 + sc;       // 8 consecutive k of one tap (cin % 8 == 0)
-        float av[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) av[i] = 0.f;
+        for (int i = 0; i < 8; ++i) av[i] = av2[i] = 0.f;
         if (gm < M && kk < a.K) {
             const int tap = kk / a.cin, ci = kk - tap * a.cin;
             const int dy = tap / a.k, dx = tap - dy * a.k;
@@ -126,23 +130,19 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
                 if (a.amode == SV_A_ADD) {
                     const float4* q = reinterpret_cast<const float4*>(a.src2 + pos * a.lda2 + ci);
                     const float4 y0 = q[0], y1 = q[1];
-                    av[0] += y0.x; av[1] += y0.y; av[2] += y0.z; av[3] += y0.w;
-                    av[4] += y1.x; av[5] += y1.y; av[6] += y1.z; av[7] += y1.w;
+                    av2[0] = y0.x; av2[1] = y0.y; av2[2] = y0.z; av2[3] = y0.w;
+                    av2[4] = y1.x; av2[5] = y1.y; av2[6] = y1.z; av2[7] = y1.w;
                 }
             }
         }
         if (H) {
-            uint4 hw = make_uint4(0u, 0u, 0u, 0u), lw = make_uint4(0u, 0u, 0u, 0u);
+            hw = make_uint4(0u, 0u, 0u, 0u);
+            lw = make_uint4(0u, 0u, 0u, 0u);
             if (gn < a.cout && kk < a.K) {
                 hw = *reinterpret_cast<const uint4*>(a.wh + (long)gn * a.K + kk);
                 lw = *reinterpret_cast<const uint4*>(a.wl + (long)gn * a.K + kk);
             }
-            *reinterpret_cast<float4*>(&As[sr][sc]) = make_float4(av[0], av[1], av[2], av[3]);
-            *reinterpret_cast<float4*>(&As[sr][sc + 4]) = make_float4(av[4], av[5], av[6], av[7]);
-            *reinterpret_cast<uint4*>(&Wh[sr][sc]) = hw;
-            *reinterpret_cast<uint4*>(&Wl[sr][sc]) = lw;
         } else {
-            float wv8[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) wv8[i] = 0.f;
             if (gn < a.cout && kk < a.K) {
@@ -151,6 +151,20 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
                 wv8[0] = x0.x; wv8[1] = x0.y; wv8[2] = x0.z; wv8[3] = x0.w;
                 wv8[4] = x1.x; wv8[5] = x1.y; wv8[6] = x1.z; wv8[7] = x1.w;
             }
+        }
+    };
+    if (k_lo < k_hi) load(k_lo);
+    for (int k0 = k_lo; k0 < k_hi; k0 += 32) {
+        if (a.amode == SV_A_ADD) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) av[i] += av2[i];
+        }
+        if (H) {
+            *reinterpret_cast<float4*>(&As[sr][sc]) = make_float4(av[0], av[1], av[2], av[3]);
+            *reinterpret_cast<float4*>(&As[sr][sc + 4]) = make_float4(av[4], av[5], av[6], av[7]);
+            *reinterpret_cast<uint4*>(&Wh[sr][sc]) = hw;
+            *reinterpret_cast<uint4*>(&Wl[sr][sc]) = lw;
+        } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 As[sr][sc + i] = av[i];
@@ -158,6 +172,7 @@ __global__ __launch_bounds__(256) void k_sv_conv(SvConvArgs a) {
             }
         }
         __syncthreads();
+        if (k0 + 32 < k_hi) load(k0 + 32);
         if (H) {
             const int r = lane & 31, hh = lane >> 5;
 #pragma unroll

@@ -134,7 +134,10 @@ def test_tts_batch_equals_single(model, lens):
         single = gen.tts(t, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER, m.VITS, None,
                          sampler=sp)
         assert single.shape == b.shape
-        np.testing.assert_allclose(single, b, atol=1e-6)
+        # the batch's vocoder runs one generator pass over all sentences (seg_vocoder):
+        # equal to the single calls to fp32 rounding
+        rel = float(np.sqrt(np.mean((single - b) ** 2)) / np.sqrt(np.mean(single ** 2)))
+        assert rel <= 1e-5 and np.abs(single - b).max() <= 1e-4, rel
 
 
 def test_tts_stream_equals_single(model):
