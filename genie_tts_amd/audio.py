@@ -7,14 +7,13 @@ src/genie_tts/Audio/Audio.py:19-51 and Audio/ReferenceAudio.py:28-57:
 
 The reference reads with libsndfile (soundfile) and resamples with soxr 'hq';
 neither exists in this image, so reading is our own RIFF/WAVE (PCM 8/16/24/32,
-IEEE float 32/64), AIFF and FLAC (flac.py, lossless: exact samples) parsers, and
+IEEE float 32/64), AIFF, FLAC (flac.py, lossless: exact samples) and Ogg/Vorbis
+(vorbis.py, the Vorbis I float decode) parsers, and
 resampling is a rational polyphase Kaiser-windowed sinc
 (scipy.signal.resample_poly), NOT soxr's HQ filter.  Host-side, once per
 reference clip.  Parity with soxr is unpinned (a different filter: any clip not
 already at 32 kHz / the 32 -> 16 kHz step differ at the filter level);
-equal-length outputs are guaranteed (ceil(n * out / in) like soxr).  Ogg/Vorbis
-clips (accepted by the reference through libsndfile) are not decoded: rejected
-as unsupported.
+equal-length outputs are guaranteed (ceil(n * out / in) like soxr).
 """
 from __future__ import annotations
 
@@ -31,7 +30,7 @@ logger = logging.getLogger(__name__)
 MIN_DURATION_S = 3
 MAX_DURATION_S = 10
 SILENCE_TO_APPEND_S = 0.3
-SUPPORTED_AUDIO_EXTS = {".wav", ".flac", ".aiff", ".aif"}   # reference: + .ogg via libsndfile (Internal.py:38)
+SUPPORTED_AUDIO_EXTS = {".wav", ".flac", ".ogg", ".aiff", ".aif"}   # Internal.py:38 (+ AIFF)
 
 
 def _pcm_to_float(raw: bytes, width: int, big_endian: bool = False) -> np.ndarray:
@@ -95,6 +94,9 @@ def read_audio(path: str) -> Tuple[np.ndarray, int]:
     if ext == ".flac":
         from .flac import read_flac
         return read_flac(path)
+    if ext == ".ogg":
+        from .vorbis import read_ogg
+        return read_ogg(path)
     raise ValueError(f"audio format '{ext}' is not supported (supported: {sorted(SUPPORTED_AUDIO_EXTS)})")
 
 
