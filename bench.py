@@ -563,7 +563,7 @@ def main():
         except Exception:
             pass
         out["cpu_baseline"] = {"value": 1.0 / cdt, "unit": "utt/s", "cores": threads, "kind": "port",
-                               "cores_note": "all host CPUs allotted to this one-GPU job (OMP_NUM_THREADS share)",
+                               "cores_note": "min(OMP_NUM_THREADS, len(sched_getaffinity(0))): the job's CPU share on the GPU box",
                                "sample": f"1 full utterance ({cs} samples) of the same workload, "
                                          f"oracle/restate.py torch-fp32 on {model}",
                                "rtf": cdt / (cs / SR)}
