@@ -88,6 +88,11 @@ gsv_engine::~gsv_engine() {
         if (p) hipFree(p);
     for (int* p : {sgb.seg[0], sgb.seg[1], sgb.seg[2], sgb.seg[3], sgb.seg[4], sgb.seg[5], sgb.off, sgb.len, sgb.ovf})
         if (p) hipFree(p);
+    for (float* p : {sgb.ge, sgb.gem, sgb.gcond})
+        if (p) hipFree(p);
+    if (sgb.tab_dev) hipFree(sgb.tab_dev);
+    if (sgb.tab_pin) hipHostFree(sgb.tab_pin);
+    if (sgb.tab_ev) hipEventDestroy(sgb.tab_ev);
     if (sgb.ovf_host) hipHostFree(sgb.ovf_host);
     if (sgb.h_pin) hipHostFree(sgb.h_pin);
     if (sgb.done) hipEventDestroy(sgb.done);
@@ -1856,6 +1861,9 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "seg_vocoder") {   // batched vocoder: one generator pass over the batch (0: per-lane passes)
         if (int r = eng->vits_batch_finish(nullptr)) return r;
         eng->seg_vocoder = value != 0;
+    } else if (n == "seg_front") {   // ... and its front part packed into one pass too (0: per lane)
+        if (int r = eng->vits_batch_finish(nullptr)) return r;
+        eng->seg_front_on = value != 0;
     } else if (n == "vits_threads") {   // vocoder lanes issued by one host thread each (default 1)
         eng->vits_threads = value != 0;
     } else if (n == "spin_wait") {   // host waits for a decode by polling the stream (default 1)
@@ -1907,6 +1915,7 @@ extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value
     if (n == "persist_timeouts") *value = eng->persist_timeouts;
     else if (n == "persist1_f16_reruns") *value = eng->persist1_f16_reruns;
     else if (n == "vits_f32_reruns") *value = eng->vits_f32_reruns;
+    else if (n == "vits_packed_fronts") *value = eng->vits_packed_fronts;
     else if (n == "sv_f32_reruns") *value = eng->sv_f32_reruns;
     else if (n == "w16_split_tensors") *value = eng->w16_split_tensors;
     else if (n == "persist_disabled") *value = eng->persist_disabled;

@@ -173,6 +173,7 @@ struct gsv_engine {
     int* vovf = nullptr;               // f16-split conv overflow flag (device)
     int* vovf_host = nullptr;          // pinned copy
     int vits_f32_reruns = 0;           // utterances re-run on the f32 path after an overflow
+    long vits_packed_fronts = 0;       // segmented vocoder batches whose front part ran packed
     int n_cu = 0;
     unsigned long long* ptrace = nullptr;   // option "ptrace": persistent phase stamps [256][8]
 
@@ -294,9 +295,29 @@ struct gsv_engine {
                          const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,
                          const float* eps, uint64_t noise_seed, float noise_scale, float* audio, hipStream_t st,
                          int* ovf, bool timed);
+    // A segmented batch's front part in one pass (vits_front with fs): the utterances back to
+    // back along the frame axis (the generator's layout) and along the text axis, zero gaps.
+    struct FrontSeg {
+        int n = 0, Tt = 0, St = 0;             // utterances; frame / text columns incl. gaps
+        const int* segT = nullptr;             // [Tt] utterance of a frame column, -1 in a gap
+        const int* segS = nullptr;             // [St] ... of a text column
+        const int* rowT = nullptr;             // [Tt][2] {first frame, frames} of the column's utterance
+        const int* rowS = nullptr;             // [St][2] {first text column, length}
+        const int* rowX = nullptr;             // [Tt][2] the text keys of a frame (MRTE)
+        const int *offT = nullptr, *lenT = nullptr, *offS = nullptr;   // [n]
+        const int64_t* const* sems = nullptr;  // [n] device pointers
+        const int64_t* const* texts = nullptr;
+        const uint64_t* seeds = nullptr;       // [n] Philox keys (0: no noise)
+        const float* ge = nullptr;             // [n][gin] flow / dec.cond conditioning
+        const float* gem = nullptr;            // [n][512] MRTE vector
+        float* gcond = nullptr;                // [n][1536] scratch
+    };
     int vits_front(gsv::VitsWorkspace& W, const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                    const float* ref_audio, int n_audio, const float* ge, const float* ge_adv, const float* eps,
-                   uint64_t noise_seed, float noise_scale, float* dcond_out, hipStream_t st);
+                   uint64_t noise_seed, float noise_scale, float* dcond_out, hipStream_t st,
+                   const FrontSeg* fs = nullptr);
+    int seg_front(hipStream_t st);
+    int seg_front_tables(hipStream_t s);   // FrontSeg of vb_items into sgb (host build, one copy)            // the packed front of vb_items (vb_packed) into sgb.z / sgb.dcond
     // segmented vocoder batch (option "seg_vocoder", default 1): every utterance's front part
     // (vits_front) on the lanes, then ONE generator pass over all of them laid out back to
     // back along time with zero gaps (gsv::ConvArgs::seg), on lane 0's stream
@@ -312,10 +333,22 @@ struct gsv_engine {
         int* h_pin = nullptr;          // pinned staging of the offset / length tables
         std::vector<int> h_off, h_len;
         int T = 0;                     // frames of the current batch (incl. gaps)
+        int St = 0;                    // text columns of the current batch (incl. gaps)
+        gsv::VitsWorkspace fw;         // the packed front's buffers (front only, no generator)
+        float *ge = nullptr, *gem = nullptr, *gcond = nullptr;   // [cap_n][...] conditioning
+        char* tab_dev = nullptr;       // the packed front's tables (FrontSeg), device and pinned
+        char* tab_pin = nullptr;
+        size_t tab_cap = 0;
+        hipEvent_t tab_ev = nullptr;   // after the last table copy
+        FrontSeg fs;                   // pointers into tab_dev
+        const float* const* ge_ptrs = nullptr;    // [n] the items' ge / MRTE vectors (tab_dev)
+        const float* const* gem_ptrs = nullptr;
         hipEvent_t done = nullptr;
         hipStream_t st = nullptr;      // the stream the generator ran on
     } sgb;
     bool seg_vocoder = true;
+    bool seg_front_on = true;          // option "seg_front": the front part packed too (one pass)
+    bool vb_packed = false;            // the current segmented batch runs the packed front
     static constexpr int SEG_GAP = 4;  // zero frames between utterances (>= every conv halo at rate T)
     int seg_reserve(int n, int T);
     int seg_generate(hipStream_t st, bool f16);

@@ -260,10 +260,12 @@ template <int D>
 __device__ __forceinline__ void gx3_wait(int later) {
     switch (later) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory"); break;
+        // (a ring of NS stages asks for later <= NS - 2 only; the counts of the cases a
+        // configuration cannot reach are clamped to the counter's 6 bits so they assemble)
+        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D < 63 ? D : 63) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D < 63 ? 2 * D : 63) : "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D < 63 ? 3 * D : 63) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D < 63 ? 4 * D : 63) : "memory"); break;
     }
 }
 // One global -> LDS DMA of 16 B per lane (lane i -> LDS bytes [16 i, 16 i + 16) of `l`).
@@ -281,18 +283,32 @@ __device__ __forceinline__ void gx3_dma(const void* g, void* l) {
 // (W16, kernels.h).  Each product is three MFMAs, a_hi w_hi + a_lo w_hi into acc and
 // a_hi w_lo into accl, and the result is acc + accl 2^-11: a weight keeps ~22 of its
 // 24 significant bits (the reference runs such models with fp32 initializers).
-template <int BM, int BN, int NS, bool SW = false>
-__global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs a) {
-    constexpr int WV = (BM / 32) * (BN / 32);           // waves, one 32 x 32 output tile each
+// WTN > 1 (the large-M form): each wave owns WTN 32 x 32 tiles side by side in N and splits
+// its A fragment once for all of them, so the split's VALU and the A fragment reads are
+// shared by WTN MFMA pairs; every 32 x 32 tile still runs the one-tile MFMA sequence.
+// XR: blocks that share an A row tile go to one XCD (the guide's bijective remap of the
+// block id; `id % 8` labels the blocks that share an XCD), so A is fetched into one L2.
+template <int BM, int BN, int NS, bool SW = false, int WTN = 1, bool XR = false>
+__global__ __launch_bounds__(64 * (BM / 32) * (BN / 32 / WTN)) void k_gemm_x3(GemmArgs a) {
+    constexpr int WN = BN / 32 / WTN;                    // waves across N
+    constexpr int WV = (BM / 32) * WN;                   // waves, WTN 32 x 32 output tiles each
     constexpr int NA = BM / 4 / WV, NW = BN / 8 / WV;    // DMA instructions per wave per stage (A, W)
-    static_assert(NA * WV * 4 == BM && NW * WV * 8 == BN, "tile / wave split");
+    static_assert(NA * WV * 4 == BM && NW * WV * 8 == BN && WN * WTN * 32 == BN, "tile / wave split");
     constexpr int NWL = SW ? NW : 0;                     // ... of the lo plane
     __shared__ __attribute__((aligned(16))) float As[NS][BM * GX3_BK];
     __shared__ __attribute__((aligned(16))) __half Ws[NS][BN * GX3_BK];
     __shared__ __attribute__((aligned(16))) __half Wls[SW ? NS : 1][SW ? BN * GX3_BK : 8];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wm = w / (BN / 32), wn = w % (BN / 32);
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int wm = w / WN, wn = w % WN;
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (XR) {
+        const int nwg = gridDim.x * gridDim.y, orig = blockIdx.x + gridDim.x * blockIdx.y;
+        const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+        const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+        bx = id % gridDim.x;
+        by = id / gridDim.x;
+    }
+    const int m0 = by * BM, n0 = bx * BN;
     const int r = lane & 31, hh = lane >> 5;
     // K slice of this block: k_gemm_x2's partition (whole 128-k steps), in 64-k stages
     const int nsplit = gridDim.z, kz = blockIdx.z;
@@ -327,13 +343,15 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs
 #pragma unroll
         for (int i = 0; i < NWL; ++i) gx3_dma(wsrc[i] + wl_off + k0, &Wls[buf][512 * (w + WV * i)]);
     };
-    f32x16 acc, accl;
+    f32x16 acc[WTN], accl[WTN];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = accl[i] = 0.f;
+    for (int t = 0; t < WTN; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = accl[t][i] = 0.f;
 #pragma unroll
     for (int st = 0; st < NS - 1; ++st)
         if (st < nsteps) issue(st);
-    const int arow = wm * 32 + r, bcol = wn * 32 + r;
+    const int arow = wm * 32 + r, bcol = wn * WTN * 32 + r;
     for (int st = 0; st < nsteps; ++st) {
         // stage st landed (this wave's share; later ones stay in flight), then the barrier:
         // every wave's share landed, and the buffer refilled below was consumed by all.
@@ -352,32 +370,39 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32)) void k_gemm_x3(GemmArgs
             h16x8 ahi, alo;
             split8(x0, x1, ahi, alo);
             const int cb = 2 * ks + hh;       // W chunk (8 halfs)
-            const int wo = bcol * GX3_BK + 8 * (cb ^ ((bcol >> 1) & 7));
-            const h16x8 bw = *reinterpret_cast<const h16x8*>(Ws_ + wo);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bw, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bw, acc, 0, 0, 0);
-            if (SW) {
-                const h16x8 bl = *reinterpret_cast<const h16x8*>(Wls_ + wo);
-                accl = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bl, accl, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < WTN; ++t) {
+                const int bc = bcol + 32 * t;
+                const int wo = bc * GX3_BK + 8 * (cb ^ ((bc >> 1) & 7));
+                const h16x8 bw = *reinterpret_cast<const h16x8*>(Ws_ + wo);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bw, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bw, acc[t], 0, 0, 0);
+                if (SW) {
+                    const h16x8 bl = *reinterpret_cast<const h16x8*>(Wls_ + wo);
+                    accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bl, accl[t], 0, 0, 0);
+                }
             }
         }
     }
-    if (SW) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = fmaf(accl[i], W16_LO_INV, acc[i]);
-    }
-    if (a.mode == EPI_SLAB) {
-        const int col = n0 + bcol;
-        if (col >= a.N) return;
-        float* C = a.C + (long)kz * a.slab_stride;
+    for (int t = 0; t < WTN; ++t) {
+        if (SW) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int row = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (row < a.M) C[(long)row * a.ldc + col] = acc[i];
+            for (int i = 0; i < 16; ++i) acc[t][i] = fmaf(accl[t][i], W16_LO_INV, acc[t][i]);
         }
-        return;
+        const int col = n0 + bcol + 32 * t;
+        if (a.mode == EPI_SLAB) {
+            if (col >= a.N) continue;
+            float* C = a.C + (long)kz * a.slab_stride;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                if (row < a.M) C[(long)row * a.ldc + col] = acc[t][i];
+            }
+            continue;
+        }
+        gemm_epilogue(a, m0 + wm * 32, col, lane, acc[t]);
     }
-    gemm_epilogue(a, m0 + wm * 32, n0 + bcol, lane, acc);
 }
 
 // Tile configurations of k_gemm_x3 (GENIE_GEMM_CFG picks one for benchmarks; default: by shape)
@@ -390,6 +415,13 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
         return;
     }
     switch (cfg) {
+        case 9: go(k_gemm_x3<128, 128, 3, false, 4, true>, 128, 128, 256); break;   // large M
+        case 10: go(k_gemm_x3<128, 128, 2, false, 4, true>, 128, 128, 256); break;
+        case 11: go(k_gemm_x3<128, 128, 3, false, 4, false>, 128, 128, 256); break;
+        case 12: go(k_gemm_x3<128, 64, 3, false, 2, true>, 128, 64, 256); break;
+        case 13: go(k_gemm_x3<64, 128, 2, false, 2, true>, 64, 128, 256); break;   // 64 KB: 2 blocks per CU
+        case 14: go(k_gemm_x3<128, 64, 2, false, 2, true>, 128, 64, 256); break;   // 80 KB
+        case 15: go(k_gemm_x3<64, 64, 2, false, 1, true>, 64, 64, 256); break;     // 48 KB: 3 per CU
         case 1: go(k_gemm_x3<64, 64, 4>, 64, 64, 256); break;
         case 2: go(k_gemm_x3<32, 64, 4>, 32, 64, 128); break;
         case 3: go(k_gemm_x3<64, 32, 4>, 64, 32, 128); break;
@@ -407,6 +439,23 @@ static int gemm_cfg() {
         return e ? std::atoi(e) : 0;
     }();
     return c;
+}
+
+// The large-M configuration (GENIE_GEMM_BIG = its launch_x3 configuration, 0 = k_gemm_x2):
+// k_gemm_x3<64, 64, 2> with the XCD remap -- 48 KB of LDS, so three blocks (12 waves)
+// share a CU and one block's MFMAs hide another's split and LDS waits.  On the packed
+// prefill of 64 sentences (22,848 rows) it takes 0.67x k_gemm_x2's time, bit-identical;
+// the one-block-per-CU 128 x 128 forms were slower than k_gemm_x2 (profiles/r04e_gemm_big.txt).
+// Used from 1024 blocks of 64 x 64 on (4 per CU).
+static int gemm_big_cfg() {
+    static const int c = [] {
+        const char* e = std::getenv("GENIE_GEMM_BIG");
+        return e ? std::atoi(e) : 15;
+    }();
+    return c;
+}
+static bool gemm_big(const GemmArgs& a) {
+    return gemm_big_cfg() != 0 && (long)((a.M + 63) / 64) * ((a.N + 63) / 64) >= 1024;
 }
 
 static int gemm_variant() {   // GENIE_GEMM_X3=0: the register-staged k_gemm_x2
@@ -450,7 +499,9 @@ void gemm_nt(const GemmArgs& a, hipStream_t s) {
         if (a.mode == EPI_SLAB) grid.z = a.ksplit;
         // the LDS-DMA pipeline reads A as stored: a slab-summing A prologue stays on k_gemm_x2
         // (M > 512: the register-staged kernel's 128-k steps win once the grid covers the chip)
-        if (a.a_nslab == 0 && a.lda % 4 == 0 && gemm_variant() == 3 && (a.M <= 512 || gemm_cfg() != 0))
+        if (a.a_nslab == 0 && a.lda % 4 == 0 && gemm_variant() == 3 && gemm_cfg() == 0 && gemm_big(a))
+            launch_x3(a, grid.z, s, gemm_big_cfg());
+        else if (a.a_nslab == 0 && a.lda % 4 == 0 && gemm_variant() == 3 && (a.M <= 512 || gemm_cfg() != 0))
             launch_x3(a, grid.z, s, gemm_cfg());
         else
             hipLaunchKernelGGL(k_gemm_x2, grid, dim3(256), 0, s, a);

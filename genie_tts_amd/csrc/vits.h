@@ -67,9 +67,10 @@ void seg_fill(int* seg, long n, const int* off, const int* len, int nseg, int f,
 // f16-split path; returns false (nothing launched) when the shape is not covered.
 bool conv1d_h(const ConvArgs& a, hipStream_t s);
 
-// LayerNorm over channels per t: out = LN(x + y) (y may be null), eps 1e-5
+// LayerNorm over channels per t: out = LN(x + y) (y may be null), eps 1e-5; seg (segmented
+// batch, as ConvArgs::seg): a gap column is written as zeros
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
-                 const float* b, hipStream_t s);
+                 const float* b, hipStream_t s, const int* seg = nullptr);
 
 // Multi-head attention with optional relative-position terms (window W).
 //   element (i, c) of q/k/v/out at ptr[i*ts + c*cs]; head h uses channels [h*dk, (h+1)*dk)
@@ -84,7 +85,9 @@ struct MhaArgs {
     int postdiv; float scale;          // prescale: divisor sqrt(dk); postdiv: temperature
     const float* ek; const float* ev; int window;   // rel-pos (or null)
     const int* row_seg;   // optional (device) [nq][2] {first key, key count} per query row: packed
-                          // sequences attend within their own rows (no rel-pos); nk is then unused
+                          // sequences attend within their own rows; nk is then unused.  With rel-pos
+                          // terms the queries are packed as the keys (self-attention): the relative
+                          // offset is (key - first key) - (row - first key)
 };
 void mha(const MhaArgs& a, hipStream_t s);
 
@@ -99,6 +102,19 @@ void noise_zp(const float* m, const float* logs, const float* eps, float scale, 
 void noise_zp_philox(const float* m, const float* logs, uint64_t seed, float scale, float* z, int n,
                      hipStream_t s);                                              // eps ~ Philox N(0,1)
 void flip_channels(const float* in, float* out, int C, int T, hipStream_t s);
+// Segmented-batch forms (utterances back to back along time, seg[t] = utterance or -1 in
+// a gap, off[i] its first column): the per-utterance inputs through device pointer tables;
+// gap columns are written as zeros.
+void codebook_upsample2_seg(const int64_t* const* sems, const int* seg, const int* off, int T, const float* cb,
+                            float* out, hipStream_t s);
+void embed_channels_seg(const int64_t* const* ids, const int* seg, const int* off, int n, const float* emb, int C,
+                        float* out, hipStream_t s);
+// utterance i's element (c, t - off[i]) draws Philox index c * len[i] + t - off[i] under
+// seeds[i] (seed 0: no noise), as noise_zp_philox / noise_zp on that utterance alone
+void noise_zp_philox_seg(const float* m, const float* logs, const uint64_t* seeds, const int* seg, const int* off,
+                         const int* len, float scale, float* z, int C, int T, hipStream_t s);
+// out[i][0, dim) = ptrs[i][0, dim)
+void gather_vecs(const float* const* ptrs, int n, int dim, float* out, hipStream_t s);
 void reflect_pad(const float* x, int n, int pad, float* out, hipStream_t s);
 void stft_mag(const float* reim, int frames, int bins, float* spec, hipStream_t s); // [F][2*bins] -> [F][bins]
 void time_mean(const float* x, int T, int C, float* out, hipStream_t s);       // x [T][C] -> sum/T

@@ -12,6 +12,7 @@
 #include "vits.h"
 #include "vits_epi.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace gsv {
 
@@ -289,10 +290,12 @@ __global__ __launch_bounds__(256) void k_ln_channels(const float* x, const float
 // 4 time columns, lane = (t & 3) + 4 * channel group; reductions by shuffles over
 // the 16 groups, so short sequences still spread over T/4 waves.
 __global__ __launch_bounds__(64) void k_ln_channels_w(const float* x, const float* y, float* out,
-                                                     int C, int T, const float* g, const float* b) {
+                                                     int C, int T, const float* g, const float* b,
+                                                     const int* seg) {
     const int lane = threadIdx.x, tl = lane & 3, cg = lane >> 2;
     const int t = blockIdx.x * 4 + tl;
     const bool ok = t < T;
+    const bool gap = ok && seg && seg[t] < 0;
     const int nc = C >> 4;
     float v[16];
     float s = 0.f;
@@ -325,16 +328,18 @@ __global__ __launch_bounds__(64) void k_ln_channels_w(const float* x, const floa
     for (int i = 0; i < 16; ++i)
         if (i < nc) {
             const int c = cg + 16 * i;
-            out[(long)c * T + t] = (v[i] - mean) / den * g[c] + b[c];
+            out[(long)c * T + t] = gap ? 0.f : (v[i] - mean) / den * g[c] + b[c];
         }
 }
 
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
-                 const float* b, hipStream_t s) {
+                 const float* b, hipStream_t s, const int* seg) {
     if (C % 16 == 0 && C <= 256)
-        hipLaunchKernelGGL(k_ln_channels_w, dim3((T + 3) / 4), dim3(64), 0, s, x, y, out, C, T, g, b);
-    else
+        hipLaunchKernelGGL(k_ln_channels_w, dim3((T + 3) / 4), dim3(64), 0, s, x, y, out, C, T, g, b, seg);
+    else if (!seg)
         hipLaunchKernelGGL(k_ln_channels, dim3((T + 63) / 64), dim3(256), 0, s, x, y, out, C, T, g, b);
+    else
+        std::abort();   // the segmented front's LayerNorms are all 192-channel
 }
 
 // ----------------------------------------------------------------- attention
@@ -354,11 +359,13 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
     int nk = a.nk;
     const float* kb = a.k;
     const float* vb = a.v;
+    int ir = i;        // the row's index in its own sequence (rel-pos offsets)
     if (a.row_seg) {   // packed sequences: this row's keys are rows [seg0, seg0 + nk)
         const int seg0 = a.row_seg[2 * i];
         nk = a.row_seg[2 * i + 1];
         kb += (long)seg0 * a.k_ts;
         vb += (long)seg0 * a.v_ts;
+        ir = i - seg0;
     }
     for (int d = tid; d < dk; d += 256) {
         const float qv = a.q[(long)i * a.q_ts + (long)(c0 + d) * a.q_cs];
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
         for (; d < dk; ++d) s += qs[d] * kp[(long)d * a.k_cs];
         if (a.postdiv) s = s / a.scale;
         if (a.ek) {
-            const int r = j - i;
+            const int r = j - ir;
             if (r >= -a.window && r <= a.window) s = s + qe[r + a.window];
         }
         p[j] = s;
@@ -433,7 +440,7 @@ __global__ __launch_bounds__(256) void k_mha(MhaArgs a) {
             float ol = 0.f;
 #pragma unroll
             for (int r = 0; r <= 2 * MHA_MAXW; ++r) {
-                const int j = i + r - a.window;
+                const int j = ir + r - a.window;
                 if (r <= 2 * a.window && j >= 0 && j < nk) ol += p[j] * evv[r];
             }
             o = o + ol;
@@ -528,6 +535,65 @@ __global__ void k_flip(const float* in, float* out, int C, int T) {
 void flip_channels(const float* in, float* out, int C, int T, hipStream_t s) {
     const long n = (long)C * T;
     hipLaunchKernelGGL(k_flip, dim3((n + 255) / 256), dim3(256), 0, s, in, out, C, T);
+}
+
+// ---- segmented-batch forms of the front's per-utterance kernels
+__global__ void k_cb_up2_seg(const int64_t* const* sems, const int* seg, const int* off, int T, const float* cb,
+                             float* out) {
+    const int c = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int sg = seg[t];
+    out[(long)c * T + t] = sg < 0 ? 0.f : cb[sems[sg][(t - off[sg]) >> 1] * 768 + c];
+}
+void codebook_upsample2_seg(const int64_t* const* sems, const int* seg, const int* off, int T, const float* cb,
+                            float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_cb_up2_seg, dim3((T + 127) / 128, 768), dim3(128), 0, s, sems, seg, off, T, cb, out);
+}
+
+__global__ void k_embed_seg(const int64_t* const* ids, const int* seg, const int* off, int n, const float* emb,
+                            int C, float* out) {
+    const int c = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int sg = seg[t];
+    out[(long)c * n + t] = sg < 0 ? 0.f : emb[ids[sg][t - off[sg]] * C + c];
+}
+void embed_channels_seg(const int64_t* const* ids, const int* seg, const int* off, int n, const float* emb, int C,
+                        float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_embed_seg, dim3((n + 127) / 128, C), dim3(128), 0, s, ids, seg, off, n, emb, C, out);
+}
+
+__global__ void k_noise_philox_seg(const float* m, const float* logs, const uint64_t* seeds, const int* seg,
+                                   const int* off, const int* len, float sc, float* z, int C, int T) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)C * T) return;
+    const int c = (int)(i / T), t = (int)(i - (long)c * T);
+    const int sg = seg[t];
+    if (sg < 0) {
+        z[i] = 0.f;
+        return;
+    }
+    const uint64_t seed = seeds[sg];
+    float e = 0.f;   // seed 0: noise_zp without eps
+    if (seed != 0) {
+        const uint32_t k = (uint32_t)c * (uint32_t)len[sg] + (uint32_t)(t - off[sg]);
+        const uint4 r = philox4x32(make_uint4(k, 0u, 0u, 0x7Au), make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+        e = sqrtf(-2.0f * logf(u01_open(r.x))) * cospif(2.0f * u01_open(r.y));
+    }
+    z[i] = m[i] + (e * expf(logs[i])) * sc;
+}
+void noise_zp_philox_seg(const float* m, const float* logs, const uint64_t* seeds, const int* seg, const int* off,
+                         const int* len, float scale, float* z, int C, int T, hipStream_t s) {
+    const long n = (long)C * T;
+    hipLaunchKernelGGL(k_noise_philox_seg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m, logs, seeds, seg,
+                       off, len, scale, z, C, T);
+}
+
+__global__ void k_gather_vecs(const float* const* ptrs, int dim, float* out) {
+    const int i = blockIdx.x;
+    for (int d = threadIdx.x; d < dim; d += blockDim.x) out[(long)i * dim + d] = ptrs[i][d];
+}
+void gather_vecs(const float* const* ptrs, int n, int dim, float* out, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_gather_vecs, dim3(n), dim3(256), 0, s, ptrs, dim, out);
 }
 
 __global__ void k_reflect_pad(const float* x, int n, int pad, float* out) {

@@ -290,8 +290,10 @@ struct SplitkScope {
     ~SplitkScope() { tls_splitk = nullptr; tls_splitk_cap = 0; }
 };
 
-static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode = CV_STORE) {
+static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode = CV_STORE,
+                      const int* seg = nullptr) {
     ConvArgs a{};
+    a.seg = seg;
     a.part = tls_splitk; a.part_cap = tls_splitk_cap;
     a.x = x; a.x_cs = T; a.x_ts = 1; a.Cin = c.cin; a.Tin = T;
     a.w = c.w; a.Cout = c.cout; a.K = c.k; a.dil = 1; a.pad = (c.k - 1) / 2;
@@ -303,10 +305,12 @@ static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode
     return a;
 }
 
+// seg / rows: a segmented batch (ConvArgs::seg of the T columns, MhaArgs::row_seg), else null
 static void attn_encoder(gsv_engine* e, const std::vector<AttnLayer>& Ls, float* x, int T, float* qkv,
-                         float* att, float* tmp, float* ffn, hipStream_t s) {
+                         float* att, float* tmp, float* ffn, hipStream_t s, const int* seg = nullptr,
+                         const int* rows = nullptr) {
     for (const AttnLayer& L : Ls) {
-        conv1d(cargs(L.qkv, x, T, qkv), s);
+        conv1d(cargs(L.qkv, x, T, qkv, CV_STORE, seg), s);
         MhaArgs m{};
         m.q = qkv; m.q_ts = 1; m.q_cs = T;
         m.k = qkv + (size_t)192 * T; m.k_ts = 1; m.k_cs = T;
@@ -314,12 +318,13 @@ static void attn_encoder(gsv_engine* e, const std::vector<AttnLayer>& Ls, float*
         m.out = att; m.o_ts = 1; m.o_cs = T;
         m.nq = T; m.nk = T; m.heads = 2; m.dk = 96; m.postdiv = 0; m.scale = std::sqrt(96.0f);
         m.ek = L.ek; m.ev = L.ev; m.window = 4;
+        m.row_seg = rows;
         mha(m, s);
-        conv1d(cargs(L.o, att, T, tmp), s);
-        ln_channels(x, tmp, x, 192, T, L.g1, L.b1, s);
-        conv1d(cargs(L.ffn1, x, T, ffn, CV_RELU), s);
-        conv1d(cargs(L.ffn2, ffn, T, tmp), s);
-        ln_channels(x, tmp, x, 192, T, L.g2, L.b2, s);
+        conv1d(cargs(L.o, att, T, tmp, CV_STORE, seg), s);
+        ln_channels(x, tmp, x, 192, T, L.g1, L.b1, s, seg);
+        conv1d(cargs(L.ffn1, x, T, ffn, CV_RELU, seg), s);
+        conv1d(cargs(L.ffn2, ffn, T, tmp, CV_STORE, seg), s);
+        ln_channels(x, tmp, x, 192, T, L.g2, L.b2, s, seg);
     }
 }
 
@@ -374,9 +379,10 @@ static void run_ref_enc(VitsWorkspace& W, const RefEnc& R, const float* audio, i
     time_mean(W.r0, F, R.out_dim, ge, s);
 }
 
-static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_audio) {
+// with_gen = false: the front part's buffers only (the packed front of a segmented batch)
+static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_audio, bool with_gen = true) {
     const VitsWeights& V = e->vits;
-    const size_t gen = (size_t)V.upc * T * 20;    // max C*T over generator stages: upc/2^(i+1) * T*prod(u)
+    const size_t gen = with_gen ? (size_t)V.upc * T * 20 : 0;   // max C*T over generator stages: upc/2^(i+1) * T*prod(u)
     const int F = n_audio > 0 ? (n_audio + 1408 - 2048) / 640 + 1 : 0;
     if ((size_t)T <= W.cap_t && S <= W.cap_text && gen <= W.cap_gen && F <= W.cap_spec) return 0;
     const size_t t = std::max((size_t)T, W.cap_t);
@@ -393,7 +399,7 @@ static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_a
     W.stats = A(384 * t); W.z = A(192 * t); W.z2 = A(192 * t); W.fh = A(192 * t);
     W.fx = A(384 * t); W.fa = A(192 * t); W.fskip = A(192 * t); W.fm = A(96 * t);
     W.gcond = A(4 * 1536); W.dcond = A(1024); W.ge = A(1024); W.pe_ge = A(1024); W.sv = A(1024);
-    W.g0 = A(g); W.g1 = A(g); W.g2 = A(g); W.g3 = A(g); W.g4 = A(g);
+    if (g > 0) { W.g0 = A(g); W.g1 = A(g); W.g2 = A(g); W.g3 = A(g); W.g4 = A(g); }
     if (f > 0) {
         W.pad = A((size_t)f * 640 + 2048 + 1408);
         W.reim = A((size_t)f * 1408); W.spec = A((size_t)f * 704);
@@ -404,7 +410,7 @@ static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_a
         W.splitk_cap = 2L << 20;   // 8 MB: >= 384 tiles of 64 x 64
         W.splitk = A((size_t)W.splitk_cap);
     }
-    if (!W.g4 || !W.splitk) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
+    if ((g > 0 && !W.g4) || !W.splitk || !W.fm) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
     W.cap_t = t; W.cap_text = sT; W.cap_gen = g; W.cap_spec = f;
     return 0;
 }
@@ -689,23 +695,41 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
 // enc_p (codebook decode, ssl_proj, encoder_ssl, text encoder), MRTE, z_p, the reverse
 // flow -> z in W.z [192][2G]; and the generator's conditioning vector dcond_out [upc] =
 // dec.cond(ge).  The caller set the split-K scope.
+// fs (a segmented batch): every utterance of it at once, laid out back to back along the
+// frame axis (fs->Tt columns) and the text axis (fs->St), zero gaps (the convs' seg
+// epilogue, seg-aware LayerNorm / noise / embedding kernels), attention within each
+// utterance (row_seg); ge / ge_m per utterance (vec_sstride); z [192][Tt] in W.z and
+// dcond_out [n][upc].  The per-utterance arguments are unused then.
 int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text, const int64_t* sem, int G,
                            const float* ref_audio, int n_audio, const float* ge_in, const float* ge_adv_in,
                            const float* eps, uint64_t noise_seed, float noise_scale, float* dcond_out,
-                           hipStream_t s) {
+                           hipStream_t s, const FrontSeg* fs) {
     const VitsWeights& V = vits;
     if (!V.ready) return set_error(GSV_E_STATE, "VITS weights not loaded");
-    if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
     const bool pp = version == GSV_V2PP;
-    if (pp ? (!ge_in || !ge_adv_in) : (!ref_audio && !ge_in))
-        return set_error(GSV_E_ARG, "missing conditioning input");
-    const int T = 2 * G, S = n_text;
-    if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
-    if (int r = ensure_vits_ws(this, W, T, S, pp ? 0 : n_audio)) return r;
+    const int* sT = fs ? fs->segT : nullptr;
+    const int* sS = fs ? fs->segS : nullptr;
+    int T, S;
+    if (fs) {
+        T = fs->Tt;
+        S = fs->St;
+        if (int r = ensure_vits_ws(this, W, T, S, 0, false)) return r;
+    } else {
+        if (G <= 0 || n_text <= 0) return set_error(GSV_E_ARG, "empty VITS input");
+        if (pp ? (!ge_in || !ge_adv_in) : (!ref_audio && !ge_in))
+            return set_error(GSV_E_ARG, "missing conditioning input");
+        T = 2 * G;
+        S = n_text;
+        if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
+        if (int r = ensure_vits_ws(this, W, T, S, pp ? 0 : n_audio)) return r;
+    }
     // ---- conditioning: ge (flow cond / dec.cond) and MRTE vector
     const float* ge;
     const float* ge_m;
-    if (!pp && ge_in) {   // V2 with the reference's ge from gsv_ref_encode (once per reference)
+    if (fs) {   // one vector per utterance
+        ge = fs->ge;
+        ge_m = fs->gem;
+    } else if (!pp && ge_in) {   // V2 with the reference's ge from gsv_ref_encode (once per reference)
         ge = ge_in;
         ge_m = ge_in;
     } else if (!pp) {
@@ -717,65 +741,81 @@ int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text
         ge_m = ge_adv_in;
     }
     // ---- enc_p: codebook decode x2, ssl_proj, encoder_ssl
-    codebook_upsample2(sem, G, V.codebook, W.q, s);
-    conv1d(cargs(V.ssl_proj, W.q, T, W.y), s);
-    attn_encoder(this, V.enc_ssl, W.y, T, W.qkv, W.att, W.a, W.ffn, s);
-    embed_channels(text_seq, S, V.text_emb, 192, W.te, s);
-    attn_encoder(this, V.enc_text, W.te, S, W.tqkv, W.tatt, W.ta, W.tffn, s);
+    if (fs) codebook_upsample2_seg(fs->sems, sT, fs->offT, T, V.codebook, W.q, s);
+    else codebook_upsample2(sem, G, V.codebook, W.q, s);
+    conv1d(cargs(V.ssl_proj, W.q, T, W.y, CV_STORE, sT), s);
+    attn_encoder(this, V.enc_ssl, W.y, T, W.qkv, W.att, W.a, W.ffn, s, sT, fs ? fs->rowT : nullptr);
+    if (fs) embed_channels_seg(fs->texts, sS, fs->offS, S, V.text_emb, 192, W.te, s);
+    else embed_channels(text_seq, S, V.text_emb, 192, W.te, s);
+    attn_encoder(this, V.enc_text, W.te, S, W.tqkv, W.tatt, W.ta, W.tffn, s, sS, fs ? fs->rowS : nullptr);
     // ---- MRTE
-    conv1d(cargs(V.c_pre, W.y, T, W.ssl_enc), s);
-    conv1d(cargs(V.text_pre, W.te, S, W.text_enc), s);
-    conv1d(cargs(V.mrte_qkv_q, W.ssl_enc, T, W.mq), s);
-    conv1d(cargs(V.mrte_kv, W.text_enc, S, W.mkv), s);
+    conv1d(cargs(V.c_pre, W.y, T, W.ssl_enc, CV_STORE, sT), s);
+    conv1d(cargs(V.text_pre, W.te, S, W.text_enc, CV_STORE, sS), s);
+    conv1d(cargs(V.mrte_qkv_q, W.ssl_enc, T, W.mq, CV_STORE, sT), s);
+    conv1d(cargs(V.mrte_kv, W.text_enc, S, W.mkv, CV_STORE, sS), s);
     MhaArgs m{};
     m.q = W.mq; m.q_ts = 1; m.q_cs = T;
     m.k = W.mkv; m.k_ts = 1; m.k_cs = S;
     m.v = W.mkv + (size_t)512 * S; m.v_ts = 1; m.v_cs = S;
     m.out = W.mo; m.o_ts = 1; m.o_cs = T;
     m.nq = T; m.nk = S; m.heads = 4; m.dk = 128; m.postdiv = 0; m.scale = std::sqrt(128.0f);
+    m.row_seg = fs ? fs->rowX : nullptr;   // a frame attends to its own utterance's text
     mha(m, s);
-    ConvArgs co = cargs(V.mrte_o, W.mo, T, W.a, CV_RESID_VEC);
+    ConvArgs co = cargs(V.mrte_o, W.mo, T, W.a, CV_RESID_VEC, sT);
     co.res = W.ssl_enc; co.vec = ge_m;
+    if (fs) co.vec_sstride = V.mrte_o.cout;
     conv1d(co, s);
-    conv1d(cargs(V.c_post, W.a, T, W.y), s);
-    attn_encoder(this, V.enc2, W.y, T, W.qkv, W.att, W.a, W.ffn, s);
-    conv1d(cargs(V.proj, W.y, T, W.stats), s);
+    conv1d(cargs(V.c_post, W.a, T, W.y, CV_STORE, sT), s);
+    attn_encoder(this, V.enc2, W.y, T, W.qkv, W.att, W.a, W.ffn, s, sT, fs ? fs->rowT : nullptr);
+    conv1d(cargs(V.proj, W.y, T, W.stats, CV_STORE, sT), s);
     // ---- z_p = m_p + eps*exp(logs_p)*noise_scale
-    if (!eps && noise_seed != 0)
+    if (fs)
+        noise_zp_philox_seg(W.stats, W.stats + (size_t)192 * T, fs->seeds, sT, fs->offT, fs->lenT, noise_scale, W.z,
+                            192, T, s);
+    else if (!eps && noise_seed != 0)
         noise_zp_philox(W.stats, W.stats + (size_t)192 * T, noise_seed, noise_scale, W.z, 192 * T, s);
     else
         noise_zp(W.stats, W.stats + (size_t)192 * T, eps, noise_scale, W.z, 192 * T, s);
+    // conditioning convs of the whole batch: the n vectors [n][cin] as n time columns,
+    // results utterance-major [n][cout] (one CV_VEC row per utterance)
+    const int nv = fs ? fs->n : 1;
+    auto vec_conv = [&](const Conv& c, const float* x, float* out) {
+        ConvArgs a = cargs(c, x, nv, out);
+        a.x_cs = 1; a.x_ts = c.cin;
+        a.o_cs = 1; a.o_ts = c.cout;
+        conv1d(a, s);
+    };
+    float* gcond = fs ? fs->gcond : W.gcond;
     // ---- reverse flow: for f = 6,4,2,0: flip, coupling (mean-only)
     for (int fi = 3; fi >= 0; --fi) {
         const auto& fl = V.flows[fi];
         flip_channels(W.z, W.z2, 192, T, s);
-        // cond: g = cond_layer(ge) [1536]
-        ConvArgs gc = cargs(fl.cond, ge, 1, W.gcond);
-        conv1d(gc, s);
-        conv1d(cargs(fl.pre, W.z2, T, W.fh), s);                 // h = pre(x0)   (x0 = first 96 ch)
+        vec_conv(fl.cond, ge, gcond);                                    // g = cond_layer(ge) [1536]
+        conv1d(cargs(fl.pre, W.z2, T, W.fh, CV_STORE, sT), s);           // h = pre(x0)   (x0 = first 96 ch)
         hipMemsetAsync(W.fskip, 0, (size_t)192 * T * 4, s);
         for (int l = 0; l < 4; ++l) {
-            ConvArgs ci = cargs(fl.in_l[l], W.fh, T, W.fx, CV_VEC);
-            ci.vec = W.gcond + l * 384;
+            ConvArgs ci = cargs(fl.in_l[l], W.fh, T, W.fx, CV_VEC, sT);
+            ci.vec = gcond + l * 384;
+            ci.vec_sstride = fl.cond.cout;
             conv1d(ci, s);
             wn_gate(W.fx, W.fa, 192, T, s);
             if (l < 3) {
-                ConvArgs rs = cargs(fl.rs[l], W.fa, T, W.fh, CV_SPLIT_RESID);
+                ConvArgs rs = cargs(fl.rs[l], W.fa, T, W.fh, CV_SPLIT_RESID, sT);
                 rs.res = W.fh; rs.split = 192; rs.out2 = W.fskip; rs.res2 = W.fskip;
                 conv1d(rs, s);
             } else {
-                ConvArgs rs = cargs(fl.rs[l], W.fa, T, W.fskip, CV_RESID);
+                ConvArgs rs = cargs(fl.rs[l], W.fa, T, W.fskip, CV_RESID, sT);
                 rs.res = W.fskip;
                 conv1d(rs, s);
             }
         }
         // x1 = x1 - post(skip); z = cat(x0, x1)
-        ConvArgs po = cargs(fl.post, W.fskip, T, W.z2 + (size_t)96 * T, CV_SUB);
+        ConvArgs po = cargs(fl.post, W.fskip, T, W.z2 + (size_t)96 * T, CV_SUB, sT);
         po.res = W.z2 + (size_t)96 * T;
         conv1d(po, s);
         float* t = W.z; W.z = W.z2; W.z2 = t;
     }
-    conv1d(cargs(V.cond, ge, 1, dcond_out), s);
+    vec_conv(V.cond, ge, dcond_out);
     return 0;
 }
 
@@ -835,6 +875,11 @@ int gsv_engine::seg_reserve(int n, int T) {
         B.ovf_host = nullptr;
         B.h_pin = nullptr;
         B.cap_n = 0;
+        for (float** p : {&B.ge, &B.gem, &B.gcond}) { if (*p) hipFree(*p); *p = nullptr; }
+        const int gin = V.flows[0].cond.cin, gcn = V.flows[0].cond.cout;
+        if (hipMalloc(&B.ge, (size_t)n * gin * 4) != hipSuccess || hipMalloc(&B.gem, (size_t)n * 512 * 4) != hipSuccess ||
+            hipMalloc(&B.gcond, (size_t)n * gcn * 4) != hipSuccess)
+            return set_error(GSV_E_HIP, "segmented vocoder conditioning");
         if (hipMalloc(&B.dcond, (size_t)n * V.upc * 4) != hipSuccess || hipMalloc(&B.off, (size_t)n * 4) != hipSuccess ||
             hipMalloc(&B.len, (size_t)n * 4) != hipSuccess || hipMalloc(&B.ovf, 64) != hipSuccess ||
             hipHostMalloc((void**)&B.ovf_host, 64, hipHostMallocDefault) != hipSuccess ||
@@ -844,6 +889,113 @@ int gsv_engine::seg_reserve(int n, int T) {
     }
     if (!B.done && hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
         return set_error(GSV_E_HIP, "segmented vocoder event");
+    return 0;
+}
+
+// The packed front's tables (FrontSeg) for vb_items, built on the host and copied to the
+// device on stream s with one copy: text layout, per-column utterance / key-range tables,
+// per-utterance input pointers and Philox keys.  The frame layout is sgb's (h_off, h_len,
+// seg[0]).
+int gsv_engine::seg_front_tables(hipStream_t s) {
+    SegBatch& B = sgb;
+    const int n = (int)vb_items.size(), Tt = B.T;
+    std::vector<int> offS(n);
+    int St = 0;
+    for (int i = 0; i < n; ++i) {
+        offS[i] = St;
+        St += vb_items[i].n_text + (i + 1 < n ? SEG_GAP : 0);
+    }
+    B.St = St;
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    size_t o = 0;
+    const size_t o_segS = o; o = al(o + (size_t)St * 4);
+    const size_t o_rowT = o; o = al(o + (size_t)Tt * 8);
+    const size_t o_rowS = o; o = al(o + (size_t)St * 8);
+    const size_t o_rowX = o; o = al(o + (size_t)Tt * 8);
+    const size_t o_offS = o; o = al(o + (size_t)n * 4);
+    const size_t o_sems = o; o = al(o + (size_t)n * 8);
+    const size_t o_texts = o; o = al(o + (size_t)n * 8);
+    const size_t o_seeds = o; o = al(o + (size_t)n * 8);
+    const size_t o_gep = o; o = al(o + (size_t)n * 8);
+    const size_t o_gemp = o; o = al(o + (size_t)n * 8);
+    // the previous batch's copy out of the pinned staging (and its reads of tab_dev) may still
+    // be queued: wait for that copy alone
+    if (B.tab_ev && hipEventSynchronize(B.tab_ev) != hipSuccess) return set_error(GSV_E_HIP, "vocoder table sync");
+    if (!B.tab_ev && hipEventCreateWithFlags(&B.tab_ev, hipEventDisableTiming) != hipSuccess)
+        return set_error(GSV_E_HIP, "vocoder table event");
+    if (o > B.tab_cap) {
+        if (B.tab_dev && hipDeviceSynchronize() != hipSuccess) return set_error(GSV_E_HIP, "vocoder table sync");
+        if (B.tab_dev) hipFree(B.tab_dev);
+        if (B.tab_pin) hipHostFree(B.tab_pin);
+        B.tab_dev = B.tab_pin = nullptr;
+        B.tab_cap = 0;
+        const size_t cap = o + o / 4;
+        if (hipMalloc((void**)&B.tab_dev, cap) != hipSuccess ||
+            hipHostMalloc((void**)&B.tab_pin, cap, hipHostMallocDefault) != hipSuccess)
+            return set_error(GSV_E_HIP, "segmented vocoder front tables");
+        B.tab_cap = cap;
+    }
+    char* h = B.tab_pin;
+    int* segS = reinterpret_cast<int*>(h + o_segS);
+    int* rowT = reinterpret_cast<int*>(h + o_rowT);
+    int* rowS = reinterpret_cast<int*>(h + o_rowS);
+    int* rowX = reinterpret_cast<int*>(h + o_rowX);
+    std::fill(segS, segS + St, -1);
+    std::fill(rowT, rowT + 2 * (size_t)Tt, 0);
+    std::fill(rowS, rowS + 2 * (size_t)St, 0);
+    std::fill(rowX, rowX + 2 * (size_t)Tt, 0);
+    const bool pp = version == GSV_V2PP;
+    for (int i = 0; i < n; ++i) {
+        const gsv_vits_item& u = vb_items[i];
+        const int t0 = B.h_off[i], tl = B.h_len[i], s0 = offS[i], sl = u.n_text;
+        for (int t = t0; t < t0 + tl; ++t) {
+            rowT[2 * t] = t0; rowT[2 * t + 1] = tl;
+            rowX[2 * t] = s0; rowX[2 * t + 1] = sl;
+        }
+        for (int c = s0; c < s0 + sl; ++c) {
+            segS[c] = i;
+            rowS[2 * c] = s0; rowS[2 * c + 1] = sl;
+        }
+        reinterpret_cast<int*>(h + o_offS)[i] = s0;
+        reinterpret_cast<const int64_t**>(h + o_sems)[i] = u.sem;
+        reinterpret_cast<const int64_t**>(h + o_texts)[i] = u.text_seq;
+        reinterpret_cast<uint64_t*>(h + o_seeds)[i] = u.noise_mode == 2 ? u.noise_seed : 0;
+        reinterpret_cast<const float**>(h + o_gep)[i] = u.ge;
+        reinterpret_cast<const float**>(h + o_gemp)[i] = pp ? u.ge_adv : u.ge;
+    }
+    hipMemcpyAsync(B.tab_dev, B.tab_pin, o, hipMemcpyHostToDevice, s);
+    hipEventRecord(B.tab_ev, s);
+    char* d = B.tab_dev;
+    FrontSeg& f = B.fs;
+    f.n = n; f.Tt = Tt; f.St = St;
+    f.segT = B.seg[0];
+    f.segS = reinterpret_cast<const int*>(d + o_segS);
+    f.rowT = reinterpret_cast<const int*>(d + o_rowT);
+    f.rowS = reinterpret_cast<const int*>(d + o_rowS);
+    f.rowX = reinterpret_cast<const int*>(d + o_rowX);
+    f.offT = B.off; f.lenT = B.len;
+    f.offS = reinterpret_cast<const int*>(d + o_offS);
+    f.sems = reinterpret_cast<const int64_t* const*>(d + o_sems);
+    f.texts = reinterpret_cast<const int64_t* const*>(d + o_texts);
+    f.seeds = reinterpret_cast<const uint64_t*>(d + o_seeds);
+    f.ge = B.ge; f.gem = B.gem; f.gcond = B.gcond;
+    B.ge_ptrs = reinterpret_cast<const float* const*>(d + o_gep);
+    B.gem_ptrs = reinterpret_cast<const float* const*>(d + o_gemp);
+    return 0;
+}
+
+// The packed front of the batch on stream st: z into sgb.z, dec.cond(ge) into sgb.dcond.
+int gsv_engine::seg_front(hipStream_t st) {
+    SegBatch& B = sgb;
+    const int n = (int)vb_items.size();
+    gather_vecs(B.ge_ptrs, n, vits.flows[0].cond.cin, B.ge, st);
+    gather_vecs(B.gem_ptrs, n, vits.mrte_o.cout, B.gem, st);
+    if (int r = ensure_vits_ws(this, B.fw, B.T, B.St, 0, false)) return r;
+    SplitkScope sk(B.fw.splitk, B.fw.splitk_cap);
+    if (int r = vits_front(B.fw, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, 0, vb_scale, B.dcond,
+                           st, &B.fs))
+        return r;
+    hipMemcpyAsync(B.z, B.fw.z, (size_t)192 * B.T * 4, hipMemcpyDeviceToDevice, st);
     return 0;
 }
 
@@ -923,6 +1075,22 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
             seg_fill(sgb.seg[i], f * T, sgb.off, sgb.len, n, (int)f, s);
             if (i < 5) f *= V.up_rate[i];
         }
+        // the front part packed too when every item carries its conditioning vectors and
+        // draws no explicit eps (else: each item's front on a lane)
+        bool packed = seg_front_on;
+        const bool pp = version == GSV_V2PP;
+        for (int i = 0; i < n && packed; ++i) {
+            const gsv_vits_item& u = vb_items[i];
+            packed = u.noise_mode != 1 && u.n_text > 0 && 2 * u.n_sem <= MHA_MAXK_HOST &&
+                     u.n_text <= MHA_MAXK_HOST && u.ge != nullptr && (!pp || u.ge_adv != nullptr);
+        }
+        if (packed) {
+            if (int r = seg_front_tables(s)) return r;
+            ++vits_packed_fronts;
+        }
+        vb_packed = packed;
+    } else {
+        vb_packed = false;
     }
     if (timing) hipEventRecord(ev[4], s);
     hipMemsetAsync(vflags, 0, (size_t)n * 4, s);
@@ -939,7 +1107,15 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
         for (int i = l; i < n; i += K) {
             const gsv_vits_item& u = vb_items[i];
             int r = 0;
-            if (seg) {   // the front part; z and dec.cond(ge) into the batch buffers
+            if (seg && vb_packed) {   // every utterance's front part in one pass, on lane 0
+                if (l == 0) r = seg_front(L.st);
+                if (r) {
+                    vb_rcs[l] = r;
+                    vb_errs[l] = gsv_last_error();
+                    return;
+                }
+                break;
+            } else if (seg) {   // the front part; z and dec.cond(ge) into the batch buffers
                 VitsWorkspace& W = L.ws;
                 r = ensure_vits_ws(this, W, 2 * u.n_sem, u.n_text, version == GSV_V2PP ? 0 : u.n_audio);
                 if (!r) {

@@ -16,7 +16,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int co, int t, 
     if (a.seg) {   // segmented batch: gaps stay zero
         const int sg = a.seg[tp];
         if (sg < 0) {
-            (a.mode == CV_ACC_FIRST || a.mode == CV_ACC_ADD ? a.acc : a.out)[oi] = 0.f;
+            if (a.mode == CV_SPLIT_RESID && co >= a.split)
+                a.out2[(long)(co - a.split) * a.o_cs + (long)tp * a.o_ts] = 0.f;
+            else
+                (a.mode == CV_ACC_FIRST || a.mode == CV_ACC_ADD ? a.acc : a.out)[oi] = 0.f;
             return;
         }
         if (vec) vec += (long)sg * a.vec_sstride;
@@ -60,6 +63,13 @@ __device__ __forceinline__ void conv_epilogue16_(const ConvArgs& a, int cobase, 
     const float* vecp = a.vec;
     if (a.seg) {   // segmented batch: a gap column is written as zeros
         const int sg = a.seg[tp];
+        if (sg < 0 && mode == CV_SPLIT_RESID) {   // rows past `split` belong to out2
+            for (int r = 0; r < 16; ++r) {
+                const int co = cobase + (r & 3) + 8 * (r >> 2);
+                if (co < a.Cout) conv_epilogue(a, co, t, ph, 0.f);
+            }
+            return;
+        }
         if (sg < 0) {
             const int nrow = FULL ? 32 : a.Cout - cobase;
             float* dst = (mode == CV_ACC_FIRST || mode == CV_ACC_ADD ? a.acc : a.out) + (long)cobase * a.o_cs +

@@ -171,8 +171,11 @@ int gsv_vits_decode(gsv_engine* eng, const int64_t* text_seq, int32_t n_text,
  * them laid out back to back along time with zero gaps between utterances (every conv
  * treats a gap as the zero padding a single call sees), so its ~400 launches serve the
  * whole batch; each utterance matches its own gsv_vits_decode to fp32 rounding (the
- * batch's larger tiles order the reductions differently).  0: whole utterances on the
- * lanes, bit-identical to single calls.  Results are stream-ordered for the caller like
+ * batch's larger tiles order the reductions differently).  With option "seg_front" 1
+ * (default) the text/flow part is packed the same way (one pass, attention within each
+ * utterance) whenever every item carries ge (+ ge_adv) and noise_mode 0 or 2; otherwise
+ * it runs per item on the lanes.  seg_vocoder 0: whole utterances on the lanes,
+ * bit-identical to single calls.  Results are stream-ordered for the caller like
  * gsv_vits_decode.
  * Noise for z_p (vits(v2)#6490 RandomNormalLike x noise_scale):
  *   noise_mode 0: zeros; 1: eps (device [192, 2*n_sem]); 2: the engine's Philox
@@ -355,7 +358,8 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
  * after two timed-out launches in a row (64 generates / 5 s, doubling per failed re-probe).
  * "vocoder_cus" (CU split for the sentence pipeline), "decode_cus" / "decode_cu_offset",
  * "vits_lanes", "seg_vocoder" (1, default: a vocoder batch runs its generator as ONE pass
- * over all utterances laid out back to back), "convh" (MRF convs on the split-fp16 MFMA),
+ * over all utterances laid out back to back), "seg_front" (1, default: its text/flow part
+ * too, see gsv_vits_decode_batch), "convh" (MRF convs on the split-fp16 MFMA),
  * "sv_f16", "packed", test hooks ("persist_spin_ticks", "persist1_f16_limit",
  * "sv_f16_limit").  "ptrace": 1 allocates per-workgroup phase stamps of the persistent
  * launch (step 8, layer 12), read back with gsv_debug_ptrace ([256 workgroups][16
@@ -366,7 +370,8 @@ int gsv_set_option(gsv_engine* eng, const char* name, int value);
  * timed out -- e.g. other work on the device -- and re-ran as per-step graphs),
  * "persist_disabled" (back-off holds begun), "persist_hold" (generates left in the
  * current hold), "persist_launches", "persist1_f16_reruns" (fp16-range fallbacks),
- * "vits_f32_reruns", "sv_f32_reruns", "w16_split_tensors" (fp32 weights kept as hi + lo
+ * "vits_f32_reruns", "vits_packed_fronts" (vocoder batches whose text/flow part ran
+ * packed), "sv_f32_reruns", "w16_split_tensors" (fp32 weights kept as hi + lo
  * planes), "stops" (generates abandoned by gsv_request_stop). */
 int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value);
 int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);

@@ -264,7 +264,9 @@ def test_vits_batch_async_beside_t2s(setup):
 def test_v2_ref_encode_once(setup):
     """gsv_ref_encode: the V2 vocoder's reference branch computed once and passed as ge
     gives the same audio, bit for bit, as passing the reference audio to every call
-    (single, batched lanes and the overlapped batch); V2ProPlus rejects it."""
+    (per-lane front parts); with ge the batch's front part runs packed (seg_front), which
+    matches to fp32 rounding, and the overlapped batch gives the joined batch's audio bit
+    for bit; V2ProPlus rejects it."""
     from genie_tts_amd.engine import EngineError
     ver, e, _, _ = setup
     kw = _cond(ver)
@@ -280,13 +282,19 @@ def test_v2_ref_encode_once(setup):
         sem = ((np.arange(G, dtype=np.int64) * (3 + i) + i) % 1024).reshape(1, 1, G)
         items.append(dict(text_seq=txt, pred_semantic=sem, noise_seed=77 + i))
     ref = [o.cpu().numpy() for o in e.vits_decode_batch([dict(it, **kw) for it in items])]
+    e.set_option("seg_front", 0)
+    try:
+        lanes = [o.cpu().numpy() for o in e.vits_decode_batch([dict(it, ge=ge) for it in items])]
+    finally:
+        e.set_option("seg_front", 1)
     got = [o.cpu().numpy() for o in e.vits_decode_batch([dict(it, ge=ge) for it in items])]
     one = e.vits_decode(items[1]["text_seq"], items[1]["pred_semantic"], noise_seed=78, ge=ge).cpu().numpy()
     outs = e.vits_decode_batch_async([dict(it, ge=ge) for it in items])
     e.vits_batch_wait()
     for i in range(3):
-        np.testing.assert_array_equal(got[i], ref[i])
-        np.testing.assert_array_equal(outs[i].cpu().numpy(), ref[i])
+        np.testing.assert_array_equal(lanes[i], ref[i])
+        _close(got[i], ref[i], f"packed front, item {i}")
+        np.testing.assert_array_equal(outs[i].cpu().numpy(), got[i])
     _close(one, ref[1], "single vs segmented batch")
 
 
@@ -306,3 +314,41 @@ def test_vits_segmented_batch_many_utterances(setup):
     for i, it in enumerate(items):
         single = e.vits_decode(it["text_seq"], it["pred_semantic"], noise_seed=it["noise_seed"], **kw).cpu().numpy()
         _close(outs[i], single, f"item {i}")
+
+
+def test_vits_batch_packed_front_matches_single(setup):
+    """Segmented batch with the text/flow part packed too (option seg_front, the default when
+    every item carries its conditioning vectors and noise_mode 0 or 2): the utterances back
+    to back along the frame and text axes with zero gaps, self-attention (rel-pos) and the
+    MRTE cross-attention within each utterance, per-utterance ge / Philox keys.  Each item
+    matches its single call to fp32 rounding, the per-lane fronts (seg_front 0) too, the
+    zero-noise item the oracle within the north-star bar, and the packed path really ran
+    (counter vits_packed_fronts)."""
+    ver, e, vm, _ = setup
+    kw0 = _cond(ver)
+    kw = dict(ge=e.ref_encode(kw0["ref_audio"])) if ver == "v2" else kw0   # (gsv_ref_encode, as the API does)
+    items = []
+    for i, (G, S) in enumerate([(20, 12), (33, 25), (8, 9), (47, 31), (26, 18), (40, 40), (3, 2)]):
+        txt = synth.synth_phones(S, f"vp{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (11 + i) + 5 * i) % 1024).reshape(1, 1, G)
+        it = dict(text_seq=txt, pred_semantic=sem, **kw)
+        if i % 2 == 0:
+            it["noise_seed"] = 3000 + i
+        items.append(it)
+    singles = [e.vits_decode(it["text_seq"], it["pred_semantic"], noise_seed=it.get("noise_seed"), **kw).cpu().numpy()
+               for it in items]
+    n0 = e.counter("vits_packed_fronts")
+    packed = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+    assert e.counter("vits_packed_fronts") == n0 + 1
+    e.set_option("seg_front", 0)
+    try:
+        lanes = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+    finally:
+        e.set_option("seg_front", 1)
+    assert e.counter("vits_packed_fronts") == n0 + 1
+    for i, (p, l, s1) in enumerate(zip(packed, lanes, singles)):
+        _close(p, s1, f"item {i} vs single")
+        _close(p, l, f"item {i} vs lane fronts")
+    it = items[1]   # no noise: the oracle directly
+    ref = vm(it["text_seq"], it["pred_semantic"], **kw0).numpy().reshape(-1)
+    assert float(np.sqrt(np.mean((packed[1] - ref) ** 2))) <= RMS_TOL

@@ -1,6 +1,6 @@
 // Time the engine's fp16-weight GEMM (gsv::gemm_nt) on the shapes the engine runs:
 // T2S prefill (N0 = 225 rows), batched decode (B = 64), RoBERTa (40 tokens), CN-HuBERT
-// (300 frames).  Prints per-shape microseconds (hipEvents over 200 launches), the max
+// (300 frames), the packed prefill of 64 sentences (22848 rows).  Prints per-shape microseconds (hipEvents over 200 launches), the max
 // error against a double-precision host GEMM on sampled entries, and a bit hash of C
 // (identical hashes under GENIE_GEMM_X3=0 / 1 = bit-identical kernels).
 // Build: hipcc -O3 --offload-arch=gfx950 tools/gemm_bench.cpp -Igenie_tts_amd/csrc
@@ -37,6 +37,10 @@ int main() {
         {"roberta ffn2    ", 40, 1024, 4096, gsv::EPI_STORE, 1},
         {"hubert ffn1     ", 300, 3072, 768, gsv::EPI_GELU, 1},
         {"mixed prefill   ", 2400, 1536, 512, gsv::EPI_STORE, 1},
+        {"pk64 qkv        ", 22848, 1536, 512, gsv::EPI_STORE, 1},
+        {"pk64 out slab   ", 22848, 512, 512, gsv::EPI_SLAB, 4},
+        {"pk64 ffn1       ", 22848, 2048, 512, gsv::EPI_RELU, 1},
+        {"pk64 ffn2 slab  ", 22848, 512, 2048, gsv::EPI_SLAB, 8},
     };
     for (const Shape& sh : shapes) {
         const int M = sh.M, N = sh.N, K = sh.K;
@@ -64,7 +68,7 @@ int main() {
         hipEvent_t e0, e1;
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
-        const int iters = 200;
+        const int iters = M > 4096 ? 20 : 200;
         (void)hipEventRecord(e0, 0);
         for (int i = 0; i < iters; ++i) gsv::gemm_nt(g, 0);
         (void)hipEventRecord(e1, 0);

@@ -1,0 +1,68 @@
+"""batch64's vocoder alone: the 64 sentences' vits_decode_batch (synthetic V2 character,
+random semantic tokens of the workload's lengths, Philox noise), timed per call; with
+--trace DB (a rocprofv3 kernel-trace database of this run) it splits the last call's wall
+time into the per-utterance front part (lanes) and the segmented generator (from the
+first conv_pre launch, k_conv1d<7>, to the end).
+Usage: python tools/vits_batch_prof.py [N] [--seg 0|1] [--front 0|1]  |  python tools/vits_batch_prof.py --trace DIR"""
+import glob
+import os
+import sqlite3
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def trace(path):
+    db = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)[0]
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    ni = cols.index("name") if "name" in cols else cols.index("kernel_name")
+    si, ei = cols.index("start"), cols.index("end")
+    rows = sorted((r[si], r[ei], r[ni]) for r in c.execute("select * from kernels"))
+    # calls are separated by host gaps > 2 ms; take the last call
+    calls, cur = [], [rows[0]]
+    for r in rows[1:]:
+        if r[0] - max(x[1] for x in cur[-50:]) > 2e6:
+            calls.append(cur)
+            cur = []
+        cur.append(r)
+    calls.append(cur)
+    for k, call in enumerate(calls[-3:]):
+        t0, t1 = call[0][0], max(r[1] for r in call)
+        g0 = next((r[0] for r in call if "k_conv1d<7" in r[2]), t1)
+        print(f"call {k}: {len(call)} kernels, wall {(t1 - t0) / 1e6:.2f} ms: front {(g0 - t0) / 1e6:.2f} ms, "
+              f"generator {(t1 - g0) / 1e6:.2f} ms")
+
+
+def main():
+    if "--trace" in sys.argv:
+        return trace(sys.argv[sys.argv.index("--trace") + 1])
+    import numpy as np
+    import torch
+    from genie_tts_amd import synth, workloads
+    from genie_tts_amd.engine import Engine
+    n_calls = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 3
+    wl = workloads.batch64()
+    eng = Engine(synth.synthetic_character("v2"), "v2")
+    if "--seg" in sys.argv:
+        eng.set_option("seg_vocoder", int(sys.argv[sys.argv.index("--seg") + 1]))
+    if "--front" in sys.argv:
+        eng.set_option("seg_front", int(sys.argv[sys.argv.index("--front") + 1]))
+    ref = wl.reference
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    ge = eng.ref_encode(T(ref.audio_32k.reshape(-1)))
+    r = np.random.default_rng(5)
+    items = [dict(text_seq=T(it.text_seq.reshape(-1)), pred_semantic=T(r.integers(0, 1024, it.tokens)),
+                  noise_seed=0x5EED + i, ge=ge) for i, it in enumerate(wl.items)]
+    for k in range(n_calls):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.vits_decode_batch(items)
+        torch.cuda.synchronize()
+        print(f"call {k}: {(time.perf_counter() - t0) * 1e3:.2f} ms for {len(items)} utterances", flush=True)
+        time.sleep(0.01)   # a host gap between calls (the trace splitter keys on it)
+
+
+if __name__ == "__main__":
+    main()
