@@ -31,9 +31,9 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 constexpr int DMAX = 5;   // largest dilation of the MRF convs (rb_d)
 
-template <int KT, int CC, int WM, int WN, int KS>
+template <int KT, int CC, int WM, int WN, int KS, int WTM = 1>
 struct HCfg {
-    static constexpr int BM = 32 * WM, BN = 64 * WN;
+    static constexpr int BM = 32 * WM * WTM, BN = 64 * WN;
     static constexpr int G8 = CC / 8;                   // 8-channel groups per tap
     static constexpr int NG = KT * G8;                  // groups per chunk
     static constexpr int NSTEP = (NG + 1) / 2;          // MFMA K-steps (2 groups each)
@@ -44,7 +44,7 @@ struct HCfg {
     static constexpr int NWI = (BM * NG + 255) / 256;   // W 16-B items per thread
     static constexpr int X_BYTES = XW * XR * 2;
     static constexpr int W_BYTES = BM * WR * 2;
-    static constexpr int RED_BYTES = KS > 1 ? (KS - 1) * WM * WN * 2 * 16 * 64 * 4 : 0;
+    static constexpr int RED_BYTES = KS > 1 ? (KS - 1) * WM * WN * WTM * 2 * 16 * 64 * 4 : 0;
     static constexpr int MAIN_BYTES = 2 * X_BYTES + W_BYTES;
     static constexpr int LDS = MAIN_BYTES > RED_BYTES ? MAIN_BYTES : RED_BYTES;
 };
@@ -60,9 +60,14 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4& hi, uint4& lo
     lo = *reinterpret_cast<const uint4*>(l);
 }
 
-template <int KT, int CC, int WM, int WN, int KS>
+// WTM > 1 (the long-time form): each wave owns WTM x 2 accumulators, WTM 32-row output
+// blocks over the same 64 time columns, so a K-step's four B fragment reads (two time
+// blocks x hi / lo) feed 4 WTM MFMAs instead of 4.  Every accumulator runs the WTM = 1
+// MFMA sequence (bit-identical results at the same KS).
+template <int KT, int CC, int WM, int WN, int KS, int WTM = 1>
 __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
-    using C = HCfg<KT, CC, WM, WN, KS>;
+    using C = HCfg<KT, CC, WM, WN, KS, WTM>;
+    static_assert(WTM == 1 || KS == 1, "the multi-block wave form has no K split");
     __shared__ __attribute__((aligned(16))) char smem[C::LDS];
     _Float16* Xh = reinterpret_cast<_Float16*>(smem);
     _Float16* Xl = reinterpret_cast<_Float16*>(smem + C::X_BYTES);
@@ -144,14 +149,16 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
         }
     };
 
-    f32x16 acc[2];
+    f32x16 acc[WTM][2];
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+    for (int m = 0; m < WTM; ++m)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[f][i] = 0.f;
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[m][f][i] = 0.f;
 
     const int r32 = lane & 31, hsel = lane >> 5;
-    const _Float16* wrow = Ws + (wm * 32 + r32) * C::WR;
+    const _Float16* wrow = Ws + (wm * 32 * WTM + r32) * C::WR;
     load(0);
     store();
     __syncthreads();
@@ -162,15 +169,22 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
             const int g = 2 * j + hsel;                 // this lane's 8-channel group
             const bool gv = g < C::NG;
             const int tap = gv ? g / C::G8 : 0, c8 = gv ? g - tap * C::G8 : 0;
-            h8 A = *reinterpret_cast<const h8*>(wrow + tap * CC + c8 * 8);
-            if (!gv) A = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+            h8 A[WTM];
+#pragma unroll
+            for (int m = 0; m < WTM; ++m) {
+                A[m] = *reinterpret_cast<const h8*>(wrow + m * 32 * C::WR + tap * CC + c8 * 8);
+                if (!gv) A[m] = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+            }
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
                 const int row = wn * 64 + f * 32 + r32 + tap * dil;
                 const h8 Bl = *reinterpret_cast<const h8*>(Xl + row * C::XR + c8 * 8);
                 const h8 Bh = *reinterpret_cast<const h8*>(Xh + row * C::XR + c8 * 8);
-                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bl, acc[f], 0, 0, 0);
-                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bh, acc[f], 0, 0, 0);
+#pragma unroll
+                for (int m = 0; m < WTM; ++m) {
+                    acc[m][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m], Bl, acc[m][f], 0, 0, 0);
+                    acc[m][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m], Bh, acc[m][f], 0, 0, 0);
+                }
             }
         }
         __syncthreads();
@@ -190,7 +204,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
 #pragma unroll
             for (int f = 0; f < 2; ++f)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) p[(f * 16 + i) * 64 + lane] = acc[f][i];
+                for (int i = 0; i < 16; ++i) p[(f * 16 + i) * 64 + lane] = acc[0][f][i];
         }
         __syncthreads();
         if (ks > 0) return;
@@ -200,24 +214,27 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
 #pragma unroll
             for (int f = 0; f < 2; ++f)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) acc[f][i] += p[(f * 16 + i) * 64 + lane];
+                for (int i = 0; i < 16; ++i) acc[0][f][i] += p[(f * 16 + i) * 64 + lane];
         }
     }
-    const int cobase = co0 + wm * 32 + 4 * hsel;
-    float sc[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int co = cobase + (r & 3) + 8 * (r >> 2);
-        sc[r] = co < a.Cout ? a.wscale[co] : 0.f;
-    }
+    for (int m = 0; m < WTM; ++m) {
+        const int cobase = co0 + (wm * WTM + m) * 32 + 4 * hsel;
+        float sc[16];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-        const int t = t0 + wn * 64 + f * 32 + r32;
-        if (t >= a.n_t) continue;
-        float v[16];
+        for (int r = 0; r < 16; ++r) {
+            const int co = cobase + (r & 3) + 8 * (r >> 2);
+            sc[r] = co < a.Cout ? a.wscale[co] : 0.f;
+        }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = acc[f][r] * sc[r];
-        conv_epilogue16(a, cobase, t, 0, v);
+        for (int f = 0; f < 2; ++f) {
+            const int t = t0 + wn * 64 + f * 32 + r32;
+            if (t >= a.n_t) continue;
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = acc[m][f][r] * sc[r];
+            conv_epilogue16(a, cobase, t, 0, v);
+        }
     }
 }
 
@@ -248,8 +265,28 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
     return true;
 }
 
+// Long-time form (the batched generator: 10^5-10^7 columns): 128 x 128 output blocks,
+// each wave 64 output channels x 64 columns (WTM = 2); 16-channel K-chunks for the
+// 7- and 11-tap convs keep the weight tile at 31-47 KB, two blocks per CU.
+// GENIE_CONVH_BIG=0 keeps launch_h's forms.
+static bool convh_big() {
+    static const bool on = [] { const char* e = std::getenv("GENIE_CONVH_BIG"); return !(e && std::atoi(e) == 0); }();
+    return on;
+}
+template <int KT>
+bool launch_big(const ConvArgs& a, hipStream_t s) {
+    constexpr int CC = KT >= 7 ? 16 : 32;
+    if (a.Cin % CC != 0) return false;
+    const dim3 grid((a.n_t + 127) / 128, (a.Cout + 127) / 128);
+    hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1, 2>), grid, dim3(256), 0, s, a);
+    return true;
+}
+
 template <int KT>
 bool launch_kt(const ConvArgs& a, hipStream_t s) {
+    if (convh_big() && a.Cout % 128 == 0 && (long)((a.n_t + 127) / 128) * (a.Cout / 128) >= 1024 &&
+        launch_big<KT>(a, s))
+        return true;
     if (a.Cin % 32 == 0) return launch_h<KT, 32>(a, s);
     if (a.Cin % 8 == 0) return launch_h<KT, 8>(a, s);
     return false;
