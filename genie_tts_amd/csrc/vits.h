@@ -54,6 +54,10 @@ struct ConvArgs {
     // scale (weight norm g/||v||, 1 without it), overflow flag set when an
     // input does not fit fp16.  wh == nullptr -> f32 path.
     const __half* wh; const float* wscale; int* ovf;
+    // ... a ConvTranspose's polyphase weights on that path: [phases][Cout][K][Cin] (phase
+    // stride wh_phase_stride halfs); its weight norm is over the INPUT channel, applied as
+    // in_scale[ci] to the (pre-activated) input instead of to the sums
+    long wh_phase_stride; const float* in_scale;
     // segmented batch (several utterances back to back along time, zero gaps between
     // them): seg[tp] = the utterance of output time tp, or -1 in a gap, where the
     // output is written as 0 (so every buffer keeps zero gaps, and a conv whose halo
@@ -127,7 +131,9 @@ struct Conv {
     float* b = nullptr;
     int cout = 0, cin = 0, k = 0, phases = 1;
     __half* wh = nullptr;      // fp16 [Cout][K][Cin] when every weight value is fp16-exact
+                               // (ConvT: [phases][Cout][K][Cin])
     float* wscale = nullptr;   // [Cout] weight-norm scale applied to the f16 path's sums
+    float* in_scale = nullptr; // ConvT: [Cin] weight-norm scale applied to the input
 };
 
 struct AttnLayer {

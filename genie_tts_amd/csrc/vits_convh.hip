@@ -79,7 +79,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     const int dil = a.dil;
     const int xw = C::BN + (KT - 1) * dil;
     const int nch = a.Cin / CC;
-    const _Float16* __restrict__ Wg = reinterpret_cast<const _Float16*>(a.wh);
+    const int ph = a.phases > 1 ? (int)blockIdx.z : 0;   // ConvTranspose polyphase: phase of this block
+    const _Float16* __restrict__ Wg = reinterpret_cast<const _Float16*>(a.wh) + (long)ph * a.wh_phase_stride;
+    const float* __restrict__ isc = a.in_scale;
     const float* __restrict__ X = a.x;
 
     // per-thread staging items (loop invariant): X item e -> (group c8, row u)
@@ -121,13 +123,17 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
             wr[i] = v;
         }
     };
-    auto store = [&]() {
+    auto store = [&](int cis) {   // cis: the first input channel of the staged chunk
 #pragma unroll
         for (int i = 0; i < C::NXI; ++i) {
             if (xc[i] < 0) continue;
             if (a.in_act) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) xr[i][j] = xr[i][j] >= 0.f ? xr[i][j] : xr[i][j] * a.in_slope;
+            }
+            if (isc) {   // the staged channels are cis + 8 xc + j
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xr[i][j] *= isc[cis + xc[i] * 8 + j];
             }
             float m = 0.f;
 #pragma unroll
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     const int r32 = lane & 31, hsel = lane >> 5;
     const _Float16* wrow = Ws + (wm * 32 * WTM + r32) * C::WR;
     load(0);
-    store();
+    store(0);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
         if (c + 1 < nch) load((c + 1) * CC);
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
         }
         __syncthreads();
         if (c + 1 < nch) {
-            store();
+            store((c + 1) * CC);
             __syncthreads();
         }
     }
@@ -233,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
             float v[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = acc[m][f][r] * sc[r];
-            conv_epilogue16(a, cobase, t, 0, v);
+            conv_epilogue16(a, cobase, t, ph, v);
         }
     }
 }
@@ -249,7 +255,7 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
     double best_cost = 1e30;
     for (int i = 0; i < 4; ++i) {
         const int bm = 32 * cands[i].wm, bn = 64 * cands[i].wn;
-        const long blocks = (long)((a.n_t + bn - 1) / bn) * ((a.Cout + bm - 1) / bm);
+        const long blocks = (long)((a.n_t + bn - 1) / bn) * ((a.Cout + bm - 1) / bm) * (a.phases > 1 ? a.phases : 1);
         const long rounds = (blocks + 511) / 512;
         const double cost = (double)rounds * bm * bn * (1.0 + 0.1 * (cands[i].ks - 1));
         if (cost < best_cost) { best_cost = cost; best = i; }
@@ -257,7 +263,8 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
     static const int forced = [] { const char* e = std::getenv("GENIE_CONVH_CFG"); return e ? std::atoi(e) : -1; }();
     if (forced >= 0 && forced < 4) best = forced;
     const Cand c = cands[best];
-    const dim3 grid((a.n_t + 64 * c.wn - 1) / (64 * c.wn), (a.Cout + 32 * c.wm - 1) / (32 * c.wm));
+    const dim3 grid((a.n_t + 64 * c.wn - 1) / (64 * c.wn), (a.Cout + 32 * c.wm - 1) / (32 * c.wm),
+                    a.phases > 1 ? a.phases : 1);
     if (c.wm == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1>), grid, dim3(256), 0, s, a);
     else if (c.ks == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 2, 2>), grid, dim3(256), 0, s, a);
     else if (c.ks == 4) hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 1, 4>), grid, dim3(256), 0, s, a);
@@ -277,15 +284,15 @@ template <int KT>
 bool launch_big(const ConvArgs& a, hipStream_t s) {
     constexpr int CC = KT >= 7 ? 16 : 32;
     if (a.Cin % CC != 0) return false;
-    const dim3 grid((a.n_t + 127) / 128, (a.Cout + 127) / 128);
+    const dim3 grid((a.n_t + 127) / 128, (a.Cout + 127) / 128, a.phases > 1 ? a.phases : 1);
     hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1, 2>), grid, dim3(256), 0, s, a);
     return true;
 }
 
 template <int KT>
 bool launch_kt(const ConvArgs& a, hipStream_t s) {
-    if (convh_big() && a.Cout % 128 == 0 && (long)((a.n_t + 127) / 128) * (a.Cout / 128) >= 1024 &&
-        launch_big<KT>(a, s))
+    if (convh_big() && a.Cout % 128 == 0 &&
+        (long)((a.n_t + 127) / 128) * (a.Cout / 128) * (a.phases > 1 ? a.phases : 1) >= 1024 && launch_big<KT>(a, s))
         return true;
     if (a.Cin % 32 == 0) return launch_h<KT, 32>(a, s);
     if (a.Cin % 8 == 0) return launch_h<KT, 8>(a, s);
@@ -296,9 +303,16 @@ bool launch_kt(const ConvArgs& a, hipStream_t s) {
 
 bool conv1d_h(const ConvArgs& a, hipStream_t s) {
     if (!a.wh || !a.wscale || !a.ovf) return false;
-    if (a.phases > 1 || a.x_ts != 1 || a.dil < 1 || a.dil > DMAX || a.o_tstride != 1) return false;
+    // a plain conv (one phase, unit output stride) or a ConvTranspose's polyphase form
+    // (phases = output stride; dilation 1)
+    const bool poly = a.phases > 1;
+    if (poly ? (a.o_tstride != a.phases || a.dil != 1) : a.o_tstride != 1) return false;
+    if (a.x_ts != 1 || a.dil < 1 || a.dil > DMAX) return false;
     if ((reinterpret_cast<uintptr_t>(a.wh) & 15) != 0) return false;
     switch (a.K) {
+        case 1: return launch_kt<1>(a, s);
+        case 2: return launch_kt<2>(a, s);
+        case 4: return launch_kt<4>(a, s);
         case 3: return launch_kt<3>(a, s);
         case 7: return launch_kt<7>(a, s);
         case 11: return launch_kt<11>(a, s);

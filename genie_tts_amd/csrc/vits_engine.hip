@@ -128,6 +128,37 @@ static int load_convT(gsv_engine* e, const std::string& base, int u, Conv& c) {
     c.cin = cin;
     c.k = M;
     c.phases = u;
+    // the split-fp16 path's copy: the unfolded weight_v values (fp16 in the Genie bins)
+    // as [phase][Cout][M][Cin], the weight norm g/||v|| (over dim 0 = Cin) as a per-input-
+    // channel scale; absent when some value is not fp16-exact (the f32 path stays)
+    std::vector<__half> ph((size_t)u * cout * M * cin, __float2half(0.f));
+    bool exact = true;
+    for (int r = 0; r < u && exact; ++r)
+        for (int co = 0; co < cout && exact; ++co)
+            for (int j = 0; j < M && exact; ++j) {
+                const int kk = r + (M - 1 - j) * u;
+                if (kk >= k) continue;
+                for (int ci = 0; ci < cin; ++ci) {
+                    const float x = v->data[((size_t)ci * cout + co) * k + kk];
+                    const __half hx = __float2half(x);
+                    if (__half2float(hx) != x) { exact = false; break; }
+                    ph[(((size_t)r * cout + co) * M + j) * cin + ci] = hx;
+                }
+            }
+    if (exact) {
+        std::vector<float> isc(cin), one(cout, 1.f);
+        const long per = (long)cout * k;
+        for (int ci = 0; ci < cin; ++ci) {
+            double q = 0;
+            for (long t = 0; t < per; ++t) q += (double)v->data[ci * per + t] * v->data[ci * per + t];
+            isc[ci] = g->data[ci] / (float)std::sqrt(q);
+        }
+        c.wh = (__half*)e->dalloc(ph.size() * 2);
+        c.wscale = up_vec(e, one);
+        c.in_scale = up_vec(e, isc);
+        if (!c.wh || !c.wscale || !c.in_scale) return set_error(GSV_E_HIP, "ConvTranspose fp16 upload failed");
+        hipMemcpy(c.wh, ph.data(), ph.size() * 2, hipMemcpyHostToDevice);
+    }
     return 0;
 }
 
@@ -625,6 +656,13 @@ static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const fl
         ct.in_act = 1; ct.in_slope = 0.1f; ct.mode = CV_STORE;
         ct.phases = u; ct.w_phase_stride = (long)up.cout * up.cin * up.k;
         ct.seg = sg;
+        // GENIE_CONVT_F16=1: the upsample convs on the split-fp16 path (off by default: a
+        // lanes-vs-single mismatch under investigation)
+        static const bool convt_f16 = [] { const char* e = std::getenv("GENIE_CONVT_F16"); return e && std::atoi(e) != 0; }();
+        if (tls_ovf && up.wh && convt_f16) {   // the split-fp16 path (polyphase weights, input-channel weight norm)
+            ct.wh = up.wh; ct.wscale = up.wscale; ct.ovf = tls_ovf; ct.in_scale = up.in_scale;
+            ct.wh_phase_stride = (long)up.cout * up.k * up.cin;
+        }
         conv1d(ct, s);
         C = up.cout;
         Tc = Tn;
