@@ -90,6 +90,9 @@ static int load_conv(gsv_engine* e, const std::string& base, Conv& c, bool wn, b
         s = e->find(base + ".weight");
         if (!s) return set_error(GSV_E_WEIGHT, "missing weight " + base + ".weight");
         w = s->data;
+        if (f16)   // no weight norm: unit scale
+            upload_f16(e, s->data, (int)s->dims[0], (int)s->dims[1], s->dims.size() > 2 ? (int)s->dims[2] : 1,
+                       std::vector<float>((size_t)s->dims[0], 1.f), c);
     }
     c.cout = (int)s->dims[0];
     c.cin = (int)s->dims[1];
@@ -279,7 +282,7 @@ int gsv_engine::finalize_vits() {
         }
     }
     const std::string D = "vq_model.dec.";
-    if (int r = load_conv(this, D + "conv_pre", V.conv_pre, false)) return r;
+    if (int r = load_conv(this, D + "conv_pre", V.conv_pre, false, true, true)) return r;   // (split-fp16 path too)
     if (int r = load_conv(this, D + "cond", V.cond, false)) return r;
     if (int r = load_conv(this, D + "conv_post", V.conv_post, false, false)) return r;
     for (int i = 0; i < 5; ++i)

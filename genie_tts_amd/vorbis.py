@@ -130,6 +130,13 @@ class _Bits:
         self.p += 1
         return b
 
+    def peek(self, k: int) -> int:
+        """The next k bits (LSb-first, as read() would return them) without consuming
+        them; bits past the end read as 0."""
+        p = self.p
+        b = p >> 3
+        return (int.from_bytes(self.d[b:b + ((p & 7) + k + 7) // 8], "little") >> (p & 7)) & ((1 << k) - 1)
+
 
 def ilog(x: int) -> int:
     return 0 if x <= 0 else x.bit_length()
@@ -178,6 +185,7 @@ class Codebook:
                     lengths[i] = r.read(5) + 1
         self.lengths = lengths
         self.codes = self._assign(lengths)
+        self._table()
         self.lookup_type = r.read(4)
         self.vq: Optional[np.ndarray] = None
         if self.lookup_type in (1, 2):
@@ -230,10 +238,35 @@ class Codebook:
                     break
         return codes
 
+    TABLE_BITS = 12
+
+    def _table(self):
+        """Direct lookup of codewords up to TABLE_BITS long: index = the next TABLE_BITS
+        bits as read (the first bit read = the codeword's MSb = index bit 0); longer ones
+        fall back to the bit-serial walk."""
+        n = self.TABLE_BITS
+        self._ent = [-1] * (1 << n)
+        self._len = [0] * (1 << n)
+        if (0, 0) in self.codes:
+            return
+        for (ln, code), e in self.codes.items():
+            if ln > n:
+                continue
+            rev = int(format(code, f"0{ln}b")[::-1], 2)   # reading order -> LSb-first
+            for hi in range(1 << (n - ln)):
+                idx = rev | (hi << ln)
+                self._ent[idx] = e
+                self._len[idx] = ln
+
     def decode(self, r: _Bits) -> int:
         if (0, 0) in self.codes:
             r.bit()
             return self.codes[(0, 0)]
+        idx = r.peek(self.TABLE_BITS)
+        ln = self._len[idx]
+        if ln and r.p + ln <= r.n:
+            r.p += ln
+            return self._ent[idx]
         code = 0
         for ln in range(1, 33):
             code = (code << 1) | r.bit()
