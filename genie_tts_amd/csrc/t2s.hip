@@ -410,8 +410,9 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
     auto go = [&](auto kern, int bm, int bn, int threads) {
         hipLaunchKernelGGL(kern, dim3((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, z), dim3(threads), 0, s, a);
     };
-    if (a.Wl) {   // split weights: one configuration (4 x 32 KB stages)
-        go(k_gemm_x3<64, 64, 4, true>, 64, 64, 256);
+    if (a.Wl) {   // split weights: 4 x 32 KB stages; cfg 16: 2 stages + XCD remap (64 KB, 2 blocks per CU)
+        if (cfg == 16) go(k_gemm_x3<64, 64, 2, true, 1, true>, 64, 64, 256);
+        else go(k_gemm_x3<64, 64, 4, true>, 64, 64, 256);
         return;
     }
     switch (cfg) {
@@ -458,6 +459,17 @@ static bool gemm_big(const GemmArgs& a) {
     return gemm_big_cfg() != 0 && (long)((a.M + 63) / 64) * ((a.N + 63) / 64) >= 1024;
 }
 
+// Split-weight GEMMs (RoBERTa / CN-HuBERT fp32 weights): the two-stage, two-blocks-per-CU
+// form with the XCD remap (cfg 16, default; bit-identical to the four-stage one, 0.75x its
+// time on packed RoBERTa rows, profiles/r04k_gemm_sw.txt); GENIE_GEMM_SW=0 the four-stage form.
+static int gemm_sw_cfg() {
+    static const int c = [] {
+        const char* e = std::getenv("GENIE_GEMM_SW");
+        return e ? std::atoi(e) : 16;
+    }();
+    return c;
+}
+
 static int gemm_variant() {   // GENIE_GEMM_X3=0: the register-staged k_gemm_x2
     static const int v = [] {
         const char* e = std::getenv("GENIE_GEMM_X3");
@@ -489,7 +501,7 @@ void gemm_nt(const GemmArgs& a, hipStream_t s) {
             std::fprintf(stderr, "gemm_nt: split-weight GEMM with unsupported shape K=%d lda=%ld\n", a.K, a.lda);
             std::abort();
         }
-        launch_x3(a, a.mode == EPI_SLAB ? a.ksplit : 1, s, 0);
+        launch_x3(a, a.mode == EPI_SLAB ? a.ksplit : 1, s, gemm_sw_cfg());
         return;
     }
     // fp16 weights -> split-activation f16 MFMA; the VQ distance GEMM stays on the

@@ -282,7 +282,9 @@ int gsv_engine::finalize_vits() {
         }
     }
     const std::string D = "vq_model.dec.";
-    if (int r = load_conv(this, D + "conv_pre", V.conv_pre, false, true, true)) return r;   // (split-fp16 path too)
+    // (f32 path: on the split-fp16 kernel the flows' output z of the synthetic weights leaves
+    // the fp16 range and every batch re-ran its generator on f32 -- r04k, 62.6 -> 77.8 ms)
+    if (int r = load_conv(this, D + "conv_pre", V.conv_pre, false)) return r;
     if (int r = load_conv(this, D + "cond", V.cond, false)) return r;
     if (int r = load_conv(this, D + "conv_post", V.conv_post, false, false)) return r;
     for (int i = 0; i < 5; ++i)

@@ -14,7 +14,7 @@
 #include <vector>
 #include "kernels.h"
 
-struct Shape { const char* name; int M, N, K, mode, ksplit; };
+struct Shape { const char* name; int M, N, K, mode, ksplit; int sw = 0; };   // sw: split fp32 weights (hi + lo planes)
 
 static unsigned long long rng_state = 7;   // private LCG: the HIP runtime may draw from rand()
 static float frand() {
@@ -41,6 +41,10 @@ int main() {
         {"pk64 out slab   ", 22848, 512, 512, gsv::EPI_SLAB, 4},
         {"pk64 ffn1       ", 22848, 2048, 512, gsv::EPI_RELU, 1},
         {"pk64 ffn2 slab  ", 22848, 512, 2048, gsv::EPI_SLAB, 8},
+        {"rob pk qkv  W16 ", 1100, 3072, 1024, gsv::EPI_STORE, 1, 1},
+        {"rob pk ffn1 W16 ", 1100, 4096, 1024, gsv::EPI_GELU, 1, 1},
+        {"rob pk ffn2 W16 ", 1100, 1024, 4096, gsv::EPI_SLAB, 8, 1},
+        {"rob 22 ffn1 W16 ", 22, 4096, 1024, gsv::EPI_GELU, 1, 1},
     };
     for (const Shape& sh : shapes) {
         const int M = sh.M, N = sh.N, K = sh.K;
@@ -50,7 +54,7 @@ int main() {
         for (auto& v : W) v = __float2half((frand() - 0.5f) * 0.1f);
         for (auto& v : bias) v = (frand() - 0.5f);
         float *dA, *dB, *dC;
-        __half* dW;
+        __half *dW, *dWl = nullptr;
         const size_t cElems = (size_t)M * N * sh.ksplit;
         (void)hipMalloc(&dA, A.size() * 4);
         (void)hipMalloc(&dW, W.size() * 2);
@@ -58,11 +62,19 @@ int main() {
         (void)hipMalloc(&dC, cElems * 4);
         (void)hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice);
         (void)hipMemcpy(dW, W.data(), W.size() * 2, hipMemcpyHostToDevice);
+        std::vector<__half> Wl;
+        if (sh.sw) {   // a lo plane of small values (w = hi + lo 2^-11)
+            Wl.resize(W.size());
+            for (auto& v : Wl) v = __float2half((frand() - 0.5f) * 0.1f);
+            (void)hipMalloc(&dWl, Wl.size() * 2);
+            (void)hipMemcpy(dWl, Wl.data(), Wl.size() * 2, hipMemcpyHostToDevice);
+        }
         (void)hipMemcpy(dB, bias.data(), N * 4, hipMemcpyHostToDevice);
         gsv::GemmArgs g{};
         g.M = M; g.N = N; g.K = K; g.A = dA; g.lda = K; g.W = dW; g.ldw = K; g.w_f16 = 1;
         g.bias = sh.mode == gsv::EPI_SLAB ? nullptr : dB; g.C = dC; g.ldc = N; g.mode = sh.mode;
         g.ksplit = sh.ksplit; g.slab_stride = (long)M * N;
+        g.Wl = dWl;
         gsv::gemm_nt(g, 0);
         (void)hipDeviceSynchronize();
         hipEvent_t e0, e1;
@@ -82,7 +94,11 @@ int main() {
         for (int t = 0; t < 256; ++t) {
             const int m = irand(M), n = irand(N);
             double ref = 0.0;
-            for (int k = 0; k < K; ++k) ref += (double)A[(size_t)m * K + k] * (double)__half2float(W[(size_t)n * K + k]);
+            for (int k = 0; k < K; ++k) {
+                double wv = (double)__half2float(W[(size_t)n * K + k]);
+                if (sh.sw) wv += (double)__half2float(Wl[(size_t)n * K + k]) / 2048.0;
+                ref += (double)A[(size_t)m * K + k] * wv;
+            }
             double got = 0.0;
             if (sh.mode == gsv::EPI_SLAB) {
                 for (int z = 0; z < sh.ksplit; ++z) got += C[(size_t)z * M * N + (size_t)m * N + n];
@@ -105,6 +121,7 @@ int main() {
         printf("%s M=%5d N=%5d K=%5d split=%2d: %8.2f us  (%6.0f GB/s of W+A)  maxerr %.2e  hash %016llx\n", sh.name,
                M, N, K, sh.ksplit, us, (wbytes + abytes) / (us * 1e3), maxerr, hsh);
         (void)hipFree(dA); (void)hipFree(dW); (void)hipFree(dB); (void)hipFree(dC);
+        if (dWl) (void)hipFree(dWl);
     }
     return 0;
 }
