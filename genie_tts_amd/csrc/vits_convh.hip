@@ -274,25 +274,38 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
 
 // Long-time form (the batched generator: 10^5-10^7 columns): 128 x 128 output blocks,
 // each wave 64 output channels x 64 columns (WTM = 2); 16-channel K-chunks for the
-// 7- and 11-tap convs keep the weight tile at 31-47 KB, two blocks per CU.
-// GENIE_CONVH_BIG=0 keeps launch_h's forms.
+// 7- and 11-tap convs keep the weight tile at 31-47 KB, two blocks per CU.  Off by default
+// (GENIE_CONVH_BIG=1 turns it on): alone it makes a 64-sentence vocoder pass 3 % faster,
+// but beside the next batch's prefill (the batched pipeline) its long blocks hold the CUs
+// and the prefill's short GEMM launches wait -- batch64 321 -> 296 utt/s, mixed100
+// 277 -> 253 (profiles/r04m_convh_big.txt).
 static bool convh_big() {
-    static const bool on = [] { const char* e = std::getenv("GENIE_CONVH_BIG"); return !(e && std::atoi(e) == 0); }();
+    static const bool on = [] { const char* e = std::getenv("GENIE_CONVH_BIG"); return e && std::atoi(e) != 0; }();
     return on;
 }
+// Cout = 64 (not a multiple of 128): 64 x 256 blocks, four waves side by side in time.
 template <int KT>
 bool launch_big(const ConvArgs& a, hipStream_t s) {
     constexpr int CC = KT >= 7 ? 16 : 32;
     if (a.Cin % CC != 0) return false;
-    const dim3 grid((a.n_t + 127) / 128, (a.Cout + 127) / 128, a.phases > 1 ? a.phases : 1);
-    hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1, 2>), grid, dim3(256), 0, s, a);
+    const int z = a.phases > 1 ? a.phases : 1;
+    if (a.Cout % 128 == 0) {
+        const dim3 grid((a.n_t + 127) / 128, a.Cout / 128, z);
+        hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1, 2>), grid, dim3(256), 0, s, a);
+    } else {
+        const dim3 grid((a.n_t + 255) / 256, a.Cout / 64, z);
+        hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 4, 1, 2>), grid, dim3(256), 0, s, a);
+    }
     return true;
 }
 
 template <int KT>
 bool launch_kt(const ConvArgs& a, hipStream_t s) {
-    if (convh_big() && a.Cout % 128 == 0 &&
-        (long)((a.n_t + 127) / 128) * (a.Cout / 128) * (a.phases > 1 ? a.phases : 1) >= 1024 && launch_big<KT>(a, s))
+    const int z = a.phases > 1 ? a.phases : 1;
+    if (convh_big() && a.Cout % 64 == 0 &&
+        (a.Cout % 128 == 0 ? (long)((a.n_t + 127) / 128) * (a.Cout / 128) * z
+                           : (long)((a.n_t + 255) / 256) * (a.Cout / 64) * z) >= 1024 &&
+        launch_big<KT>(a, s))
         return true;
     if (a.Cin % 32 == 0) return launch_h<KT, 32>(a, s);
     if (a.Cin % 8 == 0) return launch_h<KT, 8>(a, s);

@@ -354,9 +354,10 @@ def test_stop_interrupts_a_running_decode(eng, B, persist):
     assert stopped and eng.counter("stops") == s0 + 1
     assert ran < 0.8 * t_full
     # two loop steps of this decode plus the host's wake-up; the graph path checks its
-    # stop word per step too, but its host loop notices only between 8-step chunks
+    # stop word per step too, but its host loop keeps two 8-step chunks queued ahead and
+    # notices only between them (measured r04l: 4.08 ms at 0.2 ms per step)
     step = t_full / 500
-    assert latency < 2 * step + (8 * step if persist == 0 else 0) + 2e-3, latency
+    assert latency < 2 * step + (16 * step if persist == 0 else 0) + 2e-3, latency
     # a request before the call: nothing runs
     eng.request_stop(True)
     from genie_tts_amd.engine import EngineStopped
