@@ -416,10 +416,8 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
         return;
     }
     switch (cfg) {
-        case 9: go(k_gemm_x3<128, 128, 3, false, 4, true>, 128, 128, 256); break;   // large M
-        case 10: go(k_gemm_x3<128, 128, 2, false, 4, true>, 128, 128, 256); break;
-        case 11: go(k_gemm_x3<128, 128, 3, false, 4, false>, 128, 128, 256); break;
-        case 12: go(k_gemm_x3<128, 64, 3, false, 2, true>, 128, 64, 256); break;
+        // (r04: the one-block-per-CU 128 x 128 forms, four 32 x 32 tiles per wave, measured
+        // slower than k_gemm_x2 at 22,848 rows and were removed; profiles/r04e_gemm_big.txt)
         case 13: go(k_gemm_x3<64, 128, 2, false, 2, true>, 64, 128, 256); break;   // 64 KB: 2 blocks per CU
         case 14: go(k_gemm_x3<128, 64, 2, false, 2, true>, 128, 64, 256); break;   // 80 KB
         case 15: go(k_gemm_x3<64, 64, 2, false, 1, true>, 64, 64, 256); break;     // 48 KB: 3 per CU
