@@ -23,6 +23,7 @@
 #include "../../include/genie_engine.h"
 #include "engine_internal.h"
 #include "kernels.h"
+#include "prefill_attn.h"
 
 using namespace gsv;
 
@@ -609,10 +610,13 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     const int R = off[B];
     if (int e = ensure_packed(R, B)) return e;
     // host row tables: sequence, position, visible keys; last row of each sequence
-    // tiles of <= 16 rows of one sequence for the LDS-staged attention
+    // tiles of <= TR rows of one sequence for the attention: 128 on the MFMA kernel, else
+    // 16 for the LDS-staged f32 kernels
+    const bool mfma_attn = attn_mfma_on();
+    const int TR = mfma_attn ? 128 : 16;
     int ntiles = 0, maxn0 = 0;
     for (int b = 0; b < B; ++b) {
-        ntiles += (off[b + 1] - off[b] + 15) / 16;
+        ntiles += (off[b + 1] - off[b] + TR - 1) / TR;
         maxn0 = std::max(maxn0, off[b + 1] - off[b]);
     }
     pk_host.resize((size_t)3 * R + B + 3 * (size_t)ntiles);
@@ -630,10 +634,10 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
             hl[r] = j < Ls[b] ? Ls[b] : j + 1;
         }
         hlast[b] = off[b + 1] - 1;
-        for (int r0 = off[b]; r0 < off[b + 1]; r0 += 16, ++ti) {
+        for (int r0 = off[b]; r0 < off[b + 1]; r0 += TR, ++ti) {
             htile[3 * ti] = b;
             htile[3 * ti + 1] = r0;
-            htile[3 * ti + 2] = std::min(16, off[b + 1] - r0);
+            htile[3 * ti + 2] = std::min(TR, off[b + 1] - r0);
         }
     }
     hipMemcpyAsync(pk_rowinfo, hs, (size_t)3 * R * 4, hipMemcpyHostToDevice, st);
@@ -650,7 +654,7 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     // the LDS-staged tile kernel measured slower here (prefill 62.5 vs 45.4 ms at B=64):
     // kept behind GENIE_PACKED_TILE for A/B
     static const bool tile_opt = [] { const char* e = std::getenv("GENIE_PACKED_TILE"); return e && std::atoi(e); }();
-    const bool tiled = tile_opt && maxn0 <= ATTN_TILE_MAXK;
+    const bool tiled = !mfma_attn && tile_opt && maxn0 <= ATTN_TILE_MAXK;
     // the online-softmax kernel over the same tiles (GENIE_PACKED_FLASH=0: the per-row kernel)
     static const bool flash_opt = [] { const char* e = std::getenv("GENIE_PACKED_FLASH"); return !(e && std::atoi(e) == 0); }();
     const bool flash_tiles = flash_opt;
@@ -686,7 +690,11 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
         at.q = pk_Q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l];
         at.seq_stride = sstride; at.tmax = tmax; at.row_len = row_len; at.row_seq = row_seq;
         at.out = pk_O; at.ldo = 512; at.rows = R; at.scale = qk_scale;
-        if (tiled) {
+        if (mfma_attn) {   // 128-row tiles of one sequence on the split-fp16 MFMA
+            at.tiles = pk_tiles;
+            at.ntiles = ntiles;
+            attn_rows_mfma(at, 128, st);
+        } else if (tiled) {
             at.tiles = pk_tiles;
             at.ntiles = ntiles;
             attn_rows_tiled(at, st);

@@ -6,6 +6,7 @@
 // and t2s_stage_decoder_fp32.onnx (node indices cited per kernel).
 #include "common.h"
 #include "kernels.h"
+#include "prefill_attn.h"
 #include "sampler.h"
 #include <cstdio>
 #include <cstdlib>
@@ -1101,6 +1102,218 @@ __global__ __launch_bounds__(256) void k_attn_flash(AttnArgs a) {
     }
 }
 
+// Prefill attention on the f16 MFMA (stage#91-96 per head): a block = one head x
+// 32 NW query rows of one sequence, wave w owns rows 32 w .. 32 w + 31.  Operands are
+// split hi + lo into fp16 (three MFMAs per product, f32 accumulation: the dropped term
+// is ~2^-22 of each product, as in the split-activation GEMMs).  Per 64-key chunk:
+//   S^T = K Q^T  (A = the chunk's K rows, B = the wave's q rows): lane l holds the
+//                scores of query row l % 32 for 32 of the 64 keys, the lane l ^ 32 the
+//                other 32, so the online softmax (stage#95) needs one cross-lane step;
+//   O^T += V^T P^T  (B = the P values straight from the S^T accumulator registers, the
+//                16 keys of a k-step taken in the accumulator's key order and V^T read
+//                in that same order), so O^T's lane keeps its own query row and the
+//                running rescale stays in-lane.
+// K (scaled by s, as q) and V^T are staged per chunk in LDS as fp16 hi / lo planes,
+// double-buffered: chunk c + 1 is loaded into registers while chunk c is computed.
+// A block reads its head's K/V once per 32 NW rows (k_attn_flash: once per 16).  Used by
+// the packed (batched) prefill: 128-row tiles of one sequence.
+#define AM_KC 64
+#define AM_KR 40   // K plane row stride (halfs): 32 dims + pad
+#define AM_VR 72   // V^T plane row stride (halfs): 64 keys + pad
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
+    constexpr int NT = 64 * NW, ROWS = 32 * NW, NI = AM_KC * 8 / NT;   // float4 items per thread (K and V each)
+    __shared__ __attribute__((aligned(16))) _Float16 Kh[2][AM_KC * AM_KR];
+    __shared__ __attribute__((aligned(16))) _Float16 Kl[2][AM_KC * AM_KR];
+    __shared__ __attribute__((aligned(16))) _Float16 Vh[2][32 * AM_VR];
+    __shared__ __attribute__((aligned(16))) _Float16 Vl[2][32 * AM_VR];
+    __shared__ int rl[ROWS];
+    __shared__ int kmax_s;
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r32 = lane & 31, hs = lane >> 5;
+    int r0 = blockIdx.y * ROWS, nr = min(ROWS, a.rows - r0);
+    long kvbase = (long)h * a.tmax * 32;
+    if (a.tiles) {   // packed prefill: tile {sequence, first row, rows <= ROWS}
+        const int* tl = a.tiles + 3 * blockIdx.y;
+        kvbase += (long)tl[0] * a.seq_stride;
+        r0 = tl[1];
+        nr = tl[2];
+    }
+    const float sc = a.scale;
+    if (tid == 0) kmax_s = 0;
+    __syncthreads();
+    if (tid < ROWS) {
+        rl[tid] = tid < nr ? a.row_len[r0 + tid] : 0;
+        atomicMax(&kmax_s, rl[tid]);
+    }
+    __syncthreads();
+    const int kmax = kmax_s;
+    const int row = 32 * w + r32;                  // this lane's query row (of the block)
+    const int len = rl[row];
+    const bool wave_rows = 32 * w < nr;            // a wave past the tile's rows only stages
+    // q fragments (B of S^T): row `row`, dims 16 ks + 8 hs .. + 7, scaled by s
+    h16x8 qh[2], ql[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+        if (row < nr) {
+            const float* qp = a.q + (long)(r0 + row) * a.ldq + h * 32 + 16 * ks + 8 * hs;
+            x0 = *reinterpret_cast<const float4*>(qp);
+            x1 = *reinterpret_cast<const float4*>(qp + 4);
+        }
+        x0 = make_float4(x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc);
+        x1 = make_float4(x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc);
+        split8(x0, x1, qh[ks], ql[ks]);
+    }
+    const float* K = a.k + kvbase;
+    const float* V = a.v + kvbase;
+    float4 pk[NI], pv[NI];
+    auto fetch = [&](int k0) {   // item e: key e >> 3, dims 4 (e & 7) .. + 3 (rows past kmax: 0)
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int e = tid + NT * i, t = e >> 3, c = e & 7;
+            pk[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            pv[i] = pk[i];
+            if (k0 + t < kmax) {
+                pk[i] = *reinterpret_cast<const float4*>(K + (long)(k0 + t) * 32 + 4 * c);
+                pv[i] = *reinterpret_cast<const float4*>(V + (long)(k0 + t) * 32 + 4 * c);
+            }
+        }
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int e = tid + NT * i, t = e >> 3, c = e & 7;
+            const float kx[4] = {pk[i].x * sc, pk[i].y * sc, pk[i].z * sc, pk[i].w * sc};
+            const float vx[4] = {pv[i].x, pv[i].y, pv[i].z, pv[i].w};
+            _Float16 khi[4], klo[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                khi[j] = (_Float16)kx[j];
+                klo[j] = (_Float16)(kx[j] - (float)khi[j]);
+                const _Float16 vh = (_Float16)vx[j];
+                Vh[buf][(4 * c + j) * AM_VR + t] = vh;
+                Vl[buf][(4 * c + j) * AM_VR + t] = (_Float16)(vx[j] - (float)vh);
+            }
+            *reinterpret_cast<uint2*>(&Kh[buf][t * AM_KR + 4 * c]) = *reinterpret_cast<const uint2*>(khi);
+            *reinterpret_cast<uint2*>(&Kl[buf][t * AM_KR + 4 * c]) = *reinterpret_cast<const uint2*>(klo);
+        }
+    };
+    float m = -INFINITY, l = 0.f;
+    f32x16 o;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] = 0.f;
+    const int nch = (kmax + AM_KC - 1) / AM_KC;
+    if (nch > 0) {
+        fetch(0);
+        stage(0);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1, k0 = c * AM_KC;
+        if (c + 1 < nch) fetch(k0 + AM_KC);
+        if (wave_rows) {
+            // ---- S^T: keys 32 T + {8 (i / 4) + 4 hs + i % 4} of row `row` in s[T][i]
+            f32x16 s[2];
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) s[T][i] = 0.f;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const int off = (32 * T + r32) * AM_KR + 16 * ks + 8 * hs;
+                    const h16x8 ah = *reinterpret_cast<const h16x8*>(&Kh[buf][off]);
+                    const h16x8 al = *reinterpret_cast<const h16x8*>(&Kl[buf][off]);
+                    s[T] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[ks], s[T], 0, 0, 0);
+                    s[T] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[ks], s[T], 0, 0, 0);
+                    s[T] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[ks], s[T], 0, 0, 0);
+                }
+            }
+            // ---- online softmax of the row over the chunk (keys >= len: -inf)
+            float mc = -INFINITY;
+#pragma unroll
+            for (int T = 0; T < 2; ++T)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int key = k0 + 32 * T + 8 * (i >> 2) + 4 * hs + (i & 3);
+                    if (key >= len) s[T][i] = -INFINITY;
+                    mc = fmaxf(mc, s[T][i]);
+                }
+            mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+            const float mn = fmaxf(m, mc);
+            const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+            float ps = 0.f;
+#pragma unroll
+            for (int T = 0; T < 2; ++T)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float p = s[T][i] == -INFINITY ? 0.f : __expf(s[T][i] - mn);
+                    s[T][i] = p;
+                    ps += p;
+                }
+            ps += __shfl_xor(ps, 32, 64);
+            l = l * corr + ps;
+            m = mn;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[i] *= corr;
+            // ---- O^T += V^T P^T, k-step (T, g): keys 32 T + 16 g + {0..3, 8..11} (+4 for hs = 1)
+#pragma unroll
+            for (int T = 0; T < 2; ++T)
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    h16x8 ph, pl;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float p = s[T][8 * g + j];
+                        ph[j] = (_Float16)p;
+                        pl[j] = (_Float16)(p - (float)ph[j]);
+                    }
+                    const int kb = 32 * T + 16 * g + 4 * hs;
+                    const _Float16* vh = &Vh[buf][r32 * AM_VR + kb];
+                    const _Float16* vl = &Vl[buf][r32 * AM_VR + kb];
+                    h16x8 ah, al;
+                    const uint2 h0 = *reinterpret_cast<const uint2*>(vh), h1 = *reinterpret_cast<const uint2*>(vh + 8);
+                    const uint2 l0 = *reinterpret_cast<const uint2*>(vl), l1 = *reinterpret_cast<const uint2*>(vl + 8);
+                    ah = __builtin_bit_cast(h16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+                    al = __builtin_bit_cast(h16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+                    o = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ph, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, pl, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ph, o, 0, 0, 0);
+                }
+        }
+        if (c + 1 < nch) stage(buf ^ 1);
+        __syncthreads();
+    }
+    // ---- O^T lane: row `row`, dims 8 (i / 4) + 4 hs + i % 4
+    if (row < nr) {
+        float* dst = a.out + (long)(r0 + row) * a.ldo + h * 32 + 4 * hs;
+        const float rl_ = 1.f / l;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(dst + 8 * g) =
+                make_float4(o[4 * g] * rl_, o[4 * g + 1] * rl_, o[4 * g + 2] * rl_, o[4 * g + 3] * rl_);
+    }
+}
+
+// GENIE_ATTN_MFMA=0: the prefill attention on the f32 online-softmax kernel (A/B)
+bool attn_mfma_on() {
+    static const bool on = [] { const char* e = std::getenv("GENIE_ATTN_MFMA"); return !(e && std::atoi(e) == 0); }();
+    return on;
+}
+
+void attn_rows_mfma(const AttnArgs& a, int rows_per_block, hipStream_t s) {
+    if (a.tiles ? a.ntiles <= 0 : a.rows <= 0) return;
+    if (rows_per_block == 128) {
+        const dim3 grid(16, a.tiles ? a.ntiles : (a.rows + 127) / 128);
+        hipLaunchKernelGGL(k_attn_mfma<4>, grid, dim3(256), 0, s, a);
+    } else {
+        const dim3 grid(16, a.tiles ? a.ntiles : (a.rows + 63) / 64);
+        hipLaunchKernelGGL(k_attn_mfma<2>, grid, dim3(128), 0, s, a);
+    }
+}
+
+// (One sequence's prefill stays on k_attn_flash: at ~300 rows the MFMA kernel's 80
+// blocks of 64 rows were no faster -- prefill 2.00 vs 1.91 ms, profiles/r04q_prefill_attn.txt.)
 void attn_rows(const AttnArgs& a, hipStream_t s) {
     if (a.rows <= 0) return;
     static const bool flash = [] {
