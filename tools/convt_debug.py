@@ -49,3 +49,14 @@ for i in range(len(items)):
           float(np.abs(outs[i] - s1[i]).max()))
     if d.size:   # which output phase / region: samples per frame 640 (10 x 8 x 2 x 2 x 2)
         print("   frames", np.unique(d // 640)[:20], "sample%10", np.unique(d % 10), "n_frames", s1[i].size // 640)
+
+# repeat: the same lanes batch again (stale-state vs deterministic), then one lane (no concurrency)
+def cmp(tag, outs):
+    for i in range(len(items)):
+        d = np.nonzero(outs[i] != s1[i])[0]
+        print(f"{tag} item {i}: {d.size} differ", float(np.abs(outs[i] - s1[i]).max()) if d.size else 0.0)
+cmp("lanes again", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
+e.set_option("vits_lanes", 1)
+cmp("one lane", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
+e.set_option("vits_lanes", 4)
+cmp("lanes after one-lane", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
