@@ -64,3 +64,27 @@ def test_batch64_ragged_lengths(eng):
     wl = workloads.batch64(16, tag="b64r")
     out = eng.t2s_generate(_utts(wl), make_sampler())
     assert [o.size for o in out] == [it.tokens for it in wl.items]
+
+
+def test_packed_prefill_attention_matches_per_sequence_prefill(eng):
+    """The packed prefill's attention (k_attn_mfma: 128-row tiles on the split-fp16 MFMA)
+    against the per-sequence prefill (k_attn_flash, f32): the layer-23 K/V rows that every
+    earlier layer's attention feeds, for 8 ragged utterances of batch64 (one of them longer
+    than one 128-row tile by 200+ rows).  Bar: max |diff| <= 1e-4 x max |value| (split-fp16
+    operands keep ~22 bits of each product)."""
+    from genie_tts_amd import workloads
+    from genie_tts_amd.engine import make_sampler
+    wl = workloads.batch64()
+    utts = [u[:5] + (1,) for u in _utts(wl)[:8]]   # one loop step: the prefill's K/V, then the cache
+    sp = make_sampler(top_k=5, greedy=True)
+    kv = {}
+    for packed in (1, 0):
+        eng.set_option("packed", packed)
+        eng.t2s_generate(utts, sp)
+        kv[packed] = [[t.cpu().numpy() for t in eng.t2s_read_kv(23, seq=b)] for b in range(len(utts))]
+    eng.set_option("packed", 1)
+    for b in range(len(utts)):
+        for a, r in zip(kv[1][b], kv[0][b]):
+            assert a.shape == r.shape and a.shape[0] > 128
+            err = float(np.abs(a - r).max())
+            assert err <= 1e-4 * float(np.abs(r).max()), (b, err)
