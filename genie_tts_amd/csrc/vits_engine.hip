@@ -661,9 +661,10 @@ static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const fl
         ct.in_act = 1; ct.in_slope = 0.1f; ct.mode = CV_STORE;
         ct.phases = u; ct.w_phase_stride = (long)up.cout * up.cin * up.k;
         ct.seg = sg;
-        // GENIE_CONVT_F16=1: the upsample convs on the split-fp16 path (off by default: on
-        // several concurrent vocoder lanes one utterance per batch goes wrong in a 1-2 frame
-        // window, nondeterministically; one lane and single calls are exact -- r04u)
+        // GENIE_CONVT_F16=1: the upsample convs on the split-fp16 path.  Off by default: on
+        // concurrent vocoder lanes its four-way K-split tile corrupted 1-2 frame windows
+        // (r04u / r04w; launch_h now avoids that tile for polyphase convs, cause unknown), and
+        // it gains 1.3 ms of a 64-utterance vocoder pass
         static const bool convt_f16 = [] { const char* e = std::getenv("GENIE_CONVT_F16"); return e && std::atoi(e) != 0; }();
         if (tls_ovf && up.wh && convt_f16) {   // the split-fp16 path (polyphase weights, input-channel weight norm)
             ct.wh = up.wh; ct.wscale = up.wscale; ct.ovf = tls_ovf; ct.in_scale = up.in_scale;

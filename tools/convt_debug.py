@@ -60,3 +60,11 @@ e.set_option("vits_lanes", 1)
 cmp("one lane", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
 e.set_option("vits_lanes", 4)
 cmp("lanes after one-lane", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
+
+# host threading vs GPU concurrency: lanes issued by ONE host thread (vits_threads 0), 4 streams
+e.set_option("vits_threads", 0)
+for r in range(3):
+    cmp(f"4 lanes, one issuing thread, rep {r}", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
+e.set_option("vits_threads", 1)
+for r in range(2):
+    cmp(f"4 lanes, thread per lane, rep {r}", [o.cpu().numpy() for o in e.vits_decode_batch(items)])
