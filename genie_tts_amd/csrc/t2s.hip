@@ -1113,20 +1113,25 @@ __global__ __launch_bounds__(256) void k_attn_flash(AttnArgs a) {
 //                16 keys of a k-step taken in the accumulator's key order and V^T read
 //                in that same order), so O^T's lane keeps its own query row and the
 //                running rescale stays in-lane.
-// K (scaled by s, as q) and V^T are staged per chunk in LDS as fp16 hi / lo planes,
-// double-buffered: chunk c + 1 is loaded into registers while chunk c is computed.
+// K and V chunks arrive raw (f32) by LDS-DMA in a ring of AM_RING chunks, issued
+// AM_RING - 1 chunks ahead of use; each is then split into the fp16 hi / lo planes of K
+// (scaled by s, as q) and V^T that the MFMA fragments read.
 // A block reads its head's K/V once per 32 NW rows (k_attn_flash: once per 16).  Used by
 // the packed (batched) prefill: 128-row tiles of one sequence.
 #define AM_KC 64
 #define AM_KR 40   // K plane row stride (halfs): 32 dims + pad
 #define AM_VR 72   // V^T plane row stride (halfs): 64 keys + pad
+#define AM_RING 3
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
     constexpr int NT = 64 * NW, ROWS = 32 * NW, NI = AM_KC * 8 / NT;   // float4 items per thread (K and V each)
-    __shared__ __attribute__((aligned(16))) _Float16 Kh[2][AM_KC * AM_KR];
-    __shared__ __attribute__((aligned(16))) _Float16 Kl[2][AM_KC * AM_KR];
-    __shared__ __attribute__((aligned(16))) _Float16 Vh[2][32 * AM_VR];
-    __shared__ __attribute__((aligned(16))) _Float16 Vl[2][32 * AM_VR];
+    constexpr int DPW = 16 / NW;                                       // DMA instructions per wave per chunk
+    __shared__ __attribute__((aligned(16))) float Kr[AM_RING][AM_KC * 32];   // raw chunks (LDS-DMA ring)
+    __shared__ __attribute__((aligned(16))) float Vr[AM_RING][AM_KC * 32];
+    __shared__ __attribute__((aligned(16))) _Float16 Kh[AM_KC * AM_KR];
+    __shared__ __attribute__((aligned(16))) _Float16 Kl[AM_KC * AM_KR];
+    __shared__ __attribute__((aligned(16))) _Float16 Vh[32 * AM_VR];
+    __shared__ __attribute__((aligned(16))) _Float16 Vl[32 * AM_VR];
     __shared__ int rl[ROWS];
     __shared__ int kmax_s;
     const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1167,36 +1172,41 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
     }
     const float* K = a.k + kvbase;
     const float* V = a.v + kvbase;
-    float4 pk[NI], pv[NI];
-    auto fetch = [&](int k0) {   // item e: key e >> 3, dims 4 (e & 7) .. + 3 (rows past kmax: 0)
+    // chunk c -> ring slot c % AM_RING: DMA instruction j (8 keys x 32 dims, 1 KB) of K and of
+    // V by wave j % NW; keys past kmax read row 0 (in bounds; zeroed by the split)
+    auto dma = [&](int c) {
+        const int slot = c % AM_RING;
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int e = tid + NT * i, t = e >> 3, c = e & 7;
-            pk[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            pv[i] = pk[i];
-            if (k0 + t < kmax) {
-                pk[i] = *reinterpret_cast<const float4*>(K + (long)(k0 + t) * 32 + 4 * c);
-                pv[i] = *reinterpret_cast<const float4*>(V + (long)(k0 + t) * 32 + 4 * c);
-            }
+        for (int i = 0; i < 8 / NW; ++i) {
+            const int j = w + NW * i, key = AM_KC * c + 8 * j + (lane >> 3);
+            const long src = (long)(key < kmax ? key : 0) * 32 + 4 * (lane & 7);
+            gx3_dma(K + src, &Kr[slot][j * 256]);
+            gx3_dma(V + src, &Vr[slot][j * 256]);
         }
     };
-    auto stage = [&](int buf) {
+    // ring slot of chunk c -> the split planes (keys past kmax: 0)
+    auto split_chunk = [&](int c) {
+        const int slot = c % AM_RING, k0 = AM_KC * c;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int e = tid + NT * i, t = e >> 3, c = e & 7;
-            const float kx[4] = {pk[i].x * sc, pk[i].y * sc, pk[i].z * sc, pk[i].w * sc};
-            const float vx[4] = {pv[i].x, pv[i].y, pv[i].z, pv[i].w};
+            const int e = tid + NT * i, t = e >> 3, cc = e & 7;
+            const bool ok = k0 + t < kmax;
+            const float4 kv4 = *reinterpret_cast<const float4*>(&Kr[slot][t * 32 + 4 * cc]);
+            const float4 vv4 = *reinterpret_cast<const float4*>(&Vr[slot][t * 32 + 4 * cc]);
+            const float kx[4] = {ok ? kv4.x * sc : 0.f, ok ? kv4.y * sc : 0.f, ok ? kv4.z * sc : 0.f,
+                                 ok ? kv4.w * sc : 0.f};
+            const float vx[4] = {ok ? vv4.x : 0.f, ok ? vv4.y : 0.f, ok ? vv4.z : 0.f, ok ? vv4.w : 0.f};
             _Float16 khi[4], klo[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 khi[j] = (_Float16)kx[j];
                 klo[j] = (_Float16)(kx[j] - (float)khi[j]);
                 const _Float16 vh = (_Float16)vx[j];
-                Vh[buf][(4 * c + j) * AM_VR + t] = vh;
-                Vl[buf][(4 * c + j) * AM_VR + t] = (_Float16)(vx[j] - (float)vh);
+                Vh[(4 * cc + j) * AM_VR + t] = vh;
+                Vl[(4 * cc + j) * AM_VR + t] = (_Float16)(vx[j] - (float)vh);
             }
-            *reinterpret_cast<uint2*>(&Kh[buf][t * AM_KR + 4 * c]) = *reinterpret_cast<const uint2*>(khi);
-            *reinterpret_cast<uint2*>(&Kl[buf][t * AM_KR + 4 * c]) = *reinterpret_cast<const uint2*>(klo);
+            *reinterpret_cast<uint2*>(&Kh[t * AM_KR + 4 * cc]) = *reinterpret_cast<const uint2*>(khi);
+            *reinterpret_cast<uint2*>(&Kl[t * AM_KR + 4 * cc]) = *reinterpret_cast<const uint2*>(klo);
         }
     };
     float m = -INFINITY, l = 0.f;
@@ -1205,13 +1215,14 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
     for (int i = 0; i < 16; ++i) o[i] = 0.f;
     const int nch = (kmax + AM_KC - 1) / AM_KC;
     if (nch > 0) {
-        fetch(0);
-        stage(0);
+        for (int c = 0; c < AM_RING && c < nch; ++c) dma(c);
+        gx3_wait<DPW>(min(AM_RING, nch) - 1);      // chunk 0 (this wave's part) landed
+        __syncthreads();
+        split_chunk(0);
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
-        const int buf = c & 1, k0 = c * AM_KC;
-        if (c + 1 < nch) fetch(k0 + AM_KC);
+        const int k0 = c * AM_KC;
         if (wave_rows) {
             // ---- S^T: keys 32 T + {8 (i / 4) + 4 hs + i % 4} of row `row` in s[T][i]
             f32x16 s[2];
@@ -1222,8 +1233,8 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
 #pragma unroll
                 for (int ks = 0; ks < 2; ++ks) {
                     const int off = (32 * T + r32) * AM_KR + 16 * ks + 8 * hs;
-                    const h16x8 ah = *reinterpret_cast<const h16x8*>(&Kh[buf][off]);
-                    const h16x8 al = *reinterpret_cast<const h16x8*>(&Kl[buf][off]);
+                    const h16x8 ah = *reinterpret_cast<const h16x8*>(&Kh[off]);
+                    const h16x8 al = *reinterpret_cast<const h16x8*>(&Kl[off]);
                     s[T] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[ks], s[T], 0, 0, 0);
                     s[T] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[ks], s[T], 0, 0, 0);
                     s[T] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[ks], s[T], 0, 0, 0);
@@ -1269,8 +1280,8 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
                         pl[j] = (_Float16)(p - (float)ph[j]);
                     }
                     const int kb = 32 * T + 16 * g + 4 * hs;
-                    const _Float16* vh = &Vh[buf][r32 * AM_VR + kb];
-                    const _Float16* vl = &Vl[buf][r32 * AM_VR + kb];
+                    const _Float16* vh = &Vh[r32 * AM_VR + kb];
+                    const _Float16* vl = &Vl[r32 * AM_VR + kb];
                     h16x8 ah, al;
                     const uint2 h0 = *reinterpret_cast<const uint2*>(vh), h1 = *reinterpret_cast<const uint2*>(vh + 8);
                     const uint2 l0 = *reinterpret_cast<const uint2*>(vl), l1 = *reinterpret_cast<const uint2*>(vl + 8);
@@ -1281,8 +1292,15 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
                     o = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ph, o, 0, 0, 0);
                 }
         }
-        if (c + 1 < nch) stage(buf ^ 1);
-        __syncthreads();
+        if (c + 1 < nch) {
+            // chunk c + 1 landed (this wave's part; chunk c + 2 may stay in flight), then every
+            // wave's part and every wave done with the split planes of chunk c
+            gx3_wait<DPW>(min(c + AM_RING - 1, nch - 1) - (c + 1));
+            __syncthreads();
+            if (c + AM_RING < nch) dma(c + AM_RING);   // into chunk c's slot (split last round)
+            split_chunk(c + 1);
+            __syncthreads();
+        }
     }
     // ---- O^T lane: row `row`, dims 8 (i / 4) + 4 hs + i % 4
     if (row < nr) {
