@@ -30,6 +30,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import os
+import threading
 from collections import OrderedDict
 from typing import AsyncIterator, Callable, Dict, List, Optional, Sequence, Union
 
@@ -51,6 +52,12 @@ _clip_cache: "OrderedDict[str, ReferenceAudio]" = OrderedDict()   # ReferenceAud
 _g2p: Optional[Callable] = None
 _ssl_extractor: Optional[Callable] = None
 _sv_extractor: Optional[Callable] = None
+# The player's session stop (TTSPlayer._stop_event, Core/TTSPlayer.py:208-222): set by stop(),
+# cleared when a tts / tts_async session starts (TTSPlayer.start_session, :175).  A stopped
+# session synthesizes no further sentence and saves nothing; tts_client.stop_event (GENIE's)
+# is the per-sentence word that abandons a running decode, cleared per sentence as the
+# worker loop does (:86).
+_session_stop = threading.Event()
 
 
 def _norm_language(language: Optional[str]) -> str:
@@ -231,7 +238,12 @@ def _synthesize(character_name: str, sentence, text_bert=None, sampler=None) -> 
         raise ValueError(f"character '{character_name}' is not loaded")
     ref = _reference_audios[character_name]
     _ensure_sv_emb(m, ref)
-    tts_client.stop_event.clear()
+    if _session_stop.is_set():
+        return None
+    tts_client.stop_event.clear()            # TTSPlayer.py:86, per sentence
+    if _session_stop.is_set():               # a stop() between the check and the clear
+        tts_client.stop_event.set()
+        return None
     return tts_client.tts(sentence, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER, m.VITS,
                           m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p, sampler=sampler)
 
@@ -246,7 +258,12 @@ def _synthesize_all(character_name: str, sentences: List, text_bert=None, sample
         raise ValueError(f"character '{character_name}' is not loaded")
     ref = _reference_audios[character_name]
     _ensure_sv_emb(m, ref)
+    if _session_stop.is_set():
+        return []
     tts_client.stop_event.clear()
+    if _session_stop.is_set():
+        tts_client.stop_event.set()
+        return []
     return list(tts_client.tts_stream(sentences, ref, m.T2S_ENCODER, m.T2S_FIRST_STAGE_DECODER, m.T2S_STAGE_DECODER,
                                       m.VITS, m.PROMPT_ENCODER, m.LANGUAGE, text_bert=text_bert, g2p=_g2p,
                                       sampler=sampler, vocoder_cus=VOCODER_CUS))
@@ -269,9 +286,12 @@ def tts(character_name: str, text: Union[str, Sequence[int], np.ndarray], play: 
     if character_name not in _reference_audios:
         logger.error("Please call 'set_reference_audio' first to set the reference audio.")
         return None
+    _session_stop.clear()                    # TTSPlayer.start_session
     chunks = [c for c in _synthesize_all(character_name, _sentences(text, split_sentence), text_bert, sampler)
               if c is not None]
     audio = np.concatenate(chunks) if chunks else np.zeros(0, np.float32)
+    if _session_stop.is_set():               # stopped: the session's STREAM_END (and its save) never runs
+        return audio
     if save_path:
         A.write_wav(os.fspath(save_path), audio, SAMPLE_RATE)
     if play:
@@ -286,9 +306,16 @@ async def tts_async(character_name: str, text: str, play: bool = False, split_se
     if character_name not in _reference_audios:
         raise ValueError("Please call 'set_reference_audio' first to set the reference audio.")
     loop = asyncio.get_running_loop()
+    _session_stop.clear()                    # TTSPlayer.start_session
     chunks = []
     for s in _sentences(text, split_sentence):
+        if _session_stop.is_set():
+            return
         audio = await loop.run_in_executor(None, _synthesize, character_name, s)
+        if _session_stop.is_set():
+            # stop() during the sentence: the reference's worker sends chunk_callback(None) and
+            # the iterator ends without that chunk (TTSPlayer.py:109-114, Internal.py:258-262)
+            return
         if audio is None:
             continue
         chunks.append(audio)
@@ -304,4 +331,9 @@ def wait_for_playback_done() -> None:
 
 
 def stop() -> None:
+    """TTSPlayer.stop (Core/TTSPlayer.py:208-222): the running sentence's decode is abandoned
+    (GENIE.stop_event -> the engines' stop word) and the session ends: tts returns what was
+    synthesized before the stop without saving, a tts_async iterator ends.  The next
+    tts / tts_async call starts a new session."""
+    _session_stop.set()
     tts_client.stop_event.set()

@@ -18,8 +18,15 @@ ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIB_DIR, "libgenie_engine.so")
 ARCH = os.environ.get("GENIE_OFFLOAD_ARCH", "gfx950")
+# No packed-FP32 VALU ops (v_pk_{add,mul,fma,mov}_*32) in the device code.  On gfx950 a packed op
+# whose LOW result reads the HIGH half of a source pair through op_sel (v_pk_mul_f32 d, a, b
+# op_sel:[0,1]) returned 0 in lanes 48-63 while MFMA-heavy waves ran beside it: the vocoder's
+# nondeterministic 1-2 frame errors of r04 (profiles/r05_convt_race.txt; tools/pk_opsel_probe.hip
+# reproduces it outside the engine).  hipcc forms such ops from ordinary float pairs, so the
+# feature is off for every kernel, and tests/test_isa_audit.py checks the built library.
+NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
-         "-Wno-unused-value", "-munsafe-fp-atomics"]
+         "-Wno-unused-value", "-munsafe-fp-atomics", *NO_PACKED_FP32]
 
 
 def _hipcc() -> str:

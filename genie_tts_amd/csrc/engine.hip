@@ -761,6 +761,7 @@ SampleArgs gsv_engine::sampler_args(const gsv_sampler* sp, int B) {
     sa.force_b = forceb;
     sa.prefill = 0;
     sa.stop_req = stop_word;
+    sa.stop_hit = stop_word + 1;
     return sa;
 }
 
@@ -909,6 +910,7 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     const int limit = loop_limit > 0 ? loop_limit : sp->force_steps > 0 ? sp->force_steps : sp->max_steps;
     if (stop_requested()) return stopped_error();
     if (allow_persist && use_persist && persist_family(B) && persist_admit()) return decode_persistent(B, sp, st);
+    __atomic_store_n(stop_word + 1, 0, __ATOMIC_RELEASE);   // no kernel of this engine runs: the loops are synchronous
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
     hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
@@ -956,7 +958,8 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
         }
     }
     if (hipStreamSynchronize(st) != hipSuccess) return set_error(GSV_E_HIP, "decode sync");
-    if (stop_requested()) return stopped_error();
+    // the word itself, or a sampler that ended sequences on it (the word may be cleared since)
+    if (stop_requested() || __atomic_load_n(stop_word + 1, __ATOMIC_ACQUIRE) != 0) return stopped_error();
     if (probed) {
         // one sample per decode loop: the probed step's layer-`probe_layer` FFN launch
         float ms = 0.f;
@@ -1892,10 +1895,14 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->sv_f16 = value != 0;
     } else if (n == "sv_f16_limit") {   // tests: force the f32 re-run (0: the fp16 range)
         eng->sv_f16_limit = value > 0 ? (float)value : 65000.f;
-    } else if (n == "convh") {   // a queued or pending vocoder call finishes under the mode it began with
+    } else if (n == "convh" || n == "convt_f16" || n == "convh_tile") {
+        // a queued or pending vocoder call finishes under the mode it began with
+        if (n == "convh_tile" && (value < 0 || value > 4)) return set_error(GSV_E_ARG, "convh_tile: 0..4");
         if (int r = eng->vits_wait(nullptr)) return r;
         if (int r = eng->vits_batch_finish(nullptr)) return r;
-        eng->use_convh = value != 0;
+        if (n == "convh") eng->use_convh = value != 0;
+        else if (n == "convt_f16") eng->convt_f16 = value != 0;
+        else eng->convh_tile = value;
     } else if (n == "ptrace") {
         if (value && !eng->ptrace) {
             if (hipMalloc(&eng->ptrace, (size_t)256 * 16 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");

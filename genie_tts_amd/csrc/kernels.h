@@ -239,6 +239,8 @@ struct SampleArgs {
     long long* acc_zero; long acc_n;   // per-sequence fixed-point accumulators zeroed for the next step
     int threads;                       // 256 (default) or 512: block size of the sampler body
     const int* stop_req;               // host-mapped stop word (gsv_request_stop): set -> the sequence finishes
+    int* stop_hit;                     // host-mapped, or null: set to 1 when the stop word ended a sequence, so the
+                                       // host reports STOPPED even if the word is cleared before it looks
 };
 void sample_tokens(const SampleArgs& a, hipStream_t s);
 

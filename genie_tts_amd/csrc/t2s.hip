@@ -1585,7 +1585,10 @@ __global__ __launch_bounds__(NT) void k_sample(SampleArgs a) {
     if (tid == 0) {
         if (a.ablate == 3) { a.y[(long)b * a.ldy + st_ny] = raw; a.ny[b] = st_ny + 1; return; }
         sample_commit(a, b, tok, raw, st_ny, st_steps, st_kv, seen_s);
-        if (st_stop) a.done[b] = 1;   // gsv_request_stop: the sequence ends here (the host returns STOPPED)
+        if (st_stop) {   // gsv_request_stop: the sequence ends here (the host returns STOPPED)
+            a.done[b] = 1;
+            if (a.stop_hit) __hip_atomic_store(a.stop_hit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 

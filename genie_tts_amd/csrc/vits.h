@@ -64,6 +64,9 @@ struct ConvArgs {
     // reaches into a gap reads the zero padding a single-utterance call sees);
     // CV_VEC / CV_RESID_VEC read vec + seg[tp] * vec_sstride
     const int* seg; long vec_sstride;
+    // f16-split path: 0 = the cost model's tile; 1..4 = tile candidate 0..3 of launch_h (option
+    // "convh_tile", tests)
+    int tile_force;
 };
 void conv1d(const ConvArgs& a, hipStream_t s);
 // seg[t] for t < n: i with off[i] * f <= t < (off[i] + len[i]) * f, else -1 (off ascending)

@@ -254,10 +254,6 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
     int best = -1;
     double best_cost = 1e30;
     for (int i = 0; i < 4; ++i) {
-        // a ConvTranspose's polyphase form never takes the four-way K split: on it, concurrent
-        // vocoder lanes gave nondeterministic 1-2 frame errors that no other tile shows
-        // (profiles/r04w_convt_tiles.txt)
-        if (a.phases > 1 && cands[i].ks == 4) continue;
         const int bm = 32 * cands[i].wm, bn = 64 * cands[i].wn;
         const long blocks = (long)((a.n_t + bn - 1) / bn) * ((a.Cout + bm - 1) / bm) * (a.phases > 1 ? a.phases : 1);
         const long rounds = (blocks + 511) / 512;
@@ -266,6 +262,7 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
     }
     static const int forced = [] { const char* e = std::getenv("GENIE_CONVH_CFG"); return e ? std::atoi(e) : -1; }();
     if (forced >= 0 && forced < 4) best = forced;
+    if (a.tile_force >= 1 && a.tile_force <= 4) best = a.tile_force - 1;
     const Cand c = cands[best];
     const dim3 grid((a.n_t + 64 * c.wn - 1) / (64 * c.wn), (a.Cout + 32 * c.wm - 1) / (32 * c.wm),
                     a.phases > 1 ? a.phases : 1);

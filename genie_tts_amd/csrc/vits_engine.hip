@@ -321,6 +321,13 @@ int gsv_engine::finalize_prompt_encoder() {
 static thread_local float* tls_splitk = nullptr;
 static thread_local long tls_splitk_cap = 0;
 static thread_local int* tls_ovf = nullptr;   // set while the f16-split MRF path is enabled
+static thread_local int tls_convh_tile = 0;    // the running engine's option "convh_tile"
+static thread_local bool tls_convt_f16 = false;   // ... and "convt_f16" (the ConvTransposes on the split path)
+// The per-pass thread-local state of one vocoder pass (split-fp16 flag word, tile, ConvT path).
+struct ConvhScope {
+    ConvhScope(int* ovf, int tile, bool convt) { tls_ovf = ovf; tls_convh_tile = tile; tls_convt_f16 = convt; }
+    ~ConvhScope() { tls_ovf = nullptr; tls_convh_tile = 0; tls_convt_f16 = false; }
+};
 struct SplitkScope {
     SplitkScope(float* p, long cap) { tls_splitk = p; tls_splitk_cap = cap; }
     ~SplitkScope() { tls_splitk = nullptr; tls_splitk_cap = 0; }
@@ -337,6 +344,7 @@ static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode
     a.out = out; a.o_cs = T; a.o_ts = 1; a.n_t = T; a.o_tstride = 1; a.o_toff = 0; a.o_len = T;
     a.mode = mode; a.r_cs = T; a.r_ts = 1;
     a.phases = 1;
+    a.tile_force = tls_convh_tile;
     if (tls_ovf && c.wh) { a.wh = c.wh; a.wscale = c.wscale; a.ovf = tls_ovf; }
     return a;
 }
@@ -661,12 +669,8 @@ static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const fl
         ct.in_act = 1; ct.in_slope = 0.1f; ct.mode = CV_STORE;
         ct.phases = u; ct.w_phase_stride = (long)up.cout * up.cin * up.k;
         ct.seg = sg;
-        // GENIE_CONVT_F16=1: the upsample convs on the split-fp16 path.  Off by default: on
-        // concurrent vocoder lanes its four-way K-split tile corrupted 1-2 frame windows
-        // (r04u / r04w; launch_h now avoids that tile for polyphase convs, cause unknown), and
-        // it gains 1.3 ms of a 64-utterance vocoder pass
-        static const bool convt_f16 = [] { const char* e = std::getenv("GENIE_CONVT_F16"); return e && std::atoi(e) != 0; }();
-        if (tls_ovf && up.wh && convt_f16) {   // the split-fp16 path (polyphase weights, input-channel weight norm)
+        ct.tile_force = tls_convh_tile;
+        if (tls_ovf && up.wh && tls_convt_f16) {   // the split-fp16 path (polyphase weights, input-channel weight norm)
             ct.wh = up.wh; ct.wscale = up.wscale; ct.ovf = tls_ovf; ct.in_scale = up.in_scale;
             ct.wh_phase_stride = (long)up.cout * up.k * up.cin;
         }
@@ -723,8 +727,7 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     if (2 * G > MHA_MAXK_HOST || n_text > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, W, 2 * G, n_text, version == GSV_V2PP ? 0 : n_audio)) return r;
     SplitkScope sk(W.splitk, W.splitk_cap);
-    tls_ovf = ovf;
-    struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
+    ConvhScope cs(ovf, convh_tile, convt_f16);
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timed) hipEventRecord(ev[4], s);
     if (int r = vits_front(W, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
@@ -1048,8 +1051,7 @@ int gsv_engine::seg_front(hipStream_t st) {
 // path, flagging an fp16-range input in sgb.ovf).
 int gsv_engine::seg_generate(hipStream_t st, bool f16) {
     SegBatch& B = sgb;
-    tls_ovf = f16 ? B.ovf : nullptr;
-    struct OvfReset { ~OvfReset() { tls_ovf = nullptr; } } ovf_reset;
+    ConvhScope cs(f16 ? B.ovf : nullptr, convh_tile, convt_f16);
     const int* seg[6] = {B.seg[0], B.seg[1], B.seg[2], B.seg[3], B.seg[4], B.seg[5]};
     float* const gb[5] = {B.g[0], B.g[1], B.g[2], B.g[3], B.g[4]};
     vits_generator(vits, gb, B.z, B.T, B.dcond, vits.upc, seg, B.audio, st);
@@ -1082,6 +1084,12 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     }
     if (!vfork && hipEventCreateWithFlags(&vfork, hipEventDisableTiming) != hipSuccess)
         return set_error(GSV_E_HIP, "vocoder fork event");
+    // Stream s resets buffers the previous batch may still read on the lanes (the flags,
+    // sgb's offsets / segment tables / z, the packed front's tables): order it after that
+    // batch's lane work and generator.  vits_batch_finish joined the issuing threads, so
+    // the events are recorded (an event never recorded is a no-op wait).
+    for (const VitsLane& L : vlanes) hipStreamWaitEvent(s, L.join, 0);
+    if (sgb.done) hipStreamWaitEvent(s, sgb.done, 0);
     if (n > vflag_cap) {
         if (vflags) hipFree(vflags);
         if (vflags_host) hipHostFree(vflags_host);

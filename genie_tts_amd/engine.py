@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -38,9 +39,13 @@ class EngineStopped(EngineError):
     loop returns None for the sentence then (Inference.py:96-97)."""
 
 
-# Every live engine, so one stop request reaches them all (GENIE.stop_event is process-wide
-# in the reference, Core/Inference.py:13-14), and the current request state for new engines.
+# Every live engine, so one stop request reaches them all, and the current request state for
+# new engines.  The scope is the process, as in the reference: GENIE.stop_event belongs to the
+# module-level tts_client (Core/Inference.py:13-14, 112) that every character shares, so a
+# stop() ends the synthesis of every character.  _engines_lock orders registration against
+# a stop request arriving from another thread.
 _engines: "weakref.WeakSet" = weakref.WeakSet()
+_engines_lock = threading.Lock()
 _stop_on = False
 
 
@@ -48,10 +53,12 @@ def request_stop_all(on: bool) -> None:
     """Set (or clear) the stop word of every engine of this process (gsv_request_stop).
     Writes one host word per engine: safe from any thread while a generate runs."""
     global _stop_on
-    _stop_on = bool(on)
-    for e in list(_engines):
-        if getattr(e, "h", None):
-            lib().gsv_request_stop(e.h, int(on))
+    with _engines_lock:
+        _stop_on = bool(on)
+        live = list(_engines)
+        for e in live:
+            if getattr(e, "h", None):
+                lib().gsv_request_stop(e.h, int(on))
 
 
 class Utt(ctypes.Structure):
@@ -269,9 +276,10 @@ class Engine:
             self._set("pe.div_term", np.asarray(pe_div_term, np.float32))
         _check(lib().gsv_finalize_weights(self.h), "gsv_finalize_weights")
         self.dev = torch.device("cuda", device)
-        _engines.add(self)
-        if _stop_on:
-            lib().gsv_request_stop(self.h, 1)
+        with _engines_lock:
+            _engines.add(self)
+            if _stop_on:
+                lib().gsv_request_stop(self.h, 1)
 
     def request_stop(self, on: bool = True):
         """gsv_request_stop: while set, T2S generates raise EngineStopped (a running decode

@@ -35,9 +35,10 @@ MAX_STEPS = 500          # Inference.py:95
 @dataclass
 class ReferenceAudio:
     """Reference-audio features (the fields GENIE.tts reads from the reference's
-    ReferenceAudio, src/genie_tts/Audio/ReferenceAudio.py:28-76).  Extraction from a
-    wav (soxr resampling, CN-HuBERT, SV model) is SURVEY §8(f) and not part of
-    this path: supply the features."""
+    ReferenceAudio, src/genie_tts/Audio/ReferenceAudio.py:28-76).  api.set_reference_audio
+    fills them from a clip: audio.py reads and resamples it (a polyphase restatement of
+    soxr HQ), CN-HuBERT (gsv_hubert) gives ssl_content and, for V2ProPlus, the SV model
+    (gsv_sv) gives sv_emb -- both on the engine; or the caller supplies them."""
     phonemes_seq: np.ndarray             # i64 [1, R]
     text_bert: np.ndarray                # f32 [R, 1024]
     audio_32k: np.ndarray                # f32 [1, N32]
@@ -143,6 +144,8 @@ class GENIE:
         eng = _engine_of(encoder, first_stage_decoder, stage_decoder, vocoder)
         if eng is None or vocoder_cus <= 0 or len(texts) < 2:
             for t in texts:
+                if self.stop_event.is_set():
+                    return
                 yield self.tts(t, prompt_audio, encoder, first_stage_decoder, stage_decoder, vocoder, prompt_encoder,
                                language, text_bert, g2p, sampler)
             return

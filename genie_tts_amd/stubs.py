@@ -1,6 +1,8 @@
-"""Deterministic stand-ins for the components outside the engine (SURVEY §8:
-G2P + RoBERTa BERT features, CN-HuBERT), for benchmarks and tests only -- the
-product path uses them only when a caller configures them explicitly
+"""Deterministic stand-ins for benchmarks and tests: a G2P (outside the engine, SURVEY
+§8: out of scope) and SSL features in place of a real clip's CN-HuBERT output (the
+engine runs CN-HuBERT itself, gsv_hubert, once weights are loaded; the benchmarks and
+the server's --ssl option use this stand-in instead so they need no HuBERT weights).
+The product path uses them only when a caller configures them explicitly
 (api.set_g2p / set_ssl_extractor, server --g2p/--ssl).
 
 toy_g2p maps each character to two Japanese phone ids (a 20-character sentence

@@ -312,13 +312,14 @@ int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout,
 int gsv_debug_conv1d_h(const float* x, int cin, int tin, const void* wh, const float* scale, int cout,
                        int k, int dil, int pad, const float* bias, float* out, int tout, int in_act,
                        float slope, int* ovf, void* stream);
+/* Phase timestamps (100 MHz) of the per-step-graph decode kernels (t2s_decode.hip:
+ * the fp16-range re-run / timeout / B > 64 path, not the persistent kernels) of
+ * layer 12, last step run: [kernel: QKV GEMV, attention, FFN][block 0..255][slot
+ * 0..7]; needs GENIE_KTRACE=1 in the environment at gsv_finalize_weights. */
+int gsv_debug_ktrace(gsv_engine* eng, uint64_t* host, int n);
 /* Run the decode sampler kernel once on logits (device [B][1025]) with the
  * token-presence bitmaps seen (device u32 [B][33]) at loop step `step`
  * (Philox counter); tokens (device i64 [B]) and stop flags (device u8 [B]). */
-/* Phase timestamps (100 MHz) of the decode kernels of layer 12, last step run:
- * [kernel: QKV GEMV, attention, FFN][block 0..255][slot 0..7]; needs
- * GENIE_KTRACE=1 in the environment at gsv_finalize_weights. */
-int gsv_debug_ktrace(gsv_engine* eng, uint64_t* host, int n);
 int gsv_debug_sample(const float* logits, const uint32_t* seen, int B, const gsv_sampler* s,
                      int step, int64_t* tokens, uint8_t* stop, void* stream);
 

@@ -85,3 +85,73 @@ def test_set_reference_audio_bookkeeping(tmp_path):
     with pytest.raises(ValueError):
         api.set_reference_audio("f", p, "x", "klingon", phonemes_seq=[3])
     api.clear_reference_audio_cache()
+
+
+def _fake_session(monkeypatch, stop_at=None, calls=None):
+    """api over a stand-in GENIE.tts: sentence i returns a constant chunk of value i + 1;
+    with stop_at = i, stop() arrives while sentence i is synthesized (the stop word is then
+    set, and the reference's GENIE.tts returns None, Inference.py:96-97)."""
+    from types import SimpleNamespace
+    from genie_tts_amd import api
+    model = SimpleNamespace(T2S_ENCODER=None, T2S_FIRST_STAGE_DECODER=None, T2S_STAGE_DECODER=None, VITS=None,
+                            PROMPT_ENCODER=None, LANGUAGE="Japanese")
+    monkeypatch.setattr(api.model_manager, "get", lambda name: model)
+    monkeypatch.setitem(api._reference_audios, "stop-c", SimpleNamespace(sv_emb=None))
+
+    def fake_tts(sentence, ref, *a, **k):
+        i = int(np.asarray(sentence).reshape(-1)[0])
+        if calls is not None:
+            calls.append(i)
+        if stop_at is not None and i == stop_at:
+            api.stop()
+        if api.tts_client.stop_event.is_set():
+            return None
+        return np.full(4, 0.01 * (i + 1), np.float32)
+
+    monkeypatch.setattr(api.tts_client, "tts", fake_tts)
+    return api
+
+
+def _run_async(api, **kw):
+    import asyncio
+
+    async def go():
+        return [c async for c in api.tts_async("stop-c", None, **kw)]
+
+    return asyncio.run(go())
+
+
+def test_stop_ends_a_tts_async_session(monkeypatch, tmp_path):
+    """TTSPlayer.stop (Core/TTSPlayer.py:208-222): stop() during sentence 2 of a 4-sentence
+    tts_async ends the iterator with no further chunk (the worker's chunk_callback(None),
+    TTSPlayer.py:109-114 -> Internal.py:258-262) and saves nothing; the next session
+    synthesizes every sentence again."""
+    calls = []
+    api = _fake_session(monkeypatch, stop_at=1, calls=calls)
+    monkeypatch.setattr(api, "_sentences", lambda text, split: [np.array([i]) for i in range(4)])
+    wav = tmp_path / "s.wav"
+    got = _run_async(api, save_path=str(wav))
+    assert len(got) == 1 and calls == [0, 1] and not wav.exists()
+    assert np.frombuffer(got[0], np.int16)[0] == int(0.01 * 32767)
+    calls.clear()
+    monkeypatch.setattr(api.tts_client, "tts", _fake_session(monkeypatch, calls=calls).tts_client.tts)
+    again = _run_async(api, save_path=str(wav))
+    assert len(again) == 4 and calls == [0, 1, 2, 3] and wav.exists()
+
+
+def test_stop_ends_a_tts_session(monkeypatch, tmp_path):
+    """api.tts: the sentences before the stop are returned, none after it, nothing is saved;
+    a stop() issued before a session does not leak into it."""
+    calls = []
+    api = _fake_session(monkeypatch, stop_at=2, calls=calls)
+    monkeypatch.setattr(api, "_sentences", lambda text, split: [np.array([i]) for i in range(5)])
+    monkeypatch.setattr(api, "_synthesize_all",
+                        lambda name, ss, tb, sp: [api._synthesize(name, s, tb, sp) for s in ss])
+    wav = tmp_path / "t.wav"
+    out = api.tts("stop-c", None, save_path=str(wav))
+    assert calls == [0, 1, 2] and out.shape == (8,) and not wav.exists()
+    calls.clear()
+    api.stop()                                  # between sessions
+    api2 = _fake_session(monkeypatch, calls=calls)
+    out = api2.tts("stop-c", None, save_path=str(wav))
+    assert calls == [0, 1, 2, 3, 4] and out.shape == (20,) and wav.exists()

@@ -227,6 +227,42 @@ def test_vits_batch_lanes_match_single(setup, seg):
         assert float(np.sqrt(np.mean((outs[2].cpu().numpy() - ref) ** 2))) <= RMS_TOL
 
 
+def test_convt_split_tile_ks4_on_concurrent_lanes(setup):
+    """r04's nondeterminism, pinned: the upsample ConvTransposes on the split-fp16 path with
+    every k_conv_h forced to the four-way K-split tile (1,1,4) -- the tile whose polyphase
+    instance hipcc built with an op_sel'd v_pk_mul_f32 that gfx950 corrupted beside MFMA
+    work (build.py, tests/test_isa_audit.py).  Six utterances on four concurrent lanes,
+    ten batches: every utterance equals its single call bit for bit (r04u: 5 of 60 wrong)."""
+    ver, e, vm, _ = setup
+    kw = _cond(ver)
+    items = []
+    for i, (G, S) in enumerate([(20, 12), (33, 25), (8, 9), (47, 31), (26, 18), (40, 40)]):
+        txt = synth.synth_phones(S, f"vk{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (5 + i) + 7 * i) % 1024).reshape(1, 1, G)
+        it = dict(text_seq=txt, pred_semantic=sem, **kw)
+        if i % 2:
+            it["noise_seed"] = 2000 + i
+        items.append(it)
+    e.set_option("convt_f16", 1)
+    e.set_option("convh_tile", 3)
+    try:
+        singles = [e.vits_decode(it["text_seq"], it["pred_semantic"], noise_seed=it.get("noise_seed"),
+                                 **kw).cpu().numpy() for it in items]
+        e.set_option("seg_vocoder", 0)
+        wrong = []
+        for rep in range(10):
+            outs = e.vits_decode_batch(items)
+            wrong += [(rep, i) for i, (o, s1) in enumerate(zip(outs, singles))
+                      if not np.array_equal(o.cpu().numpy(), s1)]
+    finally:
+        e.set_option("seg_vocoder", 1)
+        e.set_option("convh_tile", 0)
+    assert not wrong, f"lanes differ from single calls: {wrong}"
+    # and the forced tile is the same function as the cost model's tiles (oracle bar)
+    ref = vm(items[2]["text_seq"], items[2]["pred_semantic"], **kw).numpy().reshape(-1)
+    assert float(np.sqrt(np.mean((singles[2] - ref) ** 2))) <= RMS_TOL
+
+
 def test_vits_batch_async_beside_t2s(setup):
     """gsv_vits_decode_batch_async: the lanes run while a batched T2S generate is issued
     on the engine stream (the pipelined batch mode); audio equals the joined batch call
