@@ -124,7 +124,7 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
     const size_t need = (size_t)N * (1024 * 4 + 3072 + 4096) + (size_t)n_out + 3 * (size_t)N + 64 +
                         (size_t)zmax * N * 1024;
     if (need > bert.ws_floats) {
-        if (bert.ws) hipFree(bert.ws);
+        retire(bert.ws);
         bert.ws = nullptr;
         bert.ws_floats = 0;
         if (hipMalloc(&bert.ws, need * 4) != hipSuccess) return set_error(GSV_E_HIP, "RoBERTa workspace");

@@ -37,6 +37,10 @@ int set_error(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+
+int hip_error(const std::string& what, hipError_t e) {
+    return set_error(GSV_E_HIP, what + ": " + hipGetErrorName(e));
+}
 }  // namespace gsv
 
 // ------------------------------------------------------------ allocation
@@ -113,6 +117,17 @@ gsv_engine::~gsv_engine() {
     for (auto& e : ev) if (e) hipEventDestroy(e);
     if (ev_in) hipEventDestroy(ev_in);
     if (ev_out) hipEventDestroy(ev_out);
+    for (void* p : retired) hipFree(p);
+    for (void* p : retired_host) hipHostFree(p);
+}
+
+hipError_t gsv_engine::sync_own_streams() {
+    hipError_t r = hipSuccess;
+    for (hipStream_t s : {stream, vstream})
+        if (s && r == hipSuccess) r = hipStreamSynchronize(s);
+    for (auto& L : vlanes)
+        if (L.st && r == hipSuccess) r = hipStreamSynchronize(L.st);
+    return r;
 }
 
 // ------------------------------------------------------------ weights
@@ -354,7 +369,7 @@ int gsv_engine::reserve(int batch, int tokens) {
     for (auto& kv : graphs) hipGraphExecDestroy(kv.second);
     graphs.clear();
     const int nb = std::max(batch, max_batch), nt = std::max(tokens, tmax);
-    for (void* p : state_allocs) hipFree(p);
+    for (void* p : state_allocs) retire(p);
     state_allocs.clear();
     auto A = [&](size_t bytes) -> void* {
         void* p = nullptr;
@@ -399,12 +414,15 @@ int gsv_engine::reserve(int batch, int tokens) {
     acc64 = (long long*)A((size_t)nb * ACC_SEQ * 8);
     pSlab = (float*)A((size_t)8 * nt * 512 * 4);
     if (!pF || !prompts_buf || !acc64 || !pSlab) return set_error(GSV_E_HIP, "state allocation failed");
-    hipMemset(acc64, 0, (size_t)nb * ACC_SEQ * 8);
+    // stream-ordered (no null-stream call while another thread may be capturing), then waited
+    // for: id lives on this frame
+    hipMemsetAsync(acc64, 0, (size_t)nb * ACC_SEQ * 8, stream);
     std::vector<int> id(nb);
     for (int i = 0; i < nb; ++i) id[i] = i;
-    hipMemcpy(ident, id.data(), nb * 4, hipMemcpyHostToDevice);
-    hipMemset(done, 1, nb);
-    hipMemset(forceb, 0, nb * 4);
+    hipMemcpyAsync(ident, id.data(), nb * 4, hipMemcpyHostToDevice, stream);
+    hipMemsetAsync(done, 1, nb, stream);
+    hipMemsetAsync(forceb, 0, nb * 4, stream);
+    if (hipStreamSynchronize(stream) != hipSuccess) return set_error(GSV_E_HIP, "state init");
     max_batch = nb;
     tmax = nt;
     return 0;
@@ -473,7 +491,8 @@ int gsv_engine::encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t
     }
     text_embed(u->ref_seq, u->n_ref, u->text_seq, u->n_text, text_emb, bproj, bert_b, alpha_text,
                pe_tab, x, st);
-    return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "encode launch");
+    const hipError_t le = hipGetLastError();
+    return le == hipSuccess ? 0 : hip_error("encode launch", le);
 }
 
 // ------------------------------------------------------------ prefill
@@ -569,7 +588,7 @@ static __global__ void k_gather_rows512(const float* src, const int* rows, float
 int gsv_engine::ensure_packed(int rows, int B) {
     if (rows <= pk_rows && B <= pk_batch) return 0;
     const int nr = std::max(rows, pk_rows), nb = std::max(B, pk_batch);
-    for (void* p : pk_allocs) hipFree(p);
+    for (void* p : pk_allocs) retire(p);
     pk_allocs.clear();
     auto A = [&](size_t bytes) -> void* {
         void* p = nullptr;
@@ -643,7 +662,7 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     hipMemcpyAsync(pk_rowinfo, hs, (size_t)3 * R * 4, hipMemcpyHostToDevice, st);
     hipMemcpyAsync(pk_last, hlast, (size_t)B * 4, hipMemcpyHostToDevice, st);
     if (ntiles > pk_tile_cap) {
-        if (pk_tiles) hipFree(pk_tiles);
+        retire(pk_tiles);
         pk_tiles = nullptr;
         pk_tile_cap = 0;
         if (hipMalloc((void**)&pk_tiles, (size_t)3 * ntiles * 4) != hipSuccess)
@@ -893,11 +912,29 @@ hipGraphExec_t gsv_engine::step_graph(int B, const gsv_sampler* sp, int chunk, h
     auto it = graphs.find(key);
     if (it != graphs.end()) return it->second;
     hipGraph_t g = nullptr;
-    if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return nullptr;
+    if ((graph_err = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
     for (int i = 0; i < chunk; ++i) decode_step(B, sp, nullptr, st);
-    if (hipStreamEndCapture(st, &g) != hipSuccess) return nullptr;
+    if ((graph_err = hipStreamEndCapture(st, &g)) != hipSuccess) {
+        if (g) hipGraphDestroy(g);
+        // an invalidated capture can leave the stream in capture mode: end it, or every later
+        // launch on the stream fails with hipErrorStreamCaptureInvalidated (r05k)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+            hipGraph_t g2 = nullptr;
+            hipStreamEndCapture(st, &g2);
+            if (g2) hipGraphDestroy(g2);
+        }
+        (void)hipGetLastError();
+        return nullptr;
+    }
     hipGraphExec_t ex = nullptr;
-    if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) ex = nullptr;
+    if ((graph_err = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0)) != hipSuccess) {
+        ex = nullptr;
+        (void)hipGetLastError();
+    }
     hipGraphDestroy(g);
     if (ex) graphs[key] = ex;
     return ex;
@@ -913,8 +950,25 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
     __atomic_store_n(stop_word + 1, 0, __ATOMIC_RELEASE);   // no kernel of this engine runs: the loops are synchronous
     const int chunk = 8;
     hipGraphExec_t ex8 = step_graph(B, sp, chunk, st);
-    hipGraphExec_t ex1 = step_graph(B, sp, 1, st);
-    if (!ex8 || !ex1) return set_error(GSV_E_HIP, "decode graph capture failed");
+    hipGraphExec_t ex1 = ex8 ? step_graph(B, sp, 1, st) : nullptr;
+    // A capture that fails (another host thread's device-wide synchronisation -- hipFree,
+    // hipDeviceSynchronize -- can invalidate it) leaves this loop on eager launches of the
+    // same kernels: same results, more launch overhead; the next loop tries to capture again.
+    const bool eager = !ex8 || !ex1;
+    if (eager) {
+        ++graph_fallbacks;
+        static const bool log = std::getenv("GENIE_LOG_GRAPH") != nullptr;
+        if (log) fprintf(stderr, "[genie] step-graph capture failed (%s): eager decode steps\n", hipGetErrorName(graph_err));
+    }
+    auto run_steps = [&](hipGraphExec_t ex, int n) -> int {
+        if (eager) {
+            for (int i = 0; i < n; ++i) decode_step(B, sp, nullptr, st);
+            const hipError_t le = hipGetLastError();
+            return le == hipSuccess ? 0 : hip_error("decode step launch", le);
+        }
+        if (const hipError_t ge = hipGraphLaunch(ex, st)) return hip_error("graph launch", ge);
+        return 0;
+    };
     if (!done_host) {
         if (hipHostMalloc((void**)&done_host, 2 * 64, hipHostMallocDefault) != hipSuccess)
             return set_error(GSV_E_HIP, "pinned alloc");
@@ -938,10 +992,10 @@ int gsv_engine::decode_loop(int B, const gsv_sampler* sp, hipStream_t st, bool a
             probe_pending = false;
             probed = true;
         } else if (n == chunk) {
-            if (hipGraphLaunch(ex8, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
+            if (int r = run_steps(ex8, chunk)) return r;
         } else {
             for (int i = 0; i < n; ++i)
-                if (hipGraphLaunch(ex1, st) != hipSuccess) return set_error(GSV_E_HIP, "graph launch");
+                if (int r = run_steps(ex1, 1)) return r;
         }
         launched += n;
         const int slot = k & 1;
@@ -1006,7 +1060,7 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, in
     const int layout = B == 1 ? -1 : -100 - B;   // ring layout key: the kernels slot the ring differently
     if (need > pws_bytes || layout != pws_batch) {
         if (need > pws_bytes) {
-            if (pws) hipFree(pws);
+            retire(pws);
             pws = nullptr;
             pws_bytes = 0;
             if (hipMalloc(&pws, need) != hipSuccess) return set_error(GSV_E_HIP, "persistent ring");
@@ -1131,7 +1185,7 @@ int gsv_engine::decode_persistent_as(int B, const gsv_sampler* sp, hipStream_t s
     if (int r = persist_enqueue(B, sp, st, perr_host, probe ? kev[0] : nullptr, probe ? kev[1] : nullptr,
                                 res_batch ? res_pin : nullptr, res_batch))
         return r;
-    if (host_wait(st) != hipSuccess) return set_error(GSV_E_HIP, "persistent decode sync");
+    if (const hipError_t we = host_wait(st)) return hip_error("persistent decode sync", we);
     // code 3 (or any code under a pending stop): a stop request abandoned the launch
     if (*perr_host == 3 || (*perr_host != 0 && stop_requested())) return stopped_error();
     // code 2: the kernel met an activation beyond the fp16 range of its split-operand
@@ -1284,13 +1338,7 @@ hipError_t gsv_engine::host_wait(hipStream_t st) {
 int gsv_engine::ensure_res_pin(int batch) {
     const size_t need = (size_t)batch * 8 + (size_t)batch * tmax * 8;
     if (need <= res_pin_bytes) return 0;
-    if (res_pin) hipHostFree(res_pin);
-    for (GenSlot& g : gq) {
-        if (g.res) hipHostFree(g.res);
-        if (g.perr_h) hipHostFree(g.perr_h);
-        for (hipEvent_t e : {g.d0, g.done, g.k0, g.k1})
-            if (e) hipEventDestroy(e);
-    }
+    retire_host(res_pin);
     res_pin = nullptr;
     res_pin_bytes = 0;
     if (hipHostMalloc((void**)&res_pin, need, hipHostMallocDefault) != hipSuccess)
@@ -1362,7 +1410,7 @@ extern "C" int gsv_engine_destroy(gsv_engine* eng) {
     hipSetDevice(eng->device);
     for (auto& t : eng->vb_threads) t.join();   // lane threads of an unfinished async batch
     eng->vb_threads.clear();
-    hipDeviceSynchronize();
+    eng->sync_own_streams();   // not a device-wide sync: other engines of the process keep running
     delete eng;
     return 0;
 }
@@ -1609,7 +1657,7 @@ int gsv_engine::gen_start(const gsv_utt& u, const gsv_sampler& sp, hipStream_t c
     GenSlot& g = gq[(gq_head + gq_n) % 2];
     const size_t rb = 8 + (size_t)tmax * 8;
     if (g.res_bytes < rb) {
-        if (g.res) hipHostFree(g.res);
+        retire_host(g.res);
         g.res = nullptr;
         g.res_bytes = 0;
         if (hipHostMalloc((void**)&g.res, rb, hipHostMallocDefault) != hipSuccess) return set_error(GSV_E_HIP, "pinned results");
@@ -1854,7 +1902,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         const int p = std::min(std::max(value, std::min(least, greatest)), std::max(least, greatest));
         if (int r = eng->vits_batch_finish(nullptr)) return r;
         if (int r = eng->vits_wait(nullptr)) return r;
-        hipDeviceSynchronize();
+        eng->sync_own_streams();
         if (n == "lane_priority") {
             eng->lane_priority = p;
             if (int r = eng->remake_lane_streams()) return r;
@@ -1908,7 +1956,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
             if (hipMalloc(&eng->ptrace, (size_t)256 * 16 * 8) != hipSuccess) return set_error(GSV_E_HIP, "ptrace alloc");
             hipMemset(eng->ptrace, 0, (size_t)256 * 16 * 8);
         } else if (!value && eng->ptrace) {
-            hipFree(eng->ptrace);
+            eng->retire(eng->ptrace);
             eng->ptrace = nullptr;
         }
     } else {
@@ -1937,6 +1985,7 @@ extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value
     else if (n == "persist_launches") *value = eng->persist_launches;
     else if (n == "persist_hold") *value = eng->persist_hold;
     else if (n == "stops") *value = eng->stops;
+    else if (n == "graph_fallbacks") *value = eng->graph_fallbacks;
     else return set_error(GSV_E_ARG, "unknown counter " + n);
     return 0;
 }

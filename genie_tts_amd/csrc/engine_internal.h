@@ -15,6 +15,7 @@
 
 namespace gsv {
 int set_error(int code, const std::string& msg);
+int hip_error(const std::string& what, hipError_t e);   // GSV_E_HIP, the message naming the HIP error
 int f16_inexact_error(const std::string& weight, const float* v, int64_t index);
 struct StreamScope;
 constexpr long ACC_SEQ = 24 * 2 * 512;   // fixed-point hand-off accumulators per sequence
@@ -142,6 +143,8 @@ struct gsv_engine {
     int sv_f32_reruns = 0;            // SV calls re-run on the f32 path after an overflow
 
     std::map<std::string, hipGraphExec_t> graphs;
+    hipError_t graph_err = hipSuccess;   // the last step-graph capture's failure
+    int64_t graph_fallbacks = 0;         // decode loops run eagerly after a failed capture (counter)
     bool timing = false;
     float ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
@@ -182,6 +185,15 @@ struct gsv_engine {
     ~gsv_engine();
     void* dalloc(size_t bytes);
     void release_all();
+    // Buffers replaced while the engine runs are retired, not freed: hipFree / hipHostFree
+    // synchronise the device, which invalidates a hipGraph capture running on another thread
+    // (another engine of the process) and fails that thread's call (hipErrorStreamCaptureImplicit,
+    // gpurun_out/r05k_*.err).  Retired buffers are freed when the engine is destroyed.
+    std::vector<void*> retired, retired_host;
+    void retire(void* p) { if (p) { std::lock_guard<std::mutex> g(alloc_mu); retired.push_back(p); } }
+    void retire_host(void* p) { if (p) { std::lock_guard<std::mutex> g(alloc_mu); retired_host.push_back(p); } }
+    // Waits for this engine's own streams (engine, vocoder, lanes) -- never a device-wide sync.
+    hipError_t sync_own_streams();
     const gsv::Staged* find(const std::string& n) const;
     float* up_f32(const std::string& n, int* err);
     __half* up_f16(const std::string& n, int* err);

@@ -273,7 +273,7 @@ int gsv_engine::finalize_hubert() {
 
 float* gsv_engine::hubert_ws(size_t floats) {
     if (floats > hubert.ws_floats) {
-        if (hubert.ws) hipFree(hubert.ws);
+        retire(hubert.ws);
         hubert.ws = nullptr;
         hubert.ws_floats = 0;
         if (hipMalloc(&hubert.ws, floats * 4) != hipSuccess) return nullptr;

@@ -530,7 +530,7 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
     const size_t P1 = (size_t)SV_NMEL * T;
     const size_t need = sv_ws_floats(T);
     if (need > sv_ws_n) {
-        if (sv_ws) hipFree(sv_ws);
+        retire(sv_ws);
         sv_ws = nullptr;
         sv_ws_n = 0;
         if (hipMalloc(&sv_ws, need * 4) != hipSuccess) return set_error(GSV_E_HIP, "SV workspace");

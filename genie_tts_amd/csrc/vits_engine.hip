@@ -467,10 +467,10 @@ int gsv_engine::vits_decode(const int64_t* text_seq, int n_text, const int64_t* 
                             const float* ref_audio, int n_audio, const float* ge_in,
                             const float* ge_adv_in, const float* eps, uint64_t noise_seed, float noise_scale,
                             float* audio, hipStream_t s) {
-    if (use_convh && !vovf) {
+    if (use_convh && !vovf) {   // stream-ordered zeroing: no null-stream call beside running lanes / captures
         if (hipMalloc(&vovf, 64) != hipSuccess || hipHostMalloc((void**)&vovf_host, 64, hipHostMallocDefault) != hipSuccess)
             return set_error(GSV_E_HIP, "overflow flag alloc");
-        hipMemset(vovf, 0, 64);
+        hipMemsetAsync(vovf, 0, 64, s);
     }
     if (vpending || vqueued)   // the overlapped vocoder call shares the workspace: finish it first
         if (int r = vits_wait(nullptr)) return r;
@@ -550,7 +550,7 @@ int gsv_engine::set_vocoder_cus(int K) {
     if (int r = vits_wait(nullptr)) return r;
     if (int r = vits_batch_finish(nullptr)) return r;
     if (int r = pf_drop()) return r;   // a launched prefetch runs on the vocoder stream
-    hipDeviceSynchronize();
+    if (sync_own_streams() != hipSuccess) return set_error(GSV_E_HIP, "vocoder_cus sync");
     hipStream_t ns = nullptr, nv = nullptr;
     if (K == 0) {
         if (hipStreamCreateWithFlags(&ns, hipStreamNonBlocking) != hipSuccess) return set_error(GSV_E_HIP, "stream");
@@ -588,7 +588,7 @@ int gsv_engine::vits_async(const gsv_vits_item& u, float noise_scale, hipStream_
     if (use_convh && !vovf) {
         if (hipMalloc(&vovf, 64) != hipSuccess || hipHostMalloc((void**)&vovf_host, 64, hipHostMallocDefault) != hipSuccess)
             return set_error(GSV_E_HIP, "overflow flag alloc");
-        hipMemset(vovf, 0, 64);
+        hipMemsetAsync(vovf, 0, 64, caller);   // ordered before the call by vev_in
     }
     hipEventRecord(vev_in, caller);   // the inputs are ready in the caller's stream order here
     vcall = u;
@@ -896,11 +896,11 @@ int gsv_engine::seg_reserve(int n, int T) {
     if ((size_t)T > B.cap_t) {
         const size_t t = std::max((size_t)T, B.cap_t + B.cap_t / 4);
         for (float** p : {&B.z, &B.audio}) {
-            if (*p) hipFree(*p);
+            retire(*p);
             *p = nullptr;
         }
-        for (auto& g : B.g) { if (g) hipFree(g); g = nullptr; }
-        for (auto& q : B.seg) { if (q) hipFree(q); q = nullptr; }
+        for (auto& g : B.g) { retire(g); g = nullptr; }
+        for (auto& q : B.seg) { retire(q); q = nullptr; }
         B.cap_t = 0;
         long f = 1;
         for (int i = 0; i < 5; ++i) f *= V.up_rate[i];
@@ -916,14 +916,14 @@ int gsv_engine::seg_reserve(int n, int T) {
         B.cap_t = t;
     }
     if (n > B.cap_n) {
-        for (float** p : {&B.dcond}) { if (*p) hipFree(*p); *p = nullptr; }
-        for (int** p : {&B.off, &B.len, &B.ovf}) { if (*p) hipFree(*p); *p = nullptr; }
-        if (B.ovf_host) hipHostFree(B.ovf_host);
-        if (B.h_pin) hipHostFree(B.h_pin);
+        for (float** p : {&B.dcond}) { retire(*p); *p = nullptr; }
+        for (int** p : {&B.off, &B.len, &B.ovf}) { retire(*p); *p = nullptr; }
+        retire_host(B.ovf_host);
+        retire_host(B.h_pin);
         B.ovf_host = nullptr;
         B.h_pin = nullptr;
         B.cap_n = 0;
-        for (float** p : {&B.ge, &B.gem, &B.gcond}) { if (*p) hipFree(*p); *p = nullptr; }
+        for (float** p : {&B.ge, &B.gem, &B.gcond}) { retire(*p); *p = nullptr; }
         const int gin = V.flows[0].cond.cin, gcn = V.flows[0].cond.cout;
         if (hipMalloc(&B.ge, (size_t)n * gin * 4) != hipSuccess || hipMalloc(&B.gem, (size_t)n * 512 * 4) != hipSuccess ||
             hipMalloc(&B.gcond, (size_t)n * gcn * 4) != hipSuccess)
@@ -972,9 +972,8 @@ int gsv_engine::seg_front_tables(hipStream_t s) {
     if (!B.tab_ev && hipEventCreateWithFlags(&B.tab_ev, hipEventDisableTiming) != hipSuccess)
         return set_error(GSV_E_HIP, "vocoder table event");
     if (o > B.tab_cap) {
-        if (B.tab_dev && hipDeviceSynchronize() != hipSuccess) return set_error(GSV_E_HIP, "vocoder table sync");
-        if (B.tab_dev) hipFree(B.tab_dev);
-        if (B.tab_pin) hipHostFree(B.tab_pin);
+        retire(B.tab_dev);   // a queued batch may still read the old table / staging: retired, not freed
+        retire_host(B.tab_pin);
         B.tab_dev = B.tab_pin = nullptr;
         B.tab_cap = 0;
         const size_t cap = o + o / 4;
@@ -1091,8 +1090,8 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     for (const VitsLane& L : vlanes) hipStreamWaitEvent(s, L.join, 0);
     if (sgb.done) hipStreamWaitEvent(s, sgb.done, 0);
     if (n > vflag_cap) {
-        if (vflags) hipFree(vflags);
-        if (vflags_host) hipHostFree(vflags_host);
+        retire(vflags);
+        retire_host(vflags_host);
         vflags = nullptr;
         vflags_host = nullptr;
         vflag_cap = 0;
@@ -1145,6 +1144,22 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     } else {
         vb_packed = false;
     }
+    // Every workspace the lanes will use is sized here, on the issuing thread: no lane thread
+    // allocates (a hipMalloc beside another thread's stream capture or launches is avoided).
+    for (int l = 0; l < K; ++l) {
+        if (seg && vb_packed) break;   // the packed front: one workspace, sized below
+        int T = 0, S = 0, A = 0;
+        for (int i = l; i < n; i += K) {
+            T = std::max(T, 2 * vb_items[i].n_sem);
+            S = std::max(S, vb_items[i].n_text);
+            A = std::max(A, version == GSV_V2PP ? 0 : vb_items[i].n_audio);
+        }
+        if (T > MHA_MAXK_HOST || S > MHA_MAXK_HOST) continue;   // the lane reports the capacity error
+        // with the generator buffers, as the lanes' own ensure_vits_ws calls ask (vits_front, the pass)
+        if (int r = ensure_vits_ws(this, vlanes[l].ws, std::max(T, 2), std::max(S, 2), A)) return r;
+    }
+    if (seg && vb_packed)
+        if (int r = ensure_vits_ws(this, sgb.fw, sgb.T, sgb.St, 0, false)) return r;
     if (timing) hipEventRecord(ev[4], s);
     hipMemsetAsync(vflags, 0, (size_t)n * 4, s);
     hipEventRecord(vfork, s);

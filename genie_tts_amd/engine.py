@@ -657,7 +657,7 @@ class Engine:
     def counter(self, name: str) -> int:
         """Engine counter (gsv_get_counter): persist_timeouts, persist1_f16_reruns, vits_f32_reruns,
         sv_f32_reruns, w16_split_tensors, persist_disabled (timeout back-off holds begun),
-        persist_launches, persist_hold (generates left in the current hold), stops."""
+        persist_launches, persist_hold (generates left in the current hold), stops, graph_fallbacks."""
         v = ctypes.c_int64()
         _check(lib().gsv_get_counter(self.h, name.encode(), ctypes.byref(v)), "gsv_get_counter")
         return v.value

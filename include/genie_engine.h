@@ -361,8 +361,9 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
  * "vits_lanes", "seg_vocoder" (1, default: a vocoder batch runs its generator as ONE pass
  * over all utterances laid out back to back), "seg_front" (1, default: its text/flow part
  * too, see gsv_vits_decode_batch), "convh" (MRF convs on the split-fp16 MFMA),
- * "sv_f16", "packed", test hooks ("persist_spin_ticks", "persist1_f16_limit",
- * "sv_f16_limit").  "ptrace": 1 allocates per-workgroup phase stamps of the persistent
+ * "convt_f16" (1, default: the upsample ConvTransposes on it too), "sv_f16", "packed",
+ * test hooks ("persist_spin_ticks", "persist1_f16_limit", "sv_f16_limit", "convh_tile":
+ * 1..4 forces that k_conv_h tile candidate, 0 the cost model).  "ptrace": 1 allocates per-workgroup phase stamps of the persistent
  * launch (step 8, layer 12), read back with gsv_debug_ptrace ([256 workgroups][16
  * slots]: 8 stamps of the 100 MHz clock, then the same 8 of the shader clock).
  * GSV_E_ARG for an unknown name. */
@@ -373,7 +374,9 @@ int gsv_set_option(gsv_engine* eng, const char* name, int value);
  * current hold), "persist_launches", "persist1_f16_reruns" (fp16-range fallbacks),
  * "vits_f32_reruns", "vits_packed_fronts" (vocoder batches whose text/flow part ran
  * packed), "sv_f32_reruns", "w16_split_tensors" (fp32 weights kept as hi + lo
- * planes), "stops" (generates abandoned by gsv_request_stop). */
+ * planes), "stops" (generates abandoned by gsv_request_stop), "graph_fallbacks"
+ * (per-step decode loops run eagerly because their hipGraph capture failed -- e.g.
+ * invalidated by another thread's device-wide synchronisation). */
 int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value);
 int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);
 

@@ -56,9 +56,9 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps * 1e3, res
 
-    # (4 engines x 16 failed with graph-capture errors across the threads, and two persistent
-    # launches cannot be co-resident: the engine's contract is one engine per process, calls
-    # serialised -- this probe only asks whether two per-step-graph streams overlap)
+    # (4 engines x 16 on threads is tools/concurrency_probe.py's case -- r04 failed it with
+    # capture errors, fixed in r05 (profiles/r05_concurrency.txt); two persistent launches
+    # cannot be co-resident, so this probe only asks whether per-step-graph streams overlap)
     for n, persist in ((1, True), (1, False), (2, False)):
         key = f"{n}x{total // n}_{'persist' if persist else 'graph'}"
         ms, res = run(n, persist)
