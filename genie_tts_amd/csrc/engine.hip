@@ -1943,13 +1943,14 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->sv_f16 = value != 0;
     } else if (n == "sv_f16_limit") {   // tests: force the f32 re-run (0: the fp16 range)
         eng->sv_f16_limit = value > 0 ? (float)value : 65000.f;
-    } else if (n == "convh" || n == "convt_f16" || n == "convh_tile") {
+    } else if (n == "convh" || n == "convt_f16" || n == "convh_tile" || n == "mrf_fused") {
         // a queued or pending vocoder call finishes under the mode it began with
         if (n == "convh_tile" && (value < 0 || value > 4)) return set_error(GSV_E_ARG, "convh_tile: 0..4");
         if (int r = eng->vits_wait(nullptr)) return r;
         if (int r = eng->vits_batch_finish(nullptr)) return r;
         if (n == "convh") eng->use_convh = value != 0;
         else if (n == "convt_f16") eng->convt_f16 = value != 0;
+        else if (n == "mrf_fused") eng->mrf_fused = value != 0;
         else eng->convh_tile = value;
     } else if (n == "ptrace") {
         if (value && !eng->ptrace) {

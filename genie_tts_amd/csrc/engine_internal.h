@@ -175,6 +175,7 @@ struct gsv_engine {
     bool use_convh = true;             // GENIE_CONVH=0: MRF convs on the f32 MFMA path
     bool convt_f16 = true;             // option "convt_f16": the upsample ConvTransposes on the split-fp16 path too
     int convh_tile = 0;                // option "convh_tile": 0 = cost model, 1..4 = force a k_conv_h tile (tests)
+    bool mrf_fused = true;             // option "mrf_fused": the C <= 32 stages' conv pairs as one kernel
     int* vovf = nullptr;               // f16-split conv overflow flag (device)
     int* vovf_host = nullptr;          // pinned copy
     int vits_f32_reruns = 0;           // utterances re-run on the f32 path after an overflow

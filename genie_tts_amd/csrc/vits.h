@@ -74,6 +74,20 @@ void seg_fill(int* seg, long n, const int* off, const int* len, int nseg, int f,
 // f16-split path; returns false (nothing launched) when the shape is not covered.
 bool conv1d_h(const ConvArgs& a, hipStream_t s);
 
+// One ResBlock1 step of a narrow generator stage (C = 16 / 32) as one kernel (vits_mrf.hip):
+// xt = lrelu(conv1_d(lrelu(r)) + b1) in LDS only, then conv2 (kernel k, dilation 1) with e
+// as its epilogue (e.bias = conv2's bias, e.res = r, e.mode / out / acc / div / seg; e.Cout
+// = C, e.n_t = T).  Weights fp16 [C][k][C] with per-output-channel scales.  e.out must not
+// alias r (neighbouring blocks read r's halo).  false: shape not covered (nothing launched).
+struct MrfPairArgs {
+    const float* r; int T, C, K, dil;
+    const __half* w1; const float* s1; const float* b1;
+    const __half* w2; const float* s2;
+    int* ovf;
+    ConvArgs e;
+};
+bool mrf_pair(const MrfPairArgs& a, hipStream_t s);
+
 // LayerNorm over channels per t: out = LN(x + y) (y may be null), eps 1e-5; seg (segmented
 // batch, as ConvArgs::seg): a gap column is written as zeros
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,

@@ -323,10 +323,13 @@ static thread_local long tls_splitk_cap = 0;
 static thread_local int* tls_ovf = nullptr;   // set while the f16-split MRF path is enabled
 static thread_local int tls_convh_tile = 0;    // the running engine's option "convh_tile"
 static thread_local bool tls_convt_f16 = false;   // ... and "convt_f16" (the ConvTransposes on the split path)
+static thread_local bool tls_mrf_fused = false;   // ... and "mrf_fused" (narrow stages' conv pairs as one kernel)
 // The per-pass thread-local state of one vocoder pass (split-fp16 flag word, tile, ConvT path).
 struct ConvhScope {
-    ConvhScope(int* ovf, int tile, bool convt) { tls_ovf = ovf; tls_convh_tile = tile; tls_convt_f16 = convt; }
-    ~ConvhScope() { tls_ovf = nullptr; tls_convh_tile = 0; tls_convt_f16 = false; }
+    ConvhScope(int* ovf, int tile, bool convt, bool fused) {
+        tls_ovf = ovf; tls_convh_tile = tile; tls_convt_f16 = convt; tls_mrf_fused = fused;
+    }
+    ~ConvhScope() { tls_ovf = nullptr; tls_convh_tile = 0; tls_convt_f16 = false; tls_mrf_fused = false; }
 };
 struct SplitkScope {
     SplitkScope(float* p, long cap) { tls_splitk = p; tls_splitk_cap = cap; }
@@ -680,7 +683,47 @@ static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const fl
         float* rbuf = bufs[1];
         float* xt = bufs[2];
         float* accb = bufs[3];
-        for (int j = 0; j < 3; ++j) {
+        // the narrow stages (C <= 32, byte-bound): each conv1 + conv2 pair as one kernel with
+        // xt in LDS (vits_mrf.hip); its output ping-pongs between rbuf and xt (no in-place update:
+        // neighbouring blocks read the input's halo)
+        const bool fuse = tls_ovf && tls_mrf_fused && C <= 32;
+        for (int j = 0; j < 3 && fuse; ++j) {
+            const int kk = V.rb_k[j];
+            const float* rcur = yb;
+            for (int mi = 0; mi < 3; ++mi) {
+                const Conv& c1 = V.rb[i * 3 + j][0][mi];
+                const Conv& c2w = V.rb[i * 3 + j][1][mi];
+                MrfPairArgs m{};
+                m.r = rcur; m.T = Tc; m.C = C; m.K = kk; m.dil = V.rb_d[mi];
+                m.w1 = c1.wh; m.s1 = c1.wscale; m.b1 = c1.b;
+                m.w2 = c2w.wh; m.s2 = c2w.wscale; m.ovf = tls_ovf;
+                m.e = cargs(c2w, rcur, Tc, mi == 0 ? rbuf : xt);
+                m.e.res = rcur;
+                m.e.seg = sg;
+                if (mi < 2) {
+                    m.e.mode = CV_RESID;
+                } else if (j == 0) {
+                    m.e.mode = CV_ACC_FIRST; m.e.acc = accb;
+                } else if (j == 1) {
+                    m.e.mode = CV_ACC_ADD; m.e.acc = accb;
+                } else {
+                    m.e.mode = CV_ACC_MEAN; m.e.acc = accb; m.e.div = 3.0f; m.e.out = x;
+                }
+                if (!mrf_pair(m, s)) {   // not covered (weights off the fp16 path): the two convs, xt in
+                    // a buffer free at this point (x is rewritten only by the last MEAN step)
+                    float* scratch = mi == 2 ? rbuf : x;
+                    ConvArgs a1 = cargs(c1, rcur, Tc, scratch);
+                    a1.dil = V.rb_d[mi]; a1.pad = (kk * V.rb_d[mi] - V.rb_d[mi]) / 2; a1.in_act = 1; a1.in_slope = 0.1f;
+                    a1.seg = sg;
+                    conv1d(a1, s);
+                    ConvArgs a2 = m.e;
+                    a2.x = scratch; a2.in_act = 1; a2.in_slope = 0.1f;
+                    conv1d(a2, s);
+                }
+                rcur = mi == 0 ? rbuf : xt;
+            }
+        }
+        for (int j = 0; j < 3 && !fuse; ++j) {
             const int kk = V.rb_k[j];
             const float* rcur = yb;
             for (int mi = 0; mi < 3; ++mi) {
@@ -727,7 +770,7 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     if (2 * G > MHA_MAXK_HOST || n_text > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, W, 2 * G, n_text, version == GSV_V2PP ? 0 : n_audio)) return r;
     SplitkScope sk(W.splitk, W.splitk_cap);
-    ConvhScope cs(ovf, convh_tile, convt_f16);
+    ConvhScope cs(ovf, convh_tile, convt_f16, mrf_fused);
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timed) hipEventRecord(ev[4], s);
     if (int r = vits_front(W, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
@@ -1050,7 +1093,7 @@ int gsv_engine::seg_front(hipStream_t st) {
 // path, flagging an fp16-range input in sgb.ovf).
 int gsv_engine::seg_generate(hipStream_t st, bool f16) {
     SegBatch& B = sgb;
-    ConvhScope cs(f16 ? B.ovf : nullptr, convh_tile, convt_f16);
+    ConvhScope cs(f16 ? B.ovf : nullptr, convh_tile, convt_f16, mrf_fused);
     const int* seg[6] = {B.seg[0], B.seg[1], B.seg[2], B.seg[3], B.seg[4], B.seg[5]};
     float* const gb[5] = {B.g[0], B.g[1], B.g[2], B.g[3], B.g[4]};
     vits_generator(vits, gb, B.z, B.T, B.dcond, vits.upc, seg, B.audio, st);

@@ -61,9 +61,11 @@ def test_vits_waveform(setup, G, S, noise):
     assert np.abs(out - ref).max() < 2e-3
 
 
-@pytest.mark.parametrize("convh", [0, 1])
-def test_vits_waveform_conv_paths(setup, convh):
-    """MRF convs on the f32 MFMA path (convh=0) and on the f16-split path (1, default)."""
+@pytest.mark.parametrize("convh,fused", [(0, 0), (1, 0), (1, 1)])
+def test_vits_waveform_conv_paths(setup, convh, fused):
+    """MRF convs on the f32 MFMA path (convh=0) and on the f16-split path (1, default);
+    on the latter the C <= 32 stages' conv pairs run separately (mrf_fused=0) or as one
+    kernel with the intermediate in LDS (1, default, vits_mrf.hip)."""
     ver, e, vm, _ = setup
     G, S = 40, 30
     txt = synth.synth_phones(S, f"vt{S}")
@@ -72,10 +74,12 @@ def test_vits_waveform_conv_paths(setup, convh):
     kw = _cond(ver)
     ref = vm(txt, sem, eps=eps, **kw).numpy()
     e.set_option("convh", convh)
+    e.set_option("mrf_fused", fused)
     try:
         out = e.vits_decode(txt, sem, eps=eps, **kw).cpu().numpy()
     finally:
         e.set_option("convh", 1)
+        e.set_option("mrf_fused", 1)
     rms = float(np.sqrt(np.mean((out - ref) ** 2)))
     assert rms <= RMS_TOL, f"rms {rms:.3e}"
 

@@ -3,7 +3,8 @@ random semantic tokens of the workload's lengths, Philox noise), timed per call;
 --trace DB (a rocprofv3 kernel-trace database of this run) it splits the last call's wall
 time into the per-utterance front part (lanes) and the segmented generator (from the
 first conv_pre launch, k_conv1d<7>, to the end).
-Usage: python tools/vits_batch_prof.py [N] [--seg 0|1] [--front 0|1]  |  python tools/vits_batch_prof.py --trace DIR"""
+Usage: python tools/vits_batch_prof.py [N] [--seg 0|1] [--front 0|1] [--opt name=value] [--n sentences]
+     | python tools/vits_batch_prof.py --trace DIR"""
 import glob
 import os
 import sqlite3
@@ -49,6 +50,12 @@ def main():
         eng.set_option("seg_vocoder", int(sys.argv[sys.argv.index("--seg") + 1]))
     if "--front" in sys.argv:
         eng.set_option("seg_front", int(sys.argv[sys.argv.index("--front") + 1]))
+    for i, a in enumerate(sys.argv):   # --opt name=value: any engine option (A/B of a vocoder path)
+        if a == "--opt":
+            k, v = sys.argv[i + 1].split("=")
+            eng.set_option(k, int(v))
+    if "--n" in sys.argv:   # the first n sentences only (n = 1: one utterance, the single-call path)
+        wl.items = wl.items[:int(sys.argv[sys.argv.index("--n") + 1])]
     ref = wl.reference
     T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
     ge = eng.ref_encode(T(ref.audio_32k.reshape(-1)))
