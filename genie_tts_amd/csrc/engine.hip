@@ -247,6 +247,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_PERSIST")) use_persist = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST1")) use_persist1 = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST1M")) use_persist1m = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_PERSISTM")) use_persistm = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
@@ -1108,7 +1109,13 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, in
     perr_zeroed = false;
     // a queued prefetch starts once this stream's prefill (same workspaces) is done
     if (pf_queued && !pf_pending) hipEventRecord(pf_fork, st);
-    const hipError_t le = B == 1 ? decode_persist1(a, st, k0, k1) : decode_persist1m(a, st, k0, k1);
+    // B >= persistm_min_b: the batched kernel, one group of <= 4 sequences per 16 CUs
+    const int pm_groups = std::min({persistm_max_groups(), decode_cus() / persistm_grid(1), B});
+    const bool pm = B > 1 && use_persistm && B >= persistm_min_b && pm_groups >= persistm_groups(B);
+    if (pm) a.groups = pm_groups;
+    const hipError_t le = B == 1 ? decode_persist1(a, st, k0, k1)
+                          : pm   ? decode_persistm(a, st, k0, k1)
+                                 : decode_persist1m(a, st, k0, k1);
     if (le != hipSuccess)
         return set_error(GSV_E_HIP, "persistent decode launch");
     ++persist_launches;
@@ -1883,6 +1890,11 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_persist1 = value != 0;
     } else if (n == "persist1m") {   // B = 2..64: the multi-sequence form of persist1 (0: per-step graphs)
         eng->use_persist1m = value != 0;
+    } else if (n == "persistm") {    // the batched persistent decode (t2s_persistm.hip) from persistm_min_b on
+        eng->use_persistm = value != 0;
+    } else if (n == "persistm_min_b") {
+        if (value < 2) return set_error(GSV_E_ARG, "persistm_min_b: >= 2");
+        eng->persistm_min_b = value;
     } else if (n == "persist_spin_ticks") {   // test hook: bound of a hand-off wait (100 MHz ticks)
         eng->persist_spin_ticks = value > 0 ? (unsigned long long)value : gsv_engine::PERSIST_SPIN_TICKS;
     } else if (n == "persist1_f16_limit") {   // test hook: force the fp16-range fallback

@@ -300,5 +300,12 @@ hipError_t decode_persist1(const PersistArgs& a, hipStream_t s, hipEvent_t start
 int persist1m_max_batch();
 size_t persist1m_ring_bytes(int B);
 hipError_t decode_persist1m(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
+// The batched form (k_decode_persistm, t2s_persistm.hip): a.groups sequence groups x 16
+// workgroups, each group decoding up to 4 sequences (b = g, g + groups, ...) through all
+// 24 layers with the batch on the MFMA M dimension.  Same ring layout as persist1m.
+int persistm_groups(int B);      // the fewest groups that hold B sequences
+int persistm_max_groups();
+int persistm_grid(int groups);
+hipError_t decode_persistm(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 
 }  // namespace gsv

@@ -325,8 +325,8 @@ constexpr int ERR_F16_RANGE = 2;   // error word: an activation left the fp16 ra
 // out of line so the common path keeps its registers.  Returns the lane's max.
 // (templates on V: each kernel gets its own out-of-line copy, so the multi-sequence
 // kernel does not change the single-sequence kernel's register allocation)
-template <int V>
-__device__ __noinline__ float scores_general1(Shared1& sh, const float* Kw, int kv, int T, float q0, float q1,
+template <int V, class SH>
+__device__ __noinline__ float scores_general1(SH& sh, const float* Kw, int kv, int T, float q0, float q1,
                                               float q2, float q3, float sc, float4 knew, int c8, int g) {
     float lmax = -INFINITY;
     for (int base = 0; base < T; base += 512) {
@@ -383,7 +383,8 @@ __device__ __forceinline__ float swap_sum32(float x) {
 // Head output from the 8 wave partials (m_w, l_w in sh.wred, o_w in sh.at.ov4),
 // merged by EVERY wave into its own operand copy (no barrier after): lane j < 8
 // weighs wave j, e_j = exp(m_j - M); O = sum e_j o_j / sum e_j l_j.
-__device__ __forceinline__ void merge_waves1(Shared1& sh, int w, int lane) {
+template <class SH>
+__device__ __forceinline__ void merge_waves1(SH& sh, int w, int lane) {
     const int j = lane & 7;
     const float mj = sh.wred[0][j];
     float M = mj;
@@ -404,8 +405,8 @@ __device__ __forceinline__ void merge_waves1(Shared1& sh, int w, int lane) {
     __builtin_amdgcn_wave_barrier();
 }
 
-template <int NU>
-__device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, float q2, float q3, float sc,
+template <int NU, class SH>
+__device__ __forceinline__ void wave_attn1(SH& sh, float q0, float q1, float q2, float q3, float sc,
                                            int kv, int T, int c8, int g, int w, int lane) {
     float4 kr[NU];
 #pragma unroll
@@ -472,8 +473,8 @@ __device__ __forceinline__ void wave_attn1(Shared1& sh, float q0, float q1, floa
 // The general case (more than 512 keys or rows beyond the LDS stage): scores into
 // sh.at.p, block softmax, P.V over 16 key groups, head output -> sh.osh/osl.  Out
 // of line so the common path keeps its registers.
-template <int V>
-__device__ __noinline__ void attn_general1(Shared1& sh, const float* Kw, const float* Vw, int kv, int T, float q0,
+template <int V, class SH>
+__device__ __noinline__ void attn_general1(SH& sh, const float* Kw, const float* Vw, int kv, int T, float q0,
                                            float q1, float q2, float q3, float sc, float4 knew, int c8, int g, int w,
                                            int lane, int tid) {
     const float lmax = scores_general1<V>(sh, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
@@ -1356,7 +1357,8 @@ __device__ __forceinline__ void pub_all(const W& ws, Shared1& sh, int row, unsig
 
 // The head's K/V rows [0, min(kv, KVL1)) of sequence b, layer l -> the LDS stage
 // (LDS-DMA by the six non-publishing waves)
-__device__ __forceinline__ void stage_kv(const PersistArgs& a, Shared1& sh, int l, int b, int h, int kv, int w,
+template <class SH>
+__device__ __forceinline__ void stage_kv(const PersistArgs& a, SH& sh, int l, int b, int h, int kv, int w,
                                          int lane) {
     if (is_pub_wave(w)) return;
     const int wi = w < 3 ? w : w - 1;   // 0..5
@@ -1959,6 +1961,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
     }
 }
 
+#ifndef PERSIST1_NO_ENTRY   // (t2s_persistm.hip reuses the helpers above, not this kernel)
 __global__ __launch_bounds__(PT) void k_decode_persist1m(PersistArgs a) {
     __shared__ Shared1 sh;
     WsSeq ws;
@@ -1975,6 +1978,7 @@ __global__ __launch_bounds__(PT) void k_decode_persist1m(PersistArgs a) {
     if (r < 16) run_attn_m(a, ws, sh, grp, r);
     else run_ffn_m(a, ws, sh, grp, r - 16);
 }
+#endif
 
 #else   // the single-sequence kernel
 
@@ -1989,7 +1993,8 @@ __global__ __launch_bounds__(PT) void k_decode_persist1(PersistArgs a) {
 
 }  // namespace
 
-#ifdef PERSIST1_MULTI
+#if defined(PERSIST1_MULTI) && defined(PERSIST1_NO_ENTRY)
+#elif defined(PERSIST1_MULTI)
 int persist1m_max_batch() { return MB; }
 size_t persist1m_ring_bytes(int B) { return (size_t)wsm_slot(B) * RING1 * 8; }
 

@@ -1,0 +1,683 @@
+// Batched persistent decode (k_decode_persistm): the AR loop of the stage decoder
+// (t2s_stage_decoder_fp32.onnx#43-114, loop Inference.py:95-106) for B sequences with
+// the batch on the MFMA M dimension.
+//
+// The multi-sequence kernel k_decode_persist1m keeps each layer's weights in registers
+// and runs the live sequences one after another through every workgroup: a step costs
+// ~B workgroup passes of ~6 us (a hand-off round trip plus one sequence's compute), and
+// at B = 64 the decode runs at 1.28 ms per step, ~18 % of its K/V-streaming bound.
+// Here the chip is split into sequence GROUPS instead of layer groups:
+//   group g (up to 16 of 16 workgroups each) decodes sequences b = g, g + G, g + 2G, ...
+//   (at most MG = 4) through ALL 24 layers; workgroup r of the group is attention head r
+//   AND FFN slice r (hidden units [128 r, 128 r + 128)).
+// A layer is the single-sequence kernel's two hand-offs (head partials -> FFN, FFN2
+// partials -> next layer), but every pass serves the group's sequences together:
+//   - one gather round trip for all of them (one thread sums a granule column's 16 rows
+//     in row order -- the arithmetic of gather_pfh's two threads);
+//   - q/k/v, out-projection, FFN1, FFN2 and the logits as 16x16x32 MFMAs whose A rows
+//     2i / 2i + 1 are sequence i's hi / lo split (t2s_persist1.hip puts one sequence's
+//     hi / lo in rows 0 / 1; an MFMA output row depends on its own A row only, and the
+//     K chains, folds and sums are the single-sequence kernel's, so every sequence's
+//     values -- and tokens -- are bit-identical to its own launch);
+//   - the weights stream from L2 once per pass (blocks r of every group sit on XCD r % 8,
+//     so one XCD's L2 serves two heads' slices to 16 groups) instead of living in VGPRs.
+// Attention stays per (sequence, head) with the single-sequence kernel's code (K/V rows
+// staged in LDS by LDS-DMA, the new row from the q/k/v epilogue).  Greedy: every
+// workgroup resolves its group's tokens from the logits candidates itself (one hop);
+// sampled: workgroup i of the group samples sequence i.  Ring, tags, error word, stop
+// word and sequence state are persist1m's (WsSeq), so the host treats both alike.
+#define PERSIST1_MULTI
+#define PERSIST1_NO_ENTRY
+#include "t2s_persist1.hip"
+
+namespace gsv {
+namespace {
+
+constexpr int MG = 4;           // sequences per group
+constexpr int NSG_MAX = 16;     // groups (x 16 workgroups: the whole chip)
+constexpr int GWM = 16;         // workgroups per group
+constexpr int AST = 512 + 8;    // A-tile row strides (halves; 16-B pad)
+constexpr int FST = 128 + 8;
+constexpr int OST = 32 + 8;
+
+struct SharedM {
+    struct {                                  // names as Shared1::at (the shared attention helpers)
+        float k[KVL1 * 32];                   // K/V rows [0, min(kv, KVL1)) of (layer, sequence, head r)
+        float v[KVL1 * 32];
+        float ov[16][32];
+        float ov4[PWV][32];
+        union {
+            float p[TMAX1];                   // general-path scores
+            struct {
+                _Float16 A[2 * MG][AST];      // MFMA A tile: rows 2i / 2i + 1 = hi / lo of sequence i's input
+                float lnb[MG][512];           // the input rows (LayerNorm statistics)
+            } g;
+            float pk[MG][512];                // the rows a pass publishes
+            float lg[1056];                   // sampler: one sequence's logits
+        };
+    } at;
+    _Float16 F[2 * MG][FST];                  // FFN2's A tile (FFN1 outputs)
+    _Float16 O[2 * MG][OST];                  // the out-projection's A tile (head outputs)
+    float qkvs[MG][96];                       // head r's q, k, v per sequence
+    float qkv[96];                            // ... of the sequence in attention (the helpers' operand)
+    _Float16 osh[PWV][32], osl[PWV][32];      // merge_waves1's per-wave head output
+    float h1s[MG][32];                        // block r of the published x_l / h1 rows
+    float cand[MG][5][4];                     // greedy candidates of this slice's 4 waves + EOS
+    float wred[2][PWV];
+    uint32_t seenq[MG][33];
+    int tok[MG], act[MG], ny0[MG], kv0[MG], st0[MG], nexe[MG], lstop[MG], lfin[MG];
+    int fail, stopreq;
+    SampleLds<PT> samp;
+};
+
+__device__ __forceinline__ int nth_bit(unsigned m, int n) {   // index of the n-th set bit of m
+    for (int k = 0; k < n; ++k) m &= m - 1;
+    return __builtin_ctz(m);
+}
+// lane's A-operand base in a tile of 2 MG rows (rows 8..15 of the MFMA repeat 0..7; unused)
+__device__ __forceinline__ const _Float16* abase_m(const _Float16* tile, int stride, int lane) {
+    return tile + (lane & 7) * stride + 8 * (lane >> 4);
+}
+__device__ __forceinline__ bool ok_all(bool ok, SharedM& sh) {
+    if (!ok) sh.fail = 1;
+    bar_nf();
+    return sh.fail == 0;
+}
+
+// The 17-row granule blocks of the live sequences (byte offsets blk(i) of row 0; rows
+// 0..15 partials, row 16 the residual row) -> u = row16 + (vec[c] + sum of rows 0..15
+// in row order) into lnb[i], the fp16 split of u * mul[c] into A rows 2i, 2i + 1.  One
+// thread per (sequence, granule column), all 17 loads in flight.  Ends with a barrier.
+template <class Blk>
+__device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, SharedM& sh, unsigned live,
+                                         unsigned tag, Blk blk, const float* vec, const float* mul) {
+    constexpr int RB = (int)Ws1::ROW * 8;
+    const int nl = __builtin_popcount(live);
+    bool ok = true;
+    for (int it = opaque_tid(); it < nl * GQ; it += PT) {
+        const int n = it / GQ, q = it - n * GQ;
+        const int i = nth_bit(live, n);
+        // rows 0..8, then 9..16 (two round trips of 9 / 8 granules: 17 in flight spill)
+        const int off = blk(i) + 16 * q;
+        float f[3];
+        {
+            u32x4 g[9];
+            wait_g16_n<9>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                f[k] = __uint_as_float(g[0][1 + k]);
+#pragma unroll
+                for (int r = 1; r < 9; ++r) f[k] += __uint_as_float(g[r][1 + k]);
+            }
+        }
+        if (!ok) break;
+        u32x4 g[8];
+        wait_g16_n<8>(ws, off + 9 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+        if (!ok) break;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k == 2 && gq_n(q) == 2) break;
+#pragma unroll
+            for (int r = 0; r < 7; ++r) f[k] += __uint_as_float(g[r][1 + k]);
+            const int c = gq_col(q, k);
+            const float u = __uint_as_float(g[7][1 + k]) + (ldg(vec, c) + f[k]);
+            sh.at.g.lnb[i][c] = u;
+            const float un = u * ldg(mul, c);
+            _Float16 hi, lo;
+            if (!split_h(un, hi, lo) || !(fabsf(un) < a.f16_limit)) {
+                atomicCAS(a.err, 0, ERR_F16_RANGE);
+                ok = false;
+            }
+            sh.at.g.A[2 * i][c] = hi;
+            sh.at.g.A[2 * i + 1][c] = lo;
+        }
+    }
+    return ok_all(ok, sh);
+}
+
+// LayerNorm statistics of the live sequences' rows (every wave, the same order)
+__device__ __forceinline__ void stats_m(const SharedM& sh, unsigned live, float (&mean)[MG], float (&rden)[MG]) {
+#pragma unroll
+    for (int i = 0; i < MG; ++i) {
+        mean[i] = 0.f;
+        rden[i] = 1.f;
+        if ((live >> i) & 1u) ln_row_stats(sh.at.g.lnb[i], mean[i], rden[i]);
+    }
+}
+
+// Sequence i's row of 512 published columns (pk[i]) as its GQ granules at byte offset
+// `row`, and its 32-column block h1s[i] (11 granules) at `blk`; waves 3 and 7 store
+// (persist1m's pub_all layout).  Every operand is in registers before the first store.
+__device__ __forceinline__ void pub_m(const WsSeq& ws, SharedM& sh, int i, int row, int blk, unsigned tag, int w,
+                                      int lane) {
+    if (!is_pub_wave(w)) return;
+    const float* pk = sh.at.pk[i];
+    const int q0 = (w == 3 ? 0 : 88) + lane, q1 = q0 + 64;
+    const int c0 = gq_col(q0, 0);
+    float a0 = pk[c0], a1 = pk[c0 + 1], a2 = gq_n(q0) == 2 ? 0.f : pk[c0 + 2];
+    float b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    int o0 = row + 16 * q0, o1 = row + 16 * q1;
+    bool second = lane < 24;
+    if (second) {
+        const int c1 = gq_col(q1, 0);
+        b0 = pk[c1]; b1 = pk[c1 + 1]; b2 = gq_n(q1) == 2 ? 0.f : pk[c1 + 2];
+    }
+    if (w == 7 && lane >= 40 && lane < 51) {
+        const int r = lane - 40;
+        const float* p = sh.h1s[i] + 3 * r;
+        b0 = p[0]; b1 = p[1]; b2 = r == 10 ? 0.f : p[2];
+        o1 = blk + 16 * r;
+        second = true;
+    }
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(o0), "+v"(o1));
+    st_g16(ws, o0, tag, a0, a1, a2);
+    if (second) st_g16(ws, o1, tag, b0, b1, b2);
+}
+
+// Greedy token of step s - 1 of group sequence i (global b), resolved by ONE wave from
+// the logits candidates LG(s - 1) (resolve_m's arithmetic).  Lane 0 updates the state.
+__device__ void resolve_w(const PersistArgs& a, const WsSeq& ws, int s, int i, int b, bool publisher, SharedM& sh,
+                          bool& ok) {
+    const int lane = threadIdx.x & 63;
+    float f[4];
+    wait_gran_n<4>(ws.LG(s - 1) + 4 * lane, 1, ws.tag(s - 1), f, a.err, ok, a.spin_ticks);
+    float gv = f[0], rv = f[2];
+    int gi = __float_as_int(f[1]), ri = __float_as_int(f[3]);
+    if (lane == 0) {
+        float e[4];
+        wait_gran_n<4>(ws.LG(s - 1) + 256, 1, ws.tag(s - 1), e, a.err, ok, a.spin_ticks);
+        argmax_merge(gv, gi, e[0], __float_as_int(e[1]));
+        argmax_merge(rv, ri, e[2], __float_as_int(e[3]));
+    }
+    const float gm = wave_max_dpp(gv), rm = wave_max_dpp(rv);
+    const int tok = wave_min_dpp(gv == gm ? gi : 0x7fffffff);
+    const int raw = wave_min_dpp(rv == rm ? ri : 0x7fffffff);
+    if (lane == 0) {
+        const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
+        const bool fin = seq_finished(a.force_b, b, a.force_steps, a.max_steps, sh.st0[i] + s, stop);
+        if (sh.stopreq) stop_launch(a, ok);
+        sh.tok[i] = tok;
+        sh.act[i] = fin ? 0 : 1;
+        sh.seenq[i][tok >> 5] |= 1u << (tok & 31);
+        if (publisher && ok) {
+            a.y[(long)b * a.ldy + sh.ny0[i] + s - 1] = tok;
+            sh.lstop[i] = stop;
+            sh.lfin[i] = fin ? 1 : 0;
+            sh.nexe[i] = s;
+            st_gran(ws.TK(s), ws.tag(s), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+        }
+    }
+}
+
+__device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, int g, int r) {
+    const int nsg = a.groups, nb = a.B;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nloc = g < nb ? (nb - g + nsg - 1) / nsg : 0;   // this group's sequences: b = g + i nsg
+    const bool fused = a.greedy && a.knob[0] == 0;
+    const bool publisher = fused && r == 0;
+    const bool sampler = !fused && r < nloc;                 // samples sequence i = r
+    {
+        const int tid = threadIdx.x;
+        if (tid < nloc) {
+            const int i = tid, b = g + i * nsg, ny0 = a.ny[b];
+            sh.ny0[i] = ny0;
+            sh.kv0[i] = a.kvlen[b];
+            sh.st0[i] = a.steps[b];
+            sh.tok[i] = (int)a.y[(long)b * a.ldy + ny0 - 1];
+            sh.act[i] = a.done[b] ? 0 : 1;
+            sh.nexe[i] = 0;
+            sh.lstop[i] = 0;
+            sh.lfin[i] = a.done[b] ? 1 : 0;
+        }
+        for (int e = tid; e < nloc * 33; e += PT) sh.seenq[e / 33][e % 33] = a.seen[(long)(g + (e / 33) * nsg) * 33 + e % 33];
+        if (tid == 0) {
+            sh.fail = 0;
+            sh.stopreq = 0;
+        }
+    }
+    __syncthreads();
+    unsigned live = 0;
+    for (int i = 0; i < nloc; ++i) live |= sh.act[i] ? 1u << i : 0u;
+    int staged = -1;   // l * MG + i whose K/V rows are in (or on their way to) the LDS stage
+    int n_exec = 0;
+    for (int s = 0; s < a.smax && live && sh.fail == 0; ++s) {
+        const unsigned tag = base.tag(s);
+        if (s > 0) {   // ---- the tokens of step s - 1
+            if (fused) {
+                bool ok = true;
+                if (w < MG && ((live >> w) & 1u)) resolve_w(a, base.seq(g + w * nsg), s, w, g + w * nsg, publisher, sh, ok);
+                if (!ok_all(ok, sh)) return;
+            } else {
+                bool ok = true;
+                const int tid = threadIdx.x;
+                if (tid < MG && ((live >> tid) & 1u)) {
+                    const WsSeq ws = base.seq(g + tid * nsg);
+                    const float v = wait_gran(ws.TK(s), ws.tag(s), a.err, ok, a.spin_ticks);
+                    if (ok) {
+                        const unsigned u = __float_as_uint(v);
+                        sh.tok[tid] = (int)(u & 0xffff);
+                        sh.act[tid] = ((u >> 16) & 1) ? 0 : 1;
+                    }
+                }
+                if (!ok_all(ok, sh)) return;
+            }
+            unsigned nl = 0;
+            for (int i = 0; i < nloc; ++i) nl |= ((live >> i) & 1u) && sh.act[i] ? 1u << i : 0u;
+            live = nl;
+            bar_nf();
+            if (!live) break;
+        }
+        for (int l = 0; l < 24; ++l) {
+            const PLayer& P = a.L[l];
+            const int tid = opaque_tid(), lane = tid & 63;
+            const int n16 = lane & 15, k8 = 8 * (lane >> 4);
+            const bool up = lane >= 16;   // lanes 0..15: sequences 0, 1; 16..31: 2, 3 (MFMA rows 0..3 / 4..7)
+            // ================= attention role: head r =================
+            uint4 wq[16], wo[4];
+            float qfB = 0.f, qfC = 0.f;
+            if (w < 6) {
+                const int row = (w >> 1) * 512 + r * 32 + 16 * (w & 1) + n16;
+#pragma unroll
+                for (int c = 0; c < 16; ++c) wq[c] = ldg16(P.w_in + (long)row * 512 + 32 * c + k8, 0);
+                qfB = ldg(a.fold, (long)l * FOLD_LAYER + row);
+                qfC = ldg(a.fold, (long)l * FOLD_LAYER + 1536 + row);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + r * 32 + k8, 0);
+            if (l == 0) {   // x_0 = E_audio[tok] + alpha pe[n]
+                bool ok = true;
+                const int nl = __builtin_popcount(live);
+                for (int it = tid; it < nl * 512; it += PT) {
+                    const int i = nth_bit(live, it >> 9), c = it & 511;
+                    const float u = ldg_h(a.emb, (long)sh.tok[i] * 512 + c) +
+                                    ldg(a.alpha, 0) * ldg(a.pe, (long)(sh.ny0[i] + s) * 512 + c);
+                    sh.at.g.lnb[i][c] = u;
+                    _Float16 hi, lo;
+                    if (!split_h(u, hi, lo) || !(fabsf(u) < a.f16_limit)) {
+                        atomicCAS(a.err, 0, ERR_F16_RANGE);
+                        ok = false;
+                    }
+                    sh.at.g.A[2 * i][c] = hi;
+                    sh.at.g.A[2 * i + 1][c] = lo;
+                }
+                if (!ok_all(ok, sh)) return;
+            } else {
+                const PLayer& Q = a.L[l - 1];
+                if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PFH(s, l - 1, 0); },
+                              Q.b2, Q.n2w))
+                    return;
+            }
+            {
+                float mean[MG], rden[MG];
+                stats_m(sh, live, mean, rden);
+                if (w == 0 && lane < 32) {   // block r of x_l (form_x's arithmetic) for the FFN's PA row 16
+                    const int c = 32 * r + lane;
+#pragma unroll
+                    for (int i = 0; i < MG; ++i)
+                        if ((live >> i) & 1u)
+                            sh.h1s[i][lane] = l > 0 ? ln_apply(sh.at.g.lnb[i][c], mean[i], rden[i],
+                                                               ldg(a.L[l - 1].n2w, c), ldg(a.L[l - 1].n2b, c))
+                                                    : sh.at.g.lnb[i][c];
+                }
+                if (w < 6) {
+                    const _Float16* ab = abase_m(&sh.at.g.A[0][0], AST, lane);
+                    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int cb = 0; cb < 16; cb += 8) {
+                        h8v af[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
+#pragma unroll
+                        for (int i = 0; i < 8; i += 2) {
+                            c0 = mfma16(af[i], bfrag(wq[cb + i]), c0);
+                            c1 = mfma16(af[i + 1], bfrag(wq[cb + i + 1]), c1);
+                        }
+                    }
+                    if (lane < 32) {
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) {
+                            const int i = (up ? 2 : 0) + k;
+                            if ((live >> i) & 1u) {
+                                const float mn = l > 0 ? (up ? mean[2 + k] : mean[k]) : 0.f;
+                                const float rd = l > 0 ? (up ? rden[2 + k] : rden[k]) : 1.f;
+                                sh.qkvs[i][16 * w + n16] =
+                                    rd * (((c0[2 * k] + c1[2 * k]) + (c0[2 * k + 1] + c1[2 * k + 1])) - mn * qfB) + qfC;
+                            }
+                        }
+                    }
+                }
+            }
+            bar_nf();   // q/k/v of every sequence; the A tile / lnb are free (the general path's scores)
+            for (unsigned m = live; m; m &= m - 1) {
+                const int i = __builtin_ctz(m), b = g + i * nsg;
+                const int kv = sh.kv0[i] + s, T = kv + 1;
+                if (staged != l * MG + i) {
+                    stage_kv(a, sh, l, b, r, kv, w, lane);
+                    staged = l * MG + i;
+                }
+                if (!is_pub_wave(w)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its K/V LDS-DMA landed
+                if (kv < KVL1 && w >= 2 && w < 6 && lane < 16)
+                    ((w < 4 ? sh.at.k : sh.at.v) + kv * 32 + 16 * (w & 1))[lane] = sh.qkvs[i][16 * w + lane];
+                if (tid < 96) sh.qkv[tid] = sh.qkvs[i][tid];
+                bar_nf();
+                const long kvoff = (long)b * a.sstride + (long)r * a.tmax * 32;
+                const float* Kw = a.kc[l] + kvoff;
+                const float* Vw = a.vc[l] + kvoff;
+                const float sc = a.scale;
+                const int c8 = lane & 7, gk = (w << 3) | (lane >> 3);
+                const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
+                const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
+                const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
+                if (T <= 512 && kv < KVL1) {
+                    const int nu = (T + 63) >> 6;
+                    if (nu <= 2) wave_attn1<2>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu <= 4) wave_attn1<4>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else wave_attn1<8>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    bar_nf();   // the stage is read
+                    merge_waves1(sh, w, lane);
+                } else {
+                    attn_general1<2>(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, gk, w, lane, tid);
+                    bar_nf();
+                }
+                const unsigned nx = m & (m - 1);
+                if (nx) {   // the next sequence's K/V rows land while this one's output is formed
+                    const int i2 = __builtin_ctz(nx);
+                    stage_kv(a, sh, l, g + i2 * nsg, r, sh.kv0[i2] + s, w, lane);
+                    staged = l * MG + i2;
+                }
+                if (w == 0 && lane < 32) {
+                    sh.O[2 * i][lane] = sh.osh[0][lane];
+                    sh.O[2 * i + 1][lane] = sh.osl[0][lane];
+                }
+                if (w == 7) {   // the new K/V row (read by this workgroup only, next step)
+                    float* Kg = a.kc[l] + kvoff;
+                    float* Vg = a.vc[l] + kvoff;
+                    if (lane < 32) Kg[(long)kv * 32 + lane] = sh.qkvs[i][32 + lane];
+                    else Vg[(long)kv * 32 + lane - 32] = sh.qkvs[i][64 + lane - 32];
+                }
+            }
+            bar_nf();   // O complete
+            {
+                const h8v af = afrag(abase_m(&sh.O[0][0], OST, lane), 0);
+                f32x4 acc[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[t] = mfma16(af, bfrag(wo[t]), f32x4{0.f, 0.f, 0.f, 0.f});
+                if (lane < 32) {
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int i = (up ? 2 : 0) + k;
+                        if ((live >> i) & 1u) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) sh.at.pk[i][64 * w + 16 * t + n16] = acc[t][2 * k] + acc[t][2 * k + 1];
+                        }
+                    }
+                }
+            }
+            bar_nf();
+            for (unsigned m = live; m; m &= m - 1) {
+                const int i = __builtin_ctz(m);
+                const WsSeq ws = base.seq(g + i * nsg);
+                pub_m(ws, sh, i, ws.PA(s, l, r), ws.PA(s, l, 16) + 16 * 11 * r, tag, w, lane);
+            }
+            bar_nf();   // pk consumed
+            // ================= FFN role: slice r =================
+            uint4 w1r[16], w2r[16];   // W2's columns are loaded once FFN1 has consumed W1's rows
+            float ffB, ffC;
+            {
+                const int tid2 = opaque_tid(), lane2 = tid2 & 63, m16 = lane2 & 15, q8 = 8 * (lane2 >> 4);
+#pragma unroll
+                for (int c = 0; c < 16; ++c) w1r[c] = ldg16(P.w1 + (long)(r * 128 + w * 16 + m16) * 512 + 32 * c + q8, 0);
+                ffB = ldg(a.fold, (long)l * FOLD_LAYER + 3072 + r * 128 + w * 16 + m16);
+                ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + r * 128 + w * 16 + m16);
+            }
+            if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PA(s, l, 0); }, P.b_out,
+                          P.n1w))
+                return;
+            {
+                const int tid2 = opaque_tid(), lane2 = tid2 & 63;
+                float mean[MG], rden[MG];
+                stats_m(sh, live, mean, rden);
+                const _Float16* ab = abase_m(&sh.at.g.A[0][0], AST, lane2);
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int cb = 0; cb < 16; cb += 8) {
+                    h8v af[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) af[i] = afrag(ab, 32 * (cb + i));
+#pragma unroll
+                    for (int i = 0; i < 8; i += 2) {
+                        c0 = mfma16(af[i], bfrag(w1r[cb + i]), c0);
+                        c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
+                    }
+                }
+                {
+                    const int m16 = lane2 & 15, q8 = 8 * (lane2 >> 4);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + m16) * 2048 + r * 128 + 32 * c + q8, 0);
+                }
+                if ((tid2 >> 5) == r) {   // block r of h1 = LN1(v) for the next layer's PFH row 16
+                    const float n1w = ldg(P.n1w, tid2), n1b = ldg(P.n1b, tid2);
+#pragma unroll
+                    for (int i = 0; i < MG; ++i)
+                        if ((live >> i) & 1u) sh.h1s[i][tid2 & 31] = (sh.at.g.lnb[i][tid2] - mean[i]) * rden[i] * n1w + n1b;
+                }
+                bool ok = true;
+                if (lane2 < 32) {
+                    const bool up2 = lane2 >= 16;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int i = (up2 ? 2 : 0) + k;
+                        if ((live >> i) & 1u) {
+                            const float mn = up2 ? mean[2 + k] : mean[k], rd = up2 ? rden[2 + k] : rden[k];
+                            const float f =
+                                fmaxf(rd * (((c0[2 * k] + c1[2 * k]) + (c0[2 * k + 1] + c1[2 * k + 1])) - mn * ffB) + ffC, 0.f);
+                            split_h(f, sh.F[2 * i][w * 16 + (lane2 & 15)], sh.F[2 * i + 1][w * 16 + (lane2 & 15)]);
+                            if (!(fabsf(f) < a.f16_limit)) {
+                                atomicCAS(a.err, 0, ERR_F16_RANGE);
+                                ok = false;
+                            }
+                        }
+                    }
+                }
+                if (!ok_all(ok, sh)) return;   // F complete; lnb / A free
+            }
+            {
+                const int tid2 = opaque_tid(), lane2 = tid2 & 63;
+                const _Float16* ab = abase_m(&sh.F[0][0], FST, lane2);
+                h8v af[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) af[c] = afrag(ab, 32 * c);
+                f32x4 acc[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) acc[t] = mfma16(af[c], bfrag(w2r[4 * t + c]), acc[t]);
+                if (lane2 < 32) {
+                    const bool up2 = lane2 >= 16;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int i = (up2 ? 2 : 0) + k;
+                        if ((live >> i) & 1u) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                sh.at.pk[i][64 * w + 16 * t + (lane2 & 15)] = acc[t][2 * k] + acc[t][2 * k + 1];
+                        }
+                    }
+                }
+            }
+            bar_nf();
+            {
+                const int lane2 = opaque_tid() & 63;
+                for (unsigned m = live; m; m &= m - 1) {
+                    const int i = __builtin_ctz(m);
+                    const WsSeq ws = base.seq(g + i * nsg);
+                    pub_m(ws, sh, i, ws.PFH(s, l, r), ws.PFH(s, l, 16) + 16 * 11 * r, tag, w, lane2);
+                }
+            }
+            bar_nf();   // pk consumed
+        }
+        // ================= logits of step s: rows 64 r .. 64 r + 63 (+ EOS on r = 15) =================
+        {
+            if (threadIdx.x == 64) sh.stopreq = ld_stop(a.stop_req);   // used by the next resolve
+            if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PFH(s, 23, 0); },
+                          a.L[23].b2, a.L[23].n2w))
+                return;
+            const int tid = opaque_tid(), lane = tid & 63, n16 = lane & 15, k8 = 8 * (lane >> 4);
+            const bool up = lane >= 16;
+            float mean[MG], rden[MG];
+            stats_m(sh, live, mean, rden);
+            if (w < 4 || (w == 4 && r == NF - 1)) {
+                const int row = w < 4 ? 64 * r + 16 * w + n16 : 1024;
+                const _Float16* ab = abase_m(&sh.at.g.A[0][0], AST, lane);
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int cb = 0; cb < 16; cb += 2) {
+                    c0 = mfma16(afrag(ab, 32 * cb), bfrag(ldg16(a.w_pred, (long)row * 512 + 32 * cb + k8)), c0);
+                    c1 = mfma16(afrag(ab, 32 * (cb + 1)), bfrag(ldg16(a.w_pred, (long)row * 512 + 32 * (cb + 1) + k8)), c1);
+                }
+                const float lfB = ldg(a.fold, LOGIT_FOLD + row), lfC = ldg(a.fold, LOGIT_FOLD + 1025 + row);
+                const bool lv = w < 4 || n16 == 0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = (up ? 2 : 0) + k;
+                    const float mn = up ? mean[2 + k] : mean[k], rd = up ? rden[2 + k] : rden[k];
+                    const float v = rd * (((c0[2 * k] + c1[2 * k]) + (c0[2 * k + 1] + c1[2 * k + 1])) - mn * lfB) + lfC;
+                    const bool mine = lane < 32 && ((live >> i) & 1u);
+                    if (!fused) {
+                        if (mine && lv) {
+                            const WsSeq ws = base.seq(g + i * nsg);
+                            st_gran(ws.LG(s) + row, tag, v);
+                        }
+                    } else {
+                        // (rows 2, 3 of lanes 32..63 reduce garbage and are never read)
+                        const uint32_t* seen = sh.seenq[i & (MG - 1)];
+                        float pv = ((seen[row >> 5] >> (row & 31)) & 1u) ? (v < 0.f ? v * a.rep_penalty : v / a.rep_penalty)
+                                                                         : v;
+                        pv = pv / a.temperature;
+                        float gv = lv ? pv : -INFINITY, rv = lv ? v : -INFINITY;
+                        gv = fmaxf(gv, dpp_f<0xB1, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0xB1, 0xF>(rv));
+                        gv = fmaxf(gv, dpp_f<0x4E, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x4E, 0xF>(rv));
+                        gv = fmaxf(gv, dpp_f<0x141, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x141, 0xF>(rv));
+                        gv = fmaxf(gv, dpp_f<0x140, 0xF>(gv)); rv = fmaxf(rv, dpp_f<0x140, 0xF>(rv));
+                        int gmi = (lv && pv == gv) ? row : 0x7fffffff, rmi = (lv && v == rv) ? row : 0x7fffffff;
+                        gmi = min(gmi, dpp_i<0xB1, 0xF>(gmi)); rmi = min(rmi, dpp_i<0xB1, 0xF>(rmi));
+                        gmi = min(gmi, dpp_i<0x4E, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x4E, 0xF>(rmi));
+                        gmi = min(gmi, dpp_i<0x141, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x141, 0xF>(rmi));
+                        gmi = min(gmi, dpp_i<0x140, 0xF>(gmi)); rmi = min(rmi, dpp_i<0x140, 0xF>(rmi));
+                        if (mine && n16 < 4)
+                            sh.cand[i][w][n16] = n16 == 0 ? gv : n16 == 1 ? __int_as_float(gmi) : n16 == 2 ? rv
+                                                                                                    : __int_as_float(rmi);
+                    }
+                }
+            }
+            bar_nf();
+            if (fused && w == 7) {   // this slice's candidates: 16 granules per sequence (+ 4 EOS on r = 15)
+                const bool eos = r == NF - 1;
+                for (unsigned m = live; m; m &= m - 1) {
+                    const int i = __builtin_ctz(m);
+                    const WsSeq ws = base.seq(g + i * nsg);
+                    if (lane < 16 || (lane < 20 && eos)) {
+                        const int ww = lane >> 2, k = lane & 3;
+                        st_gran(ws.LG(s) + 4 * (ww < 4 ? 4 * r + ww : 64) + k, tag, sh.cand[i][ww][k]);
+                    }
+                }
+            }
+            bar_nf();   // A / lnb consumed
+        }
+        // ---- sampler (sampled decoding): sequence i = r of the group
+        if (sampler && ((live >> r) & 1u)) {
+            const int tid = threadIdx.x, i = r, b = g + i * nsg;
+            const WsSeq ws = base.seq(b);
+            bool ok = true;
+            const u64* lgg = ws.LG(s);
+            for (int k = tid; k < 1025; k += PT) sh.at.lg[k] = wait_gran(lgg + k, tag, a.err, ok, a.spin_ticks);
+            if (!ok) sh.fail = 1;
+            __syncthreads();
+            if (sh.fail) return;
+            const int st = sh.st0[i] + s;
+            uint32_t* seen = sh.seenq[i];
+            int raw = 0;
+            const int tok = sample_block<PT>([&](int k) { return sh.at.lg[k]; }, seen, b, st + 1, a.top_k,
+                                             a.temperature, a.rep_penalty, a.greedy, a.seed, 0, nullptr, &raw, sh.samp);
+            if (tid == 0) {
+                const int stop = (raw == 1024 || tok == 1024) ? 1 : 0;
+                const int fin = seq_finished(a.force_b, b, a.force_steps, a.max_steps, st + 1, stop) ? 1 : 0;
+                a.y[(long)b * a.ldy + sh.ny0[i] + s] = tok;
+                seen[tok >> 5] |= 1u << (tok & 31);
+                sh.lstop[i] = stop;
+                sh.lfin[i] = fin;
+                sh.nexe[i] = s + 1;
+                bool go = true;
+                if (ld_stop(a.stop_req)) stop_launch(a, go);
+                else st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
+            }
+            __syncthreads();   // sh.at.lg / sh.samp consumed
+        }
+        ++n_exec;
+    }
+    // fused greedy at the launch's step cap: the live sequences' last tokens are unresolved
+    if (fused && n_exec == a.smax && n_exec > 0 && sh.fail == 0) {
+        bool ok = true;
+        if (w < MG && ((live >> w) & 1u)) resolve_w(a, base.seq(g + w * nsg), n_exec, w, g + w * nsg, publisher, sh, ok);
+        if (!ok_all(ok, sh)) return;
+    }
+    // ---- sequence state write-back (the publisher: every sequence of the group; a sampler:
+    // its sequence), only when no workgroup failed
+    __syncthreads();
+    if ((publisher || sampler) && sh.fail == 0) {
+        if (threadIdx.x == 0) __threadfence();   // thread 0's y stores have reached L2
+        __syncthreads();
+        if (ld_rlx(a.err) != 0) return;
+        const int tid = threadIdx.x;
+        for (int i = 0; i < nloc; ++i) {
+            if (sampler && i != r) continue;
+            const int ne = sh.nexe[i], b = g + i * nsg;
+            if (ne <= 0) continue;
+            if (tid < 33) a.seen[(long)b * 33 + tid] = sh.seenq[i][tid];
+            if (tid == 0) {
+                a.ny[b] = sh.ny0[i] + ne;
+                a.steps[b] = sh.st0[i] + ne;
+                a.kvlen[b] = sh.kv0[i] + ne;
+                a.done[b] = (uint8_t)sh.lfin[i];
+                if (a.stop_out) a.stop_out[b] = (uint8_t)sh.lstop[i];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(PT) void k_decode_persistm(PersistArgs a) {
+    __shared__ SharedM sh;
+    WsSeq ws;
+    ws.ring = a.ring;
+    ws.epoch = a.epoch;
+    ws.rs = __builtin_amdgcn_make_buffer_rsrc(a.ring, 0, 0x7fffffff, 0x00020000);
+    ws.nb = a.B;
+    ws.b = 0;
+    ws.oPFH = wsm_oPFH(a.B);
+    ws.oLG = wsm_oLG(a.B);
+    ws.oTK = wsm_oTK(a.B);
+    ws.slot_u64 = wsm_slot(a.B);
+    // block = 16 g + r: block b runs on XCD b % 8, so head / slice r of every group shares XCD r % 8
+    run_group(a, ws, sh, blockIdx.x / GWM, blockIdx.x % GWM);
+}
+
+}  // namespace
+
+int persistm_groups(int B) { return (B + MG - 1) / MG; }
+int persistm_max_groups() { return NSG_MAX; }
+int persistm_grid(int groups) { return groups * GWM; }
+
+hipError_t decode_persistm(const PersistArgs& a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    if (a.groups < 1 || a.groups > NSG_MAX || a.B < 1 || a.B > MB || a.B > MG * a.groups) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL(k_decode_persistm, dim3(a.groups * GWM), dim3(PT), 0, s, start, stop, 0, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsv

@@ -1,0 +1,112 @@
+"""GPU: the batched persistent decode (k_decode_persistm, t2s_persistm.hip; the batch on
+the MFMA M dimension, up to 4 sequences per group of 16 workgroups) against the
+multi-sequence kernel (k_decode_persist1m) and against single launches (k_decode_persist1).
+
+Every sequence's values are the single-sequence kernel's (same K chains, folds and sum
+orders; an MFMA output row depends on its own A row only), so greedy tokens are
+bit-identical to a launch of its own and to persist1m, and sampled tokens (Philox top-k)
+to persist1m's sampler.  Reference loop: Inference.py:95-106 (t2s_stage_decoder_fp32.onnx).
+"""
+import pytest
+
+from tests.common import character, t2s_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from genie_tts_amd.engine import Engine
+    w = character("v2")
+    e = Engine({"t2s_encoder": w["t2s_encoder"], "t2s": w["t2s"]}, "v2")
+    e.set_option("persist", 1)
+    e.set_option("persistm", 1)
+    e.set_option("persistm_min_b", 2)   # every B > 1 on the batched kernel unless persistm = 0
+    yield e
+    e.close()
+
+
+def _both(eng, inps, sp):
+    n0 = eng.counter("persist_launches")
+    eng.set_option("persistm", 1)
+    a = [x.tolist() for x in eng.t2s_generate(inps, sp)]
+    eng.set_option("persistm", 0)
+    try:
+        b = [x.tolist() for x in eng.t2s_generate(inps, sp)]
+    finally:
+        eng.set_option("persistm", 1)
+    assert eng.counter("persist_launches") >= n0 + 2   # both ran as persistent launches
+    return a, b
+
+
+@pytest.mark.parametrize("B", [2, 4, 5, 17, 40, 64])
+def test_batched_matches_multi_sequence_kernel(eng, B):
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=10 + 3 * i, S=8 + 2 * i, H=30 + 6 * i, tag=f"pm{B}_{i}") for i in range(B)]
+    a, b = _both(eng, inps, make_sampler(force_steps=22))
+    for i in range(B):
+        assert a[i] == b[i], f"sequence {i}"
+
+
+def test_batched_matches_single_launches(eng):
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=12 + 5 * i, S=9 + 3 * i, H=40 + 9 * i, tag=f"pms{i}") for i in range(7)]
+    sp = make_sampler(force_steps=30)
+    got = [x.tolist() for x in eng.t2s_generate(inps, sp)]
+    assert got == [eng.t2s_generate([inp], sp)[0].tolist() for inp in inps]
+
+
+@pytest.mark.parametrize("top_k,temp", [(15, 1.0), (5, 0.8)])
+def test_batched_sampled_matches_multi_sequence_kernel(eng, top_k, temp):
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=12 + i, S=9 + i, H=36 + 2 * i, tag=f"pmk{i}") for i in range(6)]
+    a, b = _both(eng, inps, make_sampler(top_k=top_k, temperature=temp, greedy=False, seed=77, force_steps=24))
+    for i in range(len(inps)):
+        assert a[i] == b[i], f"sequence {i}"
+
+
+def test_batched_ragged_lengths(eng):
+    """Per-sequence forced lengths: sequences leave the launch one by one, the others keep
+    their tokens; every sequence stops at its own step."""
+    from genie_tts_amd.engine import make_sampler
+    lens = [9, 25, 4, 17, 12, 30, 2, 21, 14]
+    inps = [t2s_inputs(R=11 + i, S=9 + i, H=32 + 4 * i, tag=f"pmr{i}") + (n,) for i, n in enumerate(lens)]
+    a, b = _both(eng, inps, make_sampler(force_steps=30))
+    assert a == b
+    assert [len(x) for x in a] == [len(x) for x in b]
+    assert len({len(x) for x in a}) == len(set(lens))
+
+
+def test_batched_long_context(eng):
+    """Keys past the 448-row LDS stage (the general attention path) and past 512 keys."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=40 + 10 * i, S=30 + 5 * i, H=400 + 60 * i, tag=f"pml{i}") for i in range(5)]
+    a, b = _both(eng, inps, make_sampler(force_steps=40))
+    assert a == b
+
+
+def test_batched_fp16_range_fallback(eng):
+    """An activation past the fp16 range stops the batched launch (error 2) before any
+    sequence state is written; the steps re-run as per-step graphs with the same tokens."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=10 + i, S=8 + i, H=30 + 2 * i, tag=f"pmf{i}") for i in range(9)]
+    sp = make_sampler(force_steps=14)
+    ref = eng.t2s_generate(inps, sp)
+    before = eng.counter("persist1_f16_reruns")
+    eng.set_option("persist1_f16_limit", 1)
+    try:
+        got = eng.t2s_generate(inps, sp)
+    finally:
+        eng.set_option("persist1_f16_limit", 0)
+    assert eng.counter("persist1_f16_reruns") > before
+    assert [g.tolist() for g in got] == [r.tolist() for r in ref]
+
+
+def test_batched_full_500_step_loop(eng):
+    """The reference's whole loop (Inference.py:95, range(500)) with no EOS (random
+    weights): keys grow past the LDS stage; tokens equal persist1m's at the maximum length."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=40 + 3 * i, S=30 + 2 * i, H=160 + 8 * i, tag=f"pm500_{i}") for i in range(6)]
+    a, b = _both(eng, inps, make_sampler())
+    assert a == b
+    assert all(len(x) >= 450 for x in a)
