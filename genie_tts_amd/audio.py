@@ -8,7 +8,9 @@ src/genie_tts/Audio/Audio.py:19-51 and Audio/ReferenceAudio.py:28-57:
 The reference reads with libsndfile (soundfile) and resamples with soxr 'hq';
 neither exists in this image, so reading is our own RIFF/WAVE (PCM 8/16/24/32,
 IEEE float 32/64), AIFF, FLAC (flac.py, lossless: exact samples) and Ogg/Vorbis
-(vorbis.py, the Vorbis I float decode) parsers, and
+(vorbis.py, the Vorbis I float decode; Ogg parity with libsndfile/libvorbis is
+UNPINNED: only round trips through the repo's own test encoder check it, no
+libvorbis-encoded clip exists here) parsers, and
 resampling is a rational polyphase Kaiser-windowed sinc
 (scipy.signal.resample_poly), NOT soxr's HQ filter.  Host-side, once per
 reference clip.  Parity with soxr is unpinned (a different filter: any clip not

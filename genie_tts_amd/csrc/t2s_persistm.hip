@@ -84,6 +84,14 @@ __device__ __forceinline__ bool ok_all(bool ok, SharedM& sh) {
     return sh.fail == 0;
 }
 
+// tools/ptrace_pm.py: phase stamps of step 8 (layer 12 and the step's ends), slot k of this
+// workgroup's 16, 100 MHz clock
+#define PMSTAMP(cond, k)                                                                        \
+    do {                                                                                        \
+        if (a.trace && s == 8 && (cond) && threadIdx.x == 0)                                    \
+            a.trace[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+    } while (0)
+
 // The 17-row granule blocks of the live sequences (byte offsets blk(i) of row 0; rows
 // 0..15 partials, row 16 the residual row) -> u = row16 + (vec[c] + sum of rows 0..15
 // in row order) into lnb[i], the fp16 split of u * mul[c] into A rows 2i, 2i + 1.  One
@@ -242,6 +250,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
     int n_exec = 0;
     for (int s = 0; s < a.smax && live && sh.fail == 0; ++s) {
         const unsigned tag = base.tag(s);
+        PMSTAMP(true, 12);
         if (s > 0) {   // ---- the tokens of step s - 1
             if (fused) {
                 bool ok = true;
@@ -267,12 +276,21 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             bar_nf();
             if (!live) break;
         }
+        PMSTAMP(true, 13);
+        {
+            const int i0 = __builtin_ctz(live);
+            if (staged != i0) {   // layer 0's first K/V stage (the step's first layer)
+                stage_kv(a, sh, 0, g + i0 * nsg, r, sh.kv0[i0] + s, w, threadIdx.x & 63);
+                staged = i0;
+            }
+        }
         for (int l = 0; l < 24; ++l) {
             const PLayer& P = a.L[l];
             const int tid = opaque_tid(), lane = tid & 63;
             const int n16 = lane & 15, k8 = 8 * (lane >> 4);
             const bool up = lane >= 16;   // lanes 0..15: sequences 0, 1; 16..31: 2, 3 (MFMA rows 0..3 / 4..7)
             // ================= attention role: head r =================
+            PMSTAMP(l == 12, 0);
             uint4 wq[16], wo[4];
             float qfB = 0.f, qfC = 0.f;
             if (w < 6) {
@@ -307,6 +325,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                               Q.b2, Q.n2w))
                     return;
             }
+            PMSTAMP(l == 12, 1);
             {
                 float mean[MG], rden[MG];
                 stats_m(sh, live, mean, rden);
@@ -348,6 +367,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();   // q/k/v of every sequence; the A tile / lnb are free (the general path's scores)
+            PMSTAMP(l == 12, 2);
             for (unsigned m = live; m; m &= m - 1) {
                 const int i = __builtin_ctz(m), b = g + i * nsg;
                 const int kv = sh.kv0[i] + s, T = kv + 1;
@@ -399,6 +419,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();   // O complete
+            PMSTAMP(l == 12, 3);
             {
                 const h8v af = afrag(abase_m(&sh.O[0][0], OST, lane), 0);
                 f32x4 acc[4];
@@ -422,6 +443,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 pub_m(ws, sh, i, ws.PA(s, l, r), ws.PA(s, l, 16) + 16 * 11 * r, tag, w, lane);
             }
             bar_nf();   // pk consumed
+            PMSTAMP(l == 12, 4);
             // ================= FFN role: slice r =================
             uint4 w1r[16], w2r[16];   // W2's columns are loaded once FFN1 has consumed W1's rows
             float ffB, ffC;
@@ -435,6 +457,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PA(s, l, 0); }, P.b_out,
                           P.n1w))
                 return;
+            PMSTAMP(l == 12, 5);
             {
                 const int tid2 = opaque_tid(), lane2 = tid2 & 63;
                 float mean[MG], rden[MG];
@@ -486,6 +509,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
                 if (!ok_all(ok, sh)) return;   // F complete; lnb / A free
             }
+            PMSTAMP(l == 12, 6);
             {
                 const int tid2 = opaque_tid(), lane2 = tid2 & 63;
                 const _Float16* ab = abase_m(&sh.F[0][0], FST, lane2);
@@ -520,8 +544,15 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                     const WsSeq ws = base.seq(g + i * nsg);
                     pub_m(ws, sh, i, ws.PFH(s, l, r), ws.PFH(s, l, 16) + 16 * 11 * r, tag, w, lane2);
                 }
+                if (l < 23) {   // the next layer's first K/V stage lands during the hop
+                    const int i0 = __builtin_ctz(live);
+                    stage_kv(a, sh, l + 1, g + i0 * nsg, r, sh.kv0[i0] + s, w, lane2);
+                    staged = (l + 1) * MG + i0;
+                }
             }
             bar_nf();   // pk consumed
+            PMSTAMP(l == 12, 7);
+            PMSTAMP(l == 23, 14);
         }
         // ================= logits of step s: rows 64 r .. 64 r + 63 (+ EOS on r = 15) =================
         {
@@ -620,6 +651,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             }
             __syncthreads();   // sh.at.lg / sh.samp consumed
         }
+        PMSTAMP(true, 15);
         ++n_exec;
     }
     // fused greedy at the launch's step cap: the live sequences' last tokens are unresolved

@@ -527,7 +527,9 @@ class Engine:
             outs.append(audio)
         _check(lib().gsv_vits_decode_batch_async(self.h, len(items), arr, ctypes.c_float(noise_scale),
                                                  _stream()), "gsv_vits_decode_batch_async")
-        self._vits_batch_keep = (arr, keep, outs)   # items and device buffers live until the wait
+        # items and device buffers live until the wait -- also a previous batch's, which this
+        # call only ordered behind the engine stream (its lanes may still read them)
+        self._vits_batch_keep = (arr, keep, outs, getattr(self, "_vits_batch_keep", None))
         return outs
 
     def vits_batch_wait(self):

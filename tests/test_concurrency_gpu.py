@@ -107,3 +107,32 @@ def test_engines_capturing_on_concurrent_threads():
     finally:
         for e in engines:
             e.close()
+
+
+def test_back_to_back_async_batches_on_the_f32_path():
+    """Two gsv_vits_decode_batch_async batches in a row from a stream other than the engine
+    stream, on the f32 conv path (convh = 0, no fp16-range host sync), segmented and per
+    lane: the second batch's setup (offset tables, zeroed buffers) waits for the first
+    batch's lanes, so each batch equals its synchronous call bit for bit."""
+    import torch
+    from genie_tts_amd.engine import Engine
+    e = Engine({k: v for k, v in character("v2").items() if k in ("t2s_encoder", "t2s", "vits")}, "v2")
+    try:
+        e.set_option("convh", 0)
+        first, second = _items(5, 30, "ba"), _items(4, 52, "bb")
+        for seg in (1, 0):
+            e.set_option("seg_vocoder", seg)
+            want = [[o.cpu().numpy() for o in e.vits_decode_batch(b)] for b in (first, second)]
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                outs_a = e.vits_decode_batch_async(first)
+                outs_b = e.vits_decode_batch_async(second)
+                e.vits_batch_wait()
+            st.synchronize()
+            for k, (outs, w) in enumerate(zip((outs_a, outs_b), want)):
+                for i, (o, x) in enumerate(zip(outs, w)):
+                    np.testing.assert_array_equal(o.cpu().numpy(), x, err_msg=f"seg {seg} batch {k} item {i}")
+    finally:
+        e.set_option("seg_vocoder", 1)
+        e.set_option("convh", 1)
+        e.close()
