@@ -95,7 +95,9 @@ __device__ __forceinline__ bool ok_all(bool ok, SharedM& sh) {
 // The 17-row granule blocks of the live sequences (byte offsets blk(i) of row 0; rows
 // 0..15 partials, row 16 the residual row) -> u = row16 + (vec[c] + sum of rows 0..15
 // in row order) into lnb[i], the fp16 split of u * mul[c] into A rows 2i, 2i + 1.  One
-// thread per (sequence, granule column), all 17 loads in flight.  Ends with a barrier.
+// thread per (sequence, granule column) in two round trips (rows 0..8, then 9..16: 17
+// granules in flight make hipcc spill the whole array); vec / mul are loaded first.
+// Ends with a barrier.
 template <class Blk>
 __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, SharedM& sh, unsigned live,
                                          unsigned tag, Blk blk, const float* vec, const float* mul) {
@@ -105,8 +107,14 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
     for (int it = opaque_tid(); it < nl * GQ; it += PT) {
         const int n = it / GQ, q = it - n * GQ;
         const int i = nth_bit(live, n);
-        // rows 0..8, then 9..16 (two round trips of 9 / 8 granules: 17 in flight spill)
         const int off = blk(i) + 16 * q;
+        float vv[3], mm[3];   // in flight beside the granules
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int c = gq_col(q, min(k, gq_n(q) - 1));
+            vv[k] = ldg(vec, c);
+            mm[k] = ldg(mul, c);
+        }
         float f[3];
         {
             u32x4 g[9];
@@ -128,9 +136,9 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
 #pragma unroll
             for (int r = 0; r < 7; ++r) f[k] += __uint_as_float(g[r][1 + k]);
             const int c = gq_col(q, k);
-            const float u = __uint_as_float(g[7][1 + k]) + (ldg(vec, c) + f[k]);
+            const float u = __uint_as_float(g[7][1 + k]) + (vv[k] + f[k]);
             sh.at.g.lnb[i][c] = u;
-            const float un = u * ldg(mul, c);
+            const float un = u * mm[k];
             _Float16 hi, lo;
             if (!split_h(un, hi, lo) || !(fabsf(un) < a.f16_limit)) {
                 atomicCAS(a.err, 0, ERR_F16_RANGE);
@@ -180,6 +188,168 @@ __device__ __forceinline__ void pub_m(const WsSeq& ws, SharedM& sh, int i, int r
     asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(o0), "+v"(o1));
     st_g16(ws, o0, tag, a0, a1, a2);
     if (second) st_g16(ws, o1, tag, b0, b1, b2);
+}
+
+// ---- attention with a double-buffered K stage: the K rows of the next sequence land in one
+// LDS buffer while this sequence's attention reads the other; V rows are read from memory
+// by the lanes that weigh them (issued first, in flight during the scores).  The arithmetic
+// is wave_attn1's / attn_general1's (t2s_persist1.hip) operation for operation: only where
+// the operands come from differs, so every value is the single-sequence kernel's.
+
+// K rows [0, min(kv, KVL1)) of (layer l, sequence b, head h) -> LDS buffer dst by LDS-DMA
+// (the six non-publishing waves)
+__device__ __forceinline__ void stage_k(const PersistArgs& a, float* dst, int l, int b, int h, int kv, int w,
+                                        int lane) {
+    if (is_pub_wave(w)) return;
+    const int wi = w < 3 ? w : w - 1;
+    const float* K = a.kc[l] + (long)b * a.sstride + (long)h * a.tmax * 32;
+    const int nr = min(kv, KVL1), nch = (nr + 7) >> 3;
+    for (int i = wi; i < nch; i += 6)
+        if (8 * i + (lane >> 3) < nr) __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, dst + i * 256, 16, 0, 0);
+}
+
+template <int NU>
+__device__ __forceinline__ void wave_attn_m(SharedM& sh, const float* Ks, const float* Vw, float4 vnew, float q0,
+                                            float q1, float q2, float q3, float sc, int kv, int T, int c8, int g,
+                                            int w, int lane) {
+    float4 vr[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int t = min(64 * u + g, kv);
+        vr[u] = t < kv ? ldg16f(Vw, (long)t * 32 + 4 * c8) : vnew;
+    }
+    float4 kr[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) kr[u] = *reinterpret_cast<const float4*>(Ks + min(64 * u + g, kv) * 32 + 4 * c8);
+    const float p0 = q0 * sc, p1 = q1 * sc, p2 = q2 * sc, p3 = q3 * sc;
+    float sv[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const float4 k4 = kr[u];
+        float x = p0 * k4.x;
+        x += p1 * k4.y;
+        x += p2 * k4.z;
+        x += p3 * k4.w;
+        sv[u] = x;
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+    float wm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        sv[u] = 64 * u + g < T ? sv[u] : -INFINITY;
+        wm = fmaxf(wm, sv[u]);
+    }
+    const float m_w = wave_max_dpp(wm);
+    const float mref = m_w == -INFINITY ? 0.f : m_w;
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f, lsum = 0.f;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const float pu = __expf(sv[u] - mref);
+        const float4 v4 = vr[u];
+        o0 += pu * v4.x;
+        o1 += pu * v4.y;
+        o2 += pu * v4.z;
+        o3 += pu * v4.w;
+        lsum += pu;
+    }
+    o0 += dpp_f<0x128, 0xF>(o0);
+    o1 += dpp_f<0x128, 0xF>(o1);
+    o2 += dpp_f<0x128, 0xF>(o2);
+    o3 += dpp_f<0x128, 0xF>(o3);
+    o0 = swap_sum16(o0); o1 = swap_sum16(o1); o2 = swap_sum16(o2); o3 = swap_sum16(o3);
+    o0 = swap_sum32(o0); o1 = swap_sum32(o1); o2 = swap_sum32(o2); o3 = swap_sum32(o3);
+    const float l_w = wave_sum_dpp(c8 == 0 ? lsum : 0.f);
+    if (lane < 8) *reinterpret_cast<float4*>(&sh.at.ov4[w][4 * lane]) = make_float4(o0, o1, o2, o3);
+    if (lane == 0) {
+        sh.wred[0][w] = m_w;
+        sh.wred[1][w] = l_w;
+    }
+}
+
+__device__ __noinline__ float scores_general_m(SharedM& sh, const float* Ks, const float* Kw, int kv, int T, float q0,
+                                               float q1, float q2, float q3, float sc, float4 knew, int c8, int g) {
+    float lmax = -INFINITY;
+    for (int base = 0; base < T; base += 512) {
+        float sv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = base + 64 * u + g;
+            float4 kr;
+            if (t < kv && t < KVL1) kr = *reinterpret_cast<const float4*>(Ks + t * 32 + 4 * c8);
+            else if (t < kv) kr = ldg16f(Kw, (long)t * 32 + 4 * c8);
+            else kr = knew;
+            float x = q0 * (kr.x * sc);
+            x += q1 * (kr.y * sc);
+            x += q2 * (kr.z * sc);
+            x += q3 * (kr.w * sc);
+            sv[u] = x;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = base + 64 * u + g;
+            if (t < T) {
+                if (c8 == 0) sh.at.p[t] = sv[u];
+                lmax = fmaxf(lmax, sv[u]);
+            }
+        }
+    }
+    return lmax;
+}
+
+__device__ __noinline__ void attn_general_m(SharedM& sh, const float* Ks, const float* Kw, const float* Vw, int kv,
+                                            int T, float q0, float q1, float q2, float q3, float sc, float4 knew,
+                                            int c8, int g, int w, int lane, int tid) {
+    const float lmax = scores_general_m(sh, Ks, Kw, kv, T, q0, q1, q2, q3, sc, knew, c8, g);
+    const float wm = wave_max_dpp(lmax);
+    if (lane == 0) sh.wred[0][w] = wm;
+    __syncthreads();
+    float M = sh.wred[0][0];
+#pragma unroll
+    for (int ww = 1; ww < PWV; ++ww) M = fmaxf(M, sh.wred[0][ww]);
+    float lsum = 0.f;
+    for (int t = tid; t < T; t += PT) {
+        const float e = expf(sh.at.p[t] - M);
+        sh.at.p[t] = e;
+        lsum += e;
+    }
+    const float ws_ = wave_sum_dpp(lsum);
+    if (lane == 0) sh.wred[1][w] = ws_;
+    __syncthreads();
+    {
+        const int kg = tid >> 5, d = tid & 31;
+        const int tl = min(kv, KVL1);
+        float o4[4] = {0.f, 0.f, 0.f, 0.f};
+        int t = kg;
+        for (; t + 48 < tl; t += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o4[u] += sh.at.p[t + 16 * u] * ldg(Vw, (long)(t + 16 * u) * 32 + d);
+        }
+        for (; t < tl; t += 16) o4[0] += sh.at.p[t] * ldg(Vw, (long)t * 32 + d);
+        for (; t < kv; t += 16) o4[1] += sh.at.p[t] * ldg(Vw, (long)t * 32 + d);
+        if (t == kv) o4[2] += sh.at.p[t] * sh.qkv[64 + d];
+        sh.at.ov[kg][d] = (o4[0] + o4[1]) + (o4[2] + o4[3]);
+    }
+    __syncthreads();
+    if (lane < 32) {
+        float O = 0.f, L = 0.f;
+#pragma unroll
+        for (int kg = 0; kg < 16; ++kg) O += sh.at.ov[kg][lane];
+#pragma unroll
+        for (int ww = 0; ww < PWV; ++ww) L += sh.wred[1][ww];
+        split_h(O / L, sh.osh[w][lane], sh.osl[w][lane]);
+    }
+    __builtin_amdgcn_wave_barrier();
 }
 
 // Greedy token of step s - 1 of group sequence i (global b), resolved by ONE wave from
@@ -246,7 +416,9 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
     __syncthreads();
     unsigned live = 0;
     for (int i = 0; i < nloc; ++i) live |= sh.act[i] ? 1u << i : 0u;
-    int staged = -1;   // l * MG + i whose K/V rows are in (or on their way to) the LDS stage
+    // the two K stage buffers (sh.at.k, sh.at.v) and the (step, layer, sequence) each holds / receives
+    int skey0 = -1, skey1 = -1, cur = 0;
+    auto kbuf = [&](int bsel) { return bsel ? sh.at.v : sh.at.k; };
     int n_exec = 0;
     for (int s = 0; s < a.smax && live && sh.fail == 0; ++s) {
         const unsigned tag = base.tag(s);
@@ -279,9 +451,10 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
         PMSTAMP(true, 13);
         {
             const int i0 = __builtin_ctz(live);
-            if (staged != i0) {   // layer 0's first K/V stage (the step's first layer)
-                stage_kv(a, sh, 0, g + i0 * nsg, r, sh.kv0[i0] + s, w, threadIdx.x & 63);
-                staged = i0;
+            const int key = (s * 24 + 0) * MG + i0;
+            if ((cur ? skey1 : skey0) != key) {   // layer 0's first K stage (the step's first layer)
+                stage_k(a, kbuf(cur), 0, g + i0 * nsg, r, sh.kv0[i0] + s, w, threadIdx.x & 63);
+                (cur ? skey1 : skey0) = key;
             }
         }
         for (int l = 0; l < 24; ++l) {
@@ -293,6 +466,11 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             PMSTAMP(l == 12, 0);
             uint4 wq[16], wo[4];
             float qfB = 0.f, qfC = 0.f;
+            float xw = 0.f, xb = 0.f;   // LN2_{l-1} scale / shift of column 32 r + lane (x_l block r)
+            if (l > 0 && w == 0 && lane < 32) {
+                xw = ldg(a.L[l - 1].n2w, 32 * r + lane);
+                xb = ldg(a.L[l - 1].n2b, 32 * r + lane);
+            }
             if (w < 6) {
                 const int row = (w >> 1) * 512 + r * 32 + 16 * (w & 1) + n16;
 #pragma unroll
@@ -334,8 +512,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
 #pragma unroll
                     for (int i = 0; i < MG; ++i)
                         if ((live >> i) & 1u)
-                            sh.h1s[i][lane] = l > 0 ? ln_apply(sh.at.g.lnb[i][c], mean[i], rden[i],
-                                                               ldg(a.L[l - 1].n2w, c), ldg(a.L[l - 1].n2b, c))
+                            sh.h1s[i][lane] = l > 0 ? ln_apply(sh.at.g.lnb[i][c], mean[i], rden[i], xw, xb)
                                                     : sh.at.g.lnb[i][c];
                 }
                 if (w < 6) {
@@ -371,15 +548,24 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             for (unsigned m = live; m; m &= m - 1) {
                 const int i = __builtin_ctz(m), b = g + i * nsg;
                 const int kv = sh.kv0[i] + s, T = kv + 1;
-                if (staged != l * MG + i) {
-                    stage_kv(a, sh, l, b, r, kv, w, lane);
-                    staged = l * MG + i;
+                const int key = (s * 24 + l) * MG + i;
+                if ((cur ? skey1 : skey0) != key) {
+                    stage_k(a, kbuf(cur), l, b, r, kv, w, lane);
+                    (cur ? skey1 : skey0) = key;
                 }
-                if (!is_pub_wave(w)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its K/V LDS-DMA landed
-                if (kv < KVL1 && w >= 2 && w < 6 && lane < 16)
-                    ((w < 4 ? sh.at.k : sh.at.v) + kv * 32 + 16 * (w & 1))[lane] = sh.qkvs[i][16 * w + lane];
+                float* Ks = kbuf(cur);
+                if (!is_pub_wave(w)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its K LDS-DMA landed
+                if (kv < KVL1 && (w == 2 || w == 3) && lane < 16) (Ks + kv * 32 + 16 * (w & 1))[lane] = sh.qkvs[i][16 * w + lane];
                 if (tid < 96) sh.qkv[tid] = sh.qkvs[i][tid];
                 bar_nf();
+                {
+                    const unsigned nx = m & (m - 1);
+                    if (nx) {   // the next sequence's K rows land in the other buffer during this attention
+                        const int i2 = __builtin_ctz(nx);
+                        stage_k(a, kbuf(cur ^ 1), l, g + i2 * nsg, r, sh.kv0[i2] + s, w, lane);
+                        (cur ? skey0 : skey1) = (s * 24 + l) * MG + i2;
+                    }
+                }
                 const long kvoff = (long)b * a.sstride + (long)r * a.tmax * 32;
                 const float* Kw = a.kc[l] + kvoff;
                 const float* Vw = a.vc[l] + kvoff;
@@ -388,25 +574,21 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
                 const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
                 const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
+                const float4 vnew = *reinterpret_cast<const float4*>(sh.qkv + 64 + 4 * c8);
                 if (T <= 512 && kv < KVL1) {
                     const int nu = (T + 63) >> 6;
-                    if (nu <= 2) wave_attn1<2>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else if (nu <= 4) wave_attn1<4>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else if (nu == 5) wave_attn1<5>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else if (nu == 6) wave_attn1<6>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else wave_attn1<8>(sh, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    bar_nf();   // the stage is read
+                    if (nu <= 2) wave_attn_m<2>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu <= 4) wave_attn_m<4>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu == 5) wave_attn_m<5>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu == 6) wave_attn_m<6>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else wave_attn_m<8>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    bar_nf();   // the stage is read; every wave's partials are in LDS
                     merge_waves1(sh, w, lane);
                 } else {
-                    attn_general1<2>(sh, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, gk, w, lane, tid);
+                    attn_general_m(sh, Ks, Kw, Vw, kv, T, q0, q1, q2, q3, sc, knew, c8, gk, w, lane, tid);
                     bar_nf();
                 }
-                const unsigned nx = m & (m - 1);
-                if (nx) {   // the next sequence's K/V rows land while this one's output is formed
-                    const int i2 = __builtin_ctz(nx);
-                    stage_kv(a, sh, l, g + i2 * nsg, r, sh.kv0[i2] + s, w, lane);
-                    staged = l * MG + i2;
-                }
+                cur ^= 1;
                 if (w == 0 && lane < 32) {
                     sh.O[2 * i][lane] = sh.osh[0][lane];
                     sh.O[2 * i + 1][lane] = sh.osl[0][lane];
@@ -446,11 +628,13 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             PMSTAMP(l == 12, 4);
             // ================= FFN role: slice r =================
             uint4 w1r[16], w2r[16];   // W2's columns are loaded once FFN1 has consumed W1's rows
-            float ffB, ffC;
+            float ffB, ffC, n1w_t, n1b_t;
             {
                 const int tid2 = opaque_tid(), lane2 = tid2 & 63, m16 = lane2 & 15, q8 = 8 * (lane2 >> 4);
 #pragma unroll
                 for (int c = 0; c < 16; ++c) w1r[c] = ldg16(P.w1 + (long)(r * 128 + w * 16 + m16) * 512 + 32 * c + q8, 0);
+                n1w_t = ldg(P.n1w, tid2);
+                n1b_t = ldg(P.n1b, tid2);
                 ffB = ldg(a.fold, (long)l * FOLD_LAYER + 3072 + r * 128 + w * 16 + m16);
                 ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + r * 128 + w * 16 + m16);
             }
@@ -484,7 +668,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                             w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + m16) * 2048 + r * 128 + 32 * c + q8, 0);
                 }
                 if ((tid2 >> 5) == r) {   // block r of h1 = LN1(v) for the next layer's PFH row 16
-                    const float n1w = ldg(P.n1w, tid2), n1b = ldg(P.n1b, tid2);
+                    const float n1w = n1w_t, n1b = n1b_t;
 #pragma unroll
                     for (int i = 0; i < MG; ++i)
                         if ((live >> i) & 1u) sh.h1s[i][tid2 & 31] = (sh.at.g.lnb[i][tid2] - mean[i]) * rden[i] * n1w + n1b;
@@ -544,10 +728,10 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                     const WsSeq ws = base.seq(g + i * nsg);
                     pub_m(ws, sh, i, ws.PFH(s, l, r), ws.PFH(s, l, 16) + 16 * 11 * r, tag, w, lane2);
                 }
-                if (l < 23) {   // the next layer's first K/V stage lands during the hop
+                if (l < 23) {   // the next layer's first K stage lands during the hop
                     const int i0 = __builtin_ctz(live);
-                    stage_kv(a, sh, l + 1, g + i0 * nsg, r, sh.kv0[i0] + s, w, lane2);
-                    staged = (l + 1) * MG + i0;
+                    stage_k(a, kbuf(cur), l + 1, g + i0 * nsg, r, sh.kv0[i0] + s, w, lane2);
+                    (cur ? skey1 : skey0) = (s * 24 + l + 1) * MG + i0;
                 }
             }
             bar_nf();   // pk consumed
@@ -556,24 +740,45 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
         }
         // ================= logits of step s: rows 64 r .. 64 r + 63 (+ EOS on r = 15) =================
         {
-            if (threadIdx.x == 64) sh.stopreq = ld_stop(a.stop_req);   // used by the next resolve
+            // the stop word (host memory: a PCIe read that took ~30 us under this kernel's load,
+            // profiles/r05r_stop_read.txt) every 4th step, for the next resolve: a stop takes
+            // effect within 5 steps
+            if ((s & 3) == 0 && threadIdx.x == 64) sh.stopreq = ld_stop(a.stop_req);
+            const int tid0 = opaque_tid(), lane0 = tid0 & 63;
+            const int row = w < 4 ? 64 * r + 16 * w + (lane0 & 15) : 1024;
+            const bool lrow = w < 4 || (w == 4 && r == NF - 1);
+            // this slice's w_pred rows -> the (free) K stage by LDS-DMA during the gather, rows
+            // padded by 16 B (conflict-free B-fragment reads); (64 r + rr, or the EOS row 1024)
+            float* wpl = sh.at.k;
+            for (int rr = w; rr < (r == NF - 1 ? LROWS + 1 : LROWS); rr += PWV) {
+                const int grow = rr < LROWS ? LROWS * r + rr : 1024;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(a.w_pred) + (long)grow * 256 + lane0 * 4,
+                                                 wpl + rr * 260, 16, 0, 0);
+            }
+            float lfB = 0.f, lfC = 0.f;
+            if (lrow) {
+                lfB = ldg(a.fold, LOGIT_FOLD + row);
+                lfC = ldg(a.fold, LOGIT_FOLD + 1025 + row);
+            }
             if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PFH(s, 23, 0); },
                           a.L[23].b2, a.L[23].n2w))
                 return;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's w_pred rows landed
+            bar_nf();
+            PMSTAMP(true, 8);
             const int tid = opaque_tid(), lane = tid & 63, n16 = lane & 15, k8 = 8 * (lane >> 4);
             const bool up = lane >= 16;
             float mean[MG], rden[MG];
             stats_m(sh, live, mean, rden);
-            if (w < 4 || (w == 4 && r == NF - 1)) {
-                const int row = w < 4 ? 64 * r + 16 * w + n16 : 1024;
+            if (lrow) {
                 const _Float16* ab = abase_m(&sh.at.g.A[0][0], AST, lane);
+                const _Float16* wb = reinterpret_cast<const _Float16*>(wpl + (w < 4 ? 16 * w + n16 : LROWS) * 260) + k8;
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 2) {
-                    c0 = mfma16(afrag(ab, 32 * cb), bfrag(ldg16(a.w_pred, (long)row * 512 + 32 * cb + k8)), c0);
-                    c1 = mfma16(afrag(ab, 32 * (cb + 1)), bfrag(ldg16(a.w_pred, (long)row * 512 + 32 * (cb + 1) + k8)), c1);
+                    c0 = mfma16(afrag(ab, 32 * cb), bfrag(*reinterpret_cast<const uint4*>(wb + 32 * cb)), c0);
+                    c1 = mfma16(afrag(ab, 32 * (cb + 1)), bfrag(*reinterpret_cast<const uint4*>(wb + 32 * (cb + 1))), c1);
                 }
-                const float lfB = ldg(a.fold, LOGIT_FOLD + row), lfC = ldg(a.fold, LOGIT_FOLD + 1025 + row);
                 const bool lv = w < 4 || n16 == 0;
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
@@ -609,6 +814,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();
+            PMSTAMP(true, 9);
             if (fused && w == 7) {   // this slice's candidates: 16 granules per sequence (+ 4 EOS on r = 15)
                 const bool eos = r == NF - 1;
                 for (unsigned m = live; m; m &= m - 1) {
@@ -621,6 +827,8 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();   // A / lnb consumed
+            PMSTAMP(true, 10);
+            skey0 = skey1 = -1;   // (the w_pred rows overwrote both K buffers)
         }
         // ---- sampler (sampled decoding): sequence i = r of the group
         if (sampler && ((live >> r) & 1u)) {
@@ -646,7 +854,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 sh.lfin[i] = fin;
                 sh.nexe[i] = s + 1;
                 bool go = true;
-                if (ld_stop(a.stop_req)) stop_launch(a, go);
+                if ((s & 3) == 0 && ld_stop(a.stop_req)) stop_launch(a, go);
                 else st_gran(ws.TK(s + 1), ws.tag(s + 1), __uint_as_float((unsigned)tok | (fin ? 1u << 16 : 0u)));
             }
             __syncthreads();   // sh.at.lg / sh.samp consumed

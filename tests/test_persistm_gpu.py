@@ -1,11 +1,17 @@
 """GPU: the batched persistent decode (k_decode_persistm, t2s_persistm.hip; the batch on
-the MFMA M dimension, up to 4 sequences per group of 16 workgroups) against the
-multi-sequence kernel (k_decode_persist1m) and against single launches (k_decode_persist1).
+the MFMA M dimension, up to 4 sequences per group of 16 workgroups) against single
+launches (k_decode_persist1) and the per-step graph path (t2s_decode.hip), both pinned to
+the oracle by test_persist_gpu.py / test_golden_gpu.py.
 
 Every sequence's values are the single-sequence kernel's (same K chains, folds and sum
 orders; an MFMA output row depends on its own A row only), so greedy tokens are
-bit-identical to a launch of its own and to persist1m, and sampled tokens (Philox top-k)
-to persist1m's sampler.  Reference loop: Inference.py:95-106 (t2s_stage_decoder_fp32.onnx).
+bit-identical to a launch of its own; sampled tokens (Philox top-k) equal the graph
+path's sampler.  Reference loop: Inference.py:95-106 (t2s_stage_decoder_fp32.onnx).
+
+test_persist1m_long_context_deviation records a case found this round where the
+multi-sequence kernel k_decode_persist1m (B = 2..31) picks a different token than a
+single launch, the graph path and persistm (sequence 62 of the B = 64 set, 730 prompt
+positions); cause not found yet.
 """
 import pytest
 
@@ -27,20 +33,20 @@ def eng():
 
 
 def _both(eng, inps, sp):
+    """persistm's tokens and the per-step graph path's"""
     n0 = eng.counter("persist_launches")
-    eng.set_option("persistm", 1)
     a = [x.tolist() for x in eng.t2s_generate(inps, sp)]
-    eng.set_option("persistm", 0)
+    assert eng.counter("persist_launches") == n0 + 1   # one batched persistent launch
+    eng.set_option("persist", 0)
     try:
         b = [x.tolist() for x in eng.t2s_generate(inps, sp)]
     finally:
-        eng.set_option("persistm", 1)
-    assert eng.counter("persist_launches") >= n0 + 2   # both ran as persistent launches
+        eng.set_option("persist", 1)
     return a, b
 
 
 @pytest.mark.parametrize("B", [2, 4, 5, 17, 40, 64])
-def test_batched_matches_multi_sequence_kernel(eng, B):
+def test_batched_matches_graph_path(eng, B):
     from genie_tts_amd.engine import make_sampler
     inps = [t2s_inputs(R=10 + 3 * i, S=8 + 2 * i, H=30 + 6 * i, tag=f"pm{B}_{i}") for i in range(B)]
     a, b = _both(eng, inps, make_sampler(force_steps=22))
@@ -48,16 +54,36 @@ def test_batched_matches_multi_sequence_kernel(eng, B):
         assert a[i] == b[i], f"sequence {i}"
 
 
-def test_batched_matches_single_launches(eng):
+@pytest.mark.parametrize("B,tag", [(7, "pms"), (64, "pm64_")])
+def test_batched_matches_single_launches(eng, B, tag):
     from genie_tts_amd.engine import make_sampler
-    inps = [t2s_inputs(R=12 + 5 * i, S=9 + 3 * i, H=40 + 9 * i, tag=f"pms{i}") for i in range(7)]
-    sp = make_sampler(force_steps=30)
+    if B == 64:
+        inps = [t2s_inputs(R=10 + 3 * i, S=8 + 2 * i, H=30 + 6 * i, tag=f"{tag}{i}") for i in range(B)]
+        sp = make_sampler(force_steps=22)
+    else:
+        inps = [t2s_inputs(R=12 + 5 * i, S=9 + 3 * i, H=40 + 9 * i, tag=f"{tag}{i}") for i in range(B)]
+        sp = make_sampler(force_steps=30)
     got = [x.tolist() for x in eng.t2s_generate(inps, sp)]
     assert got == [eng.t2s_generate([inp], sp)[0].tolist() for inp in inps]
 
 
+@pytest.mark.xfail(reason="k_decode_persist1m deviates from a single launch on this input (DESIGN 4.7); "
+                          "persistm, the graph path and single launches agree", strict=False)
+def test_persist1m_long_context_deviation(eng):
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=10 + 3 * i, S=8 + 2 * i, H=30 + 6 * i, tag=f"pm64_{i}") for i in (62, 0)]
+    sp = make_sampler(force_steps=6)
+    single = eng.t2s_generate([inps[0]], sp)[0].tolist()
+    eng.set_option("persistm", 0)
+    try:
+        got = eng.t2s_generate(inps, sp)[0].tolist()
+    finally:
+        eng.set_option("persistm", 1)
+    assert got == single
+
+
 @pytest.mark.parametrize("top_k,temp", [(15, 1.0), (5, 0.8)])
-def test_batched_sampled_matches_multi_sequence_kernel(eng, top_k, temp):
+def test_batched_sampled_matches_graph_path(eng, top_k, temp):
     from genie_tts_amd.engine import make_sampler
     inps = [t2s_inputs(R=12 + i, S=9 + i, H=36 + 2 * i, tag=f"pmk{i}") for i in range(6)]
     a, b = _both(eng, inps, make_sampler(top_k=top_k, temperature=temp, greedy=False, seed=77, force_steps=24))
@@ -104,7 +130,7 @@ def test_batched_fp16_range_fallback(eng):
 
 def test_batched_full_500_step_loop(eng):
     """The reference's whole loop (Inference.py:95, range(500)) with no EOS (random
-    weights): keys grow past the LDS stage; tokens equal persist1m's at the maximum length."""
+    weights): keys grow past the LDS stage; tokens equal the graph path's at the maximum length."""
     from genie_tts_amd.engine import make_sampler
     inps = [t2s_inputs(R=40 + 3 * i, S=30 + 2 * i, H=160 + 8 * i, tag=f"pm500_{i}") for i in range(6)]
     a, b = _both(eng, inps, make_sampler())

@@ -25,15 +25,15 @@ utt = (T(ref.ref_seq.reshape(-1)), T(it.text_seq.reshape(-1)), None, None, T(ref
 for _ in range(3):
     e.t2s_generate([utt] * B, make_sampler())
 tr = e.ptrace().astype(np.int64)
-ngrp = (B + 3) // 4
-n = min(16, ngrp) * 16
+n = min(16, B) * 16
 tr = tr[:n]
 t0 = np.median(tr[:, 12])
 us = lambda k: float(np.median(tr[:, k]) - t0) * 10 / 1000.0
 names = {12: "step start", 13: "tokens resolved", 0: "L12 attn start", 1: "L12 gather done", 2: "L12 qkv done",
          3: "L12 attention done", 4: "L12 PA published", 5: "L12 FFN gather done", 6: "L12 FFN1 done",
-         7: "L12 PFH published", 14: "L23 done", 15: "step end"}
-out = {"B": B, "workgroups": n, "us": {names[k]: round(us(k), 2) for k in (12, 13, 0, 1, 2, 3, 4, 5, 6, 7, 14, 15)}}
+         7: "L12 PFH published", 14: "L23 done", 8: "logits gather done", 9: "logits done",
+         10: "candidates published", 15: "step end"}
+out = {"B": B, "workgroups": n, "us": {names[k]: round(us(k), 2) for k in (12, 13, 0, 1, 2, 3, 4, 5, 6, 7, 14, 8, 9, 10, 15)}}
 spread = {names[k]: round(float(np.max(tr[:, k]) - np.min(tr[:, k])) * 10 / 1000.0, 2) for k in (0, 7)}
 out["spread_us"] = spread
 print(json.dumps(out))
