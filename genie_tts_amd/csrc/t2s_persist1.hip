@@ -631,11 +631,17 @@ __device__ __forceinline__ void dma_half(const float* src, float* dst, int h, in
 __device__ __forceinline__ void pf_wait(int ticks) {
     for (int i = 0; i < ticks; ++i) __builtin_amdgcn_s_sleep(32);
 }
-// LN2 of layer l - 1 -> sh.p2, by waves 0..5 (call from every wave; l > 0)
+// LN2 of layer l - 1 -> sh.p2 (call from every wave; l > 0), by waves 0, 1, 2, 4, 5, 6:
+// the hop-B gather's polling waves, whose in-order vmcnt waits retire these DMAs before
+// the gather's last barrier, after which sh.p2 is read.  (Waves 3 and 7 never poll, and
+// the multi-sequence kernel has no fenced barrier between a prefetch and the next
+// gather: a DMA of wave 3 was not ordered before its readers.  Hardening found while
+// looking for the r05 persist1m deviation, profiles/r05x_persist1m_deviation.txt; it
+// did not change that case.)
 __device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int lane) {
     if (w < 2) dma_half(Q.b2, sh.p2[0], w & 1, lane);
-    else if (w < 4) dma_half(Q.n2w, sh.p2[1], w & 1, lane);
-    else if (w < 6) dma_half(Q.n2b, sh.p2[2], w & 1, lane);
+    else if (w == 2 || w == 4) dma_half(Q.n2w, sh.p2[1], w == 4, lane);
+    else if (w == 5 || w == 6) dma_half(Q.n2b, sh.p2[2], w == 6, lane);
 }
 
 // Hop B: u = h1_{l-1} + (b2 + sum_j PF[l-1][j]) (l >= 1; the partials summed in
