@@ -28,6 +28,10 @@ for s in $STEPS; do
              timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_${TAG}_mfma_$w -o pmc -- $cmd > gpurun_out/${TAG}_pmc_mfma_$w.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_mfma_$w.log; exit 1; }
              python tools/mfma_util.py gpurun_out/pmc_${TAG}_mfma_$w > gpurun_out/${TAG}_mfma_$w.txt 2>&1; head -30 gpurun_out/${TAG}_mfma_$w.txt
            done ;;
+    mfmab) # the same MFMA-busy pass over one batch64 batch (k_decode_persistm, k_mrf_pair, the packed prefill)
+           rm -rf gpurun_out/pmc_${TAG}_mfma_batch64
+           timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_${TAG}_mfma_batch64 -o pmc -- python3 bench.py --workload batch64 --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/${TAG}_pmc_mfma_batch64.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_mfma_batch64.log; exit 1; }
+           python tools/mfma_util.py gpurun_out/pmc_${TAG}_mfma_batch64 > gpurun_out/${TAG}_mfma_batch64.txt 2>&1; head -30 gpurun_out/${TAG}_mfma_batch64.txt ;;
     pmc)   for c in FETCH_SIZE WRITE_SIZE; do
              rm -rf gpurun_out/pmc_${TAG}_$c
              timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$c -o pmc -- python3 bench.py --no-cpu-baseline --concurrent-streams 0 --steps 3 --warmup 1 > gpurun_out/${TAG}_pmc_$c.log 2>&1 || { tail -30 gpurun_out/${TAG}_pmc_$c.log; exit 1; }
