@@ -204,20 +204,33 @@ __device__ __forceinline__ void stage_k(const PersistArgs& a, float* dst, int l,
     const int wi = w < 3 ? w : w - 1;
     const float* K = a.kc[l] + (long)b * a.sstride + (long)h * a.tmax * 32;
     const int nr = min(kv, KVL1), nch = (nr + 7) >> 3;
-    for (int i = wi; i < nch; i += 6)
-        if (8 * i + (lane >> 3) < nr) __builtin_amdgcn_global_load_lds(K + (long)i * 256 + lane * 4, dst + i * 256, 16, 0, 0);
+    for (int i = wi; i < nch; i += 6) {
+        if (8 * i + (lane >> 3) < nr) {
+            // from inline asm: the waitcnt pass would put a vmcnt(0) before every LDS read of
+            // the attention running beside this DMA (it cannot tell the two K buffers apart),
+            // i.e. wait for the next sequence's rows; the wait is the explicit one before use
+            const unsigned la = __builtin_amdgcn_readfirstlane(
+                (unsigned)(size_t)(__attribute__((address_space(3))) char*)(dst + i * 256));
+            asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(K + (long)i * 256 + lane * 4)
+                         : "memory", "m0");
+        }
+    }
 }
 
-template <int NU>
-__device__ __forceinline__ void wave_attn_m(SharedM& sh, const float* Ks, const float* Vw, float4 vnew, float q0,
-                                            float q1, float q2, float q3, float sc, int kv, int T, int c8, int g,
-                                            int w, int lane) {
-    float4 vr[NU];
+// This lane's V rows t = min(64 u + g, kv) (u < 8) of one sequence: rows < kv from memory,
+// row kv (and the clamped ones past it) the new row -- the values the LDS stage held.
+__device__ __forceinline__ void load_v8(float4 (&vr)[8], const float* Vw, float4 vnew, int kv, int c8, int g) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
+    for (int u = 0; u < 8; ++u) {
         const int t = min(64 * u + g, kv);
         vr[u] = t < kv ? ldg16f(Vw, (long)t * 32 + 4 * c8) : vnew;
     }
+}
+
+template <int NU>
+__device__ __forceinline__ void wave_attn_m(SharedM& sh, const float* Ks, const float4 (&vr)[8], float q0,
+                                            float q1, float q2, float q3, float sc, int kv, int T, int c8, int g,
+                                            int w, int lane) {
     float4 kr[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) kr[u] = *reinterpret_cast<const float4*>(Ks + min(64 * u + g, kv) * 32 + 4 * c8);
@@ -545,6 +558,14 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             }
             bar_nf();   // q/k/v of every sequence; the A tile / lnb are free (the general path's scores)
             PMSTAMP(l == 12, 2);
+            // V rows of the next sequence in registers, loaded while this one's attention runs
+            float4 vpre[8];
+            auto v_of = [&](int ii) {   // (after the q/k/v barrier: qkvs holds every sequence's new row)
+                const int c8 = lane & 7, gk = (w << 3) | (lane >> 3);
+                const float* Vw = a.vc[l] + (long)(g + ii * nsg) * a.sstride + (long)r * a.tmax * 32;
+                load_v8(vpre, Vw, *reinterpret_cast<const float4*>(&sh.qkvs[ii][64 + 4 * c8]), sh.kv0[ii] + s, c8, gk);
+            };
+            v_of(__builtin_ctz(live));
             for (unsigned m = live; m; m &= m - 1) {
                 const int i = __builtin_ctz(m), b = g + i * nsg;
                 const int kv = sh.kv0[i] + s, T = kv + 1;
@@ -558,12 +579,26 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 if (kv < KVL1 && (w == 2 || w == 3) && lane < 16) (Ks + kv * 32 + 16 * (w & 1))[lane] = sh.qkvs[i][16 * w + lane];
                 if (tid < 96) sh.qkv[tid] = sh.qkvs[i][tid];
                 bar_nf();
+                PMSTAMP(l == 12 && a.knob[1] == 1, 8 + i);   // (knob1 = 1: per-sequence attention stamps)
+                // this sequence's V rows (loaded one iteration ago) passed through an asm barrier
+                // after the wait: their uses below do not wait for the prefetch issued next
+                float4 vcur[8];
+                // (wave 7's one K/V row store of the previous sequence may stay in flight)
+                if (w == 7) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    vcur[u] = vpre[u];
+                    asm volatile("" : "+v"(vcur[u].x), "+v"(vcur[u].y), "+v"(vcur[u].z), "+v"(vcur[u].w));
+                }
                 {
                     const unsigned nx = m & (m - 1);
-                    if (nx) {   // the next sequence's K rows land in the other buffer during this attention
+                    if (nx) {   // the next sequence's K rows land in the other buffer, its V rows in
+                                // registers, during this attention
                         const int i2 = __builtin_ctz(nx);
                         stage_k(a, kbuf(cur ^ 1), l, g + i2 * nsg, r, sh.kv0[i2] + s, w, lane);
                         (cur ? skey0 : skey1) = (s * 24 + l) * MG + i2;
+                        v_of(i2);
                     }
                 }
                 const long kvoff = (long)b * a.sstride + (long)r * a.tmax * 32;
@@ -574,14 +609,13 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 const float4 qc = *reinterpret_cast<const float4*>(sh.qkv + 4 * c8);
                 const float q0 = qc.x * sc, q1 = qc.y * sc, q2 = qc.z * sc, q3 = qc.w * sc;
                 const float4 knew = *reinterpret_cast<const float4*>(sh.qkv + 32 + 4 * c8);
-                const float4 vnew = *reinterpret_cast<const float4*>(sh.qkv + 64 + 4 * c8);
                 if (T <= 512 && kv < KVL1) {
                     const int nu = (T + 63) >> 6;
-                    if (nu <= 2) wave_attn_m<2>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else if (nu <= 4) wave_attn_m<4>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else if (nu == 5) wave_attn_m<5>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else if (nu == 6) wave_attn_m<6>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
-                    else wave_attn_m<8>(sh, Ks, Vw, vnew, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    if (nu <= 2) wave_attn_m<2>(sh, Ks, vcur, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu <= 4) wave_attn_m<4>(sh, Ks, vcur, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu == 5) wave_attn_m<5>(sh, Ks, vcur, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else if (nu == 6) wave_attn_m<6>(sh, Ks, vcur, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
+                    else wave_attn_m<8>(sh, Ks, vcur, q0, q1, q2, q3, sc, kv, T, c8, gk, w, lane);
                     bar_nf();   // the stage is read; every wave's partials are in LDS
                     merge_waves1(sh, w, lane);
                 } else {
@@ -593,11 +627,9 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                     sh.O[2 * i][lane] = sh.osh[0][lane];
                     sh.O[2 * i + 1][lane] = sh.osl[0][lane];
                 }
-                if (w == 7) {   // the new K/V row (read by this workgroup only, next step)
-                    float* Kg = a.kc[l] + kvoff;
-                    float* Vg = a.vc[l] + kvoff;
-                    if (lane < 32) Kg[(long)kv * 32 + lane] = sh.qkvs[i][32 + lane];
-                    else Vg[(long)kv * 32 + lane - 32] = sh.qkvs[i][64 + lane - 32];
+                if (w == 7) {   // the new K/V row (read by this workgroup only, next step): one store
+                    float* dst = (lane < 32 ? a.kc[l] + kvoff : a.vc[l] + kvoff - 32) + (long)kv * 32 + lane;
+                    *dst = sh.qkvs[i][32 + lane];
                 }
             }
             bar_nf();   // O complete
@@ -765,7 +797,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 return;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's w_pred rows landed
             bar_nf();
-            PMSTAMP(true, 8);
+            PMSTAMP(a.knob[1] != 1, 8);
             const int tid = opaque_tid(), lane = tid & 63, n16 = lane & 15, k8 = 8 * (lane >> 4);
             const bool up = lane >= 16;
             float mean[MG], rden[MG];
@@ -814,7 +846,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();
-            PMSTAMP(true, 9);
+            PMSTAMP(a.knob[1] != 1, 9);
             if (fused && w == 7) {   // this slice's candidates: 16 granules per sequence (+ 4 EOS on r = 15)
                 const bool eos = r == NF - 1;
                 for (unsigned m = live; m; m &= m - 1) {
@@ -827,7 +859,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();   // A / lnb consumed
-            PMSTAMP(true, 10);
+            PMSTAMP(a.knob[1] != 1, 10);
             skey0 = skey1 = -1;   // (the w_pred rows overwrote both K buffers)
         }
         // ---- sampler (sampled decoding): sequence i = r of the group

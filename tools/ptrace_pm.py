@@ -12,7 +12,7 @@ import torch
 from genie_tts_amd import synth, workloads
 from genie_tts_amd.engine import Engine, make_sampler
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+B = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64
 wl = workloads.single()
 ref, it = wl.reference, wl.items[0]
 e = Engine(synth.synthetic_character("v2"), "v2")
@@ -20,6 +20,9 @@ e.set_option("persist", 1)
 e.set_option("persistm", 1)
 e.set_option("persistm_min_b", 2)
 e.set_option("ptrace", 1)
+ATT = "--attn" in sys.argv
+if ATT:
+    e.set_option("knob1", 1)
 T = lambda a: torch.as_tensor(a, device="cuda")
 utt = (T(ref.ref_seq.reshape(-1)), T(it.text_seq.reshape(-1)), None, None, T(ref.ssl.reshape(768, -1)), it.force_steps)
 for _ in range(3):
@@ -33,7 +36,11 @@ names = {12: "step start", 13: "tokens resolved", 0: "L12 attn start", 1: "L12 g
          3: "L12 attention done", 4: "L12 PA published", 5: "L12 FFN gather done", 6: "L12 FFN1 done",
          7: "L12 PFH published", 14: "L23 done", 8: "logits gather done", 9: "logits done",
          10: "candidates published", 15: "step end"}
-out = {"B": B, "workgroups": n, "us": {names[k]: round(us(k), 2) for k in (12, 13, 0, 1, 2, 3, 4, 5, 6, 7, 14, 8, 9, 10, 15)}}
+if ATT:
+    names.update({8: "L12 seq0 attention start", 9: "L12 seq1 attention start", 10: "L12 seq2 attention start",
+                  11: "L12 seq3 attention start"})
+    del names[14]
+out = {"B": B, "workgroups": n, "us": {names[k]: round(us(k), 2) for k in ((12, 13, 0, 1, 2, 8, 9, 10, 11, 3, 4, 5, 6, 7, 15) if ATT else (12, 13, 0, 1, 2, 3, 4, 5, 6, 7, 14, 8, 9, 10, 15))}}
 spread = {names[k]: round(float(np.max(tr[:, k]) - np.min(tr[:, k])) * 10 / 1000.0, 2) for k in (0, 7)}
 out["spread_us"] = spread
 print(json.dumps(out))
