@@ -631,17 +631,26 @@ __device__ __forceinline__ void dma_half(const float* src, float* dst, int h, in
 __device__ __forceinline__ void pf_wait(int ticks) {
     for (int i = 0; i < ticks; ++i) __builtin_amdgcn_s_sleep(32);
 }
-// LN2 of layer l - 1 -> sh.p2 (call from every wave; l > 0), by waves 0, 1, 2, 4, 5, 6:
-// the hop-B gather's polling waves, whose in-order vmcnt waits retire these DMAs before
-// the gather's last barrier, after which sh.p2 is read.  (Waves 3 and 7 never poll, and
-// the multi-sequence kernel has no fenced barrier between a prefetch and the next
-// gather: a DMA of wave 3 was not ordered before its readers.  Hardening found while
-// looking for the r05 persist1m deviation, profiles/r05x_persist1m_deviation.txt; it
-// did not change that case.)
+// LN2 of layer l - 1 -> sh.p2 (call from every wave; l > 0).  The single-sequence kernel:
+// waves 0..5 (its fenced barriers order the DMAs long before the next owned layer reads
+// them).  The multi-sequence kernel (POLLERS): waves 0, 1, 2, 4, 5, 6, the hop-B gather's
+// polling waves, whose in-order vmcnt waits retire these DMAs before the gather's last
+// barrier, after which sh.p2 is read -- waves 3 and 7 never poll and that kernel has no
+// fenced barrier between a prefetch and the next gather.  (Hardening found while looking
+// for the r05 persist1m deviation, profiles/r05x_persist1m_deviation.txt; it did not
+// change that case.  The single-sequence kernel keeps its assignment: moving its DMAs
+// cost ~0.25 ms per launch, r05b.)
+template <bool POLLERS = false>
 __device__ __forceinline__ void dma_ln2(const PLayer& Q, Shared1& sh, int w, int lane) {
-    if (w < 2) dma_half(Q.b2, sh.p2[0], w & 1, lane);
-    else if (w == 2 || w == 4) dma_half(Q.n2w, sh.p2[1], w == 4, lane);
-    else if (w == 5 || w == 6) dma_half(Q.n2b, sh.p2[2], w == 6, lane);
+    if (POLLERS) {
+        if (w < 2) dma_half(Q.b2, sh.p2[0], w & 1, lane);
+        else if (w == 2 || w == 4) dma_half(Q.n2w, sh.p2[1], w == 4, lane);
+        else if (w == 5 || w == 6) dma_half(Q.n2b, sh.p2[2], w == 6, lane);
+    } else {
+        if (w < 2) dma_half(Q.b2, sh.p2[0], w & 1, lane);
+        else if (w < 4) dma_half(Q.n2w, sh.p2[1], w & 1, lane);
+        else if (w < 6) dma_half(Q.n2b, sh.p2[2], w & 1, lane);
+    }
 }
 
 // Hop B: u = h1_{l-1} + (b2 + sum_j PF[l-1][j]) (l >= 1; the partials summed in
@@ -1493,7 +1502,7 @@ __device__ void run_attn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh,
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + h * 32 + k8, 0);
-        if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
+        if (l > 0) dma_ln2<true>(a.L[l - 1], sh, w, lane);
     };
     auto next_live = [&](u64m live, int from) {   // the next live sequence at or after `from`, else -1
         const u64m m = from < 64 ? live >> from : 0ull;
@@ -1758,7 +1767,7 @@ __device__ void run_ffn_m(const PersistArgs& a, const WsSeq& base, Shared1& sh, 
         ffB = ldg(a.fold, (long)l * FOLD_LAYER + 3072 + j * 128 + w * 16 + n16);
         ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + j * 128 + w * 16 + n16);
         bo = ldg(P.b_out, tid); n1w = ldg(P.n1w, tid); n1b = ldg(P.n1b, tid);
-        if (l > 0) dma_ln2(a.L[l - 1], sh, w, lane);
+        if (l > 0) dma_ln2<true>(a.L[l - 1], sh, w, lane);
     };
     auto next_live = [&](u64m live, int from) {
         const u64m m = from < 64 ? live >> from : 0ull;
