@@ -355,7 +355,10 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
 /* Engine options (no reference counterpart; the reference's session options are
  * ORT's).  "persist": 1 (default) runs gsv_t2s_generate's decode loop as ONE
  * persistent launch (B <= 64), 0 as replayed per-step hipGraphs; setting it also ends
- * a timeout back-off.  "persist_backoff" / "persist_backoff_ms": the first back-off hold
+ * a timeout back-off.  "persist1m" (1): B = 2..64 on the multi-sequence kernel (0: the
+ * graphs); "persistm" (1) / "persistm_min_b" (32): from that batch size on, the batched
+ * kernel with the batch on the MFMA M dimension (t2s_persistm.hip; groups of <= 4
+ * sequences per 16 CUs).  "persist_backoff" / "persist_backoff_ms": the first back-off hold
  * after two timed-out launches in a row (64 generates / 5 s, doubling per failed re-probe).
  * "vocoder_cus" (CU split for the sentence pipeline), "decode_cus" / "decode_cu_offset",
  * "vits_lanes", "seg_vocoder" (1, default: a vocoder batch runs its generator as ONE pass
