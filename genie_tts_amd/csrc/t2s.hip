@@ -276,7 +276,9 @@ __device__ __forceinline__ void gx3_wait(int later) {
 __device__ __forceinline__ void gx3_dma(const void* g, void* l) {
     const unsigned la =
         __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) char*)(l));
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(g) : "memory", "m0");
+    // M0 bound as an operand: the compiler sets and tracks it (a clobbered m0 is not
+    // preserved by the compiler's own M0 users)
+    asm volatile("global_load_lds_dwordx4 %1, off" ::"{m0}"(la), "v"(g) : "memory");
 }
 
 #define GX3_BK 64

@@ -211,8 +211,8 @@ __device__ __forceinline__ void stage_k(const PersistArgs& a, float* dst, int l,
             // i.e. wait for the next sequence's rows; the wait is the explicit one before use
             const unsigned la = __builtin_amdgcn_readfirstlane(
                 (unsigned)(size_t)(__attribute__((address_space(3))) char*)(dst + i * 256));
-            asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(K + (long)i * 256 + lane * 4)
-                         : "memory", "m0");
+            // (M0 bound as an operand, so the compiler sets and tracks it)
+            asm volatile("global_load_lds_dwordx4 %1, off" ::"{m0}"(la), "v"(K + (long)i * 256 + lane * 4) : "memory");
         }
     }
 }
@@ -691,6 +691,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                         c1 = mfma16(af[i + 1], bfrag(w1r[cb + i + 1]), c1);
                     }
                 }
+                PMSTAMP(l == 12 && a.knob[1] == 2, 8);
                 {
                     const int m16 = lane2 & 15, q8 = 8 * (lane2 >> 4);
 #pragma unroll
@@ -699,6 +700,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                         for (int c = 0; c < 4; ++c)
                             w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + m16) * 2048 + r * 128 + 32 * c + q8, 0);
                 }
+                PMSTAMP(l == 12 && a.knob[1] == 2, 9);
                 if ((tid2 >> 5) == r) {   // block r of h1 = LN1(v) for the next layer's PFH row 16
                     const float n1w = n1w_t, n1b = n1b_t;
 #pragma unroll
@@ -723,6 +725,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                         }
                     }
                 }
+                PMSTAMP(l == 12 && a.knob[1] == 2, 10);
                 if (!ok_all(ok, sh)) return;   // F complete; lnb / A free
             }
             PMSTAMP(l == 12, 6);
@@ -797,7 +800,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 return;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's w_pred rows landed
             bar_nf();
-            PMSTAMP(a.knob[1] != 1, 8);
+            PMSTAMP(a.knob[1] == 0, 8);
             const int tid = opaque_tid(), lane = tid & 63, n16 = lane & 15, k8 = 8 * (lane >> 4);
             const bool up = lane >= 16;
             float mean[MG], rden[MG];
@@ -846,7 +849,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();
-            PMSTAMP(a.knob[1] != 1, 9);
+            PMSTAMP(a.knob[1] == 0, 9);
             if (fused && w == 7) {   // this slice's candidates: 16 granules per sequence (+ 4 EOS on r = 15)
                 const bool eos = r == NF - 1;
                 for (unsigned m = live; m; m &= m - 1) {
@@ -859,7 +862,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 }
             }
             bar_nf();   // A / lnb consumed
-            PMSTAMP(a.knob[1] != 1, 10);
+            PMSTAMP(a.knob[1] == 0, 10);
             skey0 = skey1 = -1;   // (the w_pred rows overwrote both K buffers)
         }
         // ---- sampler (sampled decoding): sequence i = r of the group

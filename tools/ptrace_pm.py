@@ -21,8 +21,11 @@ e.set_option("persistm", 1)
 e.set_option("persistm_min_b", 2)
 e.set_option("ptrace", 1)
 ATT = "--attn" in sys.argv
+FFN = "--ffn" in sys.argv
 if ATT:
     e.set_option("knob1", 1)
+if FFN:
+    e.set_option("knob1", 2)
 T = lambda a: torch.as_tensor(a, device="cuda")
 utt = (T(ref.ref_seq.reshape(-1)), T(it.text_seq.reshape(-1)), None, None, T(ref.ssl.reshape(768, -1)), it.force_steps)
 for _ in range(3):
@@ -40,7 +43,10 @@ if ATT:
     names.update({8: "L12 seq0 attention start", 9: "L12 seq1 attention start", 10: "L12 seq2 attention start",
                   11: "L12 seq3 attention start"})
     del names[14]
-out = {"B": B, "workgroups": n, "us": {names[k]: round(us(k), 2) for k in ((12, 13, 0, 1, 2, 8, 9, 10, 11, 3, 4, 5, 6, 7, 15) if ATT else (12, 13, 0, 1, 2, 3, 4, 5, 6, 7, 14, 8, 9, 10, 15))}}
+if FFN:
+    names.update({8: "L12 FFN1 MFMA done (thread 0)", 9: "L12 W2 loads issued", 10: "L12 F written"})
+    del names[14]
+out = {"B": B, "workgroups": n, "us": {names[k]: round(us(k), 2) for k in ((12, 13, 0, 1, 2, 8, 9, 10, 11, 3, 4, 5, 6, 7, 15) if ATT else (12, 13, 0, 1, 2, 3, 4, 5, 8, 9, 10, 6, 7, 15) if FFN else (12, 13, 0, 1, 2, 3, 4, 5, 6, 7, 14, 8, 9, 10, 15))}}
 spread = {names[k]: round(float(np.max(tr[:, k]) - np.min(tr[:, k])) * 10 / 1000.0, 2) for k in (0, 7)}
 out["spread_us"] = spread
 print(json.dumps(out))
