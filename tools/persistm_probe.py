@@ -50,9 +50,12 @@ def main():
                it.force_steps)
         sp = make_sampler()
         rows = []
+        knobs = [int(x) for x in os.environ.get("PM_KNOB2", "0").split(",")]
         for B in [int(x) for x in os.environ.get("PM_BS", "8,16,32,48,64").split(",")]:
             row = {"B": B}
-            for pm in (1, 0):
+            for pm in [(1, k) for k in knobs] + [(0, 0)]:
+                pm, k2 = pm
+                e.set_option("knob2", k2)
                 e.set_option("persistm", pm)
                 e.t2s_generate([utt] * B, sp)
                 torch.cuda.synchronize()
@@ -61,7 +64,9 @@ def main():
                 for _ in range(n):
                     e.t2s_generate([utt] * B, sp)
                 torch.cuda.synchronize()
-                row["persistm" if pm else "persist1m"] = round((time.perf_counter() - t0) / n * 1e3, 2)
+                row[(f"persistm_split{k2}" if len(knobs) > 1 else "persistm") if pm else "persist1m"] = \
+                    round((time.perf_counter() - t0) / n * 1e3, 2)
+            e.set_option("knob2", 0)
             rows.append(row)
             print(json.dumps(row), file=sys.stderr, flush=True)
         out["time_ms_per_generate"] = rows
