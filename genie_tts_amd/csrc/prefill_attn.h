@@ -7,7 +7,8 @@ namespace gsv {
 // Blocks of rows_per_block (64 or 128) query rows of one head, or a.tiles of
 // <= rows_per_block rows of one sequence (any key count).
 void attn_rows_mfma(const AttnArgs& a, int rows_per_block, hipStream_t s);
-// default on; GENIE_ATTN_MFMA=0 keeps the prefill attention on the f32 kernels
+// default off (GENIE_ATTN_MFMA=1 turns it on): the packed prefill's attention stays on the
+// f32 kernels a single sentence's prefill uses, so batched and single tokens agree
 bool attn_mfma_on();
 
 }  // namespace gsv

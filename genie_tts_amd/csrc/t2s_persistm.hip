@@ -78,6 +78,20 @@ __device__ __forceinline__ int nth_bit(unsigned m, int n) {   // index of the n-
 __device__ __forceinline__ const _Float16* abase_m(const _Float16* tile, int stride, int lane) {
     return tile + (lane & 7) * stride + 8 * (lane >> 4);
 }
+// hi + lo split of the product u m, as the single-sequence kernel's compiled split of
+// `un = u * m; split_h(un, ...)` computes it: hipcc contracts the product into the
+// conversions there, hi = f16(u m) and lo = f16(u m - hi) with the product exact (two
+// v_fma_mixlo_f16), which differs from converting the f32-rounded product when u m
+// sits at an f16 rounding tie.  Written out here so every sequence's operands -- and
+// values -- are the single kernel's bit for bit (profiles/r05x_persist1m_deviation.txt).
+__device__ __forceinline__ void split_mul_h(float u, float m, _Float16& hi, _Float16& lo) {
+    unsigned h, l;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(u), "v"(m));
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(u), "v"(m), "v"(h));
+    hi = __builtin_bit_cast(_Float16, (unsigned short)(h & 0xffffu));
+    lo = __builtin_bit_cast(_Float16, (unsigned short)(l & 0xffffu));
+}
+
 __device__ __forceinline__ bool ok_all(bool ok, SharedM& sh) {
     if (!ok) sh.fail = 1;
     bar_nf();
@@ -100,7 +114,7 @@ __device__ __forceinline__ bool ok_all(bool ok, SharedM& sh) {
 // Ends with a barrier.
 template <class Blk>
 __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, SharedM& sh, unsigned live,
-                                         unsigned tag, Blk blk, const float* vec, const float* mul) {
+                                         unsigned tag, Blk blk, const float* vec, const float* mul, bool dbg_ffn = false) {
     constexpr int RB = (int)Ws1::ROW * 8;
     const int nl = __builtin_popcount(live);
     bool ok = true;
@@ -140,10 +154,17 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
             sh.at.g.lnb[i][c] = u;
             const float un = u * mm[k];
             _Float16 hi, lo;
-            if (!split_h(un, hi, lo) || !(fabsf(un) < a.f16_limit)) {
+            split_mul_h(u, mm[k], hi, lo);
+            if (!(fabsf(un) < 65504.f) || !(fabsf(un) < a.f16_limit)) {   // (split_h's range test)
                 atomicCAS(a.err, 0, ERR_F16_RANGE);
                 ok = false;
             }
+#ifdef PERSIST_DBG
+            if (a.knob[3] == 12 && dbg_ffn && i == 0) {
+                float* tf = reinterpret_cast<float*>(a.trace);
+                tf[3000 + c] = un; tf[3512 + c] = (float)hi; tf[4024 + c] = u; tf[4536 + c] = mm[k];
+            }
+#endif
             sh.at.g.A[2 * i][c] = hi;
             sh.at.g.A[2 * i + 1][c] = lo;
         }
@@ -627,6 +648,11 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                     sh.O[2 * i][lane] = sh.osh[0][lane];
                     sh.O[2 * i + 1][lane] = sh.osl[0][lane];
                 }
+#ifdef PERSIST_DBG   // tools/persist_dbg.py (debug build only)
+                if (a.knob[3] == 7 && s == 1 && l < 8 && w == 0 && b == 0)
+                    reinterpret_cast<float*>(a.trace)[(l * 16 + r) * 64 + lane] =
+                        lane < 32 ? sh.qkv[lane] : (float)sh.osh[0][lane - 32] + (float)sh.osl[0][lane - 32];
+#endif
                 if (w == 7) {   // the new K/V row (read by this workgroup only, next step): one store
                     float* dst = (lane < 32 ? a.kc[l] + kvoff : a.vc[l] + kvoff - 32) + (long)kv * 32 + lane;
                     *dst = sh.qkvs[i][32 + lane];
@@ -646,6 +672,11 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                         if ((live >> i) & 1u) {
 #pragma unroll
                             for (int t = 0; t < 4; ++t) sh.at.pk[i][64 * w + 16 * t + n16] = acc[t][2 * k] + acc[t][2 * k + 1];
+#ifdef PERSIST_DBG
+                            if (a.knob[3] == 9 && s == 1 && l == 0 && g == 0 && i == 0)
+                                for (int t = 0; t < 4; ++t)
+                                    reinterpret_cast<float*>(a.trace)[r * 512 + 64 * w + 16 * t + n16] = acc[t][2 * k] + acc[t][2 * k + 1];
+#endif
                         }
                     }
                 }
@@ -671,14 +702,19 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + r * 128 + w * 16 + m16);
             }
             if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PA(s, l, 0); }, P.b_out,
-                          P.n1w))
+                          P.n1w, s == 1 && l == 0 && g == 0 && r == 0))
                 return;
             PMSTAMP(l == 12, 5);
             {
                 const int tid2 = opaque_tid(), lane2 = tid2 & 63;
                 float mean[MG], rden[MG];
                 stats_m(sh, live, mean, rden);
+#ifdef PERSIST_DBG   // knob3 = 11: FFN1's A rows as the single-sequence kernel lays them out (row 0 hi, 1..15 lo)
+                const _Float16* ab = a.knob[3] == 11 ? ((lane2 & 15) == 0 ? &sh.at.g.A[0][0] : &sh.at.g.A[1][0]) + 8 * (lane2 >> 4)
+                                                     : abase_m(&sh.at.g.A[0][0], AST, lane2);
+#else
                 const _Float16* ab = abase_m(&sh.at.g.A[0][0], AST, lane2);
+#endif
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int cb = 0; cb < 16; cb += 8) {
@@ -701,6 +737,19 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                             w2r[4 * t + c] = ldg16(P.w2 + (long)(64 * w + 16 * t + m16) * 2048 + r * 128 + 32 * c + q8, 0);
                 }
                 PMSTAMP(l == 12 && a.knob[1] == 2, 9);
+#ifdef PERSIST_DBG
+                if (a.knob[3] == 12 && s == 1 && l == 0 && g == 0 && r == 0) {
+                    float* tf = reinterpret_cast<float*>(a.trace);
+                    if (w == 0 && lane2 < 16) {
+                        tf[lane2 * 4 + 0] = c0[0]; tf[lane2 * 4 + 1] = c1[0]; tf[lane2 * 4 + 2] = c0[1]; tf[lane2 * 4 + 3] = c1[1];
+                    }
+                    tf[64 + tid2] = sh.at.g.lnb[0][tid2];
+                    tf[576 + tid2] = (float)sh.at.g.A[0][tid2] + (float)sh.at.g.A[1][tid2];
+                    tf[1088 + tid2] = ffB;
+                    tf[1600 + tid2] = sh.at.g.lnb[0][tid2] * ldg(P.n1w, tid2);
+                    tf[2112 + tid2] = (float)sh.at.g.A[0][tid2];
+                }
+#endif
                 if ((tid2 >> 5) == r) {   // block r of h1 = LN1(v) for the next layer's PFH row 16
                     const float n1w = n1w_t, n1b = n1b_t;
 #pragma unroll
@@ -718,6 +767,13 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                             const float f =
                                 fmaxf(rd * (((c0[2 * k] + c1[2 * k]) + (c0[2 * k + 1] + c1[2 * k + 1])) - mn * ffB) + ffC, 0.f);
                             split_h(f, sh.F[2 * i][w * 16 + (lane2 & 15)], sh.F[2 * i + 1][w * 16 + (lane2 & 15)]);
+#ifdef PERSIST_DBG
+                            if ((a.knob[3] == 10 || a.knob[3] == 11) && s == 1 && l == 0 && g == 0 && i == 0) {
+                                float* tf = reinterpret_cast<float*>(a.trace);
+                                tf[r * 128 + w * 16 + (lane2 & 15)] = f;
+                                if (w == 0 && lane2 == 0) { tf[2048 + 2 * r] = mn; tf[2049 + 2 * r] = rd; }
+                            }
+#endif
                             if (!(fabsf(f) < a.f16_limit)) {
                                 atomicCAS(a.err, 0, ERR_F16_RANGE);
                                 ok = false;
@@ -751,6 +807,11 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
 #pragma unroll
                             for (int t = 0; t < 4; ++t)
                                 sh.at.pk[i][64 * w + 16 * t + (lane2 & 15)] = acc[t][2 * k] + acc[t][2 * k + 1];
+#ifdef PERSIST_DBG
+                            if (a.knob[3] == 8 && s == 1 && l == 0 && g == 0 && i == 0)
+                                for (int t = 0; t < 4; ++t)
+                                    reinterpret_cast<float*>(a.trace)[r * 512 + 64 * w + 16 * t + (lane2 & 15)] = acc[t][2 * k] + acc[t][2 * k + 1];
+#endif
                         }
                     }
                 }

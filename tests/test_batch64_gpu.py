@@ -67,11 +67,13 @@ def test_batch64_ragged_lengths(eng):
 
 
 def test_packed_prefill_attention_matches_per_sequence_prefill(eng):
-    """The packed prefill's attention (k_attn_mfma: 128-row tiles on the split-fp16 MFMA)
-    against the per-sequence prefill (k_attn_flash, f32): the layer-23 K/V rows that every
-    earlier layer's attention feeds, for 8 ragged utterances of batch64 (one of them longer
-    than one 128-row tile by 200+ rows).  Bar: max |diff| <= 1e-4 x max |value| (split-fp16
-    operands keep ~22 bits of each product)."""
+    """The packed prefill against the per-sequence prefill: the layer-23 K/V rows that every
+    earlier layer's attention feeds, for 8 ragged utterances of batch64.  Since r05 the
+    packed prefill's attention runs the f32 kernels the per-sequence prefill runs (the
+    split-fp16 MFMA kernel k_attn_mfma is opt-in, GENIE_ATTN_MFMA=1: it flipped a near-tie
+    token against the sentence alone, test_persistm_gpu.py), so the rows are bit-identical;
+    with the MFMA kernel the bar is max |diff| <= 1e-4 x max |value|."""
+    import os
     from genie_tts_amd import workloads
     from genie_tts_amd.engine import make_sampler
     wl = workloads.batch64()
@@ -87,4 +89,7 @@ def test_packed_prefill_attention_matches_per_sequence_prefill(eng):
         for a, r in zip(kv[1][b], kv[0][b]):
             assert a.shape == r.shape and a.shape[0] > 128
             err = float(np.abs(a - r).max())
-            assert err <= 1e-4 * float(np.abs(r).max()), (b, err)
+            if os.environ.get("GENIE_ATTN_MFMA", "0") not in ("", "0"):
+                assert err <= 1e-4 * float(np.abs(r).max()), (b, err)
+            else:
+                assert err == 0.0, (b, err)
