@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mfma(AttnArgs a) {
 // default since r05: its rounding differs from the f32 online-softmax kernels a sentence's
 // own prefill runs, so a batched generate could pick a different token than the same
 // sentence alone (and than the oracle) at a near-tie -- found on one input of the B = 64
-// test set (profiles/r05x_persist1m_deviation.txt).  With the f32 kernels a batch's tokens
+// test set (profiles/r05x_batched_near_tie.txt).  With the f32 kernels a batch's tokens
 // are each sentence's own.
 bool attn_mfma_on() {
     static const bool on = [] { const char* e = std::getenv("GENIE_ATTN_MFMA"); return e && std::atoi(e) != 0; }();
