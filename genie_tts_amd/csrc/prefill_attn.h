@@ -10,5 +10,9 @@ void attn_rows_mfma(const AttnArgs& a, int rows_per_block, hipStream_t s);
 // default off (GENIE_ATTN_MFMA=1 turns it on): the packed prefill's attention stays on the
 // f32 kernels a single sentence's prefill uses, so batched and single tokens agree
 bool attn_mfma_on();
+// f32, k_attn_flash's per-row arithmetic with one query row per lane: a.tiles of
+// <= 64 ROWLANE_NW rows of one sequence
+constexpr int ROWLANE_NW = 2;
+void attn_rows_rowlane(const AttnArgs& a, hipStream_t s);
 
 }  // namespace gsv

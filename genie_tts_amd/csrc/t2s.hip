@@ -1337,6 +1337,156 @@ void attn_rows_mfma(const AttnArgs& a, int rows_per_block, hipStream_t s) {
     }
 }
 
+// Packed-prefill attention in f32 with k_attn_flash's exact per-row arithmetic, one
+// query row per lane (stage#91-96 per head).  A block = one head x 64 NW rows of one
+// sequence; wave w owns rows 64 w .. 64 w + 63.  k_attn_flash puts a chunk's 64 keys on
+// the lanes and reduces each row's scores across the wave; here the lane owns its row, so
+// per 64-key chunk it runs the same operations in-lane:
+//   score(row, key): two fma chains over the even / odd dims of (q s)(k s), summed;
+//   max over the chunk's 64 scores (exact, any order);
+//   sum of the 64 exp(s - max) in wave_sum's xor-butterfly tree (offsets 32, 16, .. 1);
+//   l = l corr + sum; o = o corr, then o += p_j v_j for j = 0 .. 63 in key order.
+// So a row's output is bit-identical to k_attn_flash's (and the packed prefill's tokens
+// to a sentence's own prefill) while every K/V element read from LDS is a broadcast that
+// feeds 64 rows: k_attn_flash reads ~57 KB of LDS per 4 rows and 64 keys and is
+// LDS-bound (281 us per layer of batch64).  K and V chunks land by LDS-DMA in a 2-slot
+// ring one chunk ahead; K is then scaled by s in place.  The fused multiply-adds are
+// explicit: k_attn_flash compiles to o = o corr, then fma(p, v, o), and a contraction
+// left to the compiler here fused o corr into the first product's add instead.
+#define AR_KC 64
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_attn_rowlane(AttnArgs a) {
+    constexpr int NT = 64 * NW, ROWS = 64 * NW;
+    constexpr int DPW = 16 / NW;   // DMA instructions (1 KB) per wave per chunk, K and V
+    static_assert(16 % NW == 0, "waves");
+    __shared__ __attribute__((aligned(16))) float Ks[2][AR_KC * 32];
+    __shared__ __attribute__((aligned(16))) float Vs[2][AR_KC * 32];
+    __shared__ int wk[NW];
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int* tl = a.tiles + 3 * blockIdx.y;
+    const long kvbase = (long)h * a.tmax * 32 + (long)tl[0] * a.seq_stride;
+    const int r0 = tl[1], nr = tl[2];
+    const float sc = a.scale;
+    const int rr = 64 * w + lane;   // this lane's row of the tile
+    const int len = rr < nr ? a.row_len[r0 + rr] : 0;
+    int wkmax = len;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wkmax = max(wkmax, __shfl_xor(wkmax, o, 64));
+    if (lane == 0) wk[w] = wkmax;
+    float q[32];
+    {
+        const float* qp = a.q + (long)(r0 + (rr < nr ? rr : 0)) * a.ldq + h * 32;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float4 v = *reinterpret_cast<const float4*>(qp + 4 * c);
+            q[4 * c] = v.x * sc;
+            q[4 * c + 1] = v.y * sc;
+            q[4 * c + 2] = v.z * sc;
+            q[4 * c + 3] = v.w * sc;
+        }
+    }
+    __syncthreads();
+    int kmax = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) kmax = max(kmax, wk[i]);
+    const float* K = a.k + kvbase;
+    const float* V = a.v + kvbase;
+    // chunk c -> slot c & 1: DMA instruction j (8 keys x 32 dims) of K and of V by wave
+    // j % NW; keys past kmax read key 0 (in bounds, never weighted)
+    auto dma = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < 8 / NW; ++i) {
+            const int j = w + NW * i, key = AR_KC * c + 8 * j + (lane >> 3);
+            const long src = (long)(key < kmax ? key : 0) * 32 + 4 * (lane & 7);
+            gx3_dma(K + src, &Ks[c & 1][j * 256]);
+            gx3_dma(V + src, &Vs[c & 1][j * 256]);
+        }
+    };
+    float m = -INFINITY, l = 0.f;
+    float o[32];
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] = 0.f;
+    const int nch = (kmax + AR_KC - 1) / AR_KC;
+    if (nch > 0) dma(0);
+    if (nch > 1) dma(1);
+    for (int c = 0; c < nch; ++c) {
+        const int k0 = AR_KC * c, sl = c & 1;
+        gx3_wait<DPW>(c + 1 < nch ? 1 : 0);   // this wave's part of chunk c landed
+        __syncthreads();
+        // K chunk scaled in place (k s, as k_attn_flash's kr)
+#pragma unroll
+        for (int i = 0; i < AR_KC * 8 / NT; ++i) {
+            float4* p = reinterpret_cast<float4*>(&Ks[sl][4 * (tid + NT * i)]);
+            const float4 v = *p;
+            *p = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+        }
+        __syncthreads();
+        if (k0 < wkmax) {
+            float s[AR_KC];
+#pragma unroll
+            for (int j = 0; j < AR_KC; ++j) {
+                const float* kr = &Ks[sl][32 * j];
+                float ax = 0.f, ay = 0.f;
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    const float4 k4 = *reinterpret_cast<const float4*>(kr + 4 * cc);
+                    ax = __builtin_fmaf(q[4 * cc], k4.x, ax);
+                    ay = __builtin_fmaf(q[4 * cc + 1], k4.y, ay);
+                    ax = __builtin_fmaf(q[4 * cc + 2], k4.z, ax);
+                    ay = __builtin_fmaf(q[4 * cc + 3], k4.w, ay);
+                }
+                s[j] = k0 + j < len ? ax + ay : -INFINITY;
+            }
+            float mc = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < AR_KC; ++j) mc = fmaxf(mc, s[j]);
+            const float mn = fmaxf(m, mc);
+            const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+#pragma unroll
+            for (int j = 0; j < AR_KC; ++j) s[j] = s[j] == -INFINITY ? 0.f : __expf(s[j] - mn);
+            // wave_sum's tree: t[k] = t[k] + t[k ^ off], off = 32 .. 1 (lane 0's operands)
+            float t[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k) t[k] = s[k] + s[k + 32];
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1)
+#pragma unroll
+                for (int k = 0; k < off; ++k) t[k] = t[k] + t[k + off];
+            l = __builtin_fmaf(l, corr, t[0]);
+            m = mn;
+#pragma unroll
+            for (int d = 0; d < 32; ++d) o[d] *= corr;
+#pragma unroll
+            for (int j = 0; j < AR_KC; ++j) {
+                const float* vr = &Vs[sl][32 * j];
+                const float p = s[j];
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    const float4 v4 = *reinterpret_cast<const float4*>(vr + 4 * cc);
+                    o[4 * cc] = __builtin_fmaf(p, v4.x, o[4 * cc]);
+                    o[4 * cc + 1] = __builtin_fmaf(p, v4.y, o[4 * cc + 1]);
+                    o[4 * cc + 2] = __builtin_fmaf(p, v4.z, o[4 * cc + 2]);
+                    o[4 * cc + 3] = __builtin_fmaf(p, v4.w, o[4 * cc + 3]);
+                }
+            }
+        }
+        __syncthreads();                    // slot sl consumed by every wave
+        if (c + 2 < nch) dma(c + 2);
+    }
+    if (rr < nr) {
+        float* dst = a.out + (long)(r0 + rr) * a.ldo + h * 32;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            *reinterpret_cast<float4*>(dst + 4 * c) =
+                make_float4(o[4 * c] / l, o[4 * c + 1] / l, o[4 * c + 2] / l, o[4 * c + 3] / l);
+    }
+}
+
+void attn_rows_rowlane(const AttnArgs& a, hipStream_t s) {
+    if (a.ntiles <= 0) return;
+    hipLaunchKernelGGL(k_attn_rowlane<ROWLANE_NW>, dim3(16, a.ntiles), dim3(64 * ROWLANE_NW), 0, s, a);
+}
+
 // (One sequence's prefill stays on k_attn_flash: at ~300 rows the MFMA kernel's 80
 // blocks of 64 rows were no faster -- prefill 2.00 vs 1.91 ms, profiles/r04q_prefill_attn.txt.)
 void attn_rows(const AttnArgs& a, hipStream_t s) {
