@@ -636,8 +636,11 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     // the row-per-lane f32 kernel (k_attn_rowlane; GENIE_PACKED_ROWLANE=0: k_attn_flash
     // over 16-row tiles, the same results)
     static const bool rowlane_opt = [] { const char* e = std::getenv("GENIE_PACKED_ROWLANE"); return !(e && std::atoi(e) == 0); }();
-    const bool rowlane = !mfma_attn && rowlane_opt;
-    const int TR = mfma_attn ? 128 : rowlane ? 64 * ROWLANE_NW : 16;
+    // the same arithmetic on the f32 MFMA (k_attn_mf32; GENIE_PACKED_MF32=0: k_attn_rowlane)
+    static const bool mf32_opt = [] { const char* e = std::getenv("GENIE_PACKED_MF32"); return !(e && std::atoi(e) == 0); }();
+    const bool mf32 = !mfma_attn && mf32_opt;
+    const bool rowlane = !mfma_attn && !mf32 && rowlane_opt;
+    const int TR = mfma_attn ? 128 : mf32 ? 32 * MF32_NW : rowlane ? 64 * ROWLANE_NW : 16;
     int ntiles = 0, maxn0 = 0;
     for (int b = 0; b < B; ++b) {
         ntiles += (off[b + 1] - off[b] + TR - 1) / TR;
@@ -678,7 +681,7 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     // the LDS-staged tile kernel measured slower here (prefill 62.5 vs 45.4 ms at B=64):
     // kept behind GENIE_PACKED_TILE for A/B
     static const bool tile_opt = [] { const char* e = std::getenv("GENIE_PACKED_TILE"); return e && std::atoi(e); }();
-    const bool tiled = !mfma_attn && !rowlane && tile_opt && maxn0 <= ATTN_TILE_MAXK;
+    const bool tiled = !mfma_attn && !mf32 && !rowlane && tile_opt && maxn0 <= ATTN_TILE_MAXK;
     // the online-softmax kernel over the same tiles (GENIE_PACKED_FLASH=0: the per-row kernel)
     static const bool flash_opt = [] { const char* e = std::getenv("GENIE_PACKED_FLASH"); return !(e && std::atoi(e) == 0); }();
     const bool flash_tiles = flash_opt;
@@ -718,6 +721,10 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
             at.tiles = pk_tiles;
             at.ntiles = ntiles;
             attn_rows_mfma(at, 128, st);
+        } else if (mf32) {   // tiles of 32 MF32_NW rows on the f32 MFMA
+            at.tiles = pk_tiles;
+            at.ntiles = ntiles;
+            attn_rows_mf32(at, st);
         } else if (rowlane) {   // tiles of 64 ROWLANE_NW rows, one row per lane
             at.tiles = pk_tiles;
             at.ntiles = ntiles;

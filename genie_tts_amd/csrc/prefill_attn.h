@@ -14,5 +14,9 @@ bool attn_mfma_on();
 // <= 64 ROWLANE_NW rows of one sequence
 constexpr int ROWLANE_NW = 2;
 void attn_rows_rowlane(const AttnArgs& a, hipStream_t s);
+// f32 MFMA, the same per-row arithmetic (v_mfma_f32_32x32x2f32 is a sequential fma
+// chain): a.tiles of <= 32 MF32_NW rows of one sequence
+constexpr int MF32_NW = 4;
+void attn_rows_mf32(const AttnArgs& a, hipStream_t s);
 
 }  // namespace gsv

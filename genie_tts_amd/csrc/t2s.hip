@@ -1482,6 +1482,180 @@ __global__ __launch_bounds__(64 * NW) void k_attn_rowlane(AttnArgs a) {
     }
 }
 
+// Packed-prefill attention on the f32 MFMA with k_attn_flash's exact per-row arithmetic.
+// v_mfma_f32_32x32x2f32 computes each element as a sequential fma chain in k order,
+// fma(a1, b1, fma(a0, b0, c)) -- bit for bit on 204,800 random elements
+// (tools/mfma_f32_probe.hip, profiles/r05k_mfma_f32_chain.txt) -- so the flash kernel's
+// fma chains map onto it step for step.  A block = one head x 32 NW rows of one
+// sequence, wave w owns rows 32 w .. 32 w + 31.  Per 64-key chunk:
+//   S^T = K Q^T twice, A = the chunk's (k s) rows, B = the wave's (q s) rows: step t of
+//     one accumulator takes dims (4t, 4t + 2), of the other (4t + 1, 4t + 3), i.e.
+//     k_attn_flash's even and odd chains; s = even + odd.  Lane l holds its query row
+//     l % 32 for keys 32 T + 8 (i / 4) + 4 (l / 32) + i % 4;
+//   max, exp and wave_sum's butterfly tree in-lane (the offset-4 level across the
+//     lane halves), l = fma(l, corr, sum);
+//   O^T = O^T corr, then O^T += V^T P^T in 32 steps of keys (2s, 2s + 1): fma(v, p, o)
+//     in key order.  P^T's operand for key 2s + h comes from the lane half that holds
+//     it (one swap across the halves per step).
+// K and V arrive raw by LDS-DMA in a 3-chunk ring, two chunks ahead; K is scaled by s
+// into a padded plane (row stride 34: conflict-free 8-byte fragment reads).
+#define MF_KC 64
+#define MF_KR 34
+#define MF_RING 3
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_attn_mf32(AttnArgs a) {
+    constexpr int NT = 64 * NW, ROWS = 32 * NW;
+    constexpr int DPW = 16 / NW;
+    __shared__ __attribute__((aligned(16))) float Kr[MF_RING][MF_KC * 32];
+    __shared__ __attribute__((aligned(16))) float Vr[MF_RING][MF_KC * 32];
+    __shared__ __attribute__((aligned(16))) float Kp[MF_KC * MF_KR];
+    __shared__ int wk[NW];
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r32 = lane & 31, hs = lane >> 5;
+    const int* tl = a.tiles + 3 * blockIdx.y;
+    const long kvbase = (long)h * a.tmax * 32 + (long)tl[0] * a.seq_stride;
+    const int r0 = tl[1], nr = tl[2];
+    const float sc = a.scale;
+    const int row = 32 * w + r32;
+    const int len = row < nr ? a.row_len[r0 + row] : 0;
+    int wkmax = len;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wkmax = max(wkmax, __shfl_xor(wkmax, o, 64));
+    if (lane == 0) wk[w] = wkmax;
+    // B fragments of S^T: (q s)[row][4t + 2 hs] (even chain) and [4t + 2 hs + 1] (odd)
+    float qe[8], qo[8];
+    {
+        const float* qp = a.q + (long)(r0 + (row < nr ? row : 0)) * a.ldq + h * 32 + 2 * hs;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const float2 v = *reinterpret_cast<const float2*>(qp + 4 * t);
+            qe[t] = v.x * sc;
+            qo[t] = v.y * sc;
+        }
+    }
+    __syncthreads();
+    int kmax = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) kmax = max(kmax, wk[i]);
+    const float* K = a.k + kvbase;
+    const float* V = a.v + kvbase;
+    auto dma = [&](int c) {
+        const int slot = c % MF_RING;
+#pragma unroll
+        for (int i = 0; i < 8 / NW; ++i) {
+            const int j = w + NW * i, key = MF_KC * c + 8 * j + (lane >> 3);
+            const long src = (long)(key < kmax ? key : 0) * 32 + 4 * (lane & 7);
+            gx3_dma(K + src, &Kr[slot][j * 256]);
+            gx3_dma(V + src, &Vr[slot][j * 256]);
+        }
+    };
+    // raw K of chunk c -> Kp = k s (padded rows)
+    auto scale_k = [&](int c) {
+        const int slot = c % MF_RING;
+#pragma unroll
+        for (int i = 0; i < MF_KC * 8 / NT; ++i) {
+            const int e = tid + NT * i, t = e >> 3, cc = e & 7;
+            const float4 v = *reinterpret_cast<const float4*>(&Kr[slot][t * 32 + 4 * cc]);
+            float2* d = reinterpret_cast<float2*>(&Kp[t * MF_KR + 4 * cc]);
+            d[0] = make_float2(v.x * sc, v.y * sc);
+            d[1] = make_float2(v.z * sc, v.w * sc);
+        }
+    };
+    float m = -INFINITY, l = 0.f;
+    f32x16 o;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] = 0.f;
+    const int nch = (kmax + MF_KC - 1) / MF_KC;
+    if (nch > 0) {
+        for (int c = 0; c < MF_RING && c < nch; ++c) dma(c);
+        gx3_wait<DPW>(min(MF_RING, nch) - 1);
+        __syncthreads();
+        scale_k(0);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const int k0 = c * MF_KC, slot = c % MF_RING;
+        if (k0 < wkmax) {
+            f32x16 s[2];
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+                f32x16 se, so;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { se[i] = 0.f; so[i] = 0.f; }
+                const float* kr = &Kp[(32 * T + r32) * MF_KR + 2 * hs];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const float2 kk = *reinterpret_cast<const float2*>(kr + 4 * t);
+                    se = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.x, qe[t], se, 0, 0, 0);
+                    so = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.y, qo[t], so, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int key = k0 + 32 * T + 8 * (i >> 2) + 4 * hs + (i & 3);
+                    s[T][i] = key < len ? se[i] + so[i] : -INFINITY;
+                }
+            }
+            float mc = -INFINITY;
+#pragma unroll
+            for (int T = 0; T < 2; ++T)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) mc = fmaxf(mc, s[T][i]);
+            mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+            const float mn = fmaxf(m, mc);
+            const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+#pragma unroll
+            for (int T = 0; T < 2; ++T)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) s[T][i] = s[T][i] == -INFINITY ? 0.f : __expf(s[T][i] - mn);
+            // wave_sum's tree over the chunk's key index k: k + 32 (T), + 16 (i + 8), + 8
+            // (i + 4), + 4 (the other lane half), + 2 (i + 2), + 1 (i + 1)
+            float u[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) u[i] = (s[0][i] + s[1][i]) + (s[0][i + 8] + s[1][i + 8]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) u[i] = u[i] + u[i + 4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) u[i] = u[i] + __shfl_xor(u[i], 32, 64);
+            const float sum = (u[0] + u[2]) + (u[1] + u[3]);
+            l = __builtin_fmaf(l, corr, sum);
+            m = mn;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[i] *= corr;
+            // O^T += V^T P^T: step st takes keys (2 st, 2 st + 1); lane half hs supplies key 2 st + hs
+            const float* vr = &Vr[slot][hs * 32 + r32];
+#pragma unroll
+            for (int st = 0; st < 32; ++st) {
+                const int kk = (2 * st) & 31, T = (2 * st) >> 5;
+                const int hold = (kk >> 2) & 1;                 // lane half holding keys 2 st, 2 st + 1
+                const int ri = 4 * (kk >> 3) + (kk & 3);        // their register index: ri, ri + 1
+                const float give = hs ? s[T][ri] : s[T][ri + 1];   // the key the other half needs
+                const float got = __shfl_xor(give, 32, 64);
+                const float p = hs == hold ? (hs ? s[T][ri + 1] : s[T][ri]) : got;
+                o = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[64 * st], p, o, 0, 0, 0);
+            }
+        }
+        if (c + 1 < nch) {
+            gx3_wait<DPW>(min(c + MF_RING - 1, nch - 1) - (c + 1));
+            __syncthreads();   // chunk c + 1 landed; every wave done with Kp and slot c
+            if (c + MF_RING < nch) dma(c + MF_RING);
+            scale_k(c + 1);
+            __syncthreads();
+        }
+    }
+    if (row < nr) {
+        float* dst = a.out + (long)(r0 + row) * a.ldo + h * 32 + 4 * hs;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(dst + 8 * g) =
+                make_float4(o[4 * g] / l, o[4 * g + 1] / l, o[4 * g + 2] / l, o[4 * g + 3] / l);
+    }
+}
+
+void attn_rows_mf32(const AttnArgs& a, hipStream_t s) {
+    if (a.ntiles <= 0) return;
+    hipLaunchKernelGGL(k_attn_mf32<MF32_NW>, dim3(16, a.ntiles), dim3(64 * MF32_NW), 0, s, a);
+}
+
 void attn_rows_rowlane(const AttnArgs& a, hipStream_t s) {
     if (a.ntiles <= 0) return;
     hipLaunchKernelGGL(k_attn_rowlane<ROWLANE_NW>, dim3(16, a.ntiles), dim3(64 * ROWLANE_NW), 0, s, a);
