@@ -519,7 +519,8 @@ int gsv_engine::prefill_slot(int b, const float* x, int L, const int64_t* pr, in
         at.q = pQ; at.ldq = 512; at.k = kcache[l] + b * sstride; at.v = vcache[l] + b * sstride;
         at.seq_stride = sstride; at.tmax = tmax; at.row_len = prow_len; at.out = pO; at.ldo = 512;
         at.rows = N0; at.scale = qk_scale;
-        attn_rows(at, st);
+        if (use_attn_mf32 && prefill_mf32_on()) attn_rows_mf32_seq(at, st);   // the f32 MFMA, k_attn_flash's arithmetic
+        else attn_rows(at, st);
         // out-proj and FFN2 have 32 output tiles: split K over 4 / 8 blocks into slabs,
         // reduced in fixed order (+ bias + residual) by the LayerNorm that follows
         const bool slabs = gemm_slabs_supported(512, 512, 512) && gemm_slabs_supported(2048, 2048, 2048);
@@ -638,7 +639,7 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     static const bool rowlane_opt = [] { const char* e = std::getenv("GENIE_PACKED_ROWLANE"); return !(e && std::atoi(e) == 0); }();
     // the same arithmetic on the f32 MFMA (k_attn_mf32; GENIE_PACKED_MF32=0: k_attn_rowlane)
     static const bool mf32_opt = [] { const char* e = std::getenv("GENIE_PACKED_MF32"); return !(e && std::atoi(e) == 0); }();
-    const bool mf32 = !mfma_attn && mf32_opt;
+    const bool mf32 = !mfma_attn && mf32_opt && use_attn_mf32;
     const bool rowlane = !mfma_attn && !mf32 && rowlane_opt;
     const int TR = mfma_attn ? 128 : mf32 ? 32 * MF32_NW : rowlane ? 64 * ROWLANE_NW : 16;
     int ntiles = 0, maxn0 = 0;
@@ -1891,6 +1892,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     const std::string n(name);
     if (n == "packed") {          // batched generate: one packed prefill over all utterances
         eng->use_packed = value != 0;
+    } else if (n == "attn_mf32") {   // prefill attention on the f32 MFMA (0: k_attn_flash; same results)
+        eng->use_attn_mf32 = value != 0;
     } else if (n == "persist") {   // also ends a timeout back-off
         eng->use_persist = value != 0;
         eng->persist_hold = 0;

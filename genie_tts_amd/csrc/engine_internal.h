@@ -227,6 +227,7 @@ struct gsv_engine {
     int encode(const gsv_utt* u, float* x, int64_t* prompts, hipStream_t st, bool do_prompts = true);
     // packed (multi-utterance) prefill
     bool use_packed = true;            // option "packed"
+    bool use_attn_mf32 = true;         // option "attn_mf32": prefill attention on k_attn_mf32 (else k_attn_flash)
     int pk_rows = 0, pk_batch = 0;
     std::vector<void*> pk_allocs;
     float *pk_H = nullptr, *pk_Q = nullptr, *pk_O = nullptr, *pk_S = nullptr, *pk_H1 = nullptr, *pk_F = nullptr;

@@ -18,5 +18,8 @@ void attn_rows_rowlane(const AttnArgs& a, hipStream_t s);
 // chain): a.tiles of <= 32 MF32_NW rows of one sequence
 constexpr int MF32_NW = 4;
 void attn_rows_mf32(const AttnArgs& a, hipStream_t s);
+// one sequence (a.tiles null, rows from 0), 32 rows per single-wave block
+bool prefill_mf32_on();
+void attn_rows_mf32_seq(const AttnArgs& a, hipStream_t s);
 
 }  // namespace gsv

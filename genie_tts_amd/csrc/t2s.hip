@@ -1512,9 +1512,16 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mf32(AttnArgs a) {
     __shared__ int wk[NW];
     const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r32 = lane & 31, hs = lane >> 5;
-    const int* tl = a.tiles + 3 * blockIdx.y;
-    const long kvbase = (long)h * a.tmax * 32 + (long)tl[0] * a.seq_stride;
-    const int r0 = tl[1], nr = tl[2];
+    // a.tiles: tile blockIdx.y {sequence, first row, rows <= ROWS}; else rows
+    // ROWS blockIdx.y .. of the one sequence at a.k / a.v
+    long kvbase = (long)h * a.tmax * 32;
+    int r0 = ROWS * blockIdx.y, nr = min(ROWS, a.rows - r0);
+    if (a.tiles) {
+        const int* tl = a.tiles + 3 * blockIdx.y;
+        kvbase += (long)tl[0] * a.seq_stride;
+        r0 = tl[1];
+        nr = tl[2];
+    }
     const float sc = a.scale;
     const int row = 32 * w + r32;
     const int len = row < nr ? a.row_len[r0 + row] : 0;
@@ -1654,6 +1661,18 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mf32(AttnArgs a) {
 void attn_rows_mf32(const AttnArgs& a, hipStream_t s) {
     if (a.ntiles <= 0) return;
     hipLaunchKernelGGL(k_attn_mf32<MF32_NW>, dim3(16, a.ntiles), dim3(64 * MF32_NW), 0, s, a);
+}
+
+// One sequence's prefill (rows = its N0 positions) on k_attn_mf32, one wave per 32 rows.
+// Opt-in (GENIE_PREFILL_MF32=1): bit-identical to k_attn_flash, but no faster at ~300 rows
+// in the single-sentence stream (15.28 vs 15.32 ms per utterance, profiles/r05m_prefill_mf32_ab.txt)
+bool prefill_mf32_on() {
+    static const bool on = [] { const char* e = std::getenv("GENIE_PREFILL_MF32"); return e && std::atoi(e) != 0; }();
+    return on;
+}
+void attn_rows_mf32_seq(const AttnArgs& a, hipStream_t s) {
+    if (a.rows <= 0) return;
+    hipLaunchKernelGGL(k_attn_mf32<1>, dim3(16, (a.rows + 31) / 32), dim3(64), 0, s, a);
 }
 
 void attn_rows_rowlane(const AttnArgs& a, hipStream_t s) {

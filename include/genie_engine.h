@@ -366,7 +366,9 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
  * too, see gsv_vits_decode_batch), "convh" (MRF convs on the split-fp16 MFMA),
  * "convt_f16" (1, default: the upsample ConvTransposes on it too), "mrf_fused" (1, default:
  * each conv pair of an MRF resblock step of the C <= 32 stages as one kernel, its
- * intermediate in LDS), "sv_f16", "packed",
+ * intermediate in LDS), "sv_f16", "packed", "attn_mf32" (1, default: the prefill's
+ * attention on the f32 MFMA with k_attn_flash's exact fma chains; 0: k_attn_flash itself,
+ * bit-identical results),
  * test hooks ("persist_spin_ticks", "persist1_f16_limit", "sv_f16_limit", "convh_tile":
  * 1..4 forces that k_conv_h tile candidate, 0 the cost model).  "ptrace": 1 allocates per-workgroup phase stamps of the persistent
  * launch (step 8, layer 12), read back with gsv_debug_ptrace ([256 workgroups][16

@@ -72,7 +72,9 @@ def test_packed_prefill_attention_matches_per_sequence_prefill(eng):
     packed prefill's attention runs the f32 kernels the per-sequence prefill runs (the
     split-fp16 MFMA kernel k_attn_mfma is opt-in, GENIE_ATTN_MFMA=1: it flipped a near-tie
     token against the sentence alone, test_persistm_gpu.py), so the rows are bit-identical;
-    with the MFMA kernel the bar is max |diff| <= 1e-4 x max |value|."""
+    with the MFMA kernel the bar is max |diff| <= 1e-4 x max |value|.  The packed side runs
+    k_attn_mf32 (the f32 MFMA, 128-row tiles), the per-sequence side k_attn_flash itself
+    (option attn_mf32 = 0)."""
     import os
     from genie_tts_amd import workloads
     from genie_tts_amd.engine import make_sampler
@@ -80,11 +82,15 @@ def test_packed_prefill_attention_matches_per_sequence_prefill(eng):
     utts = [u[:5] + (1,) for u in _utts(wl)[:8]]   # one loop step: the prefill's K/V, then the cache
     sp = make_sampler(top_k=5, greedy=True)
     kv = {}
-    for packed in (1, 0):
-        eng.set_option("packed", packed)
-        eng.t2s_generate(utts, sp)
-        kv[packed] = [[t.cpu().numpy() for t in eng.t2s_read_kv(23, seq=b)] for b in range(len(utts))]
-    eng.set_option("packed", 1)
+    try:
+        for packed in (1, 0):
+            eng.set_option("packed", packed)
+            eng.set_option("attn_mf32", packed)   # per-sequence side on k_attn_flash itself
+            eng.t2s_generate(utts, sp)
+            kv[packed] = [[t.cpu().numpy() for t in eng.t2s_read_kv(23, seq=b)] for b in range(len(utts))]
+    finally:
+        eng.set_option("packed", 1)
+        eng.set_option("attn_mf32", 1)
     for b in range(len(utts)):
         for a, r in zip(kv[1][b], kv[0][b]):
             assert a.shape == r.shape and a.shape[0] > 128
@@ -93,3 +99,30 @@ def test_packed_prefill_attention_matches_per_sequence_prefill(eng):
                 assert err <= 1e-4 * float(np.abs(r).max()), (b, err)
             else:
                 assert err == 0.0, (b, err)
+
+
+def test_single_prefill_attention_mf32_matches_flash(eng):
+    """One sentence's prefill with its attention on k_attn_mf32 (32-row single-wave
+    blocks; GENIE_PREFILL_MF32=1, else this compares k_attn_flash with itself) and on
+    k_attn_flash (option attn_mf32 = 0): layer-0 and layer-23 K/V bit-identical, and the
+    same tokens over 20 steps.  The f32 MFMA computes each element as a sequential fma
+    chain (tools/mfma_f32_probe.hip), so the kernels' per-row arithmetic is the same;
+    r05m ran it with GENIE_PREFILL_MF32=1."""
+    from genie_tts_amd import workloads
+    from genie_tts_amd.engine import make_sampler
+    wl = workloads.batch64(4, tag="mf32")
+    sp = make_sampler(top_k=5, greedy=True)
+    for u in _utts(wl):
+        u = u[:5] + (20,)
+        got = {}
+        try:
+            for mf in (1, 0):
+                eng.set_option("attn_mf32", mf)
+                toks = eng.t2s_generate([u], sp)[0]
+                got[mf] = (toks.tolist(), [[t.cpu().numpy() for t in eng.t2s_read_kv(l, seq=0)] for l in (0, 23)])
+        finally:
+            eng.set_option("attn_mf32", 1)
+        assert got[1][0] == got[0][0]
+        for la, lr in zip(got[1][1], got[0][1]):
+            for a, r in zip(la, lr):
+                assert a.shape == r.shape and np.array_equal(a, r)
