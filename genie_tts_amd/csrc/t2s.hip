@@ -1490,13 +1490,13 @@ __global__ __launch_bounds__(64 * NW) void k_attn_rowlane(AttnArgs a) {
 // sequence, wave w owns rows 32 w .. 32 w + 31.  Per 64-key chunk:
 //   S^T = K Q^T twice, A = the chunk's (k s) rows, B = the wave's (q s) rows: step t of
 //     one accumulator takes dims (4t, 4t + 2), of the other (4t + 1, 4t + 3), i.e.
-//     k_attn_flash's even and odd chains; s = even + odd.  Lane l holds its query row
-//     l % 32 for keys 32 T + 8 (i / 4) + 4 (l / 32) + i % 4;
-//   max, exp and wave_sum's butterfly tree in-lane (the offset-4 level across the
+//     k_attn_flash's even and odd chains; s = even + odd.  A row r of a 32-key tile T
+//     holds key 8 (r / 8) + 2 (r % 4) + (r / 4) % 2, so accumulator element i of lane
+//     l holds query row l % 32 and key 32 T + 2 i + l / 32;
+//   max, exp and wave_sum's butterfly tree in-lane (the offset-1 level across the
 //     lane halves), l = fma(l, corr, sum);
 //   O^T = O^T corr, then O^T += V^T P^T in 32 steps of keys (2s, 2s + 1): fma(v, p, o)
-//     in key order.  P^T's operand for key 2s + h comes from the lane half that holds
-//     it (one swap across the halves per step).
+//     in key order; lane half h's P^T operand, key 2s + h, is its own element s % 16.
 // K and V arrive raw by LDS-DMA in a 3-chunk ring, two chunks ahead; K is scaled by s
 // into a padded plane (row stride 34: conflict-free 8-byte fragment reads).
 #define MF_KC 64
@@ -1589,7 +1589,10 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mf32(AttnArgs a) {
                 f32x16 se, so;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) { se[i] = 0.f; so[i] = 0.f; }
-                const float* kr = &Kp[(32 * T + r32) * MF_KR + 2 * hs];
+                // A row r32 holds key krow: accumulator element i of lane half hs is then
+                // key 2 i + hs (see above)
+                const int krow = 8 * (r32 >> 3) + 2 * (r32 & 3) + ((r32 >> 2) & 1);
+                const float* kr = &Kp[(32 * T + krow) * MF_KR + 2 * hs];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     const float2 kk = *reinterpret_cast<const float2*>(kr + 4 * t);
@@ -1598,7 +1601,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mf32(AttnArgs a) {
                 }
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const int key = k0 + 32 * T + 8 * (i >> 2) + 4 * hs + (i & 3);
+                    const int key = k0 + 32 * T + 2 * i + hs;
                     s[T][i] = key < len ? se[i] + so[i] : -INFINITY;
                 }
             }
@@ -1614,32 +1617,25 @@ __global__ __launch_bounds__(64 * NW) void k_attn_mf32(AttnArgs a) {
             for (int T = 0; T < 2; ++T)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) s[T][i] = s[T][i] == -INFINITY ? 0.f : __expf(s[T][i] - mn);
-            // wave_sum's tree over the chunk's key index k: k + 32 (T), + 16 (i + 8), + 8
-            // (i + 4), + 4 (the other lane half), + 2 (i + 2), + 1 (i + 1)
+            // wave_sum's tree over the chunk's key index k = 32 T + 2 i + hs: k + 32 (T),
+            // + 16 (i + 8), + 8 (i + 4), + 4 (i + 2), + 2 (i + 1), + 1 (the other lane half)
             float u[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) u[i] = (s[0][i] + s[1][i]) + (s[0][i + 8] + s[1][i + 8]);
 #pragma unroll
             for (int i = 0; i < 4; ++i) u[i] = u[i] + u[i + 4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) u[i] = u[i] + __shfl_xor(u[i], 32, 64);
-            const float sum = (u[0] + u[2]) + (u[1] + u[3]);
+            float sum = (u[0] + u[2]) + (u[1] + u[3]);
+            sum = sum + __shfl_xor(sum, 32, 64);
             l = __builtin_fmaf(l, corr, sum);
             m = mn;
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[i] *= corr;
-            // O^T += V^T P^T: step st takes keys (2 st, 2 st + 1); lane half hs supplies key 2 st + hs
+            // O^T += V^T P^T: step st takes keys (2 st, 2 st + 1); lane half hs supplies key
+            // 2 st + hs, its own element st % 16 of tile st / 16
             const float* vr = &Vr[slot][hs * 32 + r32];
 #pragma unroll
-            for (int st = 0; st < 32; ++st) {
-                const int kk = (2 * st) & 31, T = (2 * st) >> 5;
-                const int hold = (kk >> 2) & 1;                 // lane half holding keys 2 st, 2 st + 1
-                const int ri = 4 * (kk >> 3) + (kk & 3);        // their register index: ri, ri + 1
-                const float give = hs ? s[T][ri] : s[T][ri + 1];   // the key the other half needs
-                const float got = __shfl_xor(give, 32, 64);
-                const float p = hs == hold ? (hs ? s[T][ri + 1] : s[T][ri]) : got;
-                o = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[64 * st], p, o, 0, 0, 0);
-            }
+            for (int st = 0; st < 32; ++st)
+                o = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[64 * st], s[st >> 4][st & 15], o, 0, 0, 0);
         }
         if (c + 1 < nch) {
             gx3_wait<DPW>(min(c + MF_RING - 1, nch - 1) - (c + 1));
