@@ -1,11 +1,13 @@
 """Build libgenie_engine.so (gfx950) in-tree with hipcc.
 
 One shared library, no torch dependency: C ABI in include/genie_engine.h.
-Objects are rebuilt when their source, a .hip it includes, or any header is newer.
+Objects are rebuilt when their source, a .hip it includes, or any header is newer, and all
+of them when the compiler flags change (a hash of FLAGS is kept beside the objects).
 """
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import re
 import subprocess
@@ -41,8 +43,17 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def flags_hash() -> str:
+    return hashlib.sha256(" ".join(FLAGS).encode()).hexdigest()[:16]
+
+
 def build(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(os.path.join(LIB_DIR, "obj"), exist_ok=True)
+    # objects built with other flags (e.g. before NO_PACKED_FP32) are stale whatever their mtime
+    stamp = os.path.join(LIB_DIR, "obj", "FLAGS")
+    fh = flags_hash()
+    if not os.path.exists(stamp) or open(stamp).read().strip() != fh:
+        force = True
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     hdr = _headers_mtime()
     cc = _hipcc()
@@ -76,6 +87,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    with open(stamp, "w") as f:
+        f.write(fh + "\n")
     return LIB
 
 

@@ -124,11 +124,13 @@ int gsv_engine::roberta_forward(const int64_t* ids, int N, const int* rows, int 
     const size_t need = (size_t)N * (1024 * 4 + 3072 + 4096) + (size_t)n_out + 3 * (size_t)N + 64 +
                         (size_t)zmax * N * 1024;
     if (need > bert.ws_floats) {
+        const size_t cap = grow_cap(need, bert.ws_floats);
         retire(bert.ws);
         bert.ws = nullptr;
         bert.ws_floats = 0;
-        if (hipMalloc(&bert.ws, need * 4) != hipSuccess) return set_error(GSV_E_HIP, "RoBERTa workspace");
-        bert.ws_floats = need;
+        reclaim();
+        if (hipMalloc(&bert.ws, cap * 4) != hipSuccess) return set_error(GSV_E_HIP, "RoBERTa workspace");
+        bert.ws_floats = cap;
     }
     float* h = bert.ws;
     float *tmp = h + (size_t)N * 1024, *att = tmp + (size_t)N * 1024, *qkv = att + (size_t)N * 1024;

@@ -44,6 +44,58 @@ int hip_error(const std::string& what, hipError_t e) {
 }  // namespace gsv
 
 // ------------------------------------------------------------ allocation
+std::shared_mutex gsv::capture_mu;
+
+static int64_t alloc_bytes(void* p) {
+    size_t n = 0;
+    return p && hipMemPtrGetInfo(p, &n) == hipSuccess ? (int64_t)n : 0;
+}
+
+void gsv_engine::retire(void* p) {
+    if (!p) return;
+    const int64_t n = alloc_bytes(p);
+    std::lock_guard<std::mutex> g(alloc_mu);
+    retired.push_back(p);
+    retired_bytes += n;
+}
+
+void gsv_engine::retire_host(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(alloc_mu);
+    retired_host.push_back(p);
+}
+
+// Free the retired buffers.  Skipped while a vocoder batch's lane threads may still be issuing
+// work (they are joined by vits_batch_finish; the next growth reclaims).  This engine's streams
+// are drained first, so no queued kernel still reads a retired buffer, and no capture runs in
+// the process while hipFree synchronises the device.
+void gsv_engine::reclaim() {
+    if (vb_active) return;
+    std::vector<void*> d, h;
+    int64_t nb = 0;
+    {
+        std::lock_guard<std::mutex> g(alloc_mu);
+        if (retired.empty() && retired_host.empty()) return;
+        d.swap(retired);
+        h.swap(retired_host);
+        nb = retired_bytes;
+        retired_bytes = 0;
+    }
+    std::unique_lock<std::shared_mutex> cl(gsv::capture_mu);
+    if (sync_own_streams() != hipSuccess) {   // keep them: a later pass (or the destructor) frees them
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(alloc_mu);
+        retired.insert(retired.end(), d.begin(), d.end());
+        retired_host.insert(retired_host.end(), h.begin(), h.end());
+        retired_bytes += nb;
+        return;
+    }
+    for (void* p : d) hipFree(p);
+    for (void* p : h) hipHostFree(p);
+    reclaimed_bytes += nb;
+    ++reclaims;
+}
+
 void* gsv_engine::dalloc(size_t bytes) {
     void* p = nullptr;
     if (bytes == 0) bytes = 16;
@@ -62,6 +114,7 @@ void gsv_engine::release_all() {
 
 gsv_engine::~gsv_engine() {
     for (auto& t : vb_threads) t.join();
+    std::unique_lock<std::shared_mutex> cl(gsv::capture_mu);   // hipFree below synchronises the device
     release_all();
     for (void* p : pk_allocs) hipFree(p);
     pk_allocs.clear();
@@ -113,6 +166,7 @@ gsv_engine::~gsv_engine() {
     if (perr) hipFree(perr);
     for (void* p : state_allocs) hipFree(p);
     state_allocs.clear();
+    for (void* p : enc_allocs) hipFree(p);
     for (auto& e : poll_ev) if (e) hipEventDestroy(e);
     for (auto& e : ev) if (e) hipEventDestroy(e);
     if (ev_in) hipEventDestroy(ev_in);
@@ -369,9 +423,16 @@ int gsv_engine::reserve(int batch, int tokens) {
     // graphs capture buffer addresses: drop them before reallocating
     for (auto& kv : graphs) hipGraphExecDestroy(kv.second);
     graphs.clear();
-    const int nb = std::max(batch, max_batch), nt = std::max(tokens, tmax);
+    // quantised growth: batch to a power of two (<= 64), tokens to a multiple of 256 (<= the
+    // PE table), so a server's load ramp re-allocates a few times, not once per new maximum
+    int pb = 1;
+    while (pb < batch) pb <<= 1;
+    const int nb = std::max(max_batch, std::min(64, pb));
+    const int nt = std::max(tmax, std::min(pe_max - 1, (tokens + 255) / 256 * 256));
     for (void* p : state_allocs) retire(p);
     state_allocs.clear();
+    max_batch = tmax = 0;   // nothing is allocated until the new state is complete
+    reclaim();              // the old state's memory goes back before the new state is allocated
     auto A = [&](size_t bytes) -> void* {
         void* p = nullptr;
         if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
@@ -437,14 +498,24 @@ static __global__ void k_fill_row_len(int* rl, int L, int N0) {
 
 int gsv_engine::ensure_enc_ws(int P, int L) {
     if (P <= enc_cap_p && L <= enc_cap_l) return 0;
-    const int cp = std::max(P, enc_cap_p), cl = std::max(L, enc_cap_l);
-    e_im2col = (float*)dalloc((size_t)cp * 1536 * 4);
-    e_h = (float*)dalloc((size_t)cp * 768 * 4);
-    e_hh = (float*)dalloc((size_t)cp * 4);
-    e_dist = (float*)dalloc((size_t)cp * 1024 * 4);
-    e_bproj = (float*)dalloc((size_t)cl * 512 * 4);
-    e_bert = (float*)dalloc((size_t)cl * 1024 * 4);
-    if (!e_bert) return set_error(GSV_E_HIP, "encoder workspace");
+    const int cp = (int)grow_cap(P, enc_cap_p), cl = (int)grow_cap(L, enc_cap_l);
+    for (void* p : enc_allocs) retire(p);
+    enc_allocs.clear();
+    enc_cap_p = enc_cap_l = 0;
+    reclaim();
+    auto A = [&](size_t bytes) -> float* {
+        void* p = nullptr;
+        if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
+        enc_allocs.push_back(p);
+        return (float*)p;
+    };
+    e_im2col = A((size_t)cp * 1536 * 4);
+    e_h = A((size_t)cp * 768 * 4);
+    e_hh = A((size_t)cp * 4);
+    e_dist = A((size_t)cp * 1024 * 4);
+    e_bproj = A((size_t)cl * 512 * 4);
+    e_bert = A((size_t)cl * 1024 * 4);
+    if (!e_im2col || !e_h || !e_hh || !e_dist || !e_bproj || !e_bert) return set_error(GSV_E_HIP, "encoder workspace");
     enc_cap_p = cp;
     enc_cap_l = cl;
     return 0;
@@ -589,9 +660,11 @@ static __global__ void k_gather_rows512(const float* src, const int* rows, float
 
 int gsv_engine::ensure_packed(int rows, int B) {
     if (rows <= pk_rows && B <= pk_batch) return 0;
-    const int nr = std::max(rows, pk_rows), nb = std::max(B, pk_batch);
+    const int nr = (int)grow_cap(rows, pk_rows), nb = (int)grow_cap(B, pk_batch);
     for (void* p : pk_allocs) retire(p);
     pk_allocs.clear();
+    pk_rows = pk_batch = 0;
+    reclaim();
     auto A = [&](size_t bytes) -> void* {
         void* p = nullptr;
         if (hipMalloc(&p, (bytes + 255) & ~(size_t)255) != hipSuccess) return nullptr;
@@ -671,12 +744,14 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     hipMemcpyAsync(pk_rowinfo, hs, (size_t)3 * R * 4, hipMemcpyHostToDevice, st);
     hipMemcpyAsync(pk_last, hlast, (size_t)B * 4, hipMemcpyHostToDevice, st);
     if (ntiles > pk_tile_cap) {
+        const int cap = (int)grow_cap(ntiles, pk_tile_cap);
         retire(pk_tiles);
         pk_tiles = nullptr;
         pk_tile_cap = 0;
-        if (hipMalloc((void**)&pk_tiles, (size_t)3 * ntiles * 4) != hipSuccess)
+        reclaim();
+        if (hipMalloc((void**)&pk_tiles, (size_t)3 * cap * 4) != hipSuccess)
             return set_error(GSV_E_HIP, "packed prefill tile table");
-        pk_tile_cap = ntiles;
+        pk_tile_cap = cap;
     }
     hipMemcpyAsync(pk_tiles, htile, (size_t)3 * ntiles * 4, hipMemcpyHostToDevice, st);
     // the LDS-staged tile kernel measured slower here (prefill 62.5 vs 45.4 ms at B=64):
@@ -929,6 +1004,7 @@ hipGraphExec_t gsv_engine::step_graph(int B, const gsv_sampler* sp, int chunk, h
     auto it = graphs.find(key);
     if (it != graphs.end()) return it->second;
     hipGraph_t g = nullptr;
+    std::shared_lock<std::shared_mutex> cl(gsv::capture_mu);   // no device-synchronising free meanwhile
     if ((graph_err = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal)) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
@@ -1077,11 +1153,16 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, in
     const int layout = B == 1 ? -1 : -100 - B;   // ring layout key: the kernels slot the ring differently
     if (need > pws_bytes || layout != pws_batch) {
         if (need > pws_bytes) {
+            // sized for the next power-of-two batch (<= 64): a ramp of B re-allocates log2 times
+            int pb = 2;
+            while (pb < B) pb <<= 1;
+            const size_t cap = B == 1 ? need : std::max(need, persist1m_ring_bytes(std::min(pb, 64)));
             retire(pws);
             pws = nullptr;
             pws_bytes = 0;
-            if (hipMalloc(&pws, need) != hipSuccess) return set_error(GSV_E_HIP, "persistent ring");
-            pws_bytes = need;
+            reclaim();
+            if (hipMalloc(&pws, cap) != hipSuccess) return set_error(GSV_E_HIP, "persistent ring");
+            pws_bytes = cap;
         }
         hipMemsetAsync(pws, 0, pws_bytes, st);
         pws_batch = layout;
@@ -1361,12 +1442,13 @@ hipError_t gsv_engine::host_wait(hipStream_t st) {
 int gsv_engine::ensure_res_pin(int batch) {
     const size_t need = (size_t)batch * 8 + (size_t)batch * tmax * 8;
     if (need <= res_pin_bytes) return 0;
+    const size_t cap = grow_cap(need, res_pin_bytes);
     retire_host(res_pin);
     res_pin = nullptr;
     res_pin_bytes = 0;
-    if (hipHostMalloc((void**)&res_pin, need, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&res_pin, cap, hipHostMallocDefault) != hipSuccess)
         return set_error(GSV_E_HIP, "pinned result buffer");
-    res_pin_bytes = need;
+    res_pin_bytes = cap;
     return 0;
 }
 
@@ -1462,6 +1544,8 @@ extern "C" int gsv_finalize_weights(gsv_engine* eng) {
     ENG_CHECK(eng);
     hipSetDevice(eng->device);
     if (eng->finalized) return set_error(GSV_E_STATE, "already finalized");
+    // the uploads are synchronous null-stream copies: no other thread's capture may run meanwhile
+    std::unique_lock<std::shared_mutex> cl(gsv::capture_mu);
     const bool has_hubert = eng->find("feature_extractor.conv_layers.0.conv.weight") != nullptr;
     const bool has_roberta = eng->find("embeddings.word_embeddings.weight") != nullptr;
     const bool has_sv = eng->find("layer3_ds.weight") != nullptr;
@@ -2017,6 +2101,9 @@ extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value
     else if (n == "persist_hold") *value = eng->persist_hold;
     else if (n == "stops") *value = eng->stops;
     else if (n == "graph_fallbacks") *value = eng->graph_fallbacks;
+    else if (n == "retired_bytes") { std::lock_guard<std::mutex> g(eng->alloc_mu); *value = eng->retired_bytes; }
+    else if (n == "reclaimed_bytes") *value = eng->reclaimed_bytes;
+    else if (n == "reclaims") *value = eng->reclaims;
     else return set_error(GSV_E_ARG, "unknown counter " + n);
     return 0;
 }

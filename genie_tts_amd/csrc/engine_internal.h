@@ -3,8 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <string>
 #include <vector>
@@ -18,6 +20,13 @@ int set_error(int code, const std::string& msg);
 int hip_error(const std::string& what, hipError_t e);   // GSV_E_HIP, the message naming the HIP error
 int f16_inexact_error(const std::string& weight, const float* v, int64_t index);
 struct StreamScope;
+// Process-wide: every stream capture of the library holds it shared from begin to end; code
+// that synchronises the device (hipFree / hipHostFree of retired buffers, weight upload,
+// engine teardown) holds it exclusively, so it never invalidates another thread's capture.
+extern std::shared_mutex capture_mu;
+// Growth policy of run-time buffers: at least `need`, and at least 1.25x the current capacity,
+// so a load ramp re-allocates O(log) times instead of once per new maximum.
+inline size_t grow_cap(size_t need, size_t cur) { return need <= cur ? cur : std::max(need, cur + cur / 4); }
 constexpr long ACC_SEQ = 24 * 2 * 512;   // fixed-point hand-off accumulators per sequence
 
 struct Staged {
@@ -90,6 +99,7 @@ struct gsv_engine {
     std::vector<void*> allocs;        // weights + workspaces (engine lifetime)
     std::mutex alloc_mu;              // guards allocs (vocoder lane threads)
     std::vector<void*> state_allocs;  // decode capacity (re-sized by reserve)
+    std::vector<void*> enc_allocs;    // encoder workspace (re-sized by ensure_enc_ws)
 
     // ---- T2S weights
     __half* emb_audio = nullptr;
@@ -188,13 +198,20 @@ struct gsv_engine {
     ~gsv_engine();
     void* dalloc(size_t bytes);
     void release_all();
-    // Buffers replaced while the engine runs are retired, not freed: hipFree / hipHostFree
-    // synchronise the device, which invalidates a hipGraph capture running on another thread
-    // (another engine of the process) and fails that thread's call (hipErrorStreamCaptureImplicit,
-    // gpurun_out/r05k_*.err).  Retired buffers are freed when the engine is destroyed.
+    // Buffers replaced while the engine runs are retired, then freed by reclaim(): hipFree /
+    // hipHostFree synchronise the device, which invalidates a hipGraph capture running on
+    // another thread (another engine of the process) and fails that thread's call
+    // (hipErrorStreamCaptureImplicit, gpurun_out/r05k_*.err).  reclaim() frees them under the
+    // exclusive capture_mu after this engine's own streams drained; every growth path calls it
+    // between retiring the old buffer and allocating the new one, so the footprint stays the
+    // live buffers plus one replacement.
     std::vector<void*> retired, retired_host;
-    void retire(void* p) { if (p) { std::lock_guard<std::mutex> g(alloc_mu); retired.push_back(p); } }
-    void retire_host(void* p) { if (p) { std::lock_guard<std::mutex> g(alloc_mu); retired_host.push_back(p); } }
+    int64_t retired_bytes = 0;         // retired, not yet freed (counter "retired_bytes")
+    int64_t reclaimed_bytes = 0;       // freed by reclaim (counter "reclaimed_bytes")
+    int64_t reclaims = 0;              // reclaim passes that freed something (counter "reclaims")
+    void retire(void* p);
+    void retire_host(void* p);
+    void reclaim();
     // Waits for this engine's own streams (engine, vocoder, lanes) -- never a device-wide sync.
     hipError_t sync_own_streams();
     const gsv::Staged* find(const std::string& n) const;

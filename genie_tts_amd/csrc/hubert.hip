@@ -273,11 +273,13 @@ int gsv_engine::finalize_hubert() {
 
 float* gsv_engine::hubert_ws(size_t floats) {
     if (floats > hubert.ws_floats) {
+        const size_t cap = grow_cap(floats, hubert.ws_floats);
         retire(hubert.ws);
         hubert.ws = nullptr;
         hubert.ws_floats = 0;
-        if (hipMalloc(&hubert.ws, floats * 4) != hipSuccess) return nullptr;
-        hubert.ws_floats = floats;
+        reclaim();
+        if (hipMalloc(&hubert.ws, cap * 4) != hipSuccess) return nullptr;
+        hubert.ws_floats = cap;
     }
     return hubert.ws;
 }

@@ -152,6 +152,7 @@ extern "C" int gsv_probe(gsv_engine* eng, int which, int B, int iters, float* us
     } else {
         const int per = 50;
         hipGraph_t g = nullptr;
+        std::shared_lock<std::shared_mutex> cl(gsv::capture_mu);
         if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess)
             return set_error(GSV_E_HIP, "probe capture");
         for (int i = 0; i < per; ++i) launch();

@@ -530,11 +530,13 @@ int gsv_engine::sv_forward(const float* wav, int n, float* out, hipStream_t st, 
     const size_t P1 = (size_t)SV_NMEL * T;
     const size_t need = sv_ws_floats(T);
     if (need > sv_ws_n) {
+        const size_t cap = grow_cap(need, sv_ws_n);
         retire(sv_ws);
         sv_ws = nullptr;
         sv_ws_n = 0;
-        if (hipMalloc(&sv_ws, need * 4) != hipSuccess) return set_error(GSV_E_HIP, "SV workspace");
-        sv_ws_n = need;
+        reclaim();
+        if (hipMalloc(&sv_ws, cap * 4) != hipSuccess) return set_error(GSV_E_HIP, "SV workspace");
+        sv_ws_n = cap;
     }
     float* x = sv_ws;
     float* big[3] = {x + P1, x + P1 + P1 * 256, x + P1 + 2 * P1 * 256};

@@ -206,6 +206,7 @@ struct VitsWorkspace {
     long splitk_cap = 0;
     float *sv = nullptr, *pe_ge = nullptr;
     int cap_text = 0;
+    std::vector<void*> owned;   // the buffers above except splitk (retired when the workspace grows)
 };
 
 struct PromptEncWeights {

@@ -432,11 +432,23 @@ static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_a
     const size_t gen = with_gen ? (size_t)V.upc * T * 20 : 0;   // max C*T over generator stages: upc/2^(i+1) * T*prod(u)
     const int F = n_audio > 0 ? (n_audio + 1408 - 2048) / 640 + 1 : 0;
     if ((size_t)T <= W.cap_t && S <= W.cap_text && gen <= W.cap_gen && F <= W.cap_spec) return 0;
-    const size_t t = std::max((size_t)T, W.cap_t);
-    const int sT = std::max(S, W.cap_text);
-    const size_t g = std::max(gen, W.cap_gen);
-    const int f = std::max(F, W.cap_spec);
-    auto A = [&](size_t n) { return (float*)e->dalloc(n * 4); };
+    // 1.25x headroom on every dimension that grows; the old buffers are retired (freed by
+    // reclaim once nothing queued reads them), so a ramp of utterance lengths does not accumulate
+    const size_t t = grow_cap((size_t)T, W.cap_t);
+    const int sT = (int)grow_cap(S, W.cap_text);
+    const size_t g = gen > W.cap_gen ? grow_cap(gen, W.cap_gen) : W.cap_gen;
+    const int f = (int)grow_cap(F, W.cap_spec);
+    for (void* p : W.owned) e->retire(p);
+    W.owned.clear();
+    W.cap_t = W.cap_gen = 0;
+    W.cap_text = W.cap_spec = 0;
+    e->reclaim();   // a no-op on a lane thread (vb_active): the next growth on the issuing thread frees them
+    auto A = [&](size_t n) -> float* {
+        void* p = nullptr;
+        if (hipMalloc(&p, ((n * 4) + 255) & ~(size_t)255) != hipSuccess) return nullptr;
+        W.owned.push_back(p);
+        return (float*)p;
+    };
     W.q = A(768 * t); W.y = A(192 * t); W.te = A(192 * (size_t)sT);
     W.qkv = A(576 * t); W.att = A(192 * t); W.a = A(512 * t); W.ffn = A(768 * t);
     W.tqkv = A(576 * (size_t)sT); W.tatt = A(192 * (size_t)sT); W.ta = A(192 * (size_t)sT);
@@ -454,8 +466,8 @@ static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_a
         W.r3 = A((size_t)f * 256); W.rq = A((size_t)f * 384); W.ratt = A((size_t)f * 128);
     }
     if (!W.splitk) {
-        W.splitk_cap = 2L << 20;   // 8 MB: >= 384 tiles of 64 x 64
-        W.splitk = A((size_t)W.splitk_cap);
+        W.splitk_cap = 2L << 20;   // 8 MB: >= 384 tiles of 64 x 64 (never re-sized: engine lifetime)
+        W.splitk = (float*)e->dalloc((size_t)W.splitk_cap * 4);
     }
     if ((g > 0 && !W.g4) || !W.splitk || !W.fm) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
     W.cap_t = t; W.cap_text = sT; W.cap_gen = g; W.cap_spec = f;
@@ -945,6 +957,7 @@ int gsv_engine::seg_reserve(int n, int T) {
         for (auto& g : B.g) { retire(g); g = nullptr; }
         for (auto& q : B.seg) { retire(q); q = nullptr; }
         B.cap_t = 0;
+        reclaim();
         long f = 1;
         for (int i = 0; i < 5; ++i) f *= V.up_rate[i];
         bool ok = hipMalloc(&B.z, (size_t)192 * t * 4) == hipSuccess &&
@@ -959,6 +972,7 @@ int gsv_engine::seg_reserve(int n, int T) {
         B.cap_t = t;
     }
     if (n > B.cap_n) {
+        const int cn = (int)grow_cap(n, B.cap_n);
         for (float** p : {&B.dcond}) { retire(*p); *p = nullptr; }
         for (int** p : {&B.off, &B.len, &B.ovf}) { retire(*p); *p = nullptr; }
         retire_host(B.ovf_host);
@@ -968,15 +982,16 @@ int gsv_engine::seg_reserve(int n, int T) {
         B.cap_n = 0;
         for (float** p : {&B.ge, &B.gem, &B.gcond}) { retire(*p); *p = nullptr; }
         const int gin = V.flows[0].cond.cin, gcn = V.flows[0].cond.cout;
-        if (hipMalloc(&B.ge, (size_t)n * gin * 4) != hipSuccess || hipMalloc(&B.gem, (size_t)n * 512 * 4) != hipSuccess ||
-            hipMalloc(&B.gcond, (size_t)n * gcn * 4) != hipSuccess)
+        reclaim();
+        if (hipMalloc(&B.ge, (size_t)cn * gin * 4) != hipSuccess || hipMalloc(&B.gem, (size_t)cn * 512 * 4) != hipSuccess ||
+            hipMalloc(&B.gcond, (size_t)cn * gcn * 4) != hipSuccess)
             return set_error(GSV_E_HIP, "segmented vocoder conditioning");
-        if (hipMalloc(&B.dcond, (size_t)n * V.upc * 4) != hipSuccess || hipMalloc(&B.off, (size_t)n * 4) != hipSuccess ||
-            hipMalloc(&B.len, (size_t)n * 4) != hipSuccess || hipMalloc(&B.ovf, 64) != hipSuccess ||
+        if (hipMalloc(&B.dcond, (size_t)cn * V.upc * 4) != hipSuccess || hipMalloc(&B.off, (size_t)cn * 4) != hipSuccess ||
+            hipMalloc(&B.len, (size_t)cn * 4) != hipSuccess || hipMalloc(&B.ovf, 64) != hipSuccess ||
             hipHostMalloc((void**)&B.ovf_host, 64, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc((void**)&B.h_pin, (size_t)n * 8, hipHostMallocDefault) != hipSuccess)
+            hipHostMalloc((void**)&B.h_pin, (size_t)cn * 8, hipHostMallocDefault) != hipSuccess)
             return set_error(GSV_E_HIP, "segmented vocoder tables");
-        B.cap_n = n;
+        B.cap_n = cn;
     }
     if (!B.done && hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
         return set_error(GSV_E_HIP, "segmented vocoder event");

@@ -529,7 +529,9 @@ class Engine:
                                                  _stream()), "gsv_vits_decode_batch_async")
         # items and device buffers live until the wait -- also a previous batch's, which this
         # call only ordered behind the engine stream (its lanes may still read them)
-        self._vits_batch_keep = (arr, keep, outs, getattr(self, "_vits_batch_keep", None))
+        # (one generation back: a batch older than the previous one was joined by this launch)
+        prev = getattr(self, "_vits_batch_keep", None)
+        self._vits_batch_keep = (arr, keep, outs, prev[:3] if prev else None)
         return outs
 
     def vits_batch_wait(self):
@@ -659,7 +661,8 @@ class Engine:
     def counter(self, name: str) -> int:
         """Engine counter (gsv_get_counter): persist_timeouts, persist1_f16_reruns, vits_f32_reruns,
         sv_f32_reruns, w16_split_tensors, persist_disabled (timeout back-off holds begun),
-        persist_launches, persist_hold (generates left in the current hold), stops, graph_fallbacks."""
+        persist_launches, persist_hold (generates left in the current hold), stops, graph_fallbacks,
+        retired_bytes (replaced device buffers not yet freed), reclaimed_bytes, reclaims."""
         v = ctypes.c_int64()
         _check(lib().gsv_get_counter(self.h, name.encode(), ctypes.byref(v)), "gsv_get_counter")
         return v.value

@@ -383,7 +383,11 @@ int gsv_set_option(gsv_engine* eng, const char* name, int value);
  * packed), "sv_f32_reruns", "w16_split_tensors" (fp32 weights kept as hi + lo
  * planes), "stops" (generates abandoned by gsv_request_stop), "graph_fallbacks"
  * (per-step decode loops run eagerly because their hipGraph capture failed -- e.g.
- * invalidated by another thread's device-wide synchronisation). */
+ * invalidated by another thread's device-wide synchronisation), "retired_bytes" (device
+ * buffers replaced by a capacity growth and not yet freed), "reclaimed_bytes" / "reclaims"
+ * (freed by the growth paths once the engine's streams drained; capacities grow in
+ * quantised steps: batch to a power of two, tokens to a multiple of 256, workspaces by
+ * 1.25x, so a load ramp re-allocates a few times and keeps no dead copies). */
 int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value);
 int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n);
 

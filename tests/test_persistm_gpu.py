@@ -140,3 +140,59 @@ def test_batched_full_500_step_loop(eng):
     a, b = _both(eng, inps, make_sampler())
     assert a == b
     assert all(len(x) >= 450 for x in a)
+
+
+def test_batched_stop_interrupts_and_writes_no_state(eng):
+    """gsv_request_stop during a forced 500-step batched decode at B = 32 (the default path
+    from persistm_min_b = 32; the reference's stop_event, Inference.py:96-97): the launch
+    reads the stop word every 4th step and leaves with error 3 before the sequence-state
+    write-back, so every sequence's KV length is still its prefill length; the generate
+    raises EngineStopped well before the full run, and the same batch decodes bit-exactly
+    afterwards (ADVICE r05 test_persistm_gpu.py:22)."""
+    import time
+    from genie_tts_amd.engine import make_sampler
+    from tests.test_persist_gpu import _stop_during
+    B = 32
+    inps = [t2s_inputs(R=10 + i % 7, S=8 + i % 5, H=30 + 2 * i, tag=f"pmst{i}") for i in range(B)]
+    sp = make_sampler(force_steps=500)
+    full = eng.t2s_generate(inps, sp)
+    t = time.perf_counter()
+    eng.t2s_generate(inps, sp)
+    t_full = time.perf_counter() - t
+    s0, l0 = eng.counter("stops"), eng.counter("persist_launches")
+    stopped, latency, ran = _stop_during(eng, inps, sp, 1, 0.3 * t_full)
+    print(f"B={B}: full {t_full * 1e3:.1f} ms, stopped after {ran * 1e3:.1f} ms, {latency * 1e3:.2f} ms after the request")
+    assert stopped and eng.counter("stops") == s0 + 1
+    assert eng.counter("persist_launches") == l0 + 1   # it was the batched persistent launch
+    assert ran < 0.8 * t_full
+    step = t_full / 500
+    assert latency < 6 * step + 2e-3, latency          # <= 4 steps to the next stop read, plus the exit
+    for b in (0, 13, 31):                              # no sequence state written back
+        k, _ = eng.t2s_read_kv(0, seq=b)
+        R_, S_, H_ = 10 + b % 7, 8 + b % 5, 30 + 2 * b
+        assert k.shape[0] == R_ + S_ + H_ // 2, (b, k.shape)
+    again = eng.t2s_generate(inps, sp)
+    assert [a.tolist() for a in again] == [f.tolist() for f in full]
+
+
+def test_batched_timeout_reruns_as_graphs(eng):
+    """A hand-off that waits past its bound (forced with a 0.5 us bound) makes the batched
+    launch leave without writing the sequence state (error 1); the steps re-run on the
+    per-step graphs and every sequence's tokens equal the graph path's."""
+    from genie_tts_amd.engine import make_sampler
+    inps = [t2s_inputs(R=10 + i, S=8 + i, H=30 + 3 * i, tag=f"pmto{i}") for i in range(9)]
+    sp = make_sampler(force_steps=16)
+    eng.set_option("persist", 0)
+    try:
+        want = [x.tolist() for x in eng.t2s_generate(inps, sp)]
+    finally:
+        eng.set_option("persist", 1)
+    before = eng.counter("persist_timeouts")
+    eng.set_option("persist_spin_ticks", 50)
+    try:
+        got = [x.tolist() for x in eng.t2s_generate(inps, sp)]
+    finally:
+        eng.set_option("persist_spin_ticks", 0)
+        eng.set_option("persist", 1)   # ends a back-off hold the timeout may have started
+    assert eng.counter("persist_timeouts") == before + 1
+    assert got == want
