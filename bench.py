@@ -370,6 +370,8 @@ def main():
                          "0 = one batch at a time")
     ap.add_argument("--batch-vocoder-cus", type=int, default=0,
                     help="batched workloads: CUs of the vocoder lanes (the T2S gets the rest; 0 = shared)")
+    ap.add_argument("--lanes-all-cus", action="store_true",
+                    help="with --batch-vocoder-cus: the vocoder lanes on every CU (the T2S stream keeps the split)")
     ap.add_argument("--lane-priority", type=int, default=None,
                     help="batched workloads: HIP stream priority of the vocoder lanes (lower = first)")
     ap.add_argument("--t2s-priority", type=int, default=None,
@@ -430,6 +432,8 @@ def main():
         run.eng.set_option("vits_lanes", args.vits_lanes)
     if args.batch_vocoder_cus and args.workload != "single":
         run.eng.set_vocoder_cus(args.batch_vocoder_cus)
+    if args.lanes_all_cus:
+        run.eng.set_option("lanes_all_cus", 1)
     if args.lane_priority is not None:
         run.eng.set_option("lane_priority", args.lane_priority)
     if args.t2s_priority is not None:

@@ -2008,6 +2008,11 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "vits_lanes") {   // concurrent vocoder streams of gsv_vits_decode_batch
         if (value < 1 || value > 16) return set_error(GSV_E_ARG, "vits_lanes: 1..16");
         eng->vits_lanes = value;
+    } else if (n == "lanes_all_cus") {
+        if (int r = eng->vits_batch_finish(nullptr)) return r;
+        eng->sync_own_streams();
+        eng->lanes_all_cus = value != 0;
+        if (int r = eng->remake_lane_streams()) return r;
     } else if (n == "lane_priority" || n == "t2s_priority") {
         // HIP stream priorities (lower = served first): the overlapped batch vocoder's lanes
         // beside the T2S of the next batch on the engine stream

@@ -416,6 +416,7 @@ struct gsv_engine {
     int vits_batch_finish(hipStream_t s);
     bool vits_threads = true;          // option "vits_threads": one host thread per vocoder lane
     int lane_priority = 0;             // option "lane_priority": HIP stream priority of the lanes
+    bool lanes_all_cus = false;        // option "lanes_all_cus": batch lanes unmasked under vocoder_cus
     int t2s_priority = 0;              // option "t2s_priority": of the engine stream (vocoder_cus 0)
     hipError_t make_lane_stream(hipStream_t* st);   // on the vocoder CUs under option vocoder_cus
     int remake_lane_streams();

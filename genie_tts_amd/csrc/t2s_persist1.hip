@@ -118,7 +118,9 @@ __device__ __forceinline__ u32x4 ld_g16(const W& ws, int off) {   // buffer_load
 
 // One lane waits for N 16-byte granules off + k * stride (k < N), all N loads in
 // flight; re-polls only the stale ones (persist.h wait_gran_n with 16-byte granules).
-template <int N, class W>
+// The error word and the wait bound are checked every CHK + 1 polls (the batched kernel
+// checks every 4th: its group-wide gathers resolve within a few dozen polls).
+template <int N, class W, unsigned CHK = 63>
 __device__ __forceinline__ void wait_g16_n(const W& ws, int off, int stride, unsigned tag, u32x4 (&g)[N], int* err,
                                            bool& ok, unsigned long long ticks) {
 #pragma unroll
@@ -135,7 +137,7 @@ __device__ __forceinline__ void wait_g16_n(const W& ws, int off, int stride, uns
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (g[k].x != tag) g[k] = ld_g16(ws, off + k * stride);
-        if ((it & 63) == 63) {
+        if ((it & CHK) == CHK) {
             if (ld_rlx(err) != 0) { ok = false; break; }
             if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                 atomicCAS(err, 0, 1);

@@ -132,7 +132,7 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
         float f[3];
         {
             u32x4 g[9];
-            wait_g16_n<9>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
+            wait_g16_n<9, WsSeq, 3>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 f[k] = __uint_as_float(g[0][1 + k]);
@@ -142,7 +142,7 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
         }
         if (!ok) break;
         u32x4 g[8];
-        wait_g16_n<8>(ws, off + 9 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+        wait_g16_n<8, WsSeq, 3>(ws, off + 9 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
         if (!ok) break;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {

@@ -545,9 +545,11 @@ int gsv_engine::remake_lane_streams() {
 }
 
 // A vocoder lane's stream: on the vocoder CUs when option vocoder_cus splits the chip
-// (bits [0, vocoder_cus), as the overlapped single vocoder), else on every CU.
+// (bits [0, vocoder_cus), as the overlapped single vocoder), else on every CU.  Option
+// lanes_all_cus keeps the lanes on every CU under the split: the T2S stream leaves the
+// vocoder CUs free during the persistent decode, the lanes use the whole chip otherwise.
 hipError_t gsv_engine::make_lane_stream(hipStream_t* st) {
-    if (vocoder_cus == 0) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, lane_priority);
+    if (vocoder_cus == 0 || lanes_all_cus) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, lane_priority);
     const int words = (n_cu + 31) / 32;
     std::vector<uint32_t> mv(words, 0u);
     for (int i = 0; i < vocoder_cus; ++i) mv[i / 32] |= 1u << (i % 32);
