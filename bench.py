@@ -370,6 +370,9 @@ def main():
                          "0 = one batch at a time")
     ap.add_argument("--batch-vocoder-cus", type=int, default=0,
                     help="batched workloads: CUs of the vocoder lanes (the T2S gets the rest; 0 = shared)")
+    ap.add_argument("--vocoder-first", action="store_true",
+                    help="batched workloads: each decode waits for the previous batch's vocoder (no vocoder kernel "
+                         "pending behind the persistent decode)")
     ap.add_argument("--lanes-all-cus", action="store_true",
                     help="with --batch-vocoder-cus: the vocoder lanes on every CU (the T2S stream keeps the split)")
     ap.add_argument("--lane-priority", type=int, default=None,
@@ -432,6 +435,8 @@ def main():
         run.eng.set_option("vits_lanes", args.vits_lanes)
     if args.batch_vocoder_cus and args.workload != "single":
         run.eng.set_vocoder_cus(args.batch_vocoder_cus)
+    if args.vocoder_first:
+        run.eng.set_option("vocoder_first", 1)
     if args.lanes_all_cus:
         run.eng.set_option("lanes_all_cus", 1)
     if args.lane_priority is not None:

@@ -1719,6 +1719,9 @@ extern "C" int gsv_t2s_generate(gsv_engine* eng, int batch, const gsv_utt* utts,
     if (int e = eng->ensure_res_pin(batch)) return e;
     eng->res_batch = batch;
     eng->res_ready = false;
+    // option vocoder_first: the decode waits for the overlapped vocoder batch, so none of that
+    // batch's kernels is left pending while the persistent decode holds every CU
+    if (eng->vocoder_first && eng->vb_active) eng->vits_batch_order(st);
     const int rc = eng->decode_loop(batch, &sp, st);
     eng->res_batch = 0;
     eng->perr_zeroed = false;
@@ -2008,6 +2011,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "vits_lanes") {   // concurrent vocoder streams of gsv_vits_decode_batch
         if (value < 1 || value > 16) return set_error(GSV_E_ARG, "vits_lanes: 1..16");
         eng->vits_lanes = value;
+    } else if (n == "vocoder_first") {
+        eng->vocoder_first = value != 0;
     } else if (n == "lanes_all_cus") {
         if (int r = eng->vits_batch_finish(nullptr)) return r;
         eng->sync_own_streams();

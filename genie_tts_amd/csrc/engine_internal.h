@@ -414,6 +414,8 @@ struct gsv_engine {
     bool vb_active = false;
     int vits_batch_launch(float noise_scale, hipStream_t s, bool join);
     int vits_batch_finish(hipStream_t s);
+    bool vocoder_first = false;        // option "vocoder_first": a batched decode waits for the running vocoder batch
+    void vits_batch_order(hipStream_t s);   // stream s after the running batch (issuing threads joined)
     bool vits_threads = true;          // option "vits_threads": one host thread per vocoder lane
     int lane_priority = 0;             // option "lane_priority": HIP stream priority of the lanes
     bool lanes_all_cus = false;        // option "lanes_all_cus": batch lanes unmasked under vocoder_cus

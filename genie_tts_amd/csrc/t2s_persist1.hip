@@ -675,6 +675,8 @@ __device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const W& ws, in
     }
     const int off = ws.PFH(s, l - 1, 0) + 16 * q;
     u32x4 g[9];
+    // knob1 = 1 (A/B): every wave's own loads retired before it polls
+    if (a.knob[1] == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid < GQ) {
         u32x4 h[8];
         wait_g16_n<8>(ws, off, RB, tag, h, a.err, ok, a.spin_ticks);
@@ -1086,6 +1088,7 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 sh.ff.bo[tid] = bo;
                 sh.ff.n1w[tid] = n1w;
                 u32x4 g[8];
+                if (a.knob[1] == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (A/B, as gather_pfh)
                 if (tid < GQ) {
                     wait_g16_n<8>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
                     float f0 = __uint_as_float(g[0].y), f1 = __uint_as_float(g[0].z), f2 = __uint_as_float(g[0].w);

@@ -1313,6 +1313,16 @@ int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     return 0;
 }
 
+// Order stream s after the running batch's lanes and generator without finishing it: the
+// issuing threads are joined (their events recorded), the results stay for vits_batch_finish.
+void gsv_engine::vits_batch_order(hipStream_t s) {
+    if (!vb_active) return;
+    for (auto& t : vb_threads) t.join();
+    vb_threads.clear();
+    for (int l = 0; l < vb_k; ++l) hipStreamWaitEvent(s, vlanes[l].join, 0);
+    if (vb_seg) hipStreamWaitEvent(s, sgb.done, 0);
+}
+
 // Join the batch: lanes -> stream s (NULL: the engine stream), f32 re-runs of the
 // utterances that met the fp16 range, phase time.
 int gsv_engine::vits_batch_finish(hipStream_t s) {

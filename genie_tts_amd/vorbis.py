@@ -436,8 +436,10 @@ class Floor0:
             else:
                 p = (1 - cw) / 2 * np.prod([4 * (cosc[2 * j + 1] - cw) ** 2 for j in range((o - 2) // 2 + 1)])
                 q = (1 + cw) / 2 * np.prod([4 * (cosc[2 * j] - cw) ** 2 for j in range((o - 2) // 2 + 1)])
-            val = math.exp(0.11512925 * (amp * self.amp_off / (((1 << self.amp_bits) - 1) * math.sqrt(p + q))
-                                         - self.amp_off))
+            pq = math.sqrt(p + q)
+            ex = 0.11512925 * (amp * self.amp_off / (((1 << self.amp_bits) - 1) * pq) - self.amp_off) if pq > 0 \
+                else math.inf
+            val = math.exp(ex) if ex < 709.0 else math.inf   # beyond the double range: inf, as a float curve
             while i < n2:                                # every i with the same map value
                 out[i] = val
                 i += 1

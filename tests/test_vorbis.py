@@ -32,6 +32,8 @@ def _books(seed=0):
         W.Book([2, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5, 5, 6, 6], dims=4, lookup=2,
                minimum=-8.0, delta=0.5, mults=r.integers(0, 16, 64).tolist(), value_bits=4,
                seq=1, ordered=True),                                  # 5: lookup 2, sequence
+        W.complete_book(16, dims=2, lookup=1, minimum=0.375, delta=0.046875,
+                        mults=[0, 1, 2, 3], value_bits=2, seq=1),     # 6: floor-0 LSP steps
     ]
 
 
@@ -126,7 +128,14 @@ def _packet(books, floors, residues, rtype, mode, prev_long, next_long, used, r)
         w.put(int(prev_long), 1)
         w.put(int(next_long), 1)
     fl = floors[mode]
-    finals = [_finals(fl, r) if used[c] else None for c in range(2)]
+    if isinstance(fl, W.Floor0Spec):
+        # amplitude and LSP entries; the coefficients ascend through (0, pi) like real line
+        # spectral pairs (book 6 steps 0.375..0.52, each vector offset by the previous one's last)
+        nvq = -(-fl.order // books[fl.books[0]].dims)
+        finals = [(int(r.integers(1, 1 << fl.amp_bits)), 0, [int(r.integers(0, 16)) for _ in range(nvq)])
+                  if used[c] else None for c in range(2)]
+    else:
+        finals = [_finals(fl, r) if used[c] else None for c in range(2)]
     for c in range(2):
         fl.write_packet(w, finals[c], books)
     nonzero = any(used)                                 # channels 0 and 1 are coupled
@@ -167,13 +176,20 @@ def _packet(books, floors, residues, rtype, mode, prev_long, next_long, used, r)
     y = np.zeros((n, 2))
     for c, spec in enumerate((m, a)):
         if finals[c] is not None:
-            y[:, c] = _imdct_direct(fl.curve(finals[c], n2).astype(np.float64) * spec) * win
+            curve = fl.curve(finals[c], books, n2) if isinstance(fl, W.Floor0Spec) else fl.curve(finals[c], n2)
+            y[:, c] = _imdct_direct(curve.astype(np.float64) * spec) * win
     return w.bytes(), y
 
 
-def _build(rtype, modes, used=None, seed=0, total_trim=0):
+def _floors0():
+    """Floor type 0 for both block sizes: LSP orders 6 (even) and 5 (odd), different bark maps."""
+    return [W.Floor0Spec(order=6, rate=32000, bark_size=64, amp_bits=6, amp_off=3, books=[6]),
+            W.Floor0Spec(order=5, rate=32000, bark_size=256, amp_bits=8, amp_off=3, books=[6, 6])]
+
+
+def _build(rtype, modes, used=None, seed=0, total_trim=0, floors=None):
     r = np.random.default_rng(seed)
-    books, floors, residues = _books(seed), _floors(), _residues(rtype)
+    books, floors, residues = _books(seed), floors or _floors(), _residues(rtype)
     mappings = [([(0, 1)], 0, 0), ([(0, 1)], 1, 1)]
     headers = [W.ident_packet(2, 32000, BS0, BS1), W.comment_packet(),
                W.setup_packet(books, floors, residues, mappings, [(0, 0), (1, 1)], 2)]
@@ -213,6 +229,46 @@ def test_round_trip_residue_types_long_short(rtype):
     scale = np.abs(expect).max()
     assert scale > 1.0
     np.testing.assert_allclose(pcm, expect, rtol=0, atol=2e-6 * scale)
+
+
+@pytest.mark.parametrize("rtype", [1, 2])
+def test_round_trip_floor0(rtype):
+    """Floor type 0 (LSP curve over the bark map, Vorbis I section 6) for both block sizes,
+    even and odd order, with one silent channel per packet in places: the decoder's curve,
+    times the residue, through the IMDCT and overlap-add, equals the closed form."""
+    used = [(True, True), (True, False), (True, True), (False, True), (True, True), (True, True)]
+    data, expect = _build(rtype, [1, 0, 0, 1, 1, 0], used=used, seed=20 + rtype, floors=_floors0())
+    pcm, rate = vorbis.decode(data)
+    assert rate == 32000 and pcm.shape == expect.shape
+    assert np.isfinite(expect).all()
+    scale = np.abs(expect).max()
+    assert scale > 0.1
+    np.testing.assert_allclose(pcm, expect, rtol=0, atol=2e-6 * scale)
+
+
+def test_floor0_curve_matches_the_spec_formula():
+    """The decoder's floor-0 curve alone (its run-length loop over equal map values) against
+    the vectorised spec formula, for both orders and several amplitudes."""
+    books = _books(0)
+    r = np.random.default_rng(7)
+    for spec in _floors0():
+        bits = W.BitWriter()
+        spec.write_header(bits)
+        dec_fl = vorbis.Floor0(_bits_after_type(bits))
+        for _ in range(4):
+            nvq = -(-spec.order // 2)
+            dec = (int(r.integers(1, 1 << spec.amp_bits)), 0, [int(r.integers(0, 16)) for _ in range(nvq)])
+            coef = spec.coefficients(dec, books).tolist()
+            for n2 in (128, 1024):
+                got = dec_fl.curve((dec[0], coef), n2)
+                np.testing.assert_allclose(got, spec.curve(dec, books, n2), rtol=2e-6)
+
+
+def _bits_after_type(bits: "W.BitWriter"):
+    """A reader positioned after the 16-bit floor type of a written floor header."""
+    r = vorbis._Bits(bits.bytes())
+    assert r.read(16) == 0
+    return r
 
 
 def test_unused_floors_and_granule_trim():

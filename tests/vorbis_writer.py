@@ -259,6 +259,66 @@ class Floor1Spec:
         return np.array([10.0 ** ((i - 255) * 7.0 / 256.0) for i in range(256)], np.float32)[v]
 
 
+# ---------------------------------------------------------------- floor 0
+class Floor0Spec:
+    """Floor type 0 (LSP): header fields and packets; the expected curve is the spec's
+    map/LSP formula evaluated here with numpy over the whole bark map (section 6.2.3)."""
+
+    def __init__(self, order, rate, bark_size, amp_bits, amp_off, books):
+        self.order, self.rate, self.bark_size = order, rate, bark_size
+        self.amp_bits, self.amp_off, self.books = amp_bits, amp_off, books
+
+    def write_header(self, w: BitWriter):
+        w.put(0, 16)
+        w.put(self.order, 8); w.put(self.rate, 16); w.put(self.bark_size, 16)
+        w.put(self.amp_bits, 6); w.put(self.amp_off, 8)
+        w.put(len(self.books) - 1, 4)
+        for b in self.books:
+            w.put(b, 8)
+
+    def write_packet(self, w: BitWriter, dec, books: List[Book]):
+        """dec = (amplitude, book index into self.books, VQ entries) or None (unused)."""
+        if dec is None:
+            w.put(0, self.amp_bits)
+            return
+        amp, bi, entries = dec
+        w.put(amp, self.amp_bits)
+        w.put(bi, ilog(len(self.books)))
+        for e in entries:
+            books[self.books[bi]].write(w, e)
+
+    def coefficients(self, dec, books: List[Book]) -> np.ndarray:
+        """Concatenated VQ vectors, each offset by the last scalar of the one before."""
+        _, bi, entries = dec
+        out, last = [], 0.0
+        for e in entries:
+            v = books[self.books[bi]].vector(e) + last
+            out.extend(v.tolist())
+            last = out[-1]
+        return np.array(out[:self.order])
+
+    def curve(self, dec, books: List[Book], n2: int) -> np.ndarray:
+        amp = dec[0]
+        c = np.cos(self.coefficients(dec, books))
+
+        def bark(x):
+            return 13.1 * np.arctan(0.00074 * x) + 2.24 * np.arctan(0.0000000185 * x * x) + 0.0001 * x
+        i = np.arange(n2, dtype=np.float64)
+        mp = np.minimum(self.bark_size - 1,
+                        np.floor(bark(self.rate * i / (2.0 * n2)) * self.bark_size / bark(0.5 * self.rate)))
+        cw = np.cos(np.pi * mp / self.bark_size)
+        odd, even = c[1::2], c[0::2]
+        po = np.prod(4.0 * (odd[None, :] - cw[:, None]) ** 2, axis=1)
+        pe = np.prod(4.0 * (even[None, :] - cw[:, None]) ** 2, axis=1)
+        if self.order % 2:
+            p, q = (1.0 - cw * cw) * po, 0.25 * pe
+        else:
+            p, q = (1.0 - cw) / 2.0 * po, (1.0 + cw) / 2.0 * pe
+        lin = np.exp(0.11512925 * (amp * self.amp_off / (((1 << self.amp_bits) - 1) * np.sqrt(p + q))
+                                   - self.amp_off))
+        return lin.astype(np.float32)
+
+
 # ---------------------------------------------------------------- residue
 class ResidueSpec:
     def __init__(self, rtype, begin, end, psize, nclass, classbook, books):
@@ -374,7 +434,7 @@ def comment_packet() -> bytes:
     return w.bytes()
 
 
-def setup_packet(books: List[Book], floors: List[Floor1Spec], residues: List[ResidueSpec], mappings, modes,
+def setup_packet(books: List[Book], floors: List, residues: List[ResidueSpec], mappings, modes,
                  channels: int) -> bytes:
     w = BitWriter()
     w.put(5, 8)
