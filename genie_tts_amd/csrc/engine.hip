@@ -2011,6 +2011,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "vits_lanes") {   // concurrent vocoder streams of gsv_vits_decode_batch
         if (value < 1 || value > 16) return set_error(GSV_E_ARG, "vits_lanes: 1..16");
         eng->vits_lanes = value;
+    } else if (n == "convh_persist") {
+        eng->convh_persist = value != 0;
     } else if (n == "vocoder_first") {
         eng->vocoder_first = value != 0;
     } else if (n == "lanes_all_cus") {

@@ -188,6 +188,8 @@ struct gsv_engine {
     bool convt_f16 = true;             // option "convt_f16": the upsample ConvTransposes on the split-fp16 path too
     int convh_tile = 0;                // option "convh_tile": 0 = cost model, 1..4 = force a k_conv_h tile (tests)
     bool mrf_fused = true;             // option "mrf_fused": the C <= 32 stages' conv pairs as one kernel
+    bool convh_persist = false;        // option "convh_persist": large split-fp16 convs as a persistent tile loop
+    int stream_cus(hipStream_t st) const;
     int* vovf = nullptr;               // f16-split conv overflow flag (device)
     int* vovf_host = nullptr;          // pinned copy
     int vits_f32_reruns = 0;           // utterances re-run on the f32 path after an overflow

@@ -67,6 +67,9 @@ struct ConvArgs {
     // f16-split path: 0 = the cost model's tile; 1..4 = tile candidate 0..3 of launch_h (option
     // "convh_tile", tests)
     int tile_force;
+    // f16-split path: > 0 = the CUs of the stream; large grids then run the persistent tile
+    // loop (two blocks per CU) instead of one block per tile (option "convh_persist")
+    int persist;
 };
 void conv1d(const ConvArgs& a, hipStream_t s);
 // seg[t] for t < n: i with off[i] * f <= t < (off[i] + len[i]) * f, else -1 (off ascending)

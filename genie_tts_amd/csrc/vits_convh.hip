@@ -64,10 +64,20 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4& hi, uint4& lo
 // blocks over the same 64 time columns, so a K-step's four B fragment reads (two time
 // blocks x hi / lo) feed 4 WTM MFMAs instead of 4.  Every accumulator runs the WTM = 1
 // MFMA sequence (bit-identical results at the same KS).
-template <int KT, int CC, int WM, int WN, int KS, int WTM = 1>
+//
+// PERS (the persistent form, KS = 1): a 1-D grid of two blocks per CU walks the output tiles
+// (tile = blockIdx.x, + gridDim.x, ...; time fastest, then output-channel block, then phase).
+// The (tile, chunk) pairs of a block form one pipeline: the next pair's loads -- the next
+// tile's first chunk after a tile's last -- are in flight during the current chunk's MFMAs
+// and staged before the tile's epilogue, so no tile pays the prologue load -> stage ->
+// barrier of a fresh block (the C >= 64 MRF convs have 2-8 chunks per tile, r05q: the
+// per-call cost grew with a third of the tap count).  Each tile's MFMA sequence is the
+// one-block kernel's: bit-identical results.
+template <int KT, int CC, int WM, int WN, int KS, int WTM = 1, bool PERS = false>
 __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     using C = HCfg<KT, CC, WM, WN, KS, WTM>;
     static_assert(WTM == 1 || KS == 1, "the multi-block wave form has no K split");
+    static_assert(!PERS || KS == 1, "the persistent form has no K split (its LDS holds the next stage)");
     __shared__ __attribute__((aligned(16))) char smem[C::LDS];
     _Float16* Xh = reinterpret_cast<_Float16*>(smem);
     _Float16* Xl = reinterpret_cast<_Float16*>(smem + C::X_BYTES);
@@ -75,12 +85,22 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ks = w % KS, wn = (w / KS) % WN, wm = w / (KS * WN);
-    const int t0 = blockIdx.x * C::BN, co0 = blockIdx.y * C::BM;
     const int dil = a.dil;
     const int xw = C::BN + (KT - 1) * dil;
     const int nch = a.Cin / CC;
-    const int ph = a.phases > 1 ? (int)blockIdx.z : 0;   // ConvTranspose polyphase: phase of this block
-    const _Float16* __restrict__ Wg = reinterpret_cast<const _Float16*>(a.wh) + (long)ph * a.wh_phase_stride;
+    // tile coordinates: (t0, co0, ph) of tile tl
+    const int ntn = (a.n_t + C::BN - 1) / C::BN, ntm = (a.Cout + C::BM - 1) / C::BM;
+    const long ntiles = PERS ? (long)ntn * ntm * (a.phases > 1 ? a.phases : 1) : 1;
+    auto coords = [&](long tl, int& t0, int& co0, int& ph) {
+        if (!PERS) {
+            t0 = blockIdx.x * C::BN; co0 = blockIdx.y * C::BM; ph = a.phases > 1 ? (int)blockIdx.z : 0;
+            return;
+        }
+        const long r = tl / ntn;
+        t0 = (int)(tl - r * ntn) * C::BN;
+        co0 = (int)(r % ntm) * C::BM;
+        ph = (int)(r / ntm);
+    };
     const float* __restrict__ isc = a.in_scale;
     const float* __restrict__ X = a.x;
 
@@ -97,7 +117,47 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     uint4 wr[C::NWI];
     bool ovf = false;
 
-    auto load = [&](int ci0) {
+    // PERS: buffer loads, one 32-bit VGPR offset per staging item (the tile part) and the
+    // channel / tap offsets in SGPRs, so the current and the next tile's address sets cost a
+    // few registers instead of a 64-bit pointer per load; an item outside the input (padding,
+    // another output-channel block's rows) gets an offset past the buffer and reads 0
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(X), 0, (int)(((long)(a.Cin - 1) * a.x_cs + a.Tin) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__half*>(a.wh), 0,
+        (int)((a.phases > 1 ? (long)a.phases * a.wh_phase_stride : (long)a.Cout * KT * a.Cin) * 2), 0x00020000);
+    constexpr unsigned OOB = 0x80000000u;
+    auto load_b = [&](int t0, int co0, int ph, int ci0) {
+        const int xcs4 = (int)(a.x_cs * 4);
+#pragma unroll
+        for (int i = 0; i < C::NXI; ++i) {
+            const int tin = t0 - a.pad + xu[i];
+            const bool ok = xc[i] >= 0 && tin >= 0 && tin < a.Tin;
+            const unsigned vo = ok ? (unsigned)((xc[i] * 8) * xcs4 + tin * 4) : OOB;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                xr[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, vo, (ci0 + j) * xcs4, 0));
+        }
+        const int wso = (int)(((long)ph * a.wh_phase_stride + ci0) * 2);
+#pragma unroll
+        for (int i = 0; i < C::NWI; ++i) {
+            const int e = tid + i * 256;
+            unsigned vo = OOB;
+            if (e < C::BM * C::NG) {
+                const int r = e / C::NG, g = e - r * C::NG;
+                const int tap = g / C::G8, c8 = g - tap * C::G8;
+                const int co = co0 + r;
+                if (co < a.Cout) vo = (unsigned)((((co * KT + tap) * a.Cin) + c8 * 8) * 2);
+            }
+            wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, vo, wso, 0));
+        }
+    };
+    auto load = [&](int t0, int co0, int ph, int ci0) {
+        if constexpr (PERS) {
+            load_b(t0, co0, ph, ci0);
+            return;
+        }
+        const _Float16* __restrict__ Wg = reinterpret_cast<const _Float16*>(a.wh) + (long)ph * a.wh_phase_stride;
 #pragma unroll
         for (int i = 0; i < C::NXI; ++i) {
             const int tin = t0 - a.pad + xu[i];
@@ -156,92 +216,123 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     };
 
     f32x16 acc[WTM][2];
+    auto zero_acc = [&]() {
 #pragma unroll
-    for (int m = 0; m < WTM; ++m)
+        for (int m = 0; m < WTM; ++m)
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
+            for (int f = 0; f < 2; ++f)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[m][f][i] = 0.f;
+                for (int i = 0; i < 16; ++i) acc[m][f][i] = 0.f;
+    };
+    zero_acc();
 
     const int r32 = lane & 31, hsel = lane >> 5;
     const _Float16* wrow = Ws + (wm * 32 * WTM + r32) * C::WR;
-    load(0);
+    long tile = PERS ? (long)blockIdx.x : 0;
+    if (tile >= ntiles) return;
+    int t0, co0, ph;
+    coords(tile, t0, co0, ph);
+    load(t0, co0, ph, 0);
     store(0);
     __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load((c + 1) * CC);
+    for (;;) {
+        // the tile after this one (PERS), or none
+        const long ntile = tile + (PERS ? (long)gridDim.x : 1);
+        const bool more = PERS && ntile < ntiles;
+        int nt0 = 0, nco0 = 0, nph = 0;
+        if (more) coords(ntile, nt0, nco0, nph);
+        for (int c = 0; c < nch; ++c) {
+            const bool last = c + 1 == nch;
+            if (!last) load(t0, co0, ph, (c + 1) * CC);
+            else if (more) load(nt0, nco0, nph, 0);
+            // PERS: the per-tap LDS row offsets (tap x dilation) are re-formed every chunk, not
+            // hoisted out of the tile loop: hoisted, they stayed live across the epilogue and spilled
+            int dl = dil;
+            if constexpr (PERS) asm volatile("" : "+s"(dl));
 #pragma unroll
-        for (int j = ks; j < C::NSTEP; j += KS) {
-            const int g = 2 * j + hsel;                 // this lane's 8-channel group
-            const bool gv = g < C::NG;
-            const int tap = gv ? g / C::G8 : 0, c8 = gv ? g - tap * C::G8 : 0;
-            h8 A[WTM];
+            for (int j = ks; j < C::NSTEP; j += KS) {
+                const int g = 2 * j + hsel;                 // this lane's 8-channel group
+                const bool gv = g < C::NG;
+                const int tap = gv ? g / C::G8 : 0, c8 = gv ? g - tap * C::G8 : 0;
+                h8 A[WTM];
 #pragma unroll
-            for (int m = 0; m < WTM; ++m) {
-                A[m] = *reinterpret_cast<const h8*>(wrow + m * 32 * C::WR + tap * CC + c8 * 8);
-                if (!gv) A[m] = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+                for (int m = 0; m < WTM; ++m) {
+                    A[m] = *reinterpret_cast<const h8*>(wrow + m * 32 * C::WR + tap * CC + c8 * 8);
+                    if (!gv) A[m] = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int f = 0; f < 2; ++f) {
+                    const int row = wn * 64 + f * 32 + r32 + tap * dl;
+                    const h8 Bl = *reinterpret_cast<const h8*>(Xl + row * C::XR + c8 * 8);
+                    const h8 Bh = *reinterpret_cast<const h8*>(Xh + row * C::XR + c8 * 8);
+#pragma unroll
+                    for (int m = 0; m < WTM; ++m) {
+                        acc[m][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m], Bl, acc[m][f], 0, 0, 0);
+                        acc[m][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m], Bh, acc[m][f], 0, 0, 0);
+                    }
+                }
+            }
+            __syncthreads();
+            if (!last) {
+                store((c + 1) * CC);
+                __syncthreads();
+            } else if (more) {
+                // the next tile's first chunk into the LDS this tile no longer reads (every wave
+                // passed the barrier above); its registers are free before the epilogue
+                store(0);
+            }
+        }
+        if (KS > 1) {
+            // waves ks > 0 park their partials; ks == 0 adds them in ks order
+            float* red = reinterpret_cast<float*>(smem);
+            const int tl = wm * WN + wn;
+            if (ks > 0) {
+                float* p = red + ((long)((ks - 1) * WM * WN + tl) * 2 * 16) * 64;
+#pragma unroll
+                for (int f = 0; f < 2; ++f)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) p[(f * 16 + i) * 64 + lane] = acc[0][f][i];
+            }
+            __syncthreads();
+            if (ks > 0) break;
+#pragma unroll
+            for (int s = 1; s < KS; ++s) {
+                const float* p = red + ((long)((s - 1) * WM * WN + tl) * 2 * 16) * 64;
+#pragma unroll
+                for (int f = 0; f < 2; ++f)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) acc[0][f][i] += p[(f * 16 + i) * 64 + lane];
+            }
+        }
+        // epilogue of this tile: registers and global stores only (the next tile's first chunk
+        // is already staged in LDS)
+#pragma unroll
+        for (int m = 0; m < WTM; ++m) {
+            const int cobase = co0 + (wm * WTM + m) * 32 + 4 * hsel;
+            float sc[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = cobase + (r & 3) + 8 * (r >> 2);
+                sc[r] = co < a.Cout ? a.wscale[co] : 0.f;
             }
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
-                const int row = wn * 64 + f * 32 + r32 + tap * dil;
-                const h8 Bl = *reinterpret_cast<const h8*>(Xl + row * C::XR + c8 * 8);
-                const h8 Bh = *reinterpret_cast<const h8*>(Xh + row * C::XR + c8 * 8);
+                const int t = t0 + wn * 64 + f * 32 + r32;
+                if (t >= a.n_t) continue;
+                float v[16];
 #pragma unroll
-                for (int m = 0; m < WTM; ++m) {
-                    acc[m][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m], Bl, acc[m][f], 0, 0, 0);
-                    acc[m][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m], Bh, acc[m][f], 0, 0, 0);
-                }
+                for (int r = 0; r < 16; ++r) v[r] = acc[m][f][r] * sc[r];
+                if constexpr (PERS) conv_epilogue16_lean(a, cobase, t, ph, v);
+                else conv_epilogue16(a, cobase, t, ph, v);
             }
         }
-        __syncthreads();
-        if (c + 1 < nch) {
-            store((c + 1) * CC);
-            __syncthreads();
-        }
+        if (!more) break;
+        tile = ntile;
+        t0 = nt0; co0 = nco0; ph = nph;
+        zero_acc();
+        __syncthreads();   // the staged chunk is visible to every wave
     }
     if (ovf) atomicOr(a.ovf, 1);
-
-    if (KS > 1) {
-        // waves ks > 0 park their partials; ks == 0 adds them in ks order
-        float* red = reinterpret_cast<float*>(smem);
-        const int tile = wm * WN + wn;
-        if (ks > 0) {
-            float* p = red + ((long)((ks - 1) * WM * WN + tile) * 2 * 16) * 64;
-#pragma unroll
-            for (int f = 0; f < 2; ++f)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) p[(f * 16 + i) * 64 + lane] = acc[0][f][i];
-        }
-        __syncthreads();
-        if (ks > 0) return;
-#pragma unroll
-        for (int s = 1; s < KS; ++s) {
-            const float* p = red + ((long)((s - 1) * WM * WN + tile) * 2 * 16) * 64;
-#pragma unroll
-            for (int f = 0; f < 2; ++f)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[0][f][i] += p[(f * 16 + i) * 64 + lane];
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < WTM; ++m) {
-        const int cobase = co0 + (wm * WTM + m) * 32 + 4 * hsel;
-        float sc[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int co = cobase + (r & 3) + 8 * (r >> 2);
-            sc[r] = co < a.Cout ? a.wscale[co] : 0.f;
-        }
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-            const int t = t0 + wn * 64 + f * 32 + r32;
-            if (t >= a.n_t) continue;
-            float v[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = acc[m][f][r] * sc[r];
-            conv_epilogue16(a, cobase, t, ph, v);
-        }
-    }
 }
 
 template <int KT, int CC>
@@ -266,6 +357,16 @@ bool launch_h(const ConvArgs& a, hipStream_t s) {
     const Cand c = cands[best];
     const dim3 grid((a.n_t + 64 * c.wn - 1) / (64 * c.wn), (a.Cout + 32 * c.wm - 1) / (32 * c.wm),
                     a.phases > 1 ? a.phases : 1);
+    // the persistent form: two blocks per CU over the tiles, when there are >= 4 rounds of them
+    const long nblk = (long)grid.x * grid.y * grid.z;
+    const bool lean = a.mode == CV_STORE || a.mode == CV_RESID || a.mode == CV_ACC_FIRST || a.mode == CV_ACC_ADD ||
+                      a.mode == CV_ACC_MEAN;
+    if (a.persist > 0 && c.ks == 1 && lean && nblk >= 4L * 2 * a.persist) {
+        const dim3 pg((unsigned)(2 * a.persist));
+        if (c.wm == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1, 1, true>), pg, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 4, 1, 1, true>), pg, dim3(256), 0, s, a);
+        return true;
+    }
     if (c.wm == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 2, 2, 1>), grid, dim3(256), 0, s, a);
     else if (c.ks == 2) hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 2, 2>), grid, dim3(256), 0, s, a);
     else if (c.ks == 4) hipLaunchKernelGGL((k_conv_h<KT, CC, 1, 1, 4>), grid, dim3(256), 0, s, a);

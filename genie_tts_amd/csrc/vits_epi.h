@@ -164,6 +164,61 @@ __device__ __forceinline__ void conv_epilogue16_(const ConvArgs& a, int cobase, 
     }
 }
 
+// The lean form for the persistent conv (vits_convh.hip, PERS), whose epilogue sits inside
+// its tile loop: modes STORE, RESID, ACC_FIRST / ADD / MEAN only (the MRF convs and the
+// ConvTranspose), the same arithmetic order as conv_epilogue16_.
+__device__ __forceinline__ bool conv_epilogue_lean_mode(int mode) {
+    return mode == CV_STORE || mode == CV_RESID || mode == CV_ACC_FIRST || mode == CV_ACC_ADD || mode == CV_ACC_MEAN;
+}
+__device__ __forceinline__ void conv_epilogue16_lean(const ConvArgs& a, int cobase, int t, int ph,
+                                                     const float (&val)[16]) {
+    const int tp = t * a.o_tstride + a.o_toff + ph;
+    if (tp < 0 || tp >= a.o_len) return;
+    const int mode = a.mode;
+    const int nrow = a.Cout - cobase;   // row r valid iff (r & 3) + 8 (r >> 2) < nrow
+    const bool to_acc = mode == CV_ACC_FIRST || mode == CV_ACC_ADD;
+    const long obase = (long)cobase * a.o_cs + (long)tp * a.o_ts;
+    float* dst = (to_acc ? a.acc : a.out) + obase;
+    if (a.seg && a.seg[tp] < 0) {   // a gap column of a segmented batch: zeros
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = (r & 3) + 8 * (r >> 2);
+            if (d < nrow) dst[(long)d * a.o_cs] = 0.f;
+        }
+        return;
+    }
+    float y[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int d = (r & 3) + 8 * (r >> 2);
+        y[r] = a.bias ? (d < nrow ? a.bias[cobase + d] : 0.f) + val[r] : val[r];
+    }
+    if (mode != CV_STORE) {
+        const float* R = a.res + (long)cobase * a.r_cs + (long)tp * a.r_ts;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = (r & 3) + 8 * (r >> 2);
+            y[r] = (d < nrow ? R[(long)d * a.r_cs] : 0.f) + y[r];
+        }
+    }
+    if (mode == CV_ACC_ADD || mode == CV_ACC_MEAN) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = (r & 3) + 8 * (r >> 2);
+            y[r] = (d < nrow ? a.acc[obase + (long)d * a.o_cs] : 0.f) + y[r];
+        }
+    }
+    if (mode == CV_ACC_MEAN) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[r] = y[r] / a.div;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int d = (r & 3) + 8 * (r >> 2);
+        if (d < nrow) dst[(long)d * a.o_cs] = y[r];
+    }
+}
+
 __device__ __forceinline__ void conv_epilogue16(const ConvArgs& a, int cobase, int t, int ph,
                                                 const float (&val)[16]) {
     const int tp = t * a.o_tstride + a.o_toff + ph;

@@ -392,3 +392,31 @@ def test_vits_batch_packed_front_matches_single(setup):
     it = items[1]   # no noise: the oracle directly
     ref = vm(it["text_seq"], it["pred_semantic"], **kw0).numpy().reshape(-1)
     assert float(np.sqrt(np.mean((packed[1] - ref) ** 2))) <= RMS_TOL
+
+
+@pytest.mark.parametrize("seg", [1, 0])
+def test_vits_batch_persistent_convs_bit_identical(setup, seg):
+    """Option convh_persist: the batch's large split-fp16 MRF convs and ConvTransposes run as a
+    persistent tile loop (two blocks per CU walking the output tiles, the next tile's first chunk
+    staged during the current tile's last; vits_convh.hip PERS).  Every tile runs the one-block
+    kernel's MFMA sequence, so the batch's audio is bit-identical with the option on and off --
+    on the segmented generator (seg 1: its stages 2-3 have > 2048 tiles) and on per-utterance
+    lanes (seg 0)."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    items = []
+    for i in range(14):
+        G, S = 70 + 5 * i, 30 + i
+        txt = synth.synth_phones(S, f"vp{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (11 + i) + 5 * i) % 1024).reshape(1, 1, G)
+        items.append(dict(text_seq=txt, pred_semantic=sem, noise_seed=3000 + i, **kw))
+    e.set_option("seg_vocoder", seg)
+    try:
+        want = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+        e.set_option("convh_persist", 1)
+        got = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+    finally:
+        e.set_option("convh_persist", 0)
+        e.set_option("seg_vocoder", 1)
+    for i, (g, w) in enumerate(zip(got, want)):
+        np.testing.assert_array_equal(g, w, err_msg=f"item {i}")
