@@ -62,6 +62,8 @@ struct SharedM {
     float qkv[96];                            // ... of the sequence in attention (the helpers' operand)
     _Float16 osh[PWV][32], osl[PWV][32];      // merge_waves1's per-wave head output
     float h1s[MG][32];                        // block r of the published x_l / h1 rows
+    float ovm[MG][PWV][32];                   // concurrent attention: wave w's partial o of sequence i
+    float wredm[MG][2][PWV];                  // ... and its m_w, l_w
     float cand[MG][5][4];                     // greedy candidates of this slice's 4 waves + EOS
     float wred[2][PWV];
     uint32_t seenq[MG][33];
@@ -421,6 +423,142 @@ __device__ void resolve_w(const PersistArgs& a, const WsSeq& ws, int s, int i, i
     }
 }
 
+// ---- concurrent attention (every live sequence of the group at once): wave w computes its
+// share -- keys t = 64 u + 8 w + lane / 8, wave_attn1's partition -- of EVERY live sequence's
+// head-r attention, K and V rows straight from memory into registers (row kv, the new one, from
+// the q/k/v results; rows past it read row kv and weigh 0), the next sequence's rows in flight
+// while this one is computed; then one barrier and one wave per sequence merges the 8 partials.
+// wave_part_m / merge_m are wave_attn_m / merge_waves1 operation for operation (operands from
+// registers instead of the LDS stage), so every value is the single-sequence kernel's.  The
+// serial loop paid a K stage, two barriers and a merge per sequence (~2.6 us each, four per
+// layer, profiles/r05t_persistm_trace64.json).  Rounds u >= ceil(T / 64) are masked to
+// exp(-inf) = 0 and add exact zeros, so one NU serves every live sequence.
+template <int NU>
+__device__ __forceinline__ void load_kv_m(float4 (&kr)[NU], float4 (&vr)[NU], const float* Kw, const float* Vw,
+                                          float4 knew, float4 vnew, int kv, int c8, int g) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int t = min(64 * u + g, kv);
+        kr[u] = t < kv ? ldg16f(Kw, (long)t * 32 + 4 * c8) : knew;
+        vr[u] = t < kv ? ldg16f(Vw, (long)t * 32 + 4 * c8) : vnew;
+    }
+}
+
+template <int NU>
+__device__ __forceinline__ void wave_part_m(SharedM& sh, int i, const float4 (&kr)[NU], const float4 (&vr)[NU],
+                                            float q0, float q1, float q2, float q3, float sc, int T, int c8, int g,
+                                            int w, int lane) {
+    const float p0 = q0 * sc, p1 = q1 * sc, p2 = q2 * sc, p3 = q3 * sc;
+    float sv[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const float4 k4 = kr[u];
+        float x = p0 * k4.x;
+        x += p1 * k4.y;
+        x += p2 * k4.z;
+        x += p3 * k4.w;
+        sv[u] = x;
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0xB1, 0xF>(sv[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0x4E, 0xF>(sv[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) sv[u] += dpp_f<0x141, 0xF>(sv[u]);
+    float wm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        sv[u] = 64 * u + g < T ? sv[u] : -INFINITY;
+        wm = fmaxf(wm, sv[u]);
+    }
+    const float m_w = wave_max_dpp(wm);
+    const float mref = m_w == -INFINITY ? 0.f : m_w;
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f, lsum = 0.f;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const float pu = __expf(sv[u] - mref);
+        const float4 v4 = vr[u];
+        o0 += pu * v4.x;
+        o1 += pu * v4.y;
+        o2 += pu * v4.z;
+        o3 += pu * v4.w;
+        lsum += pu;
+    }
+    o0 += dpp_f<0x128, 0xF>(o0);
+    o1 += dpp_f<0x128, 0xF>(o1);
+    o2 += dpp_f<0x128, 0xF>(o2);
+    o3 += dpp_f<0x128, 0xF>(o3);
+    o0 = swap_sum16(o0); o1 = swap_sum16(o1); o2 = swap_sum16(o2); o3 = swap_sum16(o3);
+    o0 = swap_sum32(o0); o1 = swap_sum32(o1); o2 = swap_sum32(o2); o3 = swap_sum32(o3);
+    const float l_w = wave_sum_dpp(c8 == 0 ? lsum : 0.f);
+    if (lane < 8) *reinterpret_cast<float4*>(&sh.ovm[i][w][4 * lane]) = make_float4(o0, o1, o2, o3);
+    if (lane == 0) {
+        sh.wredm[i][0][w] = m_w;
+        sh.wredm[i][1][w] = l_w;
+    }
+}
+
+// PF: the next sequence's rows in flight during this one's share (NU <= 4; at NU = 7 the two
+// register sets spilled, so longer rows are loaded one sequence at a time)
+template <int NU, bool PF = (NU <= 4)>
+__device__ void attn_conc_m(const PersistArgs& a, SharedM& sh, unsigned live, int g, int nsg, int r, int l, int s,
+                            int w, int lane) {
+    const int c8 = lane & 7, gk = (w << 3) | (lane >> 3);
+    const float sc = a.scale;
+    constexpr int NB = PF ? NU : 1;
+    float4 kA[NU], vA[NU], kB[NB], vB[NB];
+    auto ld = [&](int i, float4 (&kk)[NU], float4 (&vv)[NU]) {
+        const long off = (long)(g + i * nsg) * a.sstride + (long)r * a.tmax * 32;
+        load_kv_m<NU>(kk, vv, a.kc[l] + off, a.vc[l] + off, *reinterpret_cast<const float4*>(&sh.qkvs[i][32 + 4 * c8]),
+                      *reinterpret_cast<const float4*>(&sh.qkvs[i][64 + 4 * c8]), sh.kv0[i] + s, c8, gk);
+    };
+    unsigned m = live;
+    int i = __builtin_ctz(m);
+    ld(i, kA, vA);
+    for (;;) {
+        const unsigned nx = m & (m - 1);
+        if constexpr (PF)
+            if (nx) ld(__builtin_ctz(nx), kB, vB);   // in flight during this sequence's share
+        const float4 qc = *reinterpret_cast<const float4*>(&sh.qkvs[i][4 * c8]);
+        wave_part_m<NU>(sh, i, kA, vA, qc.x * sc, qc.y * sc, qc.z * sc, qc.w * sc, sc, sh.kv0[i] + s + 1, c8, gk, w,
+                        lane);
+        if (!nx) break;
+        m = nx;
+        i = __builtin_ctz(m);
+        if constexpr (PF) {
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                kA[u] = kB[u];
+                vA[u] = vB[u];
+            }
+        } else {
+            ld(i, kA, vA);
+        }
+    }
+}
+
+// merge_waves1's arithmetic for sequence i, by one wave, into the out-projection's A tile
+// (rows 2 i / 2 i + 1 = hi / lo of the head output)
+__device__ __forceinline__ void merge_m(SharedM& sh, int i, int lane) {
+    const int j = lane & 7;
+    const float mj = sh.wredm[i][0][j];
+    float M = mj;
+    M = fmaxf(M, dpp_f<0xB1, 0xF>(M));
+    M = fmaxf(M, dpp_f<0x4E, 0xF>(M));
+    M = fmaxf(M, dpp_f<0x141, 0xF>(M));
+    const float e = mj == -INFINITY ? 0.f : __expf(mj - M);
+    float L = e * sh.wredm[i][1][j];
+    L += dpp_f<0xB1, 0xF>(L);
+    L += dpp_f<0x4E, 0xF>(L);
+    L += dpp_f<0x141, 0xF>(L);
+    const int d = lane & 31;
+    float O = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < PWV; ++ww)
+        O += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), ww)) * sh.ovm[i][ww][d];
+    if (lane < 32) split_h(O / L, sh.O[2 * i][d], sh.O[2 * i + 1][d]);
+}
+
 __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, int g, int r) {
     const int nsg = a.groups, nb = a.B;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -483,7 +621,17 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             if (!live) break;
         }
         PMSTAMP(true, 13);
-        {
+        // this step's attention: every live sequence at once when all of them are on the
+        // single kernel's LDS path (T <= 512 keys, kv < KVL1), else one after another
+        // (knob2 = 1 forces the serial loop: A/B)
+        bool conc = a.knob[2] == 0;
+        int nu_max = 1;
+        for (unsigned m = live; m; m &= m - 1) {
+            const int kv = sh.kv0[__builtin_ctz(m)] + s;
+            conc = conc && kv + 1 <= 512 && kv < KVL1;
+            nu_max = max(nu_max, (kv + 1 + 63) >> 6);
+        }
+        if (!conc) {
             const int i0 = __builtin_ctz(live);
             const int key = (s * 24 + 0) * MG + i0;
             if ((cur ? skey1 : skey0) != key) {   // layer 0's first K stage (the step's first layer)
@@ -579,6 +727,22 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             }
             bar_nf();   // q/k/v of every sequence; the A tile / lnb are free (the general path's scores)
             PMSTAMP(l == 12, 2);
+            if (conc) {
+                if (nu_max <= 2) attn_conc_m<2>(a, sh, live, g, nsg, r, l, s, w, lane);
+                else if (nu_max <= 4) attn_conc_m<4>(a, sh, live, g, nsg, r, l, s, w, lane);
+                else if (nu_max <= 6) attn_conc_m<6>(a, sh, live, g, nsg, r, l, s, w, lane);
+                else attn_conc_m<7>(a, sh, live, g, nsg, r, l, s, w, lane);   // (kv < KVL1 = 448: T <= 448)
+                bar_nf();   // every wave's partials of every sequence in LDS
+                if (w < __builtin_popcount(live)) merge_m(sh, nth_bit(live, w), lane);
+                if (w == 7) {   // the new K/V rows (read by this workgroup only, next step)
+                    for (unsigned m = live; m; m &= m - 1) {
+                        const int i = __builtin_ctz(m), kv = sh.kv0[i] + s;
+                        const long kvoff = (long)(g + i * nsg) * a.sstride + (long)r * a.tmax * 32;
+                        float* dst = (lane < 32 ? a.kc[l] + kvoff : a.vc[l] + kvoff - 32) + (long)kv * 32 + lane;
+                        *dst = sh.qkvs[i][32 + lane];
+                    }
+                }
+            } else {
             // V rows of the next sequence in registers, loaded while this one's attention runs
             float4 vpre[8];
             auto v_of = [&](int ii) {   // (after the q/k/v barrier: qkvs holds every sequence's new row)
@@ -657,6 +821,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                     float* dst = (lane < 32 ? a.kc[l] + kvoff : a.vc[l] + kvoff - 32) + (long)kv * 32 + lane;
                     *dst = sh.qkvs[i][32 + lane];
                 }
+            }
             }
             bar_nf();   // O complete
             PMSTAMP(l == 12, 3);
@@ -824,7 +989,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                     const WsSeq ws = base.seq(g + i * nsg);
                     pub_m(ws, sh, i, ws.PFH(s, l, r), ws.PFH(s, l, 16) + 16 * 11 * r, tag, w, lane2);
                 }
-                if (l < 23) {   // the next layer's first K stage lands during the hop
+                if (l < 23 && !conc) {   // the next layer's first K stage lands during the hop
                     const int i0 = __builtin_ctz(live);
                     stage_k(a, kbuf(cur), l + 1, g + i0 * nsg, r, sh.kv0[i0] + s, w, lane2);
                     (cur ? skey1 : skey0) = (s * 24 + l + 1) * MG + i0;
