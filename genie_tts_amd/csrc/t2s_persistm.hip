@@ -33,6 +33,9 @@
 namespace gsv {
 namespace {
 
+#ifndef PERSISTM_LATE_W
+#define PERSISTM_LATE_W 0
+#endif
 constexpr int MG = 4;           // sequences per group
 constexpr int NSG_MAX = 16;     // groups (x 16 workgroups: the whole chip)
 constexpr int GWM = 16;         // workgroups per group
@@ -653,15 +656,21 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 xw = ldg(a.L[l - 1].n2w, 32 * r + lane);
                 xb = ldg(a.L[l - 1].n2b, 32 * r + lane);
             }
-            if (w < 6) {
-                const int row = (w >> 1) * 512 + r * 32 + 16 * (w & 1) + n16;
+            auto load_wq = [&]() {
+                if (w < 6) {
+                    const int row = (w >> 1) * 512 + r * 32 + 16 * (w & 1) + n16;
 #pragma unroll
-                for (int c = 0; c < 16; ++c) wq[c] = ldg16(P.w_in + (long)row * 512 + 32 * c + k8, 0);
-                qfB = ldg(a.fold, (long)l * FOLD_LAYER + row);
-                qfC = ldg(a.fold, (long)l * FOLD_LAYER + 1536 + row);
-            }
+                    for (int c = 0; c < 16; ++c) wq[c] = ldg16(P.w_in + (long)row * 512 + 32 * c + k8, 0);
+                    qfB = ldg(a.fold, (long)l * FOLD_LAYER + row);
+                    qfC = ldg(a.fold, (long)l * FOLD_LAYER + 1536 + row);
+                }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + r * 32 + k8, 0);
+                for (int t = 0; t < 4; ++t) wo[t] = ldg16(P.w_out + (long)(64 * w + 16 * t + n16) * 512 + r * 32 + k8, 0);
+            };
+            // PERSISTM_LATE_W (A/B build, tools/r06g_late_w.hip): the layer's weight loads after
+            // its gathers, so no gather polls behind ~128 KB of weight loads in its own wave's queue
+            constexpr bool late_w = PERSISTM_LATE_W != 0;
+            if constexpr (!late_w) load_wq();
             if (l == 0) {   // x_0 = E_audio[tok] + alpha pe[n]
                 bool ok = true;
                 const int nl = __builtin_popcount(live);
@@ -685,6 +694,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                               Q.b2, Q.n2w))
                     return;
             }
+            if constexpr (late_w) load_wq();
             PMSTAMP(l == 12, 1);
             {
                 float mean[MG], rden[MG];
@@ -857,7 +867,7 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
             // ================= FFN role: slice r =================
             uint4 w1r[16], w2r[16];   // W2's columns are loaded once FFN1 has consumed W1's rows
             float ffB, ffC, n1w_t, n1b_t;
-            {
+            auto load_w1 = [&]() {
                 const int tid2 = opaque_tid(), lane2 = tid2 & 63, m16 = lane2 & 15, q8 = 8 * (lane2 >> 4);
 #pragma unroll
                 for (int c = 0; c < 16; ++c) w1r[c] = ldg16(P.w1 + (long)(r * 128 + w * 16 + m16) * 512 + 32 * c + q8, 0);
@@ -865,10 +875,12 @@ __device__ void run_group(const PersistArgs& a, const WsSeq& base, SharedM& sh, 
                 n1b_t = ldg(P.n1b, tid2);
                 ffB = ldg(a.fold, (long)l * FOLD_LAYER + 3072 + r * 128 + w * 16 + m16);
                 ffC = ldg(a.fold, (long)l * FOLD_LAYER + 5120 + r * 128 + w * 16 + m16);
-            }
+            };
+            if constexpr (!late_w) load_w1();
             if (!gather_m(a, base, sh, live, tag, [&](int i) { return base.seq(g + i * nsg).PA(s, l, 0); }, P.b_out,
                           P.n1w, s == 1 && l == 0 && g == 0 && r == 0))
                 return;
+            if constexpr (late_w) load_w1();
             PMSTAMP(l == 12, 5);
             {
                 const int tid2 = opaque_tid(), lane2 = tid2 & 63;
