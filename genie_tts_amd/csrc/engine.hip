@@ -1197,7 +1197,7 @@ int gsv_engine::persist_enqueue(int B, const gsv_sampler* sp, hipStream_t st, in
     a.stop_req = stop_word;
     a.smax = std::max(1, std::min(limit, 4000));
     a.trace = ptrace;
-    a.pf_delay = persist1_pf_delay;
+    a.pf_delay = B == 1 ? persist1_pf_delay : 0;   // (the multi-sequence forms: measured only at 0)
     for (int i = 0; i < 4; ++i) a.knob[i] = persist1_knob[i];
     a.fold = ln_fold;
     a.spin_ticks = persist_spin_ticks;

@@ -26,6 +26,8 @@ if ATT:
     e.set_option("knob1", 1)
 if FFN:
     e.set_option("knob1", 2)
+if "--serial" in sys.argv:   # the serial per-sequence attention loop (knob2 = 1) instead of the concurrent one
+    e.set_option("knob2", 1)
 T = lambda a: torch.as_tensor(a, device="cuda")
 utt = (T(ref.ref_seq.reshape(-1)), T(it.text_seq.reshape(-1)), None, None, T(ref.ssl.reshape(768, -1)), it.force_steps)
 for _ in range(3):
