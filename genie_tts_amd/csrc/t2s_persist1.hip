@@ -549,7 +549,9 @@ __device__ void resolve_greedy(const PersistArgs& a, const Ws1& ws, int s, int n
     const int tid = threadIdx.x;
     bool ok = true;
     if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s - 1, 23, 0)), ws.tag(s - 1), a.err, ok, a.spin_ticks);
-    if (tid == 64) sh.stopreq = ld_stop(a.stop_req);   // wave 1: beside wave 0's (longer) wait
+    // wave 1: beside wave 0's (longer) wait; knob1 = 3 (A/B only): no read, is its PCIe round trip
+    // on the step's critical path?
+    if (tid == 64) sh.stopreq = a.knob[1] == 3 ? 0 : ld_stop(a.stop_req);
     if (!block_ok1(ok, sh)) return;
     if (tid < 64) {
         // lane q: candidate q's {penalised max, its index, raw max, its index} (16 rows of
