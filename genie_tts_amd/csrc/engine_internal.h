@@ -323,9 +323,9 @@ struct gsv_engine {
     int gen_drain();                   // wait for every started generate (their results stay queued)
     long persist1_f16_reruns = 0;      // persistent launches re-run as per-step graphs (fp16 range)
     int persist1_f16_limit = 0;
-    // GENIE_PF_DELAY / option pf_delay: s_sleep(32) x N between a B = 1 workgroup's publish and its
-    // next-layer refill; 4 measured 0.2 % faster than 0 (profiles/r06g_decode_pf_sweep.txt)
-    int persist1_pf_delay = 4;
+    // GENIE_PF_DELAY / option pf_delay: s_sleep(32) x N between a B = 1 workgroup's publish and its next-layer
+    // refill; 0: 4 was 0.2 % faster alone but equal in the pipelined stream (profiles/r06k_headline_ab.txt)
+    int persist1_pf_delay = 0;
     int persist1_knob[4] = {0, 0, 0, 0};   // options "knob0".."knob3": single-sequence kernel tuning variants
     int vits_decode(const int64_t* text_seq, int n_text, const int64_t* sem, int n_sem,
                     const float* ref_audio, int n_audio, const float* ge, const float* ge_adv,

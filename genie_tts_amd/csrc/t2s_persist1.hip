@@ -118,9 +118,7 @@ __device__ __forceinline__ u32x4 ld_g16(const W& ws, int off) {   // buffer_load
 
 // One lane waits for N 16-byte granules off + k * stride (k < N), all N loads in
 // flight; re-polls only the stale ones (persist.h wait_gran_n with 16-byte granules).
-// The error word and the wait bound are checked every CHK + 1 polls (the batched kernel
-// checks every 4th: its group-wide gathers resolve within a few dozen polls).
-template <int N, class W, unsigned CHK = 63>
+template <int N, class W>
 __device__ __forceinline__ void wait_g16_n(const W& ws, int off, int stride, unsigned tag, u32x4 (&g)[N], int* err,
                                            bool& ok, unsigned long long ticks) {
 #pragma unroll
@@ -137,7 +135,7 @@ __device__ __forceinline__ void wait_g16_n(const W& ws, int off, int stride, uns
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (g[k].x != tag) g[k] = ld_g16(ws, off + k * stride);
-        if ((it & CHK) == CHK) {
+        if ((it & 63) == 63) {
             if (ld_rlx(err) != 0) { ok = false; break; }
             if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                 atomicCAS(err, 0, 1);
@@ -549,9 +547,7 @@ __device__ void resolve_greedy(const PersistArgs& a, const Ws1& ws, int s, int n
     const int tid = threadIdx.x;
     bool ok = true;
     if (tid == 0) wait_tag16_slow(ws.at(ws.PFH(s - 1, 23, 0)), ws.tag(s - 1), a.err, ok, a.spin_ticks);
-    // wave 1: beside wave 0's (longer) wait; knob1 = 3 (A/B only): no read, is its PCIe round trip
-    // on the step's critical path?
-    if (tid == 64) sh.stopreq = a.knob[1] == 3 ? 0 : ld_stop(a.stop_req);
+    if (tid == 64) sh.stopreq = ld_stop(a.stop_req);   // wave 1: beside wave 0's (longer) wait
     if (!block_ok1(ok, sh)) return;
     if (tid < 64) {
         // lane q: candidate q's {penalised max, its index, raw max, its index} (16 rows of
@@ -677,8 +673,6 @@ __device__ __forceinline__ bool gather_pfh(const PersistArgs& a, const W& ws, in
     }
     const int off = ws.PFH(s, l - 1, 0) + 16 * q;
     u32x4 g[9];
-    // knob1 = 1 (A/B): every wave's own loads retired before it polls
-    if (a.knob[1] == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid < GQ) {
         u32x4 h[8];
         wait_g16_n<8>(ws, off, RB, tag, h, a.err, ok, a.spin_ticks);
@@ -1090,7 +1084,6 @@ __device__ void run_ffn(const PersistArgs& a, const Ws1& ws, Shared1& sh, int gr
                 sh.ff.bo[tid] = bo;
                 sh.ff.n1w[tid] = n1w;
                 u32x4 g[8];
-                if (a.knob[1] == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (A/B, as gather_pfh)
                 if (tid < GQ) {
                     wait_g16_n<8>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
                     float f0 = __uint_as_float(g[0].y), f1 = __uint_as_float(g[0].z), f2 = __uint_as_float(g[0].w);

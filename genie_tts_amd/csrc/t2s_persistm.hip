@@ -97,6 +97,37 @@ __device__ __forceinline__ void split_mul_h(float u, float m, _Float16& hi, _Flo
     lo = __builtin_bit_cast(_Float16, (unsigned short)(l & 0xffffu));
 }
 
+// wait_g16_n (t2s_persist1.hip) with the error word and the wait bound checked every 4th poll:
+// the group-wide gathers resolve within a few dozen polls, so a check every 64th (the
+// single-sequence kernel's) never fired and a forced timeout could not be tested
+template <int N>
+__device__ __forceinline__ void wait_g16_m(const WsSeq& ws, int off, int stride, unsigned tag, u32x4 (&g)[N],
+                                           int* err, bool& ok, unsigned long long ticks) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) g[k] = ld_g16(ws, off + k * stride);
+    unsigned long long t0 = 0;
+    for (unsigned it = 0;; ++it) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < N; ++k) all &= g[k].x == tag;
+        if (all) break;
+        if (it == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");   // the loads below are re-issued every round
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (g[k].x != tag) g[k] = ld_g16(ws, off + k * stride);
+        if ((it & 3) == 3) {
+            if (ld_rlx(err) != 0) { ok = false; break; }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                atomicCAS(err, 0, 1);
+                ok = false;
+                break;
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ bool ok_all(bool ok, SharedM& sh) {
     if (!ok) sh.fail = 1;
     bar_nf();
@@ -137,7 +168,7 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
         float f[3];
         {
             u32x4 g[9];
-            wait_g16_n<9, WsSeq, 3>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
+            wait_g16_m<9>(ws, off, RB, tag, g, a.err, ok, a.spin_ticks);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 f[k] = __uint_as_float(g[0][1 + k]);
@@ -147,7 +178,7 @@ __device__ __forceinline__ bool gather_m(const PersistArgs& a, const WsSeq& ws, 
         }
         if (!ok) break;
         u32x4 g[8];
-        wait_g16_n<8, WsSeq, 3>(ws, off + 9 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
+        wait_g16_m<8>(ws, off + 9 * RB, RB, tag, g, a.err, ok, a.spin_ticks);
         if (!ok) break;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {

@@ -368,11 +368,11 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
  * each conv pair of an MRF resblock step of the C <= 32 stages as one kernel, its
  * intermediate in LDS), "sv_f16", "packed", "attn_mf32" (1, default: the prefill's
  * attention on the f32 MFMA with k_attn_flash's exact fma chains; 0: k_attn_flash itself,
- * bit-identical results), "pf_delay" (4: a B = 1 decode workgroup waits 4 x s_sleep(32)
+ * bit-identical results), "pf_delay" (0: a B = 1 decode workgroup waits N x s_sleep(32)
  * between its publish and its next-layer refill), A/B options measured and left off:
  * "convh_persist" (the large split-fp16 convs as a persistent tile loop, bit-identical),
  * "vocoder_first" (a batched decode waits for the running vocoder batch), "lanes_all_cus"
- * (under vocoder_cus, the batch lanes on every CU), "knob0".."knob3" (decode variants),
+ * (under vocoder_cus, the batch lanes on every CU), "knob0".."knob3" (decode tuning variants),
  * test hooks ("persist_spin_ticks", "persist1_f16_limit", "sv_f16_limit", "convh_tile":
  * 1..4 forces that k_conv_h tile candidate, 0 the cost model).  "ptrace": 1 allocates per-workgroup phase stamps of the persistent
  * launch (step 8, layer 12), read back with gsv_debug_ptrace ([256 workgroups][16

@@ -18,7 +18,7 @@ base = None
 def run(knobs, reps=4):
     for i in range(4):
         e.set_option(f"knob{i}", knobs.get(i, 0))
-    e.set_option("pf_delay", knobs.get("pf", 4))   # (4: the engine default since r06)
+    e.set_option("pf_delay", knobs.get("pf", 0))
     ts, toks = [], None
     for _ in range(reps):
         out = e.t2s_generate([(ref, txt, None, None, ssl)], make_sampler(force_steps=81))
