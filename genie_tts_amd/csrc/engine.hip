@@ -302,6 +302,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_PERSIST1")) use_persist1 = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSIST1M")) use_persist1m = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PERSISTM")) use_persistm = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_PRESPLIT")) use_presplit = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
@@ -682,7 +683,14 @@ int gsv_engine::ensure_packed(int rows, int B) {
     pk_prompts = (int64_t*)A((size_t)nr * 8);
     pk_last = (int*)A((size_t)nb * 4);
     pk_xlast = (float*)A((size_t)nb * 512 * 4);
-    if (!pk_H || !pk_F || !pk_slab || !pk_rowinfo || !pk_prompts || !pk_last || !pk_xlast) {
+    pk_Hh = (__half*)A((size_t)nr * 512 * 2);
+    pk_Hl = (__half*)A((size_t)nr * 512 * 2);
+    pk_H1h = (__half*)A((size_t)nr * 512 * 2);
+    pk_H1l = (__half*)A((size_t)nr * 512 * 2);
+    pk_Fh = (__half*)A((size_t)nr * 2048 * 2);
+    pk_Fl = (__half*)A((size_t)nr * 2048 * 2);
+    if (!pk_H || !pk_F || !pk_slab || !pk_rowinfo || !pk_prompts || !pk_last || !pk_xlast || !pk_Hh || !pk_Hl ||
+        !pk_H1h || !pk_H1l || !pk_Fh || !pk_Fl) {
         pk_rows = pk_batch = 0;
         return set_error(GSV_E_HIP, "packed prefill allocation failed");
     }
@@ -780,6 +788,13 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
     const long sstride = (long)16 * tmax * 32;
     const long slab_stride = (long)R * 512;
     const bool slabs = gemm_slabs_supported(512, 512, 512) && gemm_slabs_supported(2048, 2048, 2048);
+    // pre-split A (r06): the LayerNorms and FFN1's epilogue write the fp16 hi / lo planes their
+    // consumer GEMM would split, where that GEMM runs on the large-M kernel (same values, same
+    // MFMA sequence: bit-identical); layer 0's q/k/v reads the encoder's f32 rows
+    const bool ps = use_presplit && slabs;
+    const bool ps_qkv = ps && gemm_presplit_path(R, 1536, 512, 512);
+    const bool ps_ffn1 = ps && gemm_presplit_path(R, 2048, 512, 512);
+    const bool ps_ffn2 = ps && gemm_presplit_path(R, 512, 2048, 2048);
     for (int l = 0; l < 24; ++l) {
         const T2SLayerW& W = layers[l];
         GemmArgs g{};
@@ -788,6 +803,7 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
         g.C = pk_Q; g.ldc = 512; g.mode = EPI_QKV;
         g.kv.k = kcache[l]; g.kv.v = vcache[l]; g.kv.tmax = tmax; g.kv.seq_stride = sstride;
         g.kv.row_seq = row_seq; g.kv.row_pos = row_pos;
+        if (ps_qkv && l > 0) { g.Ah = pk_Hh; g.Al = pk_Hl; }   // written by the previous layer's LN2
         gemm_nt(g, st);
         AttnArgs at{};
         at.q = pk_Q; at.ldq = 512; at.k = kcache[l]; at.v = vcache[l];
@@ -829,11 +845,17 @@ int gsv_engine::prefill_packed(int B, const gsv_utt* utts, const gsv_sampler* sp
         if (slabs) {
             go.C = pk_slab; go.ldc = 512; go.mode = EPI_SLAB; go.ksplit = 4; go.slab_stride = slab_stride;
             gemm_nt(go, st);
-            layernorm_rows_slabs(pk_slab, 4, slab_stride, W.b_out, pk_H, pk_H1, R, W.n1w, W.n1b, st);
+            layernorm_rows_slabs(pk_slab, 4, slab_stride, W.b_out, pk_H, pk_H1, R, W.n1w, W.n1b, st,
+                                 ps_ffn1 ? pk_H1h : nullptr, ps_ffn1 ? pk_H1l : nullptr);
+            if (ps_ffn1) { g1.Ah = pk_H1h; g1.Al = pk_H1l; }
+            if (ps_ffn2) { g1.mode = EPI_RELU_SPLIT; g1.Ch = pk_Fh; g1.Cl = pk_Fl; g1.ldc = 2048; }
             gemm_nt(g1, st);
             g2.C = pk_slab; g2.ldc = 512; g2.mode = EPI_SLAB; g2.ksplit = 8; g2.slab_stride = slab_stride;
+            if (ps_ffn2) { g2.Ah = pk_Fh; g2.Al = pk_Fl; }
             gemm_nt(g2, st);
-            layernorm_rows_slabs(pk_slab, 8, slab_stride, W.b2, pk_H1, pk_H, R, W.n2w, W.n2b, st);
+            const bool next_ps = ps_qkv && l < 23;   // the next layer's q/k/v A planes
+            layernorm_rows_slabs(pk_slab, 8, slab_stride, W.b2, pk_H1, pk_H, R, W.n2w, W.n2b, st,
+                                 next_ps ? pk_Hh : nullptr, next_ps ? pk_Hl : nullptr);
         } else {
             go.C = pk_S; go.ldc = 512; go.mode = EPI_RESID; go.res = pk_H; go.ldr = 512;
             gemm_nt(go, st);
@@ -2011,6 +2033,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
     } else if (n == "vits_lanes") {   // concurrent vocoder streams of gsv_vits_decode_batch
         if (value < 1 || value > 16) return set_error(GSV_E_ARG, "vits_lanes: 1..16");
         eng->vits_lanes = value;
+    } else if (n == "gemm_presplit") {   // the packed prefill's large GEMMs on pre-split A (same results)
+        eng->use_presplit = value != 0;
     } else if (n == "convh_persist") {
         eng->convh_persist = value != 0;
     } else if (n == "vocoder_first") {

@@ -251,6 +251,9 @@ struct gsv_engine {
     std::vector<void*> pk_allocs;
     float *pk_H = nullptr, *pk_Q = nullptr, *pk_O = nullptr, *pk_S = nullptr, *pk_H1 = nullptr, *pk_F = nullptr;
     float *pk_slab = nullptr, *pk_xlast = nullptr;
+    // fp16 hi / lo planes of pk_H, pk_H1, pk_F: the A operands of the pre-split large-M GEMMs
+    __half *pk_Hh = nullptr, *pk_Hl = nullptr, *pk_H1h = nullptr, *pk_H1l = nullptr, *pk_Fh = nullptr, *pk_Fl = nullptr;
+    bool use_presplit = true;          // option "gemm_presplit": the packed prefill's large GEMMs on pre-split A
     int *pk_rowinfo = nullptr, *pk_last = nullptr;
     int64_t* pk_prompts = nullptr;
     int* pk_tiles = nullptr;

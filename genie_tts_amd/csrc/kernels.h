@@ -19,6 +19,7 @@ enum EpiMode {
     EPI_MISH = 5,        // C = v * tanh(softplus(v))        (MelStyleEncoder spectral)
     EPI_SLAB = 6,        // split-K: C + z*slab_stride = raw partial of K slice z (no bias)
     EPI_GELU = 7,        // C = 0.5 v (1 + erf(v / sqrt 2))  (exact GELU, CN-HuBERT)
+    EPI_RELU_SPLIT = 8,  // Ch / Cl = the fp16 hi / lo split of max(v, 0) (no f32 C): the A planes of a pre-split GEMM
 };
 
 struct KVScatter {
@@ -56,6 +57,10 @@ struct GemmArgs {
     int ksplit; long slab_stride;    // EPI_SLAB: K split over grid.z (fp16-weight path only)
     // optional A prologue (fp16-weight path): A(m,k) = relu?(a_bias[k] + sum_z A[z * a_slab_stride + m*lda + k])
     int a_nslab; long a_slab_stride; const float* a_bias; int a_relu;
+    // pre-split A (large-M fp16-weight path only, gemm_presplit_path): A's fp16 hi / lo planes
+    // (lda elements per row), as the kernels' own split of the f32 values would form them
+    const __half* Ah; const __half* Al;
+    __half* Ch; __half* Cl;          // EPI_RELU_SPLIT outputs (ldc elements per row)
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 // Args of a GEMM with fp16 weights W[N][K] (ldw = K): C = epi(A W^T + bias)
@@ -68,6 +73,9 @@ GemmArgs gemm_w16(int M, int N, int K, const float* A, long lda, const W16& W, c
 bool gemm_slabs_supported(int K, long lda, long ldw);
 // shapes the split-weight (W16 with lo) GEMM runs
 bool gemm_w16_supported(int K, long lda, long ldw);
+// true when gemm_nt runs an fp16-weight GEMM of this shape on the large-M kernel, which also
+// takes pre-split A planes (GemmArgs::Ah / Al); K % 128 == 0, lda % 8 == 0 assumed
+bool gemm_presplit_path(int M, int N, int K, long lda);
 
 // --------------------------------------------------------- row kernels
 void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,
@@ -75,7 +83,7 @@ void layernorm_rows(const float* in, float* out, int rows, const float* g, const
 // LayerNorm of res + (bias + sum_z slab[z]) (fixed order) -- the split-K GEMM's reduce
 void layernorm_rows_slabs(const float* slabs, int nsplit, long slab_stride, const float* bias,
                           const float* res, float* out, int rows, const float* g, const float* b,
-                          hipStream_t s);
+                          hipStream_t s, __half* out_hi = nullptr, __half* out_lo = nullptr);
 // LayerNorm over rows of D <= 1024 values with the given eps (CN-HuBERT, RoBERTa)
 void layernorm_rows_d(const float* in, float* out, int rows, int D, const float* g, const float* b, float eps,
                       hipStream_t s);

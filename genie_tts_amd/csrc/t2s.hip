@@ -30,6 +30,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, int row0, int c
         switch (a.mode) {
             case EPI_STORE: a.C[(long)row * a.ldc + col] = v; break;
             case EPI_RELU: a.C[(long)row * a.ldc + col] = fmaxf(v, 0.f); break;
+            case EPI_RELU_SPLIT: {   // the consumer GEMM's split of the f32 value, done here
+                float x = fmaxf(v, 0.f);
+                asm volatile("" : "+v"(x));   // materialised f32: no conversion fused into its producers
+                const _Float16 h = (_Float16)x;
+                reinterpret_cast<_Float16*>(a.Ch)[(long)row * a.ldc + col] = h;
+                reinterpret_cast<_Float16*>(a.Cl)[(long)row * a.ldc + col] = (_Float16)(x - (float)h);
+            } break;
             case EPI_GELU: a.C[(long)row * a.ldc + col] = 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); break;
             case EPI_RESID: a.C[(long)row * a.ldc + col] = a.res[(long)row * a.ldr + col] + v; break;
             case EPI_MISH: {
@@ -291,7 +298,11 @@ __device__ __forceinline__ void gx3_dma(const void* g, void* l) {
 // shared by WTN MFMA pairs; every 32 x 32 tile still runs the one-tile MFMA sequence.
 // XR: blocks that share an A row tile go to one XCD (the guide's bijective remap of the
 // block id; `id % 8` labels the blocks that share an XCD), so A is fetched into one L2.
-template <int BM, int BN, int NS, bool SW = false, int WTN = 1, bool XR = false>
+// PS (pre-split A): A arrives as its fp16 hi / lo planes (a.Ah / a.Al, written by the producer
+// from the same f32 values, r06), laid out in LDS like the weights; the fragment split -- ~24
+// VALU instructions per MFMA pair, which kept the large-M form's VALU ~80 % busy
+// (profiles/r06j_gemm_pmc.txt) -- is gone, and each product runs the same two MFMAs.
+template <int BM, int BN, int NS, bool SW = false, int WTN = 1, bool XR = false, bool PS = false>
 __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32 / WTN)) void k_gemm_x3(GemmArgs a) {
     constexpr int WN = BN / 32 / WTN;                    // waves across N
     constexpr int WV = (BM / 32) * WN;                   // waves, WTN 32 x 32 output tiles each
@@ -322,11 +333,24 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32 / WTN)) void k_gemm_x3(Ge
     // (chunk slot ^ (row & 15)); W instruction j covers rows 8 j + (lane >> 3), slot lane & 7
     // (chunk slot ^ ((row >> 1) & 7))
     const float* asrc[NA];
+    // PS: plane instruction i < NA / 2 covers hi rows 8 i' + (lane >> 3) (i' = w + WV i), slot lane & 7
+    // (chunk slot ^ ((row >> 1) & 7), the weights' swizzle); i >= NA / 2 the lo plane's rows
+    constexpr int NAH = NA / 2;
+    static_assert(!PS || NAH * WV * 8 == BM, "pre-split A: whole 8-row plane instructions");
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-        const int row = 4 * (w + WV * i) + (lane >> 4), slot = lane & 15;
-        const int gm = min(m0 + row, a.M - 1);
-        asrc[i] = a.A + (long)gm * a.lda + (long)s_lo * GX3_BK + 4 * (slot ^ (row & 15));
+        if (PS) {
+            const int ip = i < NAH ? i : i - NAH;
+            const int row = 8 * (w + WV * ip) + (lane >> 3), slot = lane & 7;
+            const int gm = min(m0 + row, a.M - 1);
+            const __half* pl = i < NAH ? a.Ah : a.Al;
+            asrc[i] = reinterpret_cast<const float*>(pl + (long)gm * a.lda + (long)s_lo * GX3_BK +
+                                                     8 * (slot ^ ((row >> 1) & 7)));
+        } else {
+            const int row = 4 * (w + WV * i) + (lane >> 4), slot = lane & 15;
+            const int gm = min(m0 + row, a.M - 1);
+            asrc[i] = a.A + (long)gm * a.lda + (long)s_lo * GX3_BK + 4 * (slot ^ (row & 15));
+        }
     }
     const __half* wsrc[NW];
 #pragma unroll
@@ -340,7 +364,15 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32 / WTN)) void k_gemm_x3(Ge
     auto issue = [&](int st) {
         const int k0 = st * GX3_BK, buf = st % NS;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) gx3_dma(asrc[i] + k0, &As[buf][256 * (w + WV * i)]);
+        for (int i = 0; i < NA; ++i) {
+            if (PS) {   // 1 KB = 8 plane rows of 64 halfs; the lo plane after the hi plane's BM rows
+                const int ip = i < NAH ? i : i - NAH;
+                __half* dst = reinterpret_cast<__half*>(As[buf]) + (i < NAH ? 0 : BM * GX3_BK) + 512 * (w + WV * ip);
+                gx3_dma(reinterpret_cast<const __half*>(asrc[i]) + k0, dst);
+            } else {
+                gx3_dma(asrc[i] + k0, &As[buf][256 * (w + WV * i)]);
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NW; ++i) gx3_dma(wsrc[i] + k0, &Ws[buf][512 * (w + WV * i)]);
 #pragma unroll
@@ -367,11 +399,18 @@ __global__ __launch_bounds__(64 * (BM / 32) * (BN / 32 / WTN)) void k_gemm_x3(Ge
         const __half* Wls_ = Wls[SW ? st % NS : 0];
 #pragma unroll
         for (int ks = 0; ks < GX3_BK / 16; ++ks) {
-            const int c0 = 4 * ks + 2 * hh;   // A chunks c0, c0 + 1 (4 floats each)
-            const float4 x0 = *reinterpret_cast<const float4*>(As_ + arow * GX3_BK + 4 * (c0 ^ (arow & 15)));
-            const float4 x1 = *reinterpret_cast<const float4*>(As_ + arow * GX3_BK + 4 * ((c0 + 1) ^ (arow & 15)));
             h16x8 ahi, alo;
-            split8(x0, x1, ahi, alo);
+            if (PS) {   // this lane's 8 k of row arow: chunk 2 ks + hh of each plane
+                const __half* Ah_ = reinterpret_cast<const __half*>(As_);
+                const int ao = arow * GX3_BK + 8 * ((2 * ks + hh) ^ ((arow >> 1) & 7));
+                ahi = *reinterpret_cast<const h16x8*>(Ah_ + ao);
+                alo = *reinterpret_cast<const h16x8*>(Ah_ + BM * GX3_BK + ao);
+            } else {
+                const int c0 = 4 * ks + 2 * hh;   // A chunks c0, c0 + 1 (4 floats each)
+                const float4 x0 = *reinterpret_cast<const float4*>(As_ + arow * GX3_BK + 4 * (c0 ^ (arow & 15)));
+                const float4 x1 = *reinterpret_cast<const float4*>(As_ + arow * GX3_BK + 4 * ((c0 + 1) ^ (arow & 15)));
+                split8(x0, x1, ahi, alo);
+            }
             const int cb = 2 * ks + hh;       // W chunk (8 halfs)
 #pragma unroll
             for (int t = 0; t < WTN; ++t) {
@@ -423,7 +462,10 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
         // slower than k_gemm_x2 at 22,848 rows and were removed; profiles/r04e_gemm_big.txt)
         case 13: go(k_gemm_x3<64, 128, 2, false, 2, true>, 64, 128, 256); break;   // 64 KB: 2 blocks per CU
         case 14: go(k_gemm_x3<128, 64, 2, false, 2, true>, 128, 64, 256); break;   // 80 KB
-        case 15: go(k_gemm_x3<64, 64, 2, false, 1, true>, 64, 64, 256); break;     // 48 KB: 3 per CU
+        case 15:   // 48 KB: 3 per CU
+            if (a.Ah) go(k_gemm_x3<64, 64, 2, false, 1, true, true>, 64, 64, 256);
+            else go(k_gemm_x3<64, 64, 2, false, 1, true>, 64, 64, 256);
+            break;
         case 1: go(k_gemm_x3<64, 64, 4>, 64, 64, 256); break;
         case 2: go(k_gemm_x3<32, 64, 4>, 32, 64, 128); break;
         case 3: go(k_gemm_x3<64, 32, 4>, 64, 32, 128); break;
@@ -489,6 +531,13 @@ static bool gemm_x2_enabled() {
 
 bool gemm_w16_supported(int K, long lda, long ldw) { return K % GX_KS == 0 && lda % 4 == 0 && ldw % 8 == 0; }
 
+bool gemm_presplit_path(int M, int N, int K, long lda) {
+    if (K % GX_KS != 0 || lda % 8 != 0 || !gemm_x2_enabled() || gemm_variant() != 3 || gemm_cfg() != 0) return false;
+    GemmArgs t{};
+    t.M = M; t.N = N;
+    return gemm_big(t) && gemm_big_cfg() == 15;
+}
+
 bool gemm_slabs_supported(int K, long lda, long ldw) {
     return K % GX_KS == 0 && lda % 4 == 0 && ldw % 8 == 0 && gemm_x2_enabled();
 }
@@ -512,6 +561,10 @@ void gemm_nt(const GemmArgs& a, hipStream_t s) {
         if (a.mode == EPI_SLAB) grid.z = a.ksplit;
         // the LDS-DMA pipeline reads A as stored: a slab-summing A prologue stays on k_gemm_x2
         // (M > 512: the register-staged kernel's 128-k steps win once the grid covers the chip)
+        if (a.Ah && !gemm_presplit_path(a.M, a.N, a.K, a.lda)) {   // the caller asked gemm_presplit_path
+            std::fprintf(stderr, "gemm_nt: pre-split A on a shape without the large-M path (M=%d N=%d)\n", a.M, a.N);
+            std::abort();
+        }
         if (a.a_nslab == 0 && a.lda % 4 == 0 && gemm_variant() == 3 && gemm_cfg() == 0 && gemm_big(a))
             launch_x3(a, grid.z, s, gemm_big_cfg());
         else if (a.a_nslab == 0 && a.lda % 4 == 0 && gemm_variant() == 3 && (a.M <= 512 || gemm_cfg() != 0))
@@ -546,7 +599,8 @@ __global__ __launch_bounds__(256) void k_layernorm512(const float* in, float* ou
 
 __global__ __launch_bounds__(256) void k_layernorm512_slabs(const float* slabs, int nsplit, long sstride,
                                                             const float* bias, const float* res, float* out,
-                                                            const float* g, const float* b) {
+                                                            const float* g, const float* b, _Float16* oh,
+                                                            _Float16* ol) {
     __shared__ float red[16];
     const long r = blockIdx.x;
     const int t = threadIdx.x;
@@ -560,16 +614,25 @@ __global__ __launch_bounds__(256) void k_layernorm512_slabs(const float* slabs, 
     const float d0 = v0 - mean, d1 = v1 - mean;
     const float var = block_sum(d0 * d0 + d1 * d1, red) * (1.0f / 512.0f);
     const float den = sqrtf(var + 1e-5f);
-    out[r * 512 + t] = d0 / den * g[t] + b[t];
-    out[r * 512 + t + 256] = d1 / den * g[t + 256] + b[t + 256];
+    float o0 = d0 / den * g[t] + b[t], o1 = d1 / den * g[t + 256] + b[t + 256];
+    if (oh) {   // + the fp16 hi / lo planes of the stored values (a pre-split GEMM's A)
+        asm volatile("" : "+v"(o0), "+v"(o1));   // materialised f32: no conversion fused into them
+        const _Float16 h0 = (_Float16)o0, h1 = (_Float16)o1;
+        oh[r * 512 + t] = h0;
+        oh[r * 512 + t + 256] = h1;
+        ol[r * 512 + t] = (_Float16)(o0 - (float)h0);
+        ol[r * 512 + t + 256] = (_Float16)(o1 - (float)h1);
+    }
+    out[r * 512 + t] = o0;
+    out[r * 512 + t + 256] = o1;
 }
 
 void layernorm_rows_slabs(const float* slabs, int nsplit, long slab_stride, const float* bias,
                           const float* res, float* out, int rows, const float* g, const float* b,
-                          hipStream_t s) {
+                          hipStream_t s, __half* out_hi, __half* out_lo) {
     if (rows <= 0) return;
     hipLaunchKernelGGL(k_layernorm512_slabs, dim3(rows), dim3(256), 0, s, slabs, nsplit, slab_stride, bias,
-                       res, out, g, b);
+                       res, out, g, b, reinterpret_cast<_Float16*>(out_hi), reinterpret_cast<_Float16*>(out_lo));
 }
 
 void layernorm_rows(const float* in, float* out, int rows, const float* g, const float* b,

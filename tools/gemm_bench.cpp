@@ -14,7 +14,9 @@
 #include <vector>
 #include "kernels.h"
 
-struct Shape { const char* name; int M, N, K, mode, ksplit; int sw = 0; };   // sw: split fp32 weights (hi + lo planes)
+// sw: split fp32 weights (hi + lo planes); ps: A given as its fp16 hi / lo planes (pre-split, the
+// large-M kernel only) -- its hash must equal the same shape's f32-A hash
+struct Shape { const char* name; int M, N, K, mode, ksplit; int sw = 0; int ps = 0; };
 
 static unsigned long long rng_state = 7;   // private LCG: the HIP runtime may draw from rand()
 static float frand() {
@@ -41,6 +43,9 @@ int main() {
         {"pk64 out slab   ", 22848, 512, 512, gsv::EPI_SLAB, 4},
         {"pk64 ffn1       ", 22848, 2048, 512, gsv::EPI_RELU, 1},
         {"pk64 ffn2 slab  ", 22848, 512, 2048, gsv::EPI_SLAB, 8},
+        {"pk64 qkv    PS  ", 22848, 1536, 512, gsv::EPI_STORE, 1, 0, 1},
+        {"pk64 ffn1   PS  ", 22848, 2048, 512, gsv::EPI_RELU, 1, 0, 1},
+        {"pk64 ffn2 slb PS", 22848, 512, 2048, gsv::EPI_SLAB, 8, 0, 1},
         {"rob pk qkv  W16 ", 1100, 3072, 1024, gsv::EPI_STORE, 1, 1},
         {"rob pk ffn1 W16 ", 1100, 4096, 1024, gsv::EPI_GELU, 1, 1},
         {"rob pk ffn2 W16 ", 1100, 1024, 4096, gsv::EPI_SLAB, 8, 1},
@@ -75,6 +80,19 @@ int main() {
         g.bias = sh.mode == gsv::EPI_SLAB ? nullptr : dB; g.C = dC; g.ldc = N; g.mode = sh.mode;
         g.ksplit = sh.ksplit; g.slab_stride = (long)M * N;
         g.Wl = dWl;
+        __half *dAh = nullptr, *dAl = nullptr;
+        if (sh.ps) {   // the planes the producers write: hi = fp16(a), lo = fp16(a - hi), round to nearest even
+            std::vector<__half> ah(A.size()), al(A.size());
+            for (size_t i = 0; i < A.size(); ++i) {
+                ah[i] = __float2half(A[i]);
+                al[i] = __float2half(A[i] - __half2float(ah[i]));
+            }
+            (void)hipMalloc(&dAh, A.size() * 2);
+            (void)hipMalloc(&dAl, A.size() * 2);
+            (void)hipMemcpy(dAh, ah.data(), A.size() * 2, hipMemcpyHostToDevice);
+            (void)hipMemcpy(dAl, al.data(), A.size() * 2, hipMemcpyHostToDevice);
+            g.Ah = dAh; g.Al = dAl;
+        }
         gsv::gemm_nt(g, 0);
         (void)hipDeviceSynchronize();
         hipEvent_t e0, e1;
@@ -122,6 +140,7 @@ int main() {
                M, N, K, sh.ksplit, us, (wbytes + abytes) / (us * 1e3), maxerr, hsh);
         (void)hipFree(dA); (void)hipFree(dW); (void)hipFree(dB); (void)hipFree(dC);
         if (dWl) (void)hipFree(dWl);
+        if (dAh) { (void)hipFree(dAh); (void)hipFree(dAl); }
     }
     return 0;
 }
