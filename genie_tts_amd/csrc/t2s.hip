@@ -460,8 +460,14 @@ static void launch_x3(const GemmArgs& a, int z, hipStream_t s, int cfg) {
     switch (cfg) {
         // (r04: the one-block-per-CU 128 x 128 forms, four 32 x 32 tiles per wave, measured
         // slower than k_gemm_x2 at 22,848 rows and were removed; profiles/r04e_gemm_big.txt)
-        case 13: go(k_gemm_x3<64, 128, 2, false, 2, true>, 64, 128, 256); break;   // 64 KB: 2 blocks per CU
-        case 14: go(k_gemm_x3<128, 64, 2, false, 2, true>, 128, 64, 256); break;   // 80 KB
+        case 13:   // 64 KB: 2 blocks per CU
+            if (a.Ah) go(k_gemm_x3<64, 128, 2, false, 2, true, true>, 64, 128, 256);
+            else go(k_gemm_x3<64, 128, 2, false, 2, true>, 64, 128, 256);
+            break;
+        case 14:   // 80 KB
+            if (a.Ah) go(k_gemm_x3<128, 64, 2, false, 2, true, true>, 128, 64, 256);
+            else go(k_gemm_x3<128, 64, 2, false, 2, true>, 128, 64, 256);
+            break;
         case 15:   // 48 KB: 3 per CU
             if (a.Ah) go(k_gemm_x3<64, 64, 2, false, 1, true, true>, 64, 64, 256);
             else go(k_gemm_x3<64, 64, 2, false, 1, true>, 64, 64, 256);
@@ -535,7 +541,8 @@ bool gemm_presplit_path(int M, int N, int K, long lda) {
     if (K % GX_KS != 0 || lda % 8 != 0 || !gemm_x2_enabled() || gemm_variant() != 3 || gemm_cfg() != 0) return false;
     GemmArgs t{};
     t.M = M; t.N = N;
-    return gemm_big(t) && gemm_big_cfg() == 15;
+    const int c = gemm_big_cfg();
+    return gemm_big(t) && (c == 13 || c == 14 || c == 15);
 }
 
 bool gemm_slabs_supported(int K, long lda, long ldw) {
