@@ -4,7 +4,9 @@ random semantic tokens of the workload's lengths, Philox noise), timed per call;
 time into the per-utterance front part (lanes) and the segmented generator (from the
 first conv_pre launch, k_conv1d<7>, to the end).
 Usage: python tools/vits_batch_prof.py [N] [--seg 0|1] [--front 0|1] [--opt name=value] [--n sentences]
-     | python tools/vits_batch_prof.py --trace DIR"""
+     | python tools/vits_batch_prof.py --trace DIR
+     | python tools/vits_batch_prof.py --convs DIR   (the last call's generator convs in launch order:
+       stage, kernel, grid, microseconds -- the MRF convs of a stage are 3 resblocks x 3 dilations x 2)"""
 import glob
 import os
 import sqlite3
@@ -36,7 +38,41 @@ def trace(path):
               f"generator {(t1 - g0) / 1e6:.2f} ms")
 
 
+def convs(path):
+    db = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)[0]
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    ni = cols.index("name") if "name" in cols else cols.index("kernel_name")
+    si, ei = cols.index("start"), cols.index("end")
+    gi = [cols.index(k) for k in ("grid_size_x", "grid_size_y", "grid_size_z") if k in cols]
+    print("columns:", cols)
+    rows = sorted(c.execute("select * from kernels"), key=lambda r: r[si])
+    calls, cur = [], [rows[0]]
+    for r in rows[1:]:
+        if r[si] - max(x[ei] for x in cur[-50:]) > 2e6:
+            calls.append(cur)
+            cur = []
+        cur.append(r)
+    calls.append(cur)
+    call = calls[-1]
+    g0 = next(i for i, r in enumerate(call) if "k_conv1d<7" in r[ni])
+    stage, tot = -1, {}
+    for r in call[g0:]:
+        n = r[ni]
+        short = n.split("(")[0].replace("void gsv::(anonymous namespace)::", "").replace("gsv::", "")
+        us = (r[ei] - r[si]) / 1e3
+        grid = tuple(r[i] for i in gi)
+        if "k_conv_h" in short and grid and len(grid) == 3 and grid[2] > 1:
+            stage += 1   # the polyphase ConvTranspose (z = phases) opens a stage
+        print(f"stage {stage} {short:45s} grid {grid} {us:9.1f} us")
+        tot.setdefault((stage, short), []).append(us)
+    for (st, k), v in sorted(tot.items()):
+        print(f"total stage {st} {k:45s} {len(v):3d} x {sum(v) / len(v):8.1f} us = {sum(v) / 1e3:7.2f} ms")
+
+
 def main():
+    if "--convs" in sys.argv:
+        return convs(sys.argv[sys.argv.index("--convs") + 1])
     if "--trace" in sys.argv:
         return trace(sys.argv[sys.argv.index("--trace") + 1])
     import numpy as np
