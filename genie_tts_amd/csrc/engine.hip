@@ -304,6 +304,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_PERSISTM")) use_persistm = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PRESPLIT")) use_presplit = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_CONVH_WS")) convh_ws = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
         if (std::atoi(e) == 1 && !ktrace) {
@@ -2037,6 +2038,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_presplit = value != 0;
     } else if (n == "convh_persist") {
         eng->convh_persist = value != 0;
+    } else if (n == "convh_ws") {
+        eng->convh_ws = value != 0;
     } else if (n == "vocoder_first") {
         eng->vocoder_first = value != 0;
     } else if (n == "lanes_all_cus") {

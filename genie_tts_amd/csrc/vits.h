@@ -70,6 +70,9 @@ struct ConvArgs {
     // f16-split path: > 0 = the CUs of the stream; large grids then run the persistent tile
     // loop (two blocks per CU) instead of one block per tile (option "convh_persist")
     int persist;
+    // f16-split path: > 0 = the CUs of the stream; the wide MRF convs (Cin 64 / 128) then run
+    // the weight-stationary persistent form, k_conv_ws (option "convh_ws")
+    int ws;
 };
 void conv1d(const ConvArgs& a, hipStream_t s);
 // seg[t] for t < n: i with off[i] * f <= t < (off[i] + len[i]) * f, else -1 (off ascending)

@@ -335,6 +335,218 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     if (ovf) atomicOr(a.ovf, 1);
 }
 
+// Weight-stationary form for the wide generator stages' 7- / 11-tap MRF convs (Cin = 64 / 128,
+// Cout a multiple of 64, unit stride, one phase; option "convh_ws", off by default).  r06o (batch64's vocoder, `profiles/r06o_vocoder_stages.txt`):
+// there k_conv_h takes 2-5x the larger of its HBM and MFMA times, because every 64 x 128 block
+// stages its own copy of the chunk's weights (64 rows x taps x 32 channels, 12-45 KB) for 128
+// output columns -- more bytes into LDS than its input tile.  Here a block holds its 64 output
+// channels' whole weight slab [co][tap][ci] in LDS (25-116 KB, loaded once) and walks time tiles of
+// 256 columns (8 waves, WM = 2 x WN = 4, each wave 32 x 64 as in k_conv_h's (2, 2, 1) form);
+// per tile only the input chunks are staged (fp32 -> activation -> hi / lo -> LDS), the next
+// tile's first chunk during the current tile's last MFMAs.  Each accumulator runs k_conv_h's
+// MFMA sequence (chunk, then the chunk's (tap, 8-channel group) pairs), so the results are
+// bit-identical to the (2, 2, 1) form the cost model picks for these shapes.
+// Blocks b, b + 8, ... share an XCD (MI355X_MICROARCH.md): the Cout / 64 blocks of one tile
+// sequence are placed there, so a tile's input is fetched from HBM once per XCD.
+template <int KT, int CIN>
+struct WsCfg {
+    static constexpr int CC = 32, G8 = CC / 8, NG = KT * G8, NSTEP = NG / 2;
+    static constexpr int BM = 64, BN = 256;
+    static constexpr int XW = BN + (KT - 1) * DMAX;
+    static constexpr int XR = CC + 8;                    // halves per X row (odd x 16 B)
+    static constexpr int WR = KT * CIN + 8;              // halves per weight row (odd x 16 B)
+    static constexpr int NXI = (XW * G8 + 511) / 512;
+    static constexpr int X_BYTES = XW * XR * 2;
+    static constexpr int W_BYTES = BM * WR * 2;
+    static constexpr int LDS = 2 * X_BYTES + W_BYTES;
+    static constexpr int NCH = CIN / CC;
+    static_assert(NG % 2 == 0, "two 8-channel groups per MFMA step");
+};
+
+template <int KT, int CIN>
+__global__ __launch_bounds__(512) void k_conv_ws(ConvArgs a, int nlanes, int ncob) {
+    using C = WsCfg<KT, CIN>;
+    __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+    _Float16* Xh = reinterpret_cast<_Float16*>(smem);
+    _Float16* Xl = reinterpret_cast<_Float16*>(smem + C::X_BYTES);
+    _Float16* Ws = reinterpret_cast<_Float16*>(smem + 2 * C::X_BYTES);
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wn = w & 3, wm = w >> 2;
+    const int b = blockIdx.x;
+    const int cob = (b >> 3) % ncob;                     // output-channel block
+    const int ln = (b & 7) + 8 * ((b >> 3) / ncob);      // tile lane
+    const int co0 = cob * C::BM;
+    const int dil = a.dil;
+    const int xw = C::BN + (KT - 1) * dil;
+    const int ntn = (a.n_t + C::BN - 1) / C::BN;
+    const float* __restrict__ isc = a.in_scale;
+    const float* __restrict__ X = a.x;
+
+    // the block's weight slab, once: rows co0 .. co0 + 63, [tap][ci] contiguous per row
+    {
+        const __half* src = a.wh + (long)co0 * KT * CIN;
+        constexpr int PER_ROW = KT * CIN / 8;
+        for (int e = tid; e < C::BM * PER_ROW; e += 512) {
+            const int r = e / PER_ROW, q = e - r * PER_ROW;
+            *reinterpret_cast<uint4*>(Ws + r * C::WR + q * 8) =
+                *reinterpret_cast<const uint4*>(src + (long)r * KT * CIN + q * 8);
+        }
+    }
+
+    int xu[C::NXI], xc[C::NXI];
+#pragma unroll
+    for (int i = 0; i < C::NXI; ++i) {
+        const int e = tid + i * 512;
+        xc[i] = e / xw;
+        xu[i] = e - xc[i] * xw;
+        if (xc[i] >= C::G8) xc[i] = -1;
+    }
+    float xr[C::NXI][8];
+    bool ovf = false;
+    auto load = [&](int t0, int ci0) {   // raw values (the activation is applied in store)
+#pragma unroll
+        for (int i = 0; i < C::NXI; ++i) {
+            const int tin = t0 - a.pad + xu[i];
+            const bool ok = xc[i] >= 0 && tin >= 0 && tin < a.Tin;
+            const float* src = X + (long)(ci0 + xc[i] * 8) * a.x_cs + tin;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xr[i][j] = ok ? src[(long)j * a.x_cs] : 0.f;
+        }
+    };
+    auto store = [&](int cis) {
+#pragma unroll
+        for (int i = 0; i < C::NXI; ++i) {
+            if (xc[i] < 0) continue;
+            if (a.in_act) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xr[i][j] = xr[i][j] >= 0.f ? xr[i][j] : xr[i][j] * a.in_slope;
+            }
+            if (isc) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xr[i][j] *= isc[cis + xc[i] * 8 + j];
+            }
+            float m = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(xr[i][j]));
+            ovf |= m > 65504.f;
+            uint4 hi, lo;
+            split8(xr[i], hi, lo);
+            *reinterpret_cast<uint4*>(Xh + xu[i] * C::XR + xc[i] * 8) = hi;
+            *reinterpret_cast<uint4*>(Xl + xu[i] * C::XR + xc[i] * 8) = lo;
+        }
+    };
+
+    f32x16 acc[2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[f][i] = 0.f;
+    };
+    zero_acc();
+    const int r32 = lane & 31, hsel = lane >> 5;
+    int tile = ln;
+    if (tile >= ntn) return;   // block-uniform: no barrier is skipped by part of a block
+    int t0 = tile * C::BN;
+    load(t0, 0);
+    store(0);
+    __syncthreads();   // weights and the first chunk
+    for (;;) {
+        const int ntile = tile + nlanes;
+        const bool more = ntile < ntn;
+        const int nt0 = ntile * C::BN;
+        for (int c = 0; c < C::NCH; ++c) {
+            const bool last = c + 1 == C::NCH;
+            if (!last) load(t0, (c + 1) * C::CC);
+            else if (more) load(nt0, 0);
+            // the weight rows' offset for this chunk, opaque: re-formed per chunk, not hoisted
+            int wro = (wm * 32 + r32) * C::WR + c * C::CC;
+            asm volatile("" : "+v"(wro));
+            const _Float16* wrow = Ws + wro;
+#pragma unroll
+            for (int j = 0; j < C::NSTEP; ++j) {
+                const int g = 2 * j + hsel;
+                const int tap = g / C::G8, c8 = g - tap * C::G8;
+                const h8 A = *reinterpret_cast<const h8*>(wrow + tap * CIN + c8 * 8);
+#pragma unroll
+                for (int f = 0; f < 2; ++f) {
+                    const int row = wn * 64 + f * 32 + r32 + tap * dil;
+                    const h8 Bl = *reinterpret_cast<const h8*>(Xl + row * C::XR + c8 * 8);
+                    const h8 Bh = *reinterpret_cast<const h8*>(Xh + row * C::XR + c8 * 8);
+                    acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bl, acc[f], 0, 0, 0);
+                    acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bh, acc[f], 0, 0, 0);
+                }
+            }
+            __syncthreads();
+            if (!last) {
+                store((c + 1) * C::CC);
+                __syncthreads();
+            } else if (more) {
+                store(0);   // the next tile's first chunk, into the X this tile no longer reads
+            }
+        }
+        {
+            const int cobase = co0 + wm * 32 + 4 * hsel;
+            float sc[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[r] = a.wscale[cobase + (r & 3) + 8 * (r >> 2)];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const int t = t0 + wn * 64 + f * 32 + r32;
+                if (t >= a.n_t) continue;
+                float v[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = acc[f][r] * sc[r];
+                conv_epilogue16_lean(a, cobase, t, 0, v);
+            }
+        }
+        if (!more) break;
+        tile = ntile;
+        t0 = nt0;
+        zero_acc();
+        __syncthreads();   // the staged chunk is visible to every wave
+    }
+    if (ovf) atomicOr(a.ovf, 1);
+}
+
+template <int KT, int CIN>
+void launch_ws(const ConvArgs& a, hipStream_t s) {
+    // one block per CU (8 waves; ~190-240 VGPRs, so a second block would not be resident)
+    const int ncob = a.Cout / 64;
+    int lanes = (a.ws / (8 * ncob)) * 8;   // a multiple of 8: whole XCD rounds
+    if (lanes < 8) lanes = 8;
+    hipLaunchKernelGGL((k_conv_ws<KT, CIN>), dim3(lanes * ncob), dim3(512), 0, s, a, lanes, ncob);
+}
+
+// The weight-stationary form covers the 7- and 11-tap MRF convs of the Cin = 64 stage and the
+// 7-tap ones of Cin = 128 (the 11-tap slab of 64 x 128 channels would need 181 KB of LDS), with
+// >= 2 tiles per lane.  The 3-tap convs stay on k_conv_h: there the per-tile staging and epilogue
+// outweigh the MFMAs and one block per CU hides them worse than k_conv_h's two (r06p: 549 / 389 us
+// against 417 / 328 at Cin 128 / 64).
+template <int KT>
+bool try_ws(const ConvArgs& a, hipStream_t s) {
+    if constexpr (KT == 7 || KT == 11) {
+        if (a.ws <= 0 || a.phases > 1 || a.o_tstride != 1 || a.o_toff != 0 || a.Cout % 64 != 0 ||
+            a.Cout != a.Cin ||
+            !(a.mode == CV_STORE || a.mode == CV_RESID || a.mode == CV_ACC_FIRST || a.mode == CV_ACC_ADD ||
+              a.mode == CV_ACC_MEAN))
+            return false;
+        if ((a.n_t + 255) / 256 < 2L * a.ws) return false;   // >= 2 tiles per lane
+        if (a.Cin == 64) {
+            launch_ws<KT, 64>(a, s);
+            return true;
+        }
+        if constexpr (KT <= 7) {
+            if (a.Cin == 128) {
+                launch_ws<KT, 128>(a, s);
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
 template <int KT, int CC>
 bool launch_h(const ConvArgs& a, hipStream_t s) {
     // (WM, WN, KS) by estimated time: block rounds at 2 blocks per CU x tile area
@@ -404,6 +616,7 @@ bool launch_big(const ConvArgs& a, hipStream_t s) {
 template <int KT>
 bool launch_kt(const ConvArgs& a, hipStream_t s) {
     const int z = a.phases > 1 ? a.phases : 1;
+    if (try_ws<KT>(a, s)) return true;
     if (convh_big() && a.Cout % 64 == 0 &&
         (a.Cout % 128 == 0 ? (long)((a.n_t + 127) / 128) * (a.Cout / 128) * z
                            : (long)((a.n_t + 255) / 256) * (a.Cout / 64) * z) >= 1024 &&

@@ -324,15 +324,18 @@ static thread_local int* tls_ovf = nullptr;   // set while the f16-split MRF pat
 static thread_local int tls_convh_tile = 0;    // the running engine's option "convh_tile"
 static thread_local bool tls_convt_f16 = false;   // ... and "convt_f16" (the ConvTransposes on the split path)
 static thread_local bool tls_mrf_fused = false;   // ... and "mrf_fused" (narrow stages' conv pairs as one kernel)
+static thread_local int tls_convh_ws = 0;        // ... CUs of the pass's stream under "convh_ws" (0: off)
 static thread_local int tls_convh_persist = 0;   // ... CUs of the pass's stream under "convh_persist" (0: off)
 // The per-pass thread-local state of one vocoder pass (split-fp16 flag word, tile, ConvT path).
 struct ConvhScope {
-    ConvhScope(int* ovf, int tile, bool convt, bool fused, int persist_cus = 0) {
+    ConvhScope(int* ovf, int tile, bool convt, bool fused, int persist_cus = 0, int ws_cus = 0) {
         tls_ovf = ovf; tls_convh_tile = tile; tls_convt_f16 = convt; tls_mrf_fused = fused;
         tls_convh_persist = persist_cus;
+        tls_convh_ws = ws_cus;
     }
     ~ConvhScope() {
         tls_ovf = nullptr; tls_convh_tile = 0; tls_convt_f16 = false; tls_mrf_fused = false; tls_convh_persist = 0;
+        tls_convh_ws = 0;
     }
 };
 struct SplitkScope {
@@ -353,6 +356,7 @@ static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode
     a.phases = 1;
     a.tile_force = tls_convh_tile;
     a.persist = tls_convh_persist;
+    a.ws = tls_convh_ws;
     if (tls_ovf && c.wh) { a.wh = c.wh; a.wscale = c.wscale; a.ovf = tls_ovf; }
     return a;
 }
@@ -800,7 +804,8 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     if (2 * G > MHA_MAXK_HOST || n_text > MHA_MAXK_HOST) return set_error(GSV_E_CAPACITY, "sequence too long");
     if (int r = ensure_vits_ws(this, W, 2 * G, n_text, version == GSV_V2PP ? 0 : n_audio)) return r;
     SplitkScope sk(W.splitk, W.splitk_cap);
-    ConvhScope cs(ovf, convh_tile, convt_f16, mrf_fused, convh_persist ? stream_cus(s) : 0);
+    ConvhScope cs(ovf, convh_tile, convt_f16, mrf_fused, convh_persist ? stream_cus(s) : 0,
+                  convh_ws ? stream_cus(s) : 0);
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timed) hipEventRecord(ev[4], s);
     if (int r = vits_front(W, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
@@ -1126,7 +1131,8 @@ int gsv_engine::seg_front(hipStream_t st) {
 // path, flagging an fp16-range input in sgb.ovf).
 int gsv_engine::seg_generate(hipStream_t st, bool f16) {
     SegBatch& B = sgb;
-    ConvhScope cs(f16 ? B.ovf : nullptr, convh_tile, convt_f16, mrf_fused, convh_persist ? stream_cus(st) : 0);
+    ConvhScope cs(f16 ? B.ovf : nullptr, convh_tile, convt_f16, mrf_fused, convh_persist ? stream_cus(st) : 0,
+                  convh_ws ? stream_cus(st) : 0);
     const int* seg[6] = {B.seg[0], B.seg[1], B.seg[2], B.seg[3], B.seg[4], B.seg[5]};
     float* const gb[5] = {B.g[0], B.g[1], B.g[2], B.g[3], B.g[4]};
     vits_generator(vits, gb, B.z, B.T, B.dcond, vits.upc, seg, B.audio, st);

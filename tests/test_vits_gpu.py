@@ -420,3 +420,27 @@ def test_vits_batch_persistent_convs_bit_identical(setup, seg):
         e.set_option("seg_vocoder", 1)
     for i, (g, w) in enumerate(zip(got, want)):
         np.testing.assert_array_equal(g, w, err_msg=f"item {i}")
+
+
+def test_vits_batch_weight_stationary_convs_bit_identical(setup):
+    """Option convh_ws: the segmented generator's 7- / 11-tap MRF convs with 64 input channels and
+    its 7-tap ones with 128 run as k_conv_ws -- a block keeps its 64 output channels'
+    weights in LDS and walks 256-column tiles (vits_convh.hip).  Each accumulator runs k_conv_h's
+    MFMA sequence, so the batch's audio is bit-identical with the option on and off."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    items = []
+    for i in range(14):
+        G, S = 70 + 5 * i, 30 + i
+        txt = synth.synth_phones(S, f"vw{i}")
+        sem = ((np.arange(G, dtype=np.int64) * (13 + i) + 7 * i) % 1024).reshape(1, 1, G)
+        items.append(dict(text_seq=txt, pred_semantic=sem, noise_seed=4000 + i, **kw))
+    try:
+        e.set_option("convh_ws", 0)
+        want = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+        e.set_option("convh_ws", 1)
+        got = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+    finally:
+        e.set_option("convh_ws", 0)
+    for i, (g, w) in enumerate(zip(got, want)):
+        np.testing.assert_array_equal(g, w, err_msg=f"item {i}")

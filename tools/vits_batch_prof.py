@@ -44,8 +44,7 @@ def convs(path):
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
     ni = cols.index("name") if "name" in cols else cols.index("kernel_name")
     si, ei = cols.index("start"), cols.index("end")
-    gi = [cols.index(k) for k in ("grid_size_x", "grid_size_y", "grid_size_z") if k in cols]
-    print("columns:", cols)
+    gi = [cols.index(k) for k in ("grid_x", "grid_y", "grid_z") if k in cols]
     rows = sorted(c.execute("select * from kernels"), key=lambda r: r[si])
     calls, cur = [], [rows[0]]
     for r in rows[1:]:
@@ -59,7 +58,7 @@ def convs(path):
     stage, tot = -1, {}
     for r in call[g0:]:
         n = r[ni]
-        short = n.split("(")[0].replace("void gsv::(anonymous namespace)::", "").replace("gsv::", "")
+        short = n.replace("void ", "").replace("gsv::(anonymous namespace)::", "").replace("gsv::", "").split("(")[0]
         us = (r[ei] - r[si]) / 1e3
         grid = tuple(r[i] for i in gi)
         if "k_conv_h" in short and grid and len(grid) == 3 and grid[2] > 1:
