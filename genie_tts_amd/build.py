@@ -26,7 +26,7 @@ ARCH = os.environ.get("GENIE_OFFLOAD_ARCH", "gfx950")
 # nondeterministic 1-2 frame errors of r04 (profiles/r05_convt_race.txt; tools/pk_opsel_probe.hip
 # reproduces it outside the engine).  hipcc forms such ops from ordinary float pairs, so the
 # feature is off for every kernel, and tests/test_isa_audit.py checks the built library.
-NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-DGSV_NO_PACKED_FP32=1"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
          "-Wno-unused-value", "-munsafe-fp-atomics", *NO_PACKED_FP32]
 

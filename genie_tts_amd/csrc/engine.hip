@@ -30,7 +30,13 @@ using namespace gsv;
 static thread_local std::string g_err;
 
 const char* gsv_last_error(void) { return g_err.c_str(); }
-const char* gsv_version(void) { return "genie-mi355x 0.1 (gfx950)"; }
+// The build marks its flags in the version string: the Python loader refuses a library built
+// with the packed-FP32 target feature on (the gfx950 op_sel fault; build.py).
+#if GSV_NO_PACKED_FP32
+const char* gsv_version(void) { return "genie-mi355x 0.1 (gfx950, no packed-fp32)"; }
+#else
+const char* gsv_version(void) { return "genie-mi355x 0.1 (gfx950, packed-fp32)"; }
+#endif
 
 namespace gsv {
 int set_error(int code, const std::string& msg) {

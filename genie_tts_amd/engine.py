@@ -108,6 +108,11 @@ def lib():
         vp, i32, i64p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)
         L.gsv_last_error.restype = ctypes.c_char_p
         L.gsv_version.restype = ctypes.c_char_p
+        if b"no packed-fp32" not in L.gsv_version():
+            # built without build.py's NO_PACKED_FP32: its packed-FP32 ops can return 0 in lanes
+            # 48-63 beside MFMA-heavy waves
+            raise EngineError(f"{_LIB_PATH} was built with packed-FP32 ops: rebuild with "
+                              "`python -m genie_tts_amd.build`")
         L.gsv_engine_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         L.gsv_engine_destroy.argtypes = [vp]
         L.gsv_set_weight.argtypes = [vp, ctypes.c_char_p, vp, ctypes.c_int, i64p, ctypes.c_int]

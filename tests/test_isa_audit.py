@@ -42,3 +42,15 @@ def test_no_packed_fp32_ops_in_device_code(tmp_path):
         assert not bad, f"{b}: {len(bad)} packed-FP32 instructions, e.g. {bad[:3]}"
         n_inst += dis.count("\n")
     assert n_inst > 100_000          # the disassembly really covered the kernels
+
+
+def test_library_marks_its_build_and_the_loader_checks_it():
+    """The build defines GSV_NO_PACKED_FP32 with the target-feature flag; gsv_version reports it,
+    and engine.lib() refuses a library without the mark (build.py)."""
+    import ctypes
+    from genie_tts_amd import build as B
+    assert "-DGSV_NO_PACKED_FP32=1" in B.FLAGS
+    B.build()
+    L = ctypes.CDLL(LIB)
+    L.gsv_version.restype = ctypes.c_char_p
+    assert b"no packed-fp32" in L.gsv_version()
