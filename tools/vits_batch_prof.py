@@ -69,7 +69,43 @@ def convs(path):
         print(f"total stage {st} {k:45s} {len(v):3d} x {sum(v) / len(v):8.1f} us = {sum(v) / 1e3:7.2f} ms")
 
 
+def allk(path):
+    """Every kernel of the last call in launch order: duration, the gap since the previous end."""
+    db = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)[0]
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    ni = cols.index("name") if "name" in cols else cols.index("kernel_name")
+    si, ei = cols.index("start"), cols.index("end")
+    rows = sorted(c.execute("select * from kernels"), key=lambda r: r[si])
+    calls, cur = [], [rows[0]]
+    for r in rows[1:]:
+        if r[si] - max(x[ei] for x in cur[-50:]) > 2e6:
+            calls.append(cur)
+            cur = []
+        cur.append(r)
+    calls.append(cur)
+    call = calls[-1]
+    busy, gaps, prev, agg = 0.0, 0.0, None, {}
+    for r in call:
+        short = r[ni].replace("void ", "").replace("gsv::(anonymous namespace)::", "").replace("gsv::", "").split("(")[0]
+        us = (r[ei] - r[si]) / 1e3
+        gap = (r[si] - prev) / 1e3 if prev is not None else 0.0
+        print(f"{short:45s} {us:9.1f} us  gap {gap:7.1f}")
+        busy += us
+        gaps += max(gap, 0.0)
+        prev = max(prev or 0, r[ei])
+        a = agg.setdefault(short, [0, 0.0])
+        a[0] += 1
+        a[1] += us
+    print(f"# {len(call)} kernels, wall {(max(r[ei] for r in call) - call[0][si]) / 1e3:.1f} us, "
+          f"bodies {busy:.1f} us, gaps {gaps:.1f} us")
+    for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"total {k:45s} {n:4d} x {us / n:8.1f} us = {us:8.1f} us")
+
+
 def main():
+    if "--all" in sys.argv:
+        return allk(sys.argv[sys.argv.index("--all") + 1])
     if "--convs" in sys.argv:
         return convs(sys.argv[sys.argv.index("--convs") + 1])
     if "--trace" in sys.argv:
