@@ -535,6 +535,17 @@ def main():
                          "decode_cus": args.decode_cus or None,
                          "persist_timeouts": run.eng.counter("persist_timeouts"),
                          "vits_f32_reruns": run.eng.counter("vits_f32_reruns")}
+        if roof is not None and "achieved" in roof and rank == 0:
+            # the achievable HBM rate beside the spec peak -- a grid-stride device
+            # copy of 1 GiB (gsv_debug_hbm_copy; read + write bytes), outside the timed region
+            from genie_tts_amd.engine import hbm_copy_ms
+            src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+            dst = torch.empty_like(src)
+            ach = 2 * src.numel() * 4 / (hbm_copy_ms(src, dst, 10) * 1e-3) / 1e9
+            del src, dst
+            roof["achievable_hbm"] = {"value": ach, "unit": "GB/s", "frac": roof["achieved"] / ach,
+                                      "how": "non-temporal grid-stride copy of 1 GiB x 10 on this GPU "
+                                             "(gsv_debug_hbm_copy), read + write bytes"}
         out["roofline"] = roof
         if seq is not None:
             out["sequential"] = {"utt_s": 1.0 / seq, "ms_per_utt": seq * 1e3, "x_realtime": audio_s / seq,

@@ -2153,6 +2153,52 @@ extern "C" int gsv_get_counter(gsv_engine* eng, const char* name, int64_t* value
     return 0;
 }
 
+// The achievable HBM rate on this GPU: a grid-stride copy, 4 x 16 B per thread in
+// flight with non-temporal loads / stores, 32 workgroups of 256 threads per CU -- the fastest of the
+// shapes swept by tools/hbm_copy_probe.hip (6.04 TB/s of read + write bytes; 4.6-5.6 TB/s for one
+// plain 16-B load per thread; the guide quotes 6.29 TB/s).
+typedef float hc_f4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_hbm_copy(const hc_f4* __restrict__ src, hc_f4* __restrict__ dst, long n) {
+    const long stride = (long)gridDim.x * 1024;
+    for (long base = (long)blockIdx.x * 1024 + threadIdx.x; base < n; base += stride) {
+        hc_f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (base + 256 * u < n) v[u] = __builtin_nontemporal_load(src + base + 256 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (base + 256 * u < n) __builtin_nontemporal_store(v[u], dst + base + 256 * u);
+    }
+}
+
+extern "C" int gsv_debug_hbm_copy(const void* src, void* dst, int64_t bytes, int iters, void* stream, float* ms) {
+    if (!src || !dst || !ms || bytes < 16 || iters < 1 || (bytes & 15) ||
+        (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+        return set_error(GSV_E_ARG, "hbm copy: 16-B aligned buffers and size, iters >= 1");
+    hipStream_t s = (hipStream_t)stream;
+    int dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const long n = bytes / 16;
+    const dim3 grid((unsigned)std::max(1, 32 * cus));
+    hipLaunchKernelGGL(k_hbm_copy, grid, dim3(256), 0, s, (const hc_f4*)src, (hc_f4*)dst, n);   // warm
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+        return set_error(GSV_E_HIP, "hbm copy: event");
+    hipEventRecord(e0, s);
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL(k_hbm_copy, grid, dim3(256), 0, s, (const hc_f4*)src, (hc_f4*)dst, n);
+    hipEventRecord(e1, s);
+    const hipError_t r = hipEventSynchronize(e1);
+    float t = 0.f;
+    if (r == hipSuccess) hipEventElapsedTime(&t, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (r != hipSuccess || hipGetLastError() != hipSuccess) return set_error(GSV_E_HIP, "hbm copy launch");
+    *ms = t / iters;
+    return 0;
+}
+
 extern "C" int gsv_debug_ptrace(gsv_engine* eng, uint64_t* host, int n) {
     ENG_CHECK(eng);
     if (!eng->ptrace) return set_error(GSV_E_STATE, "enable option ptrace first");

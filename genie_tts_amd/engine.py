@@ -163,6 +163,7 @@ def lib():
         L.gsv_roberta_batch.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
         L.gsv_f16_exact.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         L.gsv_request_stop.argtypes = [vp, ctypes.c_int32]
+        L.gsv_debug_hbm_copy.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, ctypes.POINTER(ctypes.c_float)]
         _lib = L
     return _lib
 
@@ -178,8 +179,21 @@ EXPORTED = (
     "gsv_vits_decode_async",
     "gsv_vits_wait", "gsv_t2s_prefetch", "gsv_t2s_generate_start", "gsv_t2s_generate_finish",
     "gsv_vits_decode_batch_async", "gsv_vits_batch_wait", "gsv_ref_encode", "gsv_roberta_batch",
-    "gsv_f16_exact", "gsv_request_stop",
+    "gsv_f16_exact", "gsv_request_stop", "gsv_debug_hbm_copy",
 )
+
+
+def hbm_copy_ms(src, dst, iters: int = 10) -> float:
+    """Mean time of one float4 grid-stride device copy src -> dst (torch tensors, same byte
+    size), the achievable-HBM probe of bench.py (gsv_debug_hbm_copy)."""
+    import torch
+    ms = ctypes.c_float(0.0)
+    nbytes = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() == nbytes and src.is_cuda and dst.is_cuda
+    st = torch.cuda.current_stream(src.device).cuda_stream
+    _check(lib().gsv_debug_hbm_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), nbytes,
+                                    iters, ctypes.c_void_p(st), ctypes.byref(ms)), "hbm copy probe")
+    return float(ms.value)
 
 
 def f16_exact(values) -> int:

@@ -312,6 +312,11 @@ int gsv_debug_conv1d(const float* x, int cin, int tin, const float* w, int cout,
 int gsv_debug_conv1d_h(const float* x, int cin, int tin, const void* wh, const float* scale, int cout,
                        int k, int dil, int pad, const float* bias, float* out, int tout, int in_act,
                        float slope, int* ovf, void* stream);
+/* The achievable HBM rate: `iters` grid-stride copies (16-B non-temporal
+ * loads / stores, 4 per thread in flight) of `bytes`
+ * (16-B aligned device buffers) on `stream`; *ms = the mean time of one copy (HIP events).
+ * Read + write bytes = 2 x bytes per copy.  Measurement helper for bench.py. */
+int gsv_debug_hbm_copy(const void* src, void* dst, int64_t bytes, int iters, void* stream, float* ms);
 /* Phase timestamps (100 MHz) of the per-step-graph decode kernels (t2s_decode.hip:
  * the fp16-range re-run / timeout / B > 64 path, not the persistent kernels) of
  * layer 12, last step run: [kernel: QKV GEMV, attention, FFN][block 0..255][slot
