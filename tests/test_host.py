@@ -118,3 +118,13 @@ def test_fp16_only_weight_paths_refuse_fp32_values():
     from genie_tts_amd import synth, weights as W
     q = synth.synth_tensor("encoder.layer.0.attention.self.query.weight", (1024, 1024), fp16=False)
     assert engine.f16_exact(q) >= 0
+
+
+def test_hbm_copy_probe_rejects_bad_arguments_without_touching_the_gpu():
+    """gsv_debug_hbm_copy (bench.py's achievable-HBM probe) checks its arguments before any HIP call."""
+    from genie_tts_amd import engine
+    L = engine.lib()
+    ms = ctypes.c_float(0.0)
+    assert L.gsv_debug_hbm_copy(None, None, 1 << 20, 10, None, ctypes.byref(ms)) != 0
+    assert L.gsv_debug_hbm_copy(ctypes.c_void_p(16), ctypes.c_void_p(32), 100, 10, None, ctypes.byref(ms)) != 0
+    assert b"16-B aligned" in L.gsv_last_error()

@@ -56,3 +56,17 @@ def test_conv1d_f16split_overflow_flag():
     v = torch.randn(32, 32, 3).half().float()
     _, ovf = debug_conv1d_h(x.cuda(), v, torch.ones(32), None, dil=1, pad=1)
     assert ovf == 1
+
+
+def test_hbm_copy_probe_copies_and_times():
+    """gsv_debug_hbm_copy: the destination equals the source after the copies, and the rate is
+    plausible for HBM3E (bench.py's roofline.achievable_hbm)."""
+    import torch
+    from genie_tts_amd.engine import hbm_copy_ms
+    src = torch.randn(1 << 24, device="cuda")
+    dst = torch.zeros_like(src)
+    ms = hbm_copy_ms(src, dst, 3)
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    gbs = 2 * src.numel() * 4 / (ms * 1e-3) / 1e9
+    assert 500 < gbs < 9000, gbs
