@@ -125,6 +125,7 @@ gsv_engine::~gsv_engine() {
     for (void* p : pk_allocs) hipFree(p);
     pk_allocs.clear();
     if (pk_tiles) hipFree(pk_tiles);
+    drop_sides();
     if (own_stream && stream) hipStreamDestroy(stream);
     if (vstream) hipStreamDestroy(vstream);
     for (hipEvent_t e : {vev_in, vev_done, pf_in, pf_done, pf_copied, pf_fork, pf_ev[0], pf_ev[1], pf_ev[2]})
@@ -185,6 +186,11 @@ hipError_t gsv_engine::sync_own_streams() {
     hipError_t r = hipSuccess;
     for (hipStream_t s : {stream, vstream})
         if (s && r == hipSuccess) r = hipStreamSynchronize(s);
+    {
+        std::lock_guard<std::mutex> lk(side_mu);
+        for (auto& p : sides)
+            if (r == hipSuccess) r = hipStreamSynchronize(p->st);
+    }
     for (auto& L : vlanes)
         if (L.st && r == hipSuccess) r = hipStreamSynchronize(L.st);
     return r;
@@ -311,6 +317,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_PRESPLIT")) use_presplit = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH_WS")) convh_ws = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_VITS_FORK")) vits_fork = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
         if (std::atoi(e) == 1 && !ktrace) {
@@ -2046,6 +2053,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->convh_persist = value != 0;
     } else if (n == "convh_ws") {
         eng->convh_ws = value != 0;
+    } else if (n == "vits_fork") {
+        eng->vits_fork = value != 0;
     } else if (n == "vocoder_first") {
         eng->vocoder_first = value != 0;
     } else if (n == "lanes_all_cus") {
@@ -2072,6 +2081,7 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
             hipStream_t ns = nullptr;
             if (hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, p) != hipSuccess)
                 return set_error(GSV_E_HIP, "stream");
+            eng->drop_sides();
             hipStreamDestroy(eng->stream);
             eng->stream = ns;
             eng->t2s_priority = p;

@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <shared_mutex>
+#include <memory>
 #include <thread>
 #include <string>
 #include <vector>
@@ -434,6 +435,18 @@ struct gsv_engine {
     int ref_encode(const float* ref_audio, int n_audio, float* ge, hipStream_t s);
     // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
     int vocoder_cus = 0;
+    // A second stream beside each of the engine's own unmasked streams, for the VITS front's text
+    // branch (vits_front: it needs only the phones, so it runs beside the SSL branch).  Made on first
+    // use; dropped (after a sync) before any of the engine's streams is destroyed.
+    struct SideStream {
+        hipStream_t main = nullptr, st = nullptr;
+        hipEvent_t fork = nullptr, join = nullptr;
+    };
+    std::vector<std::unique_ptr<SideStream>> sides;
+    std::mutex side_mu;
+    bool vits_fork = true;             // option "vits_fork"
+    SideStream* side_of(hipStream_t s);
+    void drop_sides();
     hipStream_t vstream = nullptr;     // vocoder: K CUs (the engine stream: the other n_cu - K)
     hipEvent_t vev_in = nullptr, vev_done = nullptr;
     bool vpending = false;             // launched, not yet finished

@@ -210,6 +210,7 @@ struct VitsWorkspace {
     float *r2 = nullptr, *r3 = nullptr, *rq = nullptr, *ratt = nullptr;
     float* splitk = nullptr;   // conv split-K partial slabs
     long splitk_cap = 0;
+    float* splitk2 = nullptr;  // ... of the front's text branch on the side stream (same capacity)
     float *sv = nullptr, *pe_ge = nullptr;
     int cap_text = 0;
     std::vector<void*> owned;   // the buffers above except splitk (retired when the workspace grows)

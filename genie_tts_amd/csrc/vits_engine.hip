@@ -342,6 +342,13 @@ struct SplitkScope {
     SplitkScope(float* p, long cap) { tls_splitk = p; tls_splitk_cap = cap; }
     ~SplitkScope() { tls_splitk = nullptr; tls_splitk_cap = 0; }
 };
+// A nested split-K scratch (the front's text branch on the side stream), the outer one restored.
+struct SplitkSwap {
+    float* p;
+    long c;
+    SplitkSwap(float* np, long nc) : p(tls_splitk), c(tls_splitk_cap) { tls_splitk = np; tls_splitk_cap = nc; }
+    ~SplitkSwap() { tls_splitk = p; tls_splitk_cap = c; }
+};
 
 static ConvArgs cargs(const Conv& c, const float* x, int T, float* out, int mode = CV_STORE,
                       const int* seg = nullptr) {
@@ -477,8 +484,9 @@ static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_a
     if (!W.splitk) {
         W.splitk_cap = 2L << 20;   // 8 MB: >= 384 tiles of 64 x 64 (never re-sized: engine lifetime)
         W.splitk = (float*)e->dalloc((size_t)W.splitk_cap * 4);
+        W.splitk2 = (float*)e->dalloc((size_t)W.splitk_cap * 4);
     }
-    if ((g > 0 && !W.g4) || !W.splitk || !W.fm) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
+    if ((g > 0 && !W.g4) || !W.splitk || !W.splitk2 || !W.fm) return set_error(GSV_E_HIP, "VITS workspace allocation failed");
     W.cap_t = t; W.cap_text = sT; W.cap_gen = g; W.cap_spec = f;
     return 0;
 }
@@ -544,6 +552,7 @@ int gsv_engine::vits_read_ms() {
 // XCDs round robin).
 // Lane streams re-created after a change of vocoder_cus / lane_priority (workspaces kept).
 int gsv_engine::remake_lane_streams() {
+    drop_sides();
     for (auto& L : vlanes) {
         hipStream_t ns = nullptr;
         if (make_lane_stream(&ns) != hipSuccess) return set_error(GSV_E_HIP, "lane stream");
@@ -565,6 +574,50 @@ int gsv_engine::stream_cus(hipStream_t st) const {
     for (const VitsLane& L : vlanes)
         if (st == L.st) return lanes_all_cus ? n_cu : vocoder_cus;
     return n_cu;
+}
+
+gsv_engine::SideStream* gsv_engine::side_of(hipStream_t s) {
+    bool own = s && (s == stream || s == vstream);
+    for (const VitsLane& L : vlanes) own = own || s == L.st;
+    if (!own) return nullptr;   // a caller's stream: its lifetime is not the engine's to track
+    std::lock_guard<std::mutex> lk(side_mu);
+    for (auto& p : sides)
+        if (p->main == s) return p.get();
+    auto sd = std::make_unique<SideStream>();
+    sd->main = s;
+    const int words = (n_cu + 31) / 32;
+    std::vector<uint32_t> mask(words, 0u);
+    if (hipExtStreamGetCUMask(s, (uint32_t)words, mask.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;   // mask unknown: a side stream might land on the decode's CUs
+    }
+    bool all = true;
+    for (int i = 0; i < n_cu; ++i) all = all && ((mask[i / 32] >> (i % 32)) & 1u);
+    // CU-masked streams (the vocoder's K CUs beside a decode) keep the front in order: on 64 CUs the
+    // two branches only contend (r06w: 5.66 vs 5.16 ms per VITS beside the decode)
+    if (!all) return nullptr;
+    const hipError_t r = hipStreamCreateWithFlags(&sd->st, hipStreamNonBlocking);
+    if (r != hipSuccess || hipEventCreateWithFlags(&sd->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd->join, hipEventDisableTiming) != hipSuccess) {
+        if (sd->st) hipStreamDestroy(sd->st);
+        if (sd->fork) hipEventDestroy(sd->fork);
+        (void)hipGetLastError();
+        return nullptr;   // the front then runs its branches in order on s
+    }
+    sides.push_back(std::move(sd));
+    return sides.back().get();
+}
+
+// Before one of the engine's streams is destroyed or re-made: the side streams go with them.
+void gsv_engine::drop_sides() {
+    std::lock_guard<std::mutex> lk(side_mu);
+    for (auto& p : sides) {
+        hipStreamSynchronize(p->st);
+        hipStreamDestroy(p->st);
+        hipEventDestroy(p->fork);
+        hipEventDestroy(p->join);
+    }
+    sides.clear();
 }
 
 hipError_t gsv_engine::make_lane_stream(hipStream_t* st) {
@@ -604,6 +657,7 @@ int gsv_engine::set_vocoder_cus(int K) {
             if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
                 return set_error(GSV_E_HIP, "vocoder events");
     }
+    drop_sides();
     if (own_stream && stream) hipStreamDestroy(stream);
     if (vstream) hipStreamDestroy(vstream);
     stream = ns;
@@ -866,19 +920,34 @@ int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text
         ge = ge_in;
         ge_m = ge_adv_in;
     }
+    // ---- the text branch (text embedding, encoder_text, MRTE's text_pre and k/v projection) needs
+    // only the phones: it runs on the side stream beside the SSL branch below (both are chains of
+    // small latency-bound kernels; r06w) and joins before MRTE's attention.  Its buffers (te, t*,
+    // text_enc, mkv) and split-K scratch (splitk2) are its own; same kernels, same results.
+    SideStream* sd = vits_fork ? side_of(s) : nullptr;
+    const hipStream_t ts = sd ? sd->st : s;
+    if (sd) {
+        hipEventRecord(sd->fork, s);
+        hipStreamWaitEvent(ts, sd->fork, 0);
+    }
+    {
+        SplitkSwap sk2(W.splitk2, W.splitk_cap);
+        if (fs) embed_channels_seg(fs->texts, sS, fs->offS, S, V.text_emb, 192, W.te, ts);
+        else embed_channels(text_seq, S, V.text_emb, 192, W.te, ts);
+        attn_encoder(this, V.enc_text, W.te, S, W.tqkv, W.tatt, W.ta, W.tffn, ts, sS, fs ? fs->rowS : nullptr);
+        conv1d(cargs(V.text_pre, W.te, S, W.text_enc, CV_STORE, sS), ts);
+        conv1d(cargs(V.mrte_kv, W.text_enc, S, W.mkv, CV_STORE, sS), ts);
+    }
+    if (sd) hipEventRecord(sd->join, ts);
     // ---- enc_p: codebook decode x2, ssl_proj, encoder_ssl
     if (fs) codebook_upsample2_seg(fs->sems, sT, fs->offT, T, V.codebook, W.q, s);
     else codebook_upsample2(sem, G, V.codebook, W.q, s);
     conv1d(cargs(V.ssl_proj, W.q, T, W.y, CV_STORE, sT), s);
     attn_encoder(this, V.enc_ssl, W.y, T, W.qkv, W.att, W.a, W.ffn, s, sT, fs ? fs->rowT : nullptr);
-    if (fs) embed_channels_seg(fs->texts, sS, fs->offS, S, V.text_emb, 192, W.te, s);
-    else embed_channels(text_seq, S, V.text_emb, 192, W.te, s);
-    attn_encoder(this, V.enc_text, W.te, S, W.tqkv, W.tatt, W.ta, W.tffn, s, sS, fs ? fs->rowS : nullptr);
     // ---- MRTE
     conv1d(cargs(V.c_pre, W.y, T, W.ssl_enc, CV_STORE, sT), s);
-    conv1d(cargs(V.text_pre, W.te, S, W.text_enc, CV_STORE, sS), s);
     conv1d(cargs(V.mrte_qkv_q, W.ssl_enc, T, W.mq, CV_STORE, sT), s);
-    conv1d(cargs(V.mrte_kv, W.text_enc, S, W.mkv, CV_STORE, sS), s);
+    if (sd) hipStreamWaitEvent(s, sd->join, 0);
     MhaArgs m{};
     m.q = W.mq; m.q_ts = 1; m.q_cs = T;
     m.k = W.mkv; m.k_ts = 1; m.k_cs = S;

@@ -444,3 +444,32 @@ def test_vits_batch_weight_stationary_convs_bit_identical(setup):
         e.set_option("convh_ws", 0)
     for i, (g, w) in enumerate(zip(got, want)):
         np.testing.assert_array_equal(g, w, err_msg=f"item {i}")
+
+
+def test_vits_front_text_branch_on_the_side_stream_bit_identical(setup):
+    """Option vits_fork (default 1): the front's text branch (embedding, encoder_text, MRTE text_pre /
+    k-v) runs on a side stream beside the SSL branch and joins before MRTE's attention
+    (vits_front).  Same kernels and buffers of its own: one utterance's audio and a packed batch's
+    are bit-identical with the fork on and off."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    txt = synth.synth_phones(37, "vf")
+    sem = ((np.arange(61, dtype=np.int64) * 29 + 3) % 1024).reshape(1, 1, 61)
+    items = []
+    for i in range(5):
+        G, S = 30 + 9 * i, 14 + 5 * i
+        t = synth.synth_phones(S, f"vfb{i}")
+        sm = ((np.arange(G, dtype=np.int64) * (17 + i) + i) % 1024).reshape(1, 1, G)
+        items.append(dict(text_seq=t, pred_semantic=sm, noise_seed=5000 + i, **kw))
+    out = {}
+    try:
+        for f in (1, 0):
+            e.set_option("vits_fork", f)
+            one = e.vits_decode(txt, sem, noise_seed=77, **kw).cpu().numpy()
+            batch = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+            out[f] = (one, batch)
+    finally:
+        e.set_option("vits_fork", 1)
+    np.testing.assert_array_equal(out[1][0], out[0][0])
+    for i, (a, b) in enumerate(zip(out[1][1], out[0][1])):
+        np.testing.assert_array_equal(a, b, err_msg=f"item {i}")
