@@ -189,7 +189,8 @@ hipError_t gsv_engine::sync_own_streams() {
     {
         std::lock_guard<std::mutex> lk(side_mu);
         for (auto& p : sides)
-            if (r == hipSuccess) r = hipStreamSynchronize(p->st);
+            for (hipStream_t q : p->st)
+                if (r == hipSuccess) r = hipStreamSynchronize(q);
     }
     for (auto& L : vlanes)
         if (L.st && r == hipSuccess) r = hipStreamSynchronize(L.st);

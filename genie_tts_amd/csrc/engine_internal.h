@@ -438,9 +438,9 @@ struct gsv_engine {
     // A second stream beside each of the engine's own unmasked streams, for the VITS front's text
     // branch (vits_front: it needs only the phones, so it runs beside the SSL branch).  Made on first
     // use; dropped (after a sync) before any of the engine's streams is destroyed.
-    struct SideStream {
-        hipStream_t main = nullptr, st = nullptr;
-        hipEvent_t fork = nullptr, join = nullptr;
+    struct SideStream {   // two streams beside `main` (the generator's resblocks 1 and 2; st[0] the front's text branch)
+        hipStream_t main = nullptr, st[2] = {nullptr, nullptr};
+        hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     };
     std::vector<std::unique_ptr<SideStream>> sides;
     std::mutex side_mu;

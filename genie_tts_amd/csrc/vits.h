@@ -96,6 +96,9 @@ bool mrf_pair(const MrfPairArgs& a, hipStream_t s);
 
 // LayerNorm over channels per t: out = LN(x + y) (y may be null), eps 1e-5; seg (segmented
 // batch, as ConvArgs::seg): a gap column is written as zeros
+// out[i] = ((a[i] + b[i]) + c[i]) / div: the MRF mean of a stage's three resblocks in the order of the
+// ACC_FIRST / ACC_ADD / ACC_MEAN chain
+void mean3(const float* a, const float* b, const float* c, float* out, long n, float div, hipStream_t s);
 void ln_channels(const float* x, const float* y, float* out, int C, int T, const float* g,
                  const float* b, hipStream_t s, const int* seg = nullptr);
 
@@ -206,6 +209,7 @@ struct VitsWorkspace {
     float *stats = nullptr, *z = nullptr, *z2 = nullptr, *fh = nullptr, *fx = nullptr, *fa = nullptr;
     float *fskip = nullptr, *fm = nullptr, *gcond = nullptr, *dcond = nullptr;
     float *g0 = nullptr, *g1 = nullptr, *g2 = nullptr, *g3 = nullptr, *g4 = nullptr;
+    float* gx[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // resblocks 1 / 2 on side streams
     float *ge = nullptr, *pad = nullptr, *reim = nullptr, *spec = nullptr, *r0 = nullptr, *r1 = nullptr;
     float *r2 = nullptr, *r3 = nullptr, *rq = nullptr, *ratt = nullptr;
     float* splitk = nullptr;   // conv split-K partial slabs

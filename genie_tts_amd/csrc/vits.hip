@@ -219,6 +219,33 @@ void conv1d(const ConvArgs& a, hipStream_t s) {
     }
 }
 
+__global__ __launch_bounds__(256) void k_mean3(const float4* __restrict__ a, const float4* __restrict__ b,
+                                                const float4* __restrict__ c, float4* __restrict__ o, long n4,
+                                                float div) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float4 x = a[i], y = b[i], z = c[i];
+    o[i] = make_float4(((x.x + y.x) + z.x) / div, ((x.y + y.y) + z.y) / div, ((x.z + y.z) + z.z) / div,
+                       ((x.w + y.w) + z.w) / div);
+}
+__global__ __launch_bounds__(256) void k_mean3_tail(const float* a, const float* b, const float* c, float* o, long lo,
+                                                     long n, float div) {
+    const long i = lo + (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) o[i] = ((a[i] + b[i]) + c[i]) / div;
+}
+
+void mean3(const float* a, const float* b, const float* c, float* out, long n, float div, hipStream_t s) {
+    const bool v4 = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                      reinterpret_cast<uintptr_t>(c) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    const long n4 = v4 ? n / 4 : 0;
+    if (n4 > 0)
+        hipLaunchKernelGGL(k_mean3, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                           (const float4*)a, (const float4*)b, (const float4*)c, (float4*)out, n4, div);
+    if (4 * n4 < n)
+        hipLaunchKernelGGL(k_mean3_tail, dim3((unsigned)((n - 4 * n4 + 255) / 256)), dim3(256), 0, s, a, b, c, out,
+                           4 * n4, n, div);
+}
+
 // ------------------------------------------------------------ segment table
 __global__ __launch_bounds__(256) void k_seg_fill(int* seg, long n, const int* off, const int* len, int nseg,
                                                    int f) {

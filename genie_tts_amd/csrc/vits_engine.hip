@@ -456,6 +456,7 @@ static int ensure_vits_ws(gsv_engine* e, VitsWorkspace& W, int T, int S, int n_a
     const int f = (int)grow_cap(F, W.cap_spec);
     for (void* p : W.owned) e->retire(p);
     W.owned.clear();
+    for (float*& p : W.gx) p = nullptr;
     W.cap_t = W.cap_gen = 0;
     W.cap_text = W.cap_spec = 0;
     e->reclaim();   // a no-op on a lane thread (vb_active): the next growth on the issuing thread frees them
@@ -596,13 +597,19 @@ gsv_engine::SideStream* gsv_engine::side_of(hipStream_t s) {
     // CU-masked streams (the vocoder's K CUs beside a decode) keep the front in order: on 64 CUs the
     // two branches only contend (r06w: 5.66 vs 5.16 ms per VITS beside the decode)
     if (!all) return nullptr;
-    const hipError_t r = hipStreamCreateWithFlags(&sd->st, hipStreamNonBlocking);
-    if (r != hipSuccess || hipEventCreateWithFlags(&sd->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd->join, hipEventDisableTiming) != hipSuccess) {
-        if (sd->st) hipStreamDestroy(sd->st);
+    bool ok = true;
+    for (int k = 0; k < 2; ++k)
+        ok = ok && hipStreamCreateWithFlags(&sd->st[k], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&sd->join[k], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&sd->fork, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        for (int k = 0; k < 2; ++k) {
+            if (sd->st[k]) hipStreamDestroy(sd->st[k]);
+            if (sd->join[k]) hipEventDestroy(sd->join[k]);
+        }
         if (sd->fork) hipEventDestroy(sd->fork);
         (void)hipGetLastError();
-        return nullptr;   // the front then runs its branches in order on s
+        return nullptr;   // the front / generator then run their branches in order on s
     }
     sides.push_back(std::move(sd));
     return sides.back().get();
@@ -612,10 +619,12 @@ gsv_engine::SideStream* gsv_engine::side_of(hipStream_t s) {
 void gsv_engine::drop_sides() {
     std::lock_guard<std::mutex> lk(side_mu);
     for (auto& p : sides) {
-        hipStreamSynchronize(p->st);
-        hipStreamDestroy(p->st);
+        for (int k = 0; k < 2; ++k) {
+            hipStreamSynchronize(p->st[k]);
+            hipStreamDestroy(p->st[k]);
+            hipEventDestroy(p->join[k]);
+        }
         hipEventDestroy(p->fork);
-        hipEventDestroy(p->join);
     }
     sides.clear();
 }
@@ -736,7 +745,8 @@ int gsv_engine::vits_wait(hipStream_t caller) {
 // (segmented batch, else null): the time tables of the 6 rates (T, T u0, ...), and
 // dcond holds one vector per utterance (stride dcond_sstride); gaps stay zero.
 static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const float* z, int T, const float* dcond,
-                           long dcond_sstride, const int* const* seg, float* audio, hipStream_t s) {
+                           long dcond_sstride, const int* const* seg, float* audio, hipStream_t s,
+                           gsv_engine::SideStream* sd = nullptr, float* const* gx = nullptr) {
     float* x = gb[0];
     // x = conv_pre(z) + cond(ge)   (dec#: Conv -> Add(cond))
     ConvArgs c2 = cargs(V.conv_pre, z, T, x, CV_VEC);
@@ -774,6 +784,63 @@ static void vits_generator(const VitsWeights& V, float* const (&gb)[5], const fl
         // the narrow stages (C <= 32, byte-bound): each conv1 + conv2 pair as one kernel with
         // xt in LDS (vits_mrf.hip); its output ping-pongs between rbuf and xt (no in-place update:
         // neighbouring blocks read the input's halo)
+        // One utterance (sd, gx): the stage's three resblocks are independent given yb, so they run
+        // on three streams -- resblock j's steps on its own rbuf / xt, its last step a plain
+        // residual into out_j -- and x = ((out_0 + out_1) + out_2) / 3 afterwards: the arithmetic
+        // and order of the ACC_FIRST / ACC_ADD / ACC_MEAN chain below, so the audio is identical.
+        // Only on the split-fp16 path (no split-K scratch shared between the streams).
+        bool par = sd && gx && tls_ovf;
+        for (int j = 0; j < 3 && par; ++j)
+            for (int mi = 0; mi < 3; ++mi)
+                par = par && V.rb[i * 3 + j][0][mi].wh && V.rb[i * 3 + j][1][mi].wh;
+        if (par) {
+            hipEventRecord(sd->fork, s);
+            for (int k = 0; k < 2; ++k) hipStreamWaitEvent(sd->st[k], sd->fork, 0);
+            float* outs[3] = {accb, gx[2], gx[5]};
+            for (int j = 0; j < 3; ++j) {
+                const hipStream_t js = j == 0 ? s : sd->st[j - 1];
+                float* jr = j == 0 ? rbuf : gx[3 * (j - 1)];
+                float* jx = j == 0 ? xt : gx[3 * (j - 1) + 1];
+                const int kk = V.rb_k[j];
+                const float* rcur = yb;
+                const bool fj = tls_mrf_fused && C <= 32;
+                for (int mi = 0; mi < 3; ++mi) {
+                    const Conv& c1 = V.rb[i * 3 + j][0][mi];
+                    const Conv& c2w = V.rb[i * 3 + j][1][mi];
+                    // fused: ping-pong yb -> jr -> jx -> out (the pair reads its input's halo); unfused:
+                    // conv1 into jx, conv2's residual update in place in jr, the last into out
+                    float* dst = mi == 2 ? outs[j] : (fj ? (mi == 0 ? jr : jx) : jr);
+                    float* scratch = !fj ? jx : (mi == 0 ? jx : mi == 1 ? outs[j] : jr);
+                    bool done = false;
+                    if (fj) {
+                        MrfPairArgs m{};
+                        m.r = rcur; m.T = Tc; m.C = C; m.K = kk; m.dil = V.rb_d[mi];
+                        m.w1 = c1.wh; m.s1 = c1.wscale; m.b1 = c1.b;
+                        m.w2 = c2w.wh; m.s2 = c2w.wscale; m.ovf = tls_ovf;
+                        m.e = cargs(c2w, rcur, Tc, dst);
+                        m.e.res = rcur;
+                        m.e.seg = sg;
+                        m.e.mode = CV_RESID;
+                        done = mrf_pair(m, js);
+                    }
+                    if (!done) {
+                        ConvArgs a1 = cargs(c1, rcur, Tc, scratch);
+                        a1.dil = V.rb_d[mi]; a1.pad = (kk * V.rb_d[mi] - V.rb_d[mi]) / 2; a1.in_act = 1; a1.in_slope = 0.1f;
+                        a1.seg = sg;
+                        conv1d(a1, js);
+                        ConvArgs a2 = cargs(c2w, scratch, Tc, dst);
+                        a2.in_act = 1; a2.in_slope = 0.1f; a2.res = rcur; a2.mode = CV_RESID;
+                        a2.seg = sg;
+                        conv1d(a2, js);
+                    }
+                    rcur = dst;
+                }
+                if (j > 0) hipEventRecord(sd->join[j - 1], js);
+            }
+            for (int k = 0; k < 2; ++k) hipStreamWaitEvent(s, sd->join[k], 0);
+            mean3(outs[0], outs[1], outs[2], x, (long)C * Tc, 3.0f, s);
+            continue;
+        }
         const bool fuse = tls_ovf && tls_mrf_fused && C <= 32;
         for (int j = 0; j < 3 && fuse; ++j) {
             const int kk = V.rb_k[j];
@@ -866,7 +933,24 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
                            noise_scale, W.dcond, s))
         return r;
     float* const gb[5] = {W.g0, W.g1, W.g2, W.g3, W.g4};
-    vits_generator(vits, gb, W.z, 2 * G, W.dcond, 0, nullptr, audio, s);
+    // the three resblocks of a stage on three streams (vits_fork, an unmasked engine stream)
+    SideStream* sd = vits_fork && ovf ? side_of(s) : nullptr;
+    if (sd && !W.gx[0]) {
+        for (float*& p : W.gx) {
+            void* q = nullptr;
+            if (hipMalloc(&q, ((W.cap_gen * 4) + 255) & ~(size_t)255) != hipSuccess) {
+                sd = nullptr;
+                break;
+            }
+            W.owned.push_back(q);   // retired with the workspace's other buffers when it grows
+            p = (float*)q;
+        }
+        if (!sd) {
+            (void)hipGetLastError();
+            for (float*& p : W.gx) p = nullptr;   // (allocated ones stay in W.owned)
+        }
+    }
+    vits_generator(vits, gb, W.z, 2 * G, W.dcond, 0, nullptr, audio, s, sd, sd ? W.gx : nullptr);
     if (timed) hipEventRecord(ev[5], s);   // read by vits_read_ms once the pass is known to be final
     return hipGetLastError() == hipSuccess ? 0 : set_error(GSV_E_HIP, "vits launch");
 }
@@ -925,7 +1009,7 @@ int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text
     // small latency-bound kernels; r06w) and joins before MRTE's attention.  Its buffers (te, t*,
     // text_enc, mkv) and split-K scratch (splitk2) are its own; same kernels, same results.
     SideStream* sd = vits_fork ? side_of(s) : nullptr;
-    const hipStream_t ts = sd ? sd->st : s;
+    const hipStream_t ts = sd ? sd->st[0] : s;
     if (sd) {
         hipEventRecord(sd->fork, s);
         hipStreamWaitEvent(ts, sd->fork, 0);
@@ -938,7 +1022,7 @@ int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text
         conv1d(cargs(V.text_pre, W.te, S, W.text_enc, CV_STORE, sS), ts);
         conv1d(cargs(V.mrte_kv, W.text_enc, S, W.mkv, CV_STORE, sS), ts);
     }
-    if (sd) hipEventRecord(sd->join, ts);
+    if (sd) hipEventRecord(sd->join[0], ts);
     // ---- enc_p: codebook decode x2, ssl_proj, encoder_ssl
     if (fs) codebook_upsample2_seg(fs->sems, sT, fs->offT, T, V.codebook, W.q, s);
     else codebook_upsample2(sem, G, V.codebook, W.q, s);
@@ -947,7 +1031,7 @@ int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text
     // ---- MRTE
     conv1d(cargs(V.c_pre, W.y, T, W.ssl_enc, CV_STORE, sT), s);
     conv1d(cargs(V.mrte_qkv_q, W.ssl_enc, T, W.mq, CV_STORE, sT), s);
-    if (sd) hipStreamWaitEvent(s, sd->join, 0);
+    if (sd) hipStreamWaitEvent(s, sd->join[0], 0);
     MhaArgs m{};
     m.q = W.mq; m.q_ts = 1; m.q_cs = T;
     m.k = W.mkv; m.k_ts = 1; m.k_cs = S;
