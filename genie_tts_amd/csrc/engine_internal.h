@@ -435,9 +435,9 @@ struct gsv_engine {
     int ref_encode(const float* ref_audio, int n_audio, float* ge, hipStream_t s);
     // overlapped vocoder (option "vocoder_cus"): CU-split streams, one call in flight
     int vocoder_cus = 0;
-    // A second stream beside each of the engine's own unmasked streams, for the VITS front's text
-    // branch (vits_front: it needs only the phones, so it runs beside the SSL branch).  Made on first
-    // use; dropped (after a sync) before any of the engine's streams is destroyed.
+    // Two streams beside the engine's unmasked stream for a single VITS call (option vits_fork): the
+    // front's text branch beside its SSL branch, a generator stage's resblocks 1 and 2 beside
+    // resblock 0.  Made on first use; dropped (after a sync) before the engine's streams are destroyed.
     struct SideStream {   // two streams beside `main` (the generator's resblocks 1 and 2; st[0] the front's text branch)
         hipStream_t main = nullptr, st[2] = {nullptr, nullptr};
         hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};

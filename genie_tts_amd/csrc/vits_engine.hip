@@ -934,7 +934,7 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
         return r;
     float* const gb[5] = {W.g0, W.g1, W.g2, W.g3, W.g4};
     // the three resblocks of a stage on three streams (vits_fork, an unmasked engine stream)
-    SideStream* sd = vits_fork && ovf ? side_of(s) : nullptr;
+    SideStream* sd = vits_fork && ovf && s == stream ? side_of(s) : nullptr;
     if (sd && !W.gx[0]) {
         for (float*& p : W.gx) {
             void* q = nullptr;
@@ -1008,7 +1008,9 @@ int gsv_engine::vits_front(VitsWorkspace& W, const int64_t* text_seq, int n_text
     // only the phones: it runs on the side stream beside the SSL branch below (both are chains of
     // small latency-bound kernels; r06w) and joins before MRTE's attention.  Its buffers (te, t*,
     // text_enc, mkv) and split-K scratch (splitk2) are its own; same kernels, same results.
-    SideStream* sd = vits_fork ? side_of(s) : nullptr;
+    // only a single call on the engine stream (the single-request path): beside the next batch's T2S
+    // the batched fronts' second stream only adds contention (r06fin: mixed100 320 vs 325 utt/s)
+    SideStream* sd = vits_fork && !fs && s == stream ? side_of(s) : nullptr;
     const hipStream_t ts = sd ? sd->st[0] : s;
     if (sd) {
         hipEventRecord(sd->fork, s);
