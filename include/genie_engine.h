@@ -373,8 +373,9 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
  * each conv pair of an MRF resblock step of the C <= 32 stages as one kernel, its
  * intermediate in LDS), "sv_f16", "packed", "attn_mf32" (1, default: the prefill's
  * attention on the f32 MFMA with k_attn_flash's exact fma chains; 0: k_attn_flash itself,
- * bit-identical results), "vits_fork" (1, default: the VITS front's text branch on a second stream
- * beside its SSL branch, on the engine's unmasked streams; 0: in order on one stream; bit-identical),
+ * bit-identical results), "vits_fork" (1, default: a single VITS call on the engine's unmasked
+ * stream runs the front's text branch beside its SSL branch and a generator stage's three resblocks
+ * on three streams; 0: in order on one stream; bit-identical),
  * "pf_delay" (0: a B = 1 decode workgroup waits N x s_sleep(32)
  * between its publish and its next-layer refill), A/B options measured and left off:
  * "convh_persist" (the large split-fp16 convs as a persistent tile loop, bit-identical),
