@@ -317,7 +317,7 @@ int gsv_engine::finalize_t2s() {
     if (const char* e = std::getenv("GENIE_PERSISTM")) use_persistm = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PRESPLIT")) use_presplit = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_CONVH")) use_convh = std::atoi(e) != 0;
-    if (const char* e = std::getenv("GENIE_CONVH_WS")) convh_ws = std::atoi(e) != 0;
+    if (const char* e = std::getenv("GENIE_CONVH_WS")) convh_ws = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("GENIE_VITS_FORK")) vits_fork = std::atoi(e) != 0;
     if (const char* e = std::getenv("GENIE_PF_DELAY")) persist1_pf_delay = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GENIE_KTRACE"))
@@ -2052,8 +2052,8 @@ extern "C" int gsv_set_option(gsv_engine* eng, const char* name, int value) {
         eng->use_presplit = value != 0;
     } else if (n == "convh_persist") {
         eng->convh_persist = value != 0;
-    } else if (n == "convh_ws") {
-        eng->convh_ws = value != 0;
+    } else if (n == "convh_ws") {   // 0 off, 1 every batched generator pass, 2 (default) a batch vocoded alone
+        eng->convh_ws = std::max(0, std::min(2, value));
     } else if (n == "vits_fork") {
         eng->vits_fork = value != 0;
     } else if (n == "vocoder_first") {

@@ -188,7 +188,11 @@ struct gsv_engine {
     bool use_convh = true;             // GENIE_CONVH=0: MRF convs on the f32 MFMA path
     bool convt_f16 = true;             // option "convt_f16": the upsample ConvTransposes on the split-fp16 path too
     int convh_tile = 0;                // option "convh_tile": 0 = cost model, 1..4 = force a k_conv_h tile (tests)
-    bool convh_ws = false;             // option "convh_ws": the wide MRF convs weight-stationary (k_conv_ws)
+    // option "convh_ws": the wide MRF convs weight-stationary (k_conv_ws) -- 0 off, 1 in every batched
+    // generator pass, 2 (default) only in a batch the caller waits for (gsv_vits_decode_batch: the
+    // vocoder has the GPU; beside the next batch's T2S its LDS-heavy blocks crowd the prefill out, r06p)
+    int convh_ws = 2;
+    bool vb_alone = false;             // the batch being issued is a synchronous gsv_vits_decode_batch
     bool mrf_fused = true;             // option "mrf_fused": the C <= 32 stages' conv pairs as one kernel
     bool convh_persist = false;        // option "convh_persist": large split-fp16 convs as a persistent tile loop
     int stream_cus(hipStream_t st) const;

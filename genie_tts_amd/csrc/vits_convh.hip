@@ -336,7 +336,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
 }
 
 // Weight-stationary form for the wide generator stages' 7- / 11-tap MRF convs (Cin = 64 / 128,
-// Cout a multiple of 64, unit stride, one phase; option "convh_ws", off by default).  r06o (batch64's vocoder, `profiles/r06o_vocoder_stages.txt`):
+// Cout a multiple of 64, unit stride, one phase; option "convh_ws": by default only in a batch the
+// caller waits for, not beside the next batch's T2S).  r06o (batch64's vocoder, `profiles/r06o_vocoder_stages.txt`):
 // there k_conv_h takes 2-5x the larger of its HBM and MFMA times, because every 64 x 128 block
 // stages its own copy of the chunk's weights (64 rows x taps x 32 channels, 12-45 KB) for 128
 // output columns -- more bytes into LDS than its input tile.  Here a block holds its 64 output

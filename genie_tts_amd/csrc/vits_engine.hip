@@ -926,7 +926,7 @@ int gsv_engine::vits_decode_pass(VitsWorkspace& W, const int64_t* text_seq, int 
     if (int r = ensure_vits_ws(this, W, 2 * G, n_text, version == GSV_V2PP ? 0 : n_audio)) return r;
     SplitkScope sk(W.splitk, W.splitk_cap);
     ConvhScope cs(ovf, convh_tile, convt_f16, mrf_fused, convh_persist ? stream_cus(s) : 0,
-                  convh_ws ? stream_cus(s) : 0);
+                  convh_ws == 1 ? stream_cus(s) : 0);
     (void)hipGetLastError();   // the launches below are checked as one batch at the end
     if (timed) hipEventRecord(ev[4], s);
     if (int r = vits_front(W, text_seq, n_text, sem, G, ref_audio, n_audio, ge_in, ge_adv_in, eps, noise_seed,
@@ -1287,7 +1287,7 @@ int gsv_engine::seg_front(hipStream_t st) {
 int gsv_engine::seg_generate(hipStream_t st, bool f16) {
     SegBatch& B = sgb;
     ConvhScope cs(f16 ? B.ovf : nullptr, convh_tile, convt_f16, mrf_fused, convh_persist ? stream_cus(st) : 0,
-                  convh_ws ? stream_cus(st) : 0);
+                  convh_ws == 1 || (convh_ws == 2 && vb_alone) ? stream_cus(st) : 0);
     const int* seg[6] = {B.seg[0], B.seg[1], B.seg[2], B.seg[3], B.seg[4], B.seg[5]};
     float* const gb[5] = {B.g[0], B.g[1], B.g[2], B.g[3], B.g[4]};
     vits_generator(vits, gb, B.z, B.T, B.dcond, vits.upc, seg, B.audio, st);
@@ -1310,6 +1310,7 @@ void gsv_engine::seg_copy_out(hipStream_t st) {
 // for the issuing threads here; otherwise vits_batch_finish joins them.
 int gsv_engine::vits_batch_launch(float noise_scale, hipStream_t s, bool join) {
     const int n = (int)vb_items.size();
+    vb_alone = join;
     const int K = std::min(n, vits_lanes);
     for (int l = (int)vlanes.size(); l < K; ++l) {
         VitsLane L;

@@ -379,7 +379,9 @@ int gsv_request_stop(gsv_engine* eng, int32_t on);
  * "pf_delay" (0: a B = 1 decode workgroup waits N x s_sleep(32)
  * between its publish and its next-layer refill), A/B options measured and left off:
  * "convh_persist" (the large split-fp16 convs as a persistent tile loop, bit-identical),
- * "convh_ws" (the 7- / 11-tap MRF convs with 64 / 128 input channels weight-stationary, k_conv_ws,
+ * "convh_ws" (the 7- / 11-tap MRF convs with 64 / 128 input channels weight-stationary, k_conv_ws:
+ * 0 off, 1 in every batched generator pass, 2 -- the default -- only in a synchronous
+ * gsv_vits_decode_batch, whose vocoder has the GPU to itself;
  * bit-identical),
  * "vocoder_first" (a batched decode waits for the running vocoder batch), "lanes_all_cus"
  * (under vocoder_cus, the batch lanes on every CU), "knob0".."knob3" (decode tuning variants),

@@ -440,8 +440,12 @@ def test_vits_batch_weight_stationary_convs_bit_identical(setup):
         want = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
         e.set_option("convh_ws", 1)
         got = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
+        e.set_option("convh_ws", 2)   # the default: a synchronous batch runs the form too
+        got2 = [o.cpu().numpy() for o in e.vits_decode_batch(items)]
     finally:
-        e.set_option("convh_ws", 0)
+        e.set_option("convh_ws", 2)
+    for i, (g, w) in enumerate(zip(got2, want)):
+        np.testing.assert_array_equal(g, w, err_msg=f"item {i} (default)")
     for i, (g, w) in enumerate(zip(got, want)):
         np.testing.assert_array_equal(g, w, err_msg=f"item {i}")
 
