@@ -335,6 +335,28 @@ __global__ __launch_bounds__(256, 2) void k_conv_h(ConvArgs a) {
     if (ovf) atomicOr(a.ovf, 1);
 }
 
+// The (WM, WN, KS) candidate of launch_h for a conv (the cost model, or the test / env override).
+struct Cand { int wm, wn, ks; };
+static const Cand convh_cands[4] = {{2, 2, 1}, {1, 2, 2}, {1, 1, 4}, {1, 4, 1}};
+static int convh_choice(const ConvArgs& a) {
+    // (WM, WN, KS) by estimated time: block rounds at 2 blocks per CU x tile area
+    // (4 waves share a block's work whatever KS), a small price per K-split way
+    // (fits tools/convh_prof.sh on the generator's stage shapes).
+    int best = -1;
+    double best_cost = 1e30;
+    for (int i = 0; i < 4; ++i) {
+        const int bm = 32 * convh_cands[i].wm, bn = 64 * convh_cands[i].wn;
+        const long blocks = (long)((a.n_t + bn - 1) / bn) * ((a.Cout + bm - 1) / bm) * (a.phases > 1 ? a.phases : 1);
+        const long rounds = (blocks + 511) / 512;
+        const double cost = (double)rounds * bm * bn * (1.0 + 0.1 * (convh_cands[i].ks - 1));
+        if (cost < best_cost) { best_cost = cost; best = i; }
+    }
+    static const int forced = [] { const char* e = std::getenv("GENIE_CONVH_CFG"); return e ? std::atoi(e) : -1; }();
+    if (forced >= 0 && forced < 4) best = forced;
+    if (a.tile_force >= 1 && a.tile_force <= 4) best = a.tile_force - 1;
+    return best;
+}
+
 // Weight-stationary form for the wide generator stages' 7- / 11-tap MRF convs (Cin = 64 / 128,
 // Cout a multiple of 64, unit stride, one phase; option "convh_ws": by default only in a batch the
 // caller waits for, not beside the next batch's T2S).  r06o (batch64's vocoder, `profiles/r06o_vocoder_stages.txt`):
@@ -534,6 +556,9 @@ bool try_ws(const ConvArgs& a, hipStream_t s) {
               a.mode == CV_ACC_MEAN))
             return false;
         if ((a.n_t + 255) / 256 < 2L * a.ws) return false;   // >= 2 tiles per lane
+        // only where k_conv_h would run its (2, 2, 1) form, whose MFMA sequence k_conv_ws runs: the
+        // same bits either way (a K-split form sums in another order)
+        if (convh_choice(a) != 0) return false;
         if (a.Cin == 64) {
             launch_ws<KT, 64>(a, s);
             return true;
@@ -550,23 +575,8 @@ bool try_ws(const ConvArgs& a, hipStream_t s) {
 
 template <int KT, int CC>
 bool launch_h(const ConvArgs& a, hipStream_t s) {
-    // (WM, WN, KS) by estimated time: block rounds at 2 blocks per CU x tile area
-    // (4 waves share a block's work whatever KS), a small price per K-split way
-    // (fits tools/convh_prof.sh on the generator's stage shapes).
-    struct Cand { int wm, wn, ks; };
-    static const Cand cands[4] = {{2, 2, 1}, {1, 2, 2}, {1, 1, 4}, {1, 4, 1}};
-    int best = -1;
-    double best_cost = 1e30;
-    for (int i = 0; i < 4; ++i) {
-        const int bm = 32 * cands[i].wm, bn = 64 * cands[i].wn;
-        const long blocks = (long)((a.n_t + bn - 1) / bn) * ((a.Cout + bm - 1) / bm) * (a.phases > 1 ? a.phases : 1);
-        const long rounds = (blocks + 511) / 512;
-        const double cost = (double)rounds * bm * bn * (1.0 + 0.1 * (cands[i].ks - 1));
-        if (cost < best_cost) { best_cost = cost; best = i; }
-    }
-    static const int forced = [] { const char* e = std::getenv("GENIE_CONVH_CFG"); return e ? std::atoi(e) : -1; }();
-    if (forced >= 0 && forced < 4) best = forced;
-    if (a.tile_force >= 1 && a.tile_force <= 4) best = a.tile_force - 1;
+    const Cand* cands = convh_cands;
+    const int best = convh_choice(a);
     const Cand c = cands[best];
     const dim3 grid((a.n_t + 64 * c.wn - 1) / (64 * c.wn), (a.Cout + 32 * c.wm - 1) / (32 * c.wm),
                     a.phases > 1 ? a.phases : 1);
