@@ -477,3 +477,24 @@ def test_vits_front_text_branch_on_the_side_stream_bit_identical(setup):
     np.testing.assert_array_equal(out[1][0], out[0][0])
     for i, (a, b) in enumerate(zip(out[1][1], out[0][1])):
         np.testing.assert_array_equal(a, b, err_msg=f"item {i}")
+
+
+def test_vits_fork_survives_stream_remakes(setup):
+    """The fork's side streams are made beside the engine stream and dropped whenever the engine
+    re-makes its streams (option vocoder_cus): a forked single call, then the CU split on and an
+    overlapped call (masked stream: no fork), then the split off and a forked call again -- every
+    result equals the first, bit for bit."""
+    ver, e, _, _ = setup
+    kw = _cond(ver)
+    txt = synth.synth_phones(29, "vr")
+    sem = ((np.arange(53, dtype=np.int64) * 31 + 5) % 1024).reshape(1, 1, 53)
+    first = e.vits_decode(txt, sem, noise_seed=91, **kw).cpu().numpy()
+    try:
+        e.set_vocoder_cus(64)
+        out = e.vits_decode_async(dict(text_seq=txt, pred_semantic=sem, noise_seed=91, **kw))
+        e.vits_wait()
+        np.testing.assert_array_equal(out.cpu().numpy(), first)
+    finally:
+        e.set_vocoder_cus(0)
+    again = e.vits_decode(txt, sem, noise_seed=91, **kw).cpu().numpy()
+    np.testing.assert_array_equal(again, first)
